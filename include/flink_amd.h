@@ -1,0 +1,197 @@
+/*
+ * flink_amd.h -- C-ABI of the MI355X keyed event-time window-aggregation engine.
+ *
+ * This is the drop-in boundary for Flink's keyed windowed-aggregation hot path
+ * (SURVEY.md §8(b)). A Java shim (JNI, or Panama FFM on JDK >= 22) sitting behind
+ * the unchanged Flink operator surface calls these entry points; see INTEGRATION.md
+ * for the binding stubs. No torch types cross this boundary: plain pointers + sizes.
+ *
+ * Entry point -> reference interface it replaces:
+ *   fwa_create             WindowOperator ctor + open()
+ *                            flink-streaming-java/.../runtime/operators/windowing/WindowOperator.java:179-266
+ *                          SlicingWindowAggOperatorBuilder.build + AbstractWindowAggProcessor.open
+ *                            flink-table-runtime/.../aggregate/window/SlicingWindowAggOperatorBuilder.java:127-171
+ *   fwa_push               WindowOperator.processElement (per record, batched here)
+ *                            WindowOperator.java:278-434
+ *                          SlicingWindowProcessor.processElement  SlicingWindowProcessor.java:53
+ *                            (AbstractWindowAggProcessor.java:142-182)
+ *   fwa_advance_watermark  AbstractStreamOperator.processWatermark -> InternalTimerServiceImpl.advanceWatermark
+ *                            -> WindowOperator.onEventTime      (InternalTimerServiceImpl.java:302-314,
+ *                                                                 WindowOperator.java:437-481)
+ *                          SlicingWindowOperator.processWatermark/onTimer (SlicingWindowOperator.java:230-264)
+ *                            -> fireWindow/clearWindow (SliceSharedWindowAggProcessor.java:64-118,
+ *                               SliceUnsharedWindowAggProcessor.java:46-55)
+ *   fwa_flush              SlicingWindowProcessor.prepareCheckpoint (RecordsWindowBuffer.flush :107-118)
+ *   fwa_key_groups         KeyGroupRangeAssignment.assignToKeyGroup + computeOperatorIndexForKeyGroup
+ *                            flink-runtime/.../state/KeyGroupRangeAssignment.java:63-127
+ *                          (the keyBy partitioner KeyGroupStreamPartitioner.selectChannel :55-65)
+ *   fwa_destroy            WindowOperator.close / SlicingWindowProcessor.close
+ *
+ * Status codes mirror the Java exceptions the reference throws.
+ * Late records are not errors: they are counted (numLateRecordsDropped,
+ * WindowOperator.java:140,431; SlicingWindowOperator.java:108-110).
+ */
+#ifndef FLINK_AMD_H
+#define FLINK_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FWA_ABI_VERSION 1
+#define FWA_MAX_AGGS 8
+#define FWA_MAX_COLS 8
+
+/* Window kinds. TUMBLE: TumblingEventTimeWindows / TUMBLE TVF. SLIDE: SlidingEventTimeWindows
+ * (DataStream, any size/slide) / HOP TVF (Table, size % slide == 0). CUMULATE: CUMULATE TVF
+ * (Table only). SESSION: EventTimeSessionWindows / legacy GROUP BY SESSION (merging). */
+enum fwa_window_kind { FWA_TUMBLE = 0, FWA_SLIDE = 1, FWA_CUMULATE = 2, FWA_SESSION = 3 };
+
+/* Which operator's observable semantics to reproduce.
+ * DATASTREAM: WindowOperator + EventTimeTrigger (allowed lateness supported, late firings).
+ * TABLE:      SlicingWindowOperator + Slice{Shared,Unshared}WindowAggProcessor (HOP/CUMULATE
+ *             emit only if COUNT(*) > 0, late records routed to unfired windows). */
+enum fwa_semantics { FWA_SEM_DATASTREAM = 0, FWA_SEM_TABLE = 1 };
+
+/* How the key-group hash is computed from the int64 key column.
+ * JAVA_LONG:      Long.hashCode(key) = (int)(key ^ (key >>> 32))            (DataStream keyBy on a Long)
+ * BINROW_BIGINT:  BinaryRowData.hashCode of a 1-field BIGINT key row         (Table GROUP BY a BIGINT)
+ *                 = MurmurHashUtils.hashBytesByWords over [0, 0, lo32, hi32], seed 42
+ * PREHASHED:      the caller passes key.hashCode() in the low 32 bits of a separate column
+ *                 (fwa_push key_hash argument); the int64 key is an opaque dictionary id. */
+enum fwa_key_kind { FWA_KEY_JAVA_LONG = 0, FWA_KEY_BINROW_BIGINT = 1, FWA_KEY_PREHASHED = 2 };
+
+/* Aggregates. Result column type in brackets. */
+enum fwa_agg_kind {
+    FWA_COUNT = 0,   /* COUNT(*)                                   [i64] */
+    FWA_SUM_I64 = 1, /* SUM(BIGINT), two's-complement wrap          [i64] */
+    FWA_SUM_F32 = 2, /* SUM(FLOAT)                                  [f32] */
+    FWA_SUM_F64 = 3, /* SUM(DOUBLE)                                 [f64] */
+    FWA_MIN_I64 = 4, /*                                             [i64] */
+    FWA_MAX_I64 = 5, /*                                             [i64] */
+    FWA_MIN_F32 = 6, /*                                             [f32] */
+    FWA_MAX_F32 = 7, /*                                             [f32] */
+    FWA_MIN_F64 = 8, /*                                             [f64] */
+    FWA_MAX_F64 = 9, /*                                             [f64] */
+    FWA_AVG_I64 = 10,/* AVG(BIGINT): sum/count, truncating division [i64] */
+    FWA_AVG_F32 = 11,/* AVG(FLOAT): double sum / count, cast float  [f32] */
+    FWA_AVG_F64 = 12,/* AVG(DOUBLE)                                 [f64] */
+    FWA_AGG_KIND_COUNT = 13
+};
+
+enum fwa_status {
+    FWA_OK = 0,
+    FWA_E_ARG = -1,         /* IllegalArgumentException (e.g. abs(offset) >= size, TumblingEventTimeWindows.java:58-62) */
+    FWA_E_TS_MIN = -2,      /* Long.MIN_VALUE timestamp (TumblingEventTimeWindows.java:83-86) */
+    FWA_E_KEYGROUP = -3,    /* key group outside the owned range (StateTable.java:300-307) */
+    FWA_E_MERGE_LATE = -4,  /* merged session window ends before the watermark (WindowOperator.java:308-319) */
+    FWA_E_OOM = -5,         /* device memory exhausted */
+    FWA_E_DEVICE = -6,      /* HIP runtime error */
+    FWA_E_UNSUPPORTED = -7, /* configuration not supported by this engine build */
+    FWA_E_STATE = -8        /* API misuse (e.g. call on a destroyed handle) */
+};
+
+/* Flags for fwa_push */
+#define FWA_PUSH_DEVICE_PTRS 0x1 /* key/ts/value pointers are device (HBM) pointers */
+#define FWA_PUSH_ASYNC 0x2       /* do not synchronise; late_dropped_out is not written */
+
+typedef struct fwa_agg_spec {
+    int32_t kind; /* enum fwa_agg_kind */
+    int32_t col;  /* index into the value-column array of fwa_push (ignored for COUNT) */
+} fwa_agg_spec;
+
+typedef struct fwa_config {
+    int32_t abi_version;         /* must be FWA_ABI_VERSION */
+    int32_t window_kind;         /* enum fwa_window_kind */
+    int32_t semantics;           /* enum fwa_semantics */
+    int32_t key_kind;            /* enum fwa_key_kind */
+    int64_t size_ms;             /* TUMBLE size; SLIDE size; CUMULATE max size */
+    int64_t slide_ms;            /* SLIDE slide; CUMULATE step; unused otherwise */
+    int64_t offset_ms;           /* window offset (assigner 'offset'); 0 = epoch aligned */
+    int64_t gap_ms;              /* SESSION gap */
+    int64_t allowed_lateness_ms; /* DATASTREAM only (WindowOperator allowedLateness) */
+    int32_t max_parallelism;     /* number of key groups (pipeline.max-parallelism), default 128 */
+    int32_t kg_start;            /* owned key-group range [kg_start, kg_end] (inclusive) */
+    int32_t kg_end;
+    int32_t num_aggs;
+    fwa_agg_spec aggs[FWA_MAX_AGGS];
+    int32_t device;              /* HIP device ordinal */
+    int32_t output_on_device;    /* 1: fwa_out points into HBM; 0: engine copies rows to host */
+    int64_t key_capacity;        /* sizing hint: max distinct live keys (0 = default 1<<20) */
+    int64_t max_batch;           /* sizing hint: max records per fwa_push (0 = default 1<<26) */
+} fwa_config;
+
+typedef struct fwa_out {
+    int64_t n_rows;
+    int32_t on_device;           /* pointers below are device pointers if 1 */
+    int32_t num_aggs;
+    const int64_t* key;
+    const int64_t* win_start;
+    const int64_t* win_end;      /* DataStream record timestamp = win_end - 1 (TimeWindow.maxTimestamp) */
+    const void* agg[FWA_MAX_AGGS];
+} fwa_out;
+
+typedef struct fwa_stats {
+    int64_t records_in;
+    int64_t late_dropped;        /* numLateRecordsDropped */
+    int64_t rows_out;
+    int64_t live_keys;
+    int64_t live_slices;
+    int64_t current_watermark;
+} fwa_stats;
+
+typedef struct fwa_engine fwa_engine;
+
+/* Engine lifecycle. Handles are single-threaded (one Flink subtask / mailbox thread each);
+ * distinct handles may be used concurrently (one HIP stream per handle). */
+int fwa_create(const fwa_config* cfg, fwa_engine** out);
+void fwa_destroy(fwa_engine* e);
+const char* fwa_last_error(const fwa_engine* e);
+const char* fwa_version(void);
+
+/* Columnar batch of n records: keys[n], ts[n], val_cols[c][n] (type implied by the aggs reading c).
+ * key_hash may be NULL unless key_kind == FWA_KEY_PREHASHED (then int32 key.hashCode() per record).
+ * Input buffers are borrowed for the duration of the call only. */
+int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
+             const int32_t* key_hash, int64_t n, int32_t flags, int64_t* late_dropped_out);
+
+/* Advance the event-time watermark; fires every window whose maxTimestamp (end-1) <= wm.
+ * Non-advancing watermarks are ignored (SlicingWindowOperator.java:231, StatusWatermarkValve).
+ * Output rows (fired (key, window) results) stay valid until the next call on this handle. */
+int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out);
+
+/* Make every pushed record visible in state (checkpoint barrier, SlicingWindowOperator.java:267-269). */
+int fwa_flush(fwa_engine* e);
+
+int fwa_get_stats(fwa_engine* e, fwa_stats* out);
+
+/* Stateless key-group assignment of n keys (device or host pointers per flags):
+ * kg_out[i] = murmurHash(hash(key_i)) % max_parallelism; op_out[i] = kg*parallelism/max_parallelism.
+ * op_out may be NULL. */
+int fwa_key_groups(const int64_t* keys, const int32_t* key_hash, int64_t n, int32_t key_kind,
+                   int32_t max_parallelism, int32_t parallelism, int32_t* kg_out, int32_t* op_out,
+                   int32_t flags, int32_t device);
+
+/* ---- bench / test support (synthetic streams of SURVEY.md §8(d), generated in HBM) ---- */
+typedef struct fwa_gen_params {
+    uint64_t seed_k, seed_t, seed_v;
+    int64_t first_index;   /* global record index of element 0 (multi-GPU: rank's slice) */
+    int64_t total_records; /* N of the whole stream (drives the ts ramp) */
+    int64_t num_keys;      /* K */
+    int64_t t0_ms;         /* T0 */
+    int64_t span_ms;       /* event-time span of the whole stream */
+    int64_t max_delay_ms;  /* D (bounded out-of-orderness) */
+    int32_t key_dist;      /* 0 uniform, 1 zipf (needs cdf) */
+    int32_t val_kind;      /* 0: i64 non-negative 31-bit; 1: f32+f64 in [0,1) */
+    const double* zipf_cdf;/* device pointer, num_keys entries (key_dist==1) */
+} fwa_gen_params;
+
+int fwa_generate(const fwa_gen_params* p, int64_t n, int64_t* keys, int64_t* ts, int64_t* v_i64,
+                 float* v_f32, double* v_f64, int32_t device, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLINK_AMD_H */

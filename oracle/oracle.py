@@ -1,0 +1,159 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes wrapper of the CPU oracle (oracle/liboracle.so).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker.
+The product (flink_amd/) never imports this module.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from flink_amd import _abi as A
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        A.bind_common(L, "or_")
+        L.or_push.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                              C.c_int64, C.POINTER(C.c_int64)]
+        L.or_push.restype = C.c_int
+        for f in ("or_murmur_hash", "or_bit_mix"):
+            getattr(L, f).argtypes = [C.c_int32]
+            getattr(L, f).restype = C.c_int32
+        L.or_long_hash.argtypes = [C.c_int64]
+        L.or_long_hash.restype = C.c_int32
+        L.or_binrow_bigint_hash.argtypes = [C.c_int64]
+        L.or_binrow_bigint_hash.restype = C.c_int32
+        L.or_key_group.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32]
+        L.or_key_group.restype = C.c_int32
+        L.or_operator_index.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+        L.or_operator_index.restype = C.c_int32
+        L.or_key_group_range.argtypes = [C.c_int32, C.c_int32, C.c_int32,
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.or_window_start.argtypes = [C.c_int64, C.c_int64, C.c_int64]
+        L.or_window_start.restype = C.c_int64
+        L.or_assign_windows.argtypes = [C.POINTER(A.Config), C.c_int64, C.c_void_p, C.c_void_p, C.c_int]
+        L.or_assign_windows.restype = C.c_int
+        L.or_assign_slice_end.argtypes = [C.POINTER(A.Config), C.c_int64]
+        L.or_assign_slice_end.restype = C.c_int64
+        L.or_splitmix64.argtypes = [C.c_uint64]
+        L.or_splitmix64.restype = C.c_uint64
+        L.or_generate.argtypes = [C.POINTER(A.GenParams), C.c_int64, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_generate.restype = None
+        L.or_bench_pipeline.argtypes = [C.POINTER(A.Config), C.POINTER(A.GenParams), C.c_int64,
+                                        C.c_int64, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
+        L.or_bench_pipeline.restype = C.c_double
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (A.STATUS.get(code, code), msg))
+        self.code = code
+
+
+def rows_from_out(out, names):
+    """Copy an fwa_out (host pointers) into a dict of numpy arrays."""
+    n = out.n_rows
+    res = {}
+    for field, dt in (("key", np.int64), ("win_start", np.int64), ("win_end", np.int64)):
+        p = getattr(out, field)
+        res[field] = (np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int64)), (n,)).copy()
+                      if n else np.zeros(0, dt))
+    for j, name in enumerate(names):
+        dt = np.dtype(A.AGG_RESULT_DTYPE[name])
+        if n == 0:
+            res["agg%d" % j] = np.zeros(0, dt)
+            continue
+        # oracle stores each result in an 8-byte slot (union); f32 results sit in the low 4 bytes
+        raw = np.ctypeslib.as_array(C.cast(out.agg[j], C.POINTER(C.c_uint64)), (n,)).copy()
+        if dt.itemsize == 4:
+            res["agg%d" % j] = (raw & 0xffffffff).astype(np.uint32).view(dt)
+        else:
+            res["agg%d" % j] = raw.view(dt)
+    return res
+
+
+class Oracle:
+    """Same contract as flink_amd.WindowAggregator, computed on the CPU by the restatement."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.names = A.agg_names(cfg)
+        self.h = C.c_void_p()
+        rc = lib().or_create(C.byref(cfg), C.byref(self.h))
+        if rc:
+            raise OracleError(rc, "or_create")
+
+    def push(self, keys, ts, cols=(), key_hash=None):
+        keys = np.ascontiguousarray(keys, np.int64)
+        ts = np.ascontiguousarray(ts, np.int64)
+        cols = [np.ascontiguousarray(c) for c in cols]
+        arr = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
+        kh = None if key_hash is None else np.ascontiguousarray(key_hash, np.int32)
+        dropped = C.c_int64(0)
+        rc = lib().or_push(self.h, _ptr(keys), _ptr(ts), arr, _ptr(kh), len(keys), C.byref(dropped))
+        if rc:
+            raise OracleError(rc, lib().or_last_error(self.h).decode())
+        return dropped.value
+
+    def advance_watermark(self, wm):
+        out = A.Out()
+        rc = lib().or_advance_watermark(self.h, wm, C.byref(out))
+        if rc:
+            raise OracleError(rc, lib().or_last_error(self.h).decode())
+        return rows_from_out(out, self.names)
+
+    def stats(self):
+        st = A.Stats()
+        lib().or_get_stats(self.h, C.byref(st))
+        return st
+
+    def close(self):
+        if self.h:
+            lib().or_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def generate(params, n, want_floats=False, cdf=None):
+    """CPU generator of the synthetic stream (bit-identical to the device generator)."""
+    keys = np.empty(n, np.int64)
+    ts = np.empty(n, np.int64)
+    vi = np.empty(n, np.int64)
+    vf = np.empty(n, np.float32) if want_floats else None
+    vd = np.empty(n, np.float64) if want_floats else None
+    cdf_a = None if cdf is None else np.ascontiguousarray(cdf, np.float64)
+    lib().or_generate(C.byref(params), n, _ptr(keys), _ptr(ts), _ptr(vi), _ptr(vf), _ptr(vd), _ptr(cdf_a))
+    return keys, ts, vi, vf, vd
+
+
+def bench_pipeline(cfg, params, n, batch, threads):
+    rows = C.c_int64(0)
+    cs = C.c_uint64(0)
+    secs = lib().or_bench_pipeline(C.byref(cfg), C.byref(params), n, batch, threads, C.byref(rows), C.byref(cs))
+    return secs, rows.value, cs.value

@@ -1,0 +1,84 @@
+"""Shared test helpers: KAT replay and multiset comparison of fired rows."""
+import json
+import os
+
+import numpy as np
+
+from flink_amd import _abi as A
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load_kats():
+    with open(os.path.join(GOLDEN, "reference_kats.json")) as f:
+        return json.load(f)
+
+
+def kat_config(case, **kw):
+    return A.make_config(window_kind=case["window_kind"], semantics=case["semantics"],
+                         size_ms=case["size_ms"], slide_ms=case["slide_ms"],
+                         offset_ms=case["offset_ms"], gap_ms=case["gap_ms"],
+                         allowed_lateness_ms=case["allowed_lateness_ms"],
+                         aggs=[tuple(a) for a in case["aggs"]], **kw)
+
+
+def rows_to_tuples(rows, naggs):
+    cols = [rows["key"], rows["win_start"], rows["win_end"]] + [rows["agg%d" % j] for j in range(naggs)]
+    out = []
+    for i in range(len(rows["key"])):
+        out.append(tuple(c[i].item() for c in cols))
+    return sorted(out)
+
+
+def replay_kat(case, make_engine):
+    """Feed a KAT event sequence through an engine; assert every watermark's fired multiset."""
+    eng = make_engine(kat_config(case))
+    naggs = len(case["aggs"])
+    dropped = 0
+    pend = []
+
+    def flush():
+        nonlocal dropped, pend
+        if pend:
+            k = np.array([p[0] for p in pend], np.int64)
+            v = np.array([p[1] for p in pend], np.int64)
+            t = np.array([p[2] for p in pend], np.int64)
+            dropped += eng.push(k, t, [v])
+            pend = []
+
+    for ev in case["events"]:
+        if ev[0] == "e":
+            pend.append((ev[1], ev[2], ev[3]))
+        else:
+            flush()
+            rows = eng.advance_watermark(ev[1])
+            got = rows_to_tuples(rows, naggs)
+            exp = sorted(tuple(r) for r in ev[2])
+            assert got == exp, "%s: wm=%d expected %s got %s" % (case["name"], ev[1], exp, got)
+    flush()
+    assert dropped == case["late_dropped"], "%s: late dropped %d != %d" % (case["name"], dropped, case["late_dropped"])
+    eng.close()
+
+
+def assert_rows_equal(a, b, names, rtol=None, ctx=""):
+    """Multiset equality of two fired-row dicts. Integer columns bit-exact; float columns within rtol
+    (relative, with the same absolute floor) when rtol is given, else exact."""
+    n = len(a["key"])
+    assert n == len(b["key"]), "%s row count %d != %d" % (ctx, n, len(b["key"]))
+    if n == 0:
+        return
+    oa = np.lexsort((a["win_end"], a["win_start"], a["key"]))
+    ob = np.lexsort((b["win_end"], b["win_start"], b["key"]))
+    for f in ("key", "win_start", "win_end"):
+        assert np.array_equal(a[f][oa], b[f][ob]), "%s column %s differs" % (ctx, f)
+    for j, name in enumerate(names):
+        x = a["agg%d" % j][oa]
+        y = b["agg%d" % j][ob]
+        if x.dtype.kind == "f" and rtol is not None:
+            tol = rtol(name) if callable(rtol) else rtol
+            assert np.allclose(x, y, rtol=tol, atol=tol), "%s agg %s max rel err %g" % (
+                ctx, name, np.max(np.abs(x - y) / np.maximum(np.abs(y), 1e-30)))
+        else:
+            bad = np.nonzero(x != y)[0]
+            assert len(bad) == 0, "%s agg %s differs at %d rows, first %s vs %s" % (
+                ctx, name, len(bad), x[bad[0]], y[bad[0]])

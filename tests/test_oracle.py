@@ -1,0 +1,76 @@
+"""CPU tests: the oracle restatement against the reference's own known-answer vectors."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from flink_amd import _abi as A
+from oracle import oracle as O
+from helpers import load_kats, replay_kat
+
+KATS = load_kats()
+
+
+@pytest.mark.parametrize("case", KATS["assigners"], ids=lambda c: c["src"].split("/")[-1])
+def test_assigner_kats(case):
+    cfg = A.make_config(window_kind=case["kind"], size_ms=case["size"], slide_ms=case.get("slide", 0),
+                        offset_ms=case["offset"])
+    for ts, exp in case["cases"]:
+        starts = np.zeros(64, np.int64)
+        ends = np.zeros(64, np.int64)
+        n = O.lib().or_assign_windows(C.byref(cfg), ts, starts.ctypes.data, ends.ctypes.data, 64)
+        got = sorted(zip(starts[:n].tolist(), ends[:n].tolist()))
+        assert got == sorted(tuple(w) for w in exp), (ts, got, exp)
+
+
+@pytest.mark.parametrize("case", KATS["slice_ends"], ids=lambda c: c["src"].split("/")[-1])
+def test_slice_end_kats(case):
+    cfg = A.make_config(window_kind=case["kind"], semantics="TABLE", size_ms=case["size"],
+                        slide_ms=case["slide"], offset_ms=case["offset"])
+    for ts, exp in case["cases"]:
+        assert O.lib().or_assign_slice_end(C.byref(cfg), ts) == exp
+
+
+@pytest.mark.parametrize("case", KATS["operators"], ids=lambda c: c["name"].split(" ")[0])
+def test_operator_kats(case):
+    replay_kat(case, O.Oracle)
+
+
+def test_murmur_properties():
+    L = O.lib()
+    # murmurHash is non-negative and INT_MIN folds to 0 (MathUtils.java:150-154)
+    for code in [0, 1, -1, 42, 2**31 - 1, -2**31, 123456789, -987654321]:
+        assert L.or_murmur_hash(code) >= 0
+    # key groups within range and operator index formula
+    for k in range(-1000, 1000, 7):
+        kg = L.or_key_group(k, A.KEY_JAVA_LONG, 0, 128)
+        assert 0 <= kg < 128
+        assert L.or_operator_index(128, 8, kg) == kg * 8 // 128
+
+
+def test_key_group_ranges_partition():
+    L = O.lib()
+    for maxp, par in [(128, 1), (128, 2), (128, 3), (128, 8), (32768, 7)]:
+        covered = []
+        for i in range(par):
+            s, e = C.c_int32(), C.c_int32()
+            L.or_key_group_range(maxp, par, i, C.byref(s), C.byref(e))
+            covered.extend(range(s.value, e.value + 1))
+            for kg in (s.value, e.value):
+                assert L.or_operator_index(maxp, par, kg) == i
+        assert covered == list(range(maxp))
+
+
+def test_keygroup_violation_raises():
+    cfg = A.make_config(kg_start=0, kg_end=0)
+    o = O.Oracle(cfg)
+    with pytest.raises(O.OracleError) as ei:
+        o.push(np.arange(100), np.arange(100), [np.arange(100)])
+    assert ei.value.code == -3
+
+
+def test_ts_min_raises():
+    o = O.Oracle(A.make_config())
+    with pytest.raises(O.OracleError) as ei:
+        o.push(np.array([1]), np.array([A.LONG_MIN]), [np.array([1])])
+    assert ei.value.code == -2
