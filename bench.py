@@ -1,0 +1,197 @@
+"""Benchmark: records/sec aggregated by the MI355X window engine (BASELINE.json metric).
+
+Workload (N=1): config C2 of BASELINE.json -- event-time tumbling 10 s window, COUNT + SUM(long), over
+synthetic (long key, long ts, long val) records, 1M uniform keys, 1e9 records (15 batches of 2^26 =
+1.007e9), bounded out-of-orderness D = 1 s, wm = max_ts - D - 1 after every batch, final wm = Long.MAX.
+A step = one batch pushed through the engine + the watermark advance that fires its windows. Inputs are
+generated into HBM before timing; outputs stay in HBM.
+
+N>1 (torchrun, one rank per GPU): weak scaling -- every rank sources a stream of the same size and
+event-time range (its own key/value seeds), records are routed to their key-group owner with RCCL
+all_to_all (flink_amd.distributed, the keyBy shuffle), watermark = MIN-allreduce over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+C2_RECORDS = 1_000_000_000
+C2_SPAN_MS = 1_000_000   # 1000 s of event time for 1e9 records
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=14)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1 << 26)
+    ap.add_argument("--keys", type=int, default=1_000_000)
+    ap.add_argument("--window-ms", type=int, default=10_000)
+    ap.add_argument("--delay-ms", type=int, default=1000)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 26)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from flink_amd import _abi as A
+    from flink_amd import engine as E
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    B = args.batch
+    S = args.warmup + args.steps
+    n_rank = S * B
+    # event-time density of C2 (1e6 records per second of event time) on every rank
+    span = n_rank * C2_SPAN_MS // C2_RECORDS
+    p = A.GenParams(seed_k=0x5eed0001 ^ (rank * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF),
+                    seed_t=0x5eed0002 + rank, seed_v=0x5eed0003 + rank, first_index=0, total_records=n_rank,
+                    num_keys=args.keys, t0_ms=1_700_000_000_000, span_ms=span, max_delay_ms=args.delay_ms,
+                    key_dist=0, val_kind=0)
+    log("rank %d/%d generating %d records (%.1f GB) in HBM" % (rank, world, n_rank, n_rank * 24 / 1e9))
+    keys = torch.empty(n_rank, dtype=torch.int64, device=dev)
+    ts = torch.empty_like(keys)
+    vals = torch.empty_like(keys)
+    E.generate(p, n_rank, keys, ts, vals, device=local_rank)
+    torch.cuda.synchronize()
+    bmax = ts.view(S, B).max(dim=1).values.cpu().numpy()
+    wms = []
+    m = -2**63
+    for b in range(S):
+        m = max(m, int(bmax[b]))
+        wms.append(m - args.delay_ms - 1)          # BoundedOutOfOrdernessWatermarks.onPeriodicEmit
+    wms[-1] = A.LONG_MAX                           # final watermark flushes every window
+
+    cfg_kw = dict(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=args.window_ms,
+                  aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=args.keys,
+                  output_on_device=1, device=local_rank)
+    if world > 1:
+        from flink_amd.distributed import KeyedWindowPipeline
+        pipe = KeyedWindowPipeline(rank, world, **cfg_kw)
+        eng = pipe.engine
+        push = lambda b: pipe.push(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], [vals[b * B:(b + 1) * B]])  # noqa: E731
+        fire = lambda b: pipe.advance_watermark(wms[b], device_output=True)  # noqa: E731
+    else:
+        eng = E.WindowAggregator(A.make_config(**cfg_kw))
+        push = lambda b: eng.push(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], [vals[b * B:(b + 1) * B]])  # noqa: E731
+        fire = lambda b: eng.advance_watermark_device(wms[b])  # noqa: E731
+
+    rows = 0
+    for b in range(args.warmup):
+        push(b)
+        rows += fire(b)["key"].shape[0]
+    eng.reset_timers()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rows_t = 0
+    dropped = 0
+    for b in range(args.warmup, S):
+        dropped += push(b)
+        rows_t += fire(b)["key"].shape[0]
+        if (b - args.warmup) % 4 == 3:
+            log("step %d/%d  %.2fs" % (b - args.warmup + 1, args.steps, time.perf_counter() - t0))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        rr = torch.tensor([rows_t], dtype=torch.int64, device=dev)
+        dist.all_reduce(rr)
+        rows_all = int(rr.item())
+    else:
+        rows_all = rows_t
+    st = eng.stats()
+    recs_timed = args.steps * B * world
+    value = recs_timed / elapsed
+
+    # live roofline of the dominant kernel (ingest), HIP events on the engine's stream
+    ingest_s = st.ingest_ms / 1e3
+    alg_bytes_ingest = 24.0 * st.ingest_records       # key + ts + val, read once
+    achieved = alg_bytes_ingest / ingest_s / 1e9 if ingest_s > 0 else 0.0
+    e2e_bytes = 24.0 * recs_timed + 40.0 * rows_all    # whole-job algorithmic bytes incl. emitted rows
+    out = {
+        "metric": "records/sec aggregated (1M-key tumbling SUM)",
+        "value": value,
+        "unit": "records/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (splitmix64 counter-based stream, SURVEY.md §8(d)), generated in HBM",
+        "config": {
+            "workload": "C2: event-time tumbling %ds COUNT+SUM(long), %d uniform keys, %d records/GPU "
+                        "(%d batches of %d), D=%dms" % (args.window_ms // 1000, args.keys, args.steps * B,
+                                                        args.steps, B, args.delay_ms),
+            "records_per_gpu_timed": args.steps * B, "keys": args.keys, "batch": B,
+            "window_ms": args.window_ms, "parallelism": "key-group dp%d" % world,
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": "ingest_kernel",
+            "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+            "alg_bytes_per_record": 24, "launches": st.ingest_launches,
+            "avg_launch_ms": st.ingest_ms / max(1, st.ingest_launches),
+        },
+        "end_to_end_hbm_frac": e2e_bytes / elapsed / 1e9 / HBM_PEAK_GBPS / world,
+        "fire": {"launches": st.fire_launches, "ms": st.fire_ms, "rows": st.fire_rows},
+        "rows_emitted": rows_all,
+        "late_dropped": dropped,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, cfg_kw)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, cfg_kw):
+    """The oracle's multi-threaded restatement of the heap WindowOperator pipeline (keyBy partition +
+    one operator instance per thread owning a key-group range), timed on this host's cores."""
+    from flink_amd import _abi as A
+    from oracle import oracle as O
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    n = args.cpu_sample
+    cfg = A.make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=args.window_ms,
+                        aggs=[("COUNT", 0), ("SUM_I64", 0)])
+    p = A.GenParams(seed_k=0x5eed0001, seed_t=0x5eed0002, seed_v=0x5eed0003, first_index=0,
+                    total_records=C2_RECORDS, num_keys=args.keys, t0_ms=1_700_000_000_000, span_ms=C2_SPAN_MS,
+                    max_delay_ms=args.delay_ms, key_dist=0, val_kind=0)
+    log("cpu baseline: %d records, %d threads" % (n, threads))
+    secs, rows, _ = O.bench_pipeline(cfg, p, n, min(args.batch, n), threads)
+    return {"value": n / secs, "unit": "records/s", "cores": threads, "kind": "port",
+            "sample": "first %d records of the C2 stream (%d s of event time), oracle WindowOperator "
+                      "restatement, %d threads each owning a key-group range; %.2f s" % (n, n // 1_000_000, threads, secs)}
+
+
+if __name__ == "__main__":
+    main()

@@ -73,6 +73,8 @@ class Stats(C.Structure):
     _fields_ = [
         ("records_in", C.c_int64), ("late_dropped", C.c_int64), ("rows_out", C.c_int64),
         ("live_keys", C.c_int64), ("live_slices", C.c_int64), ("current_watermark", C.c_int64),
+        ("ingest_launches", C.c_int64), ("ingest_ms", C.c_double), ("ingest_records", C.c_int64),
+        ("fire_launches", C.c_int64), ("fire_ms", C.c_double), ("fire_rows", C.c_int64),
     ]
 
 

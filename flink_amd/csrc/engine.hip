@@ -1,0 +1,1207 @@
+// engine.hip -- MI355X (gfx950) keyed event-time window aggregation engine behind include/flink_amd.h.
+//
+// State model: every window kind is a union of fixed-size SLICES (Flink's slicing
+// design, SliceAssigners.java:134-385): tumbling g = size, sliding/hop g = gcd(size, slide),
+// cumulate g = step. Slice q covers [off + q*g, off + (q+1)*g). Per (key, slice) accumulators live
+// in HBM as dense SoA columns indexed by (slot, kid): kid = the key's position in an open-addressing
+// key table, slot = a pool entry that the host assigns to slice q and publishes in a READ-ONLY (per
+// launch) slice directory. Records whose slice has no slot yet are appended to a miss list and
+// replayed after the host allocated slots (a lookahead keeps that rare on ordered streams), so no
+// kernel needs intra-launch cross-CU hand-offs except the atomics themselves.
+//
+//   ingest kernel : one pass over the columnar batch: Java key-group check, slice assignment,
+//                   lateness test against the current watermark, key lookup/insert, accumulate.
+//   fire kernel   : on a watermark, for every newly fired window (end-1 <= wm) merge its slices per
+//                   key and emit (key, start, end, aggs) for keys with COUNT > 0.
+//
+// Semantics restated (not copied) from WindowOperator.java:278-481 (DataStream, allowed lateness 0:
+// late firings are not on this path) and AbstractWindowAggProcessor.java:142-182 +
+// Slice{Shared,Unshared}WindowAggProcessor (Table): a record contributes to every window containing
+// it that has not fired when it arrives; it is dropped (numLateRecordsDropped) iff that set is
+// empty; a window is emitted for a key iff at least one record contributed to it.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/flink_amd.h"
+#include "java_math.h"
+
+#define LONG_MIN_J ((int64_t)0x8000000000000000LL)
+#define LONG_MAX_J ((int64_t)0x7fffffffffffffffLL)
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint64_t kEmptyKey = 0x8000000000000000ull;  // key-table sentinel (INT64_MIN); that key uses a side slot
+constexpr int32_t kWantCap = 1 << 14;                   // distinct missing slices reported per launch
+
+// ------------------------------------------------------------------------------------------------
+// device-side structures
+
+struct DirEntry {               // slice directory entry (32 B), read-only during a launch
+    int64_t q;                  // slice number
+    int32_t slot;               // accumulator slot, -1: not allocated
+    int32_t flags;              // bit0 occupied, bit1 always accepted (last window end == LONG_MAX)
+    int64_t thr;                // a record is accepted iff wm < thr (or bit1)
+    int64_t first_maxts;        // maxTimestamp of the earliest window containing the slice
+};
+
+struct DevStatus {
+    int32_t error;              // first fwa_status error code raised by a kernel (0 = none)
+    int32_t spill_n;            // records whose slice had no slot (replayed)
+    int32_t want_n;             // distinct slice numbers in want[]
+    int32_t key_full;
+    unsigned long long dropped;
+    unsigned long long n_keys;  // distinct keys in the key table (incl. side slot)
+    unsigned long long late_fire;
+    unsigned long long rows;    // fire kernel output counter
+    unsigned long long max_q;   // ord-encoded max / min slice number accepted this push
+    unsigned long long min_q;
+};
+
+enum AccKind : int32_t { ACC_NONE = 0, ACC_ADD_I64 = 1, ACC_ADD_F64 = 2, ACC_MIN_ORD = 3, ACC_MAX_ORD = 4 };
+
+struct AggDesc {
+    int32_t kind;               // fwa_agg_kind
+    int32_t col;                // input column
+    int32_t acc;                // accumulator column (>=1) or 0 for COUNT
+    int32_t acc_kind;
+};
+
+struct EngineConst {
+    jm::UDiv64 g_div;           // slice size
+    int64_t g, off;
+    int32_t sem, lateness_pos;  // lateness_pos: DataStream allowed lateness > 0
+    int32_t key_kind, max_par, kg_lo, kg_hi;
+    int32_t naggs, nacc;        // nacc = 1 (count) + stateful agg columns
+    AggDesc agg[FWA_MAX_AGGS];
+    int32_t acc_kind[1 + FWA_MAX_AGGS];
+};
+
+struct IngestArgs {
+    const int64_t* keys;
+    const int64_t* ts;
+    const void* cols[FWA_MAX_COLS];
+    const int32_t* key_hash;
+    const int32_t* idx;         // optional index list (miss replay)
+    int64_t n;
+    int64_t wm;
+    unsigned long long* key_table;
+    uint64_t key_mask;          // capacity-1 (power of two); side slot at capacity
+    const DirEntry* dir;
+    uint32_t dir_mask;
+    unsigned long long* want;   // open-addressing set of ord(q), kWantCap entries, 0 = empty
+    int32_t* spill;
+    int32_t* touched;           // per slot
+    unsigned long long* const* slot_base;
+    int64_t stride;             // elements per accumulator column
+    DevStatus* st;
+};
+
+__device__ __forceinline__ void raise_error(DevStatus* st, int code) { atomicCAS(&st->error, 0, code); }
+
+// Key table: open addressing, linear probing, CAS insert. Returns kid or -1 when full.
+// A stale EMPTY read only sends us to the CAS, which returns the winner's key: no hand-off needed.
+__device__ __forceinline__ int64_t key_slot(unsigned long long* table, uint64_t mask, int64_t key, DevStatus* st) {
+    if ((uint64_t)key == kEmptyKey) {
+        const unsigned long long side = mask + 1;
+        if (table[side] != 1ull && atomicCAS(&table[side], 0ull, 1ull) == 0ull) atomicAdd(&st->n_keys, 1ull);
+        return (int64_t)side;
+    }
+    uint64_t i = jm::mix64((uint64_t)key) & mask;
+    for (uint64_t probe = 0; probe <= mask; ++probe) {
+        const unsigned long long cur = table[i];
+        if (cur == (unsigned long long)key) return (int64_t)i;
+        if (cur == kEmptyKey) {
+            const unsigned long long old = atomicCAS(&table[i], kEmptyKey, (unsigned long long)key);
+            if (old == kEmptyKey) {
+                atomicAdd(&st->n_keys, 1ull);
+                return (int64_t)i;
+            }
+            if (old == (unsigned long long)key) return (int64_t)i;
+        }
+        i = (i + 1) & mask;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ const DirEntry* dir_find(const DirEntry* dir, uint32_t mask, int64_t q) {
+    uint32_t i = (uint32_t)jm::mix64((uint64_t)q) & mask;
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
+        const DirEntry* e = &dir[i];
+        if (!(e->flags & 1)) return nullptr;
+        if (e->q == q) return e;
+        i = (i + 1) & mask;
+    }
+    return nullptr;
+}
+
+__device__ __forceinline__ void want_insert(unsigned long long* want, DevStatus* st, int64_t q) {
+    const unsigned long long key = jm::ord_i64(q) + 1ull;  // never 0: |q| <= 2^63/g < LONG_MAX for g >= 2
+    uint32_t i = (uint32_t)jm::mix64((uint64_t)q) & (kWantCap - 1);
+    for (int probe = 0; probe < kWantCap; ++probe) {
+        unsigned long long cur = want[i];
+        if (cur == key) return;
+        if (cur == 0ull) {
+            unsigned long long old = atomicCAS(&want[i], 0ull, key);
+            if (old == 0ull) { atomicAdd(&st->want_n, 1); return; }
+            if (old == key) return;
+        }
+        i = (i + 1) & (kWantCap - 1);
+    }
+    raise_error(st, FWA_E_OOM);
+}
+
+__device__ __forceinline__ uint64_t load_ord(const void* col, int64_t i, int kind) {
+    switch (kind) {
+        case FWA_MIN_I64: case FWA_MAX_I64: return jm::ord_i64(((const int64_t*)col)[i]);
+        case FWA_MIN_F32: case FWA_MAX_F32:
+            return jm::ord_bits64((uint64_t)__double_as_longlong((double)((const float*)col)[i]));
+        default: return jm::ord_bits64((uint64_t)__double_as_longlong(((const double*)col)[i]));
+    }
+}
+
+template <bool kIdx>
+__global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    const int lane = threadIdx.x & 63;
+    const int64_t stride_grid = (int64_t)gridDim.x * blockDim.x;
+    unsigned long long qmax = 0, qmin = ~0ull;
+    unsigned dropped = 0;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.n; t += stride_grid) {
+        const int64_t i = kIdx ? (int64_t)a.idx[t] : t;
+        const int64_t key = a.keys[i];
+        const int64_t ts = a.ts[i];
+        // key-group ownership (StateTable.getMapForKeyGroup :300-307)
+        const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0), c.max_par);
+        if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }
+        if (c.sem == FWA_SEM_DATASTREAM && ts == LONG_MIN_J) { raise_error(a.st, FWA_E_TS_MIN); continue; }
+        // slice number q = floor((ts - off) / g), Java wrap arithmetic (TimeWindow.java:264-272)
+        const int64_t d = jm::wsub(ts, c.off);
+        const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
+        const uint64_t uq = jm::udiv64(ud, c.g_div);
+        int64_t q;
+        if (d >= 0) q = (int64_t)uq;
+        else q = (uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1;
+        const DirEntry* e = dir_find(a.dir, a.dir_mask, q);
+        if (e == nullptr) {                                     // slice unknown to the host: replay
+            want_insert(a.want, a.st, q);
+            const unsigned long long m = __ballot(1);
+            const int leader = __ffsll((long long)m) - 1;
+            int32_t base = 0;
+            if (lane == leader) base = atomicAdd(&a.st->spill_n, __popcll(m));
+            base = __shfl(base, leader);
+            a.spill[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)i;
+            continue;
+        }
+        const bool accepted = (e->flags & 2) || a.wm < e->thr;
+        if (!accepted) { ++dropped; continue; }
+        if (c.lateness_pos && a.wm >= e->first_maxts) atomicAdd(&a.st->late_fire, 1ull);
+        if (e->slot < 0) {                                      // known slice without slot: replay
+            want_insert(a.want, a.st, q);
+            int32_t si = atomicAdd(&a.st->spill_n, 1);
+            a.spill[si] = (int32_t)i;
+            continue;
+        }
+        const uint64_t oq = jm::ord_i64(q);
+        qmax = oq > qmax ? oq : qmax;
+        qmin = oq < qmin ? oq : qmin;
+        const int64_t kid = key_slot(a.key_table, a.key_mask, key, a.st);
+        if (kid < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
+        const int32_t slot = e->slot;
+        unsigned long long* base = a.slot_base[slot];
+        if (a.touched[slot] == 0) a.touched[slot] = 1;
+        atomicAdd(&base[kid], 1ull);                            // COUNT(*)
+#pragma unroll
+        for (int j = 0; j < FWA_MAX_AGGS; ++j) {
+            if (j >= c.naggs) break;
+            const AggDesc dsc = c.agg[j];
+            if (dsc.acc == 0) continue;
+            unsigned long long* col = base + (int64_t)dsc.acc * a.stride + kid;
+            const void* in = a.cols[dsc.col];
+            switch (dsc.acc_kind) {
+                case ACC_ADD_I64: atomicAdd(col, (unsigned long long)((const int64_t*)in)[i]); break;
+                case ACC_ADD_F64: {
+                    const double v = (dsc.kind == FWA_SUM_F32 || dsc.kind == FWA_AVG_F32)
+                                         ? (double)((const float*)in)[i] : ((const double*)in)[i];
+                    atomicAdd((double*)col, v);
+                    break;
+                }
+                case ACC_MIN_ORD: atomicMin(col, (unsigned long long)load_ord(in, i, dsc.kind)); break;
+                case ACC_MAX_ORD: atomicMax(col, (unsigned long long)load_ord(in, i, dsc.kind)); break;
+                default: break;
+            }
+        }
+    }
+    // wave-level reductions of the per-thread tallies, one atomic per wave
+    for (int s = 32; s >= 1; s >>= 1) {
+        dropped += __shfl_xor(dropped, s);
+        unsigned long long x = __shfl_xor(qmax, s);
+        qmax = x > qmax ? x : qmax;
+        unsigned long long y = __shfl_xor(qmin, s);
+        qmin = y < qmin ? y : qmin;
+    }
+    if (lane == 0) {
+        if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
+        if (qmax) atomicMax(&a.st->max_q, qmax);
+        if (qmin != ~0ull) atomicMin(&a.st->min_q, qmin);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// fire
+
+struct FireWindow {
+    int64_t start, end;         // emitted window bounds
+    int32_t slot_off, nslots;
+};
+
+struct FireArgs {
+    const unsigned long long* key_table;
+    int64_t capacity;           // key table capacity (side slot at capacity)
+    int64_t stride;
+    unsigned long long* const* slot_base;
+    const FireWindow* win;
+    const int32_t* win_slots;
+    int32_t nwin;
+    int32_t blocks_per_win;
+    int64_t* o_key;
+    int64_t* o_start;
+    int64_t* o_end;
+    void* o_agg[FWA_MAX_AGGS];
+    DevStatus* st;
+};
+
+__global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    const int32_t w = blockIdx.x / f.blocks_per_win;
+    const int32_t chunk = blockIdx.x % f.blocks_per_win;
+    const FireWindow win = f.win[w];
+    const int64_t nk = f.capacity + 1;
+    const int64_t per = (int64_t)f.blocks_per_win * blockDim.x;
+    const int lane = threadIdx.x & 63;
+    // every lane of a wave walks the same number of iterations (ballot below needs full waves)
+    const int64_t kbeg = (int64_t)chunk * blockDim.x + threadIdx.x;
+    const int64_t iters = (nk - ((int64_t)chunk * blockDim.x) + per - 1) / per;
+    for (int64_t it = 0; it < iters; ++it) {
+        const int64_t k = kbeg + it * per;
+        bool present = false;
+        unsigned long long kv = 0;
+        if (k < nk) {
+            kv = f.key_table[k];
+            present = (k < f.capacity) ? (kv != kEmptyKey) : (kv == 1ull);
+        }
+        uint64_t cnt = 0;
+        if (present)
+            for (int s = 0; s < win.nslots; ++s) cnt += f.slot_base[f.win_slots[win.slot_off + s]][k];
+        const bool emit = present && cnt != 0;
+        const unsigned long long mask = __ballot(emit);
+        if (mask == 0) continue;
+        const int leader = __ffsll((long long)mask) - 1;
+        unsigned long long base_row = 0;
+        if (lane == leader) base_row = atomicAdd(&f.st->rows, (unsigned long long)__popcll(mask));
+        base_row = __shfl(base_row, leader);
+        if (!emit) continue;
+        const int64_t row = (int64_t)base_row + __popcll(mask & ((1ull << lane) - 1));
+        f.o_key[row] = (k < f.capacity) ? (int64_t)kv : LONG_MIN_J;
+        f.o_start[row] = win.start;
+        f.o_end[row] = win.end;
+        for (int j = 0; j < c.naggs; ++j) {
+            const AggDesc d = c.agg[j];
+            int64_t iv = 0;
+            double dv = 0.0;
+            uint64_t ov = (d.acc_kind == ACC_MIN_ORD) ? ~0ull : 0ull;
+            for (int s = 0; s < win.nslots; ++s) {
+                const unsigned long long x = f.slot_base[f.win_slots[win.slot_off + s]][(int64_t)d.acc * f.stride + k];
+                switch (d.acc_kind) {
+                    case ACC_ADD_I64: iv = jm::wadd(iv, (int64_t)x); break;
+                    case ACC_ADD_F64: dv += __longlong_as_double((long long)x); break;
+                    case ACC_MIN_ORD: ov = x < ov ? x : ov; break;
+                    case ACC_MAX_ORD: ov = x > ov ? x : ov; break;
+                    default: break;
+                }
+            }
+            void* out = f.o_agg[j];
+            switch (d.kind) {
+                case FWA_COUNT: ((int64_t*)out)[row] = (int64_t)cnt; break;
+                case FWA_SUM_I64: ((int64_t*)out)[row] = iv; break;
+                case FWA_SUM_F32: ((float*)out)[row] = (float)dv; break;
+                case FWA_SUM_F64: ((double*)out)[row] = dv; break;
+                case FWA_AVG_I64: {
+                    const int64_t n = (int64_t)cnt;  // AvgAggFunction: sum / count (Java long division)
+                    ((int64_t*)out)[row] = (n == -1 && iv == LONG_MIN_J) ? LONG_MIN_J : iv / n;
+                    break;
+                }
+                case FWA_AVG_F32: ((float*)out)[row] = (float)(dv / (double)(int64_t)cnt); break;
+                case FWA_AVG_F64: ((double*)out)[row] = dv / (double)(int64_t)cnt; break;
+                case FWA_MIN_I64: case FWA_MAX_I64: ((int64_t*)out)[row] = jm::unord_i64(ov); break;
+                case FWA_MIN_F32: case FWA_MAX_F32:
+                    ((float*)out)[row] = (float)__longlong_as_double((long long)jm::unord_bits64(ov));
+                    break;
+                case FWA_MIN_F64: case FWA_MAX_F64:
+                    ((double*)out)[row] = __longlong_as_double((long long)jm::unord_bits64(ov));
+                    break;
+                default: break;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// utility kernels
+
+__global__ void fill_u64_kernel(unsigned long long* p, unsigned long long v, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+__global__ void key_groups_kernel(const int64_t* keys, const int32_t* kh, int64_t n, int32_t kind, int32_t maxp,
+                                  int32_t par, int32_t* kg_out, int32_t* op_out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t kg = jm::key_group(jm::key_hash(keys[i], kind, kh ? kh[i] : 0), maxp);
+        kg_out[i] = kg;
+        if (op_out) op_out[i] = jm::operator_index(maxp, par, kg);
+    }
+}
+
+__global__ void generate_kernel(fwa_gen_params p, int64_t n, int64_t* keys, int64_t* ts, int64_t* vi, float* vf,
+                                double* vd) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = (uint64_t)(p.first_index + j);
+        const uint64_t hk = jm::splitmix64(p.seed_k ^ i);
+        int64_t key;
+        if (p.key_dist == 0) {
+            key = (int64_t)(hk % (uint64_t)p.num_keys);
+        } else {
+            const double u = (double)(hk >> 11) * (1.0 / 9007199254740992.0);
+            int64_t lo = 0, hi = p.num_keys - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (p.zipf_cdf[mid] > u) hi = mid; else lo = mid + 1;
+            }
+            key = lo;
+        }
+        if (keys) keys[j] = key;
+        const __int128 prod = (__int128)(int64_t)i * (__int128)p.span_ms;  // floor(i * span / N), exact
+        const int64_t ramp = (int64_t)(prod / (__int128)p.total_records);
+        if (ts) ts[j] = p.t0_ms + ramp - (int64_t)(jm::splitmix64(p.seed_t ^ i) % (uint64_t)(p.max_delay_ms + 1));
+        const uint64_t hv = jm::splitmix64(p.seed_v ^ i);
+        if (vi) vi[j] = (int64_t)(hv >> 33);
+        if (vf) vf[j] = (float)(hv >> 40) * (1.0f / 16777216.0f);
+        if (vd) vd[j] = (double)(jm::splitmix64(hv) >> 11) * (1.0 / 9007199254740992.0);
+    }
+}
+
+int grid_for(int64_t n, int64_t cap = 256 * 16) {
+    int64_t g = (n + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+int64_t gcd64(int64_t a, int64_t b) {
+    while (b) { int64_t t = a % b; a = b; b = t; }
+    return a < 0 ? -a : a;
+}
+
+}  // namespace
+
+// ==================================================================================================
+// host engine
+
+struct fwa_engine {
+    fwa_config cfg;
+    EngineConst ec;
+    EngineConst* d_ec = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // window geometry (host)
+    int32_t kind = 0, sem = 0;
+    int64_t g = 0, off = 0, size = 0, slide = 0, lateness = 0;
+    jm::UDiv64 slide_div, size_div;
+    // key table
+    int64_t capacity = 0;
+    unsigned long long* d_keys = nullptr;
+    // accumulators
+    int64_t stride = 0;
+    int32_t nacc = 1;
+    std::vector<void*> chunks;
+    std::vector<unsigned long long*> slot_ptr;
+    unsigned long long** d_slot_base = nullptr;
+    int32_t slot_base_cap = 0;
+    std::vector<int32_t> free_slots;
+    int32_t* d_touched = nullptr;
+    std::vector<int32_t> touched;     // host mirror
+    // slice directory
+    DirEntry* d_dir = nullptr;
+    uint32_t dir_cap = 0;
+    std::map<int64_t, int32_t> live;  // slice number -> slot (allocated slices)
+    std::set<int64_t> negative;       // slices known late during the current push (published with slot -1)
+    bool have_q = false;
+    int64_t max_q = 0;                // max slice number that received data
+    int64_t lookahead = 4;
+    unsigned long long* d_want = nullptr;
+    int32_t* d_spill = nullptr;
+    int64_t spill_cap = 0;
+    int32_t* d_replay = nullptr;
+    int64_t replay_cap = 0;
+    // status
+    DevStatus* d_st = nullptr;
+    DevStatus* h_st = nullptr;
+    // host-pointer input staging
+    void* d_in = nullptr;
+    size_t d_in_bytes = 0;
+    // output
+    int64_t out_cap = 0;
+    int64_t* o_key = nullptr;
+    int64_t* o_start = nullptr;
+    int64_t* o_end = nullptr;
+    void* o_agg[FWA_MAX_AGGS] = {};
+    std::vector<char> h_out;
+    FireWindow* d_win = nullptr;
+    int32_t win_cap = 0;
+    int32_t* d_win_slots = nullptr;
+    int32_t win_slots_cap = 0;
+    // watermark / stats
+    int64_t wm = LONG_MIN_J;
+    int64_t records_in = 0, late_dropped = 0, rows_out = 0;
+    size_t mem_budget = 0;
+    // kernel timing (HIP events on this handle's stream)
+    hipEvent_t ev[4] = {};
+    int64_t ingest_launches = 0, ingest_records = 0, fire_launches = 0, fire_rows = 0;
+    double ingest_ms = 0, fire_ms = 0;
+};
+
+namespace {
+
+int fail(fwa_engine* e, int code, const std::string& msg) {
+    if (e) e->err = msg;
+    return code;
+}
+
+#define HIPCHK(e, call)                                                                       \
+    do {                                                                                      \
+        hipError_t _r = (call);                                                               \
+        if (_r != hipSuccess) {                                                               \
+            if (_r == hipErrorOutOfMemory) return fail(e, FWA_E_OOM, "out of device memory"); \
+            return fail(e, FWA_E_DEVICE, std::string(#call) + ": " + hipGetErrorString(_r));  \
+        }                                                                                     \
+    } while (0)
+
+int acc_kind_of(int kind) {
+    switch (kind) {
+        case FWA_COUNT: return ACC_NONE;
+        case FWA_SUM_I64: case FWA_AVG_I64: return ACC_ADD_I64;
+        case FWA_SUM_F32: case FWA_SUM_F64: case FWA_AVG_F32: case FWA_AVG_F64: return ACC_ADD_F64;
+        case FWA_MIN_I64: case FWA_MIN_F32: case FWA_MIN_F64: return ACC_MIN_ORD;
+        default: return ACC_MAX_ORD;
+    }
+}
+
+size_t type_size(int kind) {  // input width == result width for every kind except COUNT
+    switch (kind) {
+        case FWA_SUM_F32: case FWA_MIN_F32: case FWA_MAX_F32: case FWA_AVG_F32: return 4;
+        default: return 8;
+    }
+}
+
+int validate(const fwa_config* c) {
+    if (c->abi_version != FWA_ABI_VERSION) return FWA_E_ARG;
+    if (c->num_aggs < 0 || c->num_aggs > FWA_MAX_AGGS) return FWA_E_ARG;
+    for (int j = 0; j < c->num_aggs; ++j) {
+        if (c->aggs[j].kind < 0 || c->aggs[j].kind >= FWA_AGG_KIND_COUNT) return FWA_E_ARG;
+        if (c->aggs[j].kind != FWA_COUNT && (c->aggs[j].col < 0 || c->aggs[j].col >= FWA_MAX_COLS)) return FWA_E_ARG;
+    }
+    const int64_t absoff = c->offset_ms < 0 ? -c->offset_ms : c->offset_ms;
+    switch (c->window_kind) {
+        case FWA_TUMBLE:
+            if (c->size_ms <= 0 || absoff >= c->size_ms) return FWA_E_ARG;  // TumblingEventTimeWindows.java:58-62
+            break;
+        case FWA_SLIDE:                                                      // SlidingEventTimeWindows.java:58-64
+            if (c->size_ms <= 0 || c->slide_ms <= 0) return FWA_E_ARG;
+            if (c->semantics == FWA_SEM_DATASTREAM && absoff >= c->slide_ms) return FWA_E_ARG;
+            if (c->semantics == FWA_SEM_TABLE && c->size_ms % c->slide_ms != 0) return FWA_E_ARG;  // SliceAssigners.java:214-220
+            break;
+        case FWA_CUMULATE:
+            if (c->semantics != FWA_SEM_TABLE || c->size_ms <= 0 || c->slide_ms <= 0 || c->size_ms % c->slide_ms)
+                return FWA_E_ARG;
+            break;
+        case FWA_SESSION:
+            return FWA_E_UNSUPPORTED;  // merging windows are a later row
+        default:
+            return FWA_E_ARG;
+    }
+    if (c->semantics != FWA_SEM_DATASTREAM && c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;
+    if (c->semantics == FWA_SEM_TABLE && c->allowed_lateness_ms != 0) return FWA_E_ARG;
+    if (c->allowed_lateness_ms < 0) return FWA_E_ARG;
+    if (c->key_kind < 0 || c->key_kind > 2) return FWA_E_ARG;
+    if (c->max_parallelism <= 0 || c->max_parallelism > 32768) return FWA_E_ARG;
+    if (c->kg_start < 0 || c->kg_end >= c->max_parallelism || c->kg_start > c->kg_end) return FWA_E_ARG;
+    return FWA_OK;
+}
+
+// ---- slice geometry (host) ----
+
+int64_t slice_start(const fwa_engine* e, int64_t q) { return jm::wadd(e->off, (int64_t)((uint64_t)q * (uint64_t)e->g)); }
+
+int64_t slice_q(const fwa_engine* e, int64_t t) {  // slice number of a timestamp / slice start
+    const int64_t d = jm::wsub(t, e->off);
+    const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
+    const uint64_t uq = ud / (uint64_t)e->g;
+    if (d >= 0) return (int64_t)uq;
+    return (uq * (uint64_t)e->g == ud) ? -(int64_t)uq : -(int64_t)uq - 1;
+}
+
+// windows containing slice q as (start, end), per kind (assigner restatements)
+void windows_of_slice(const fwa_engine* e, int64_t q, std::vector<std::pair<int64_t, int64_t>>& out) {
+    const int64_t a = slice_start(e, q);
+    if (e->kind == FWA_TUMBLE) { out.push_back({a, jm::wadd(a, e->g)}); return; }
+    if (e->kind == FWA_SLIDE) {  // SlidingEventTimeWindows.assignWindows :70-82 applied to the slice start
+        for (int64_t st = jm::window_start(a, e->off, e->slide_div); st > jm::wsub(a, e->size); st = jm::wsub(st, e->slide))
+            out.push_back({st, jm::wadd(st, e->size)});
+        return;
+    }
+    const int64_t m = jm::window_start(a, e->off, e->size_div);  // CUMULATE: max window start
+    const int64_t last = jm::wadd(m, e->size);
+    for (int64_t en = jm::wadd(a, e->g); en <= last && en > m; en = jm::wadd(en, e->g)) out.push_back({m, en});
+}
+
+int64_t last_window_end(const fwa_engine* e, int64_t q) {
+    const int64_t a = slice_start(e, q);
+    if (e->kind == FWA_TUMBLE) return jm::wadd(a, e->g);
+    if (e->kind == FWA_SLIDE) {
+        if (e->sem == FWA_SEM_TABLE) return jm::wadd(a, e->size);          // sliceEnd - sliceSize + size
+        return jm::wadd(jm::window_start(a, e->off, e->slide_div), e->size);
+    }
+    return jm::wadd(jm::window_start(a, e->off, e->size_div), e->size);    // windowStart(sliceEnd) + maxSize
+}
+
+int64_t first_window_end(const fwa_engine* e, int64_t q) {
+    std::vector<std::pair<int64_t, int64_t>> w;
+    windows_of_slice(e, q, w);
+    int64_t best = LONG_MAX_J;
+    for (auto& x : w) best = std::min(best, x.second);
+    return best;
+}
+
+// acceptance threshold: accepted iff wm < thr, or always
+void accept_threshold(const fwa_engine* e, int64_t q, int64_t* thr, bool* always) {
+    const int64_t last_end = last_window_end(e, q);
+    const int64_t mt = jm::wsub(last_end, 1);
+    *always = false;
+    if (e->sem == FWA_SEM_TABLE) {                     // !TimeWindowUtil.isWindowFired(lastWindowEnd, wm)
+        if (last_end == LONG_MAX_J) *always = true;
+        *thr = mt;
+        return;
+    }
+    int64_t cleanup = jm::wadd(mt, e->lateness);       // WindowOperator.cleanupTime :647-654
+    if (cleanup < mt) cleanup = LONG_MAX_J;
+    *thr = cleanup;                                    // !isWindowLate: cleanup > wm
+}
+
+// ---- slot pool ----
+
+int grow_slots(fwa_engine* e, int32_t add) {
+    const size_t col_bytes = (size_t)e->stride * 8;
+    const size_t slot_bytes = col_bytes * e->nacc;
+    void* chunk = nullptr;
+    HIPCHK(e, hipMalloc(&chunk, slot_bytes * add));
+    e->chunks.push_back(chunk);
+    for (int32_t s = 0; s < add; ++s) {
+        unsigned long long* base = (unsigned long long*)((char*)chunk + slot_bytes * s);
+        e->free_slots.push_back((int32_t)e->slot_ptr.size());
+        e->slot_ptr.push_back(base);
+        e->touched.push_back(0);
+        HIPCHK(e, hipMemsetAsync(base, 0, slot_bytes, e->stream));  // identities: 0; MIN columns 0xFF..
+        for (int c = 1; c < e->nacc; ++c)
+            if (e->ec.acc_kind[c] == ACC_MIN_ORD) HIPCHK(e, hipMemsetAsync(base + (int64_t)c * e->stride, 0xFF, col_bytes, e->stream));
+    }
+    const int32_t n = (int32_t)e->slot_ptr.size();
+    if (n > e->slot_base_cap) {
+        if (e->d_slot_base) HIPCHK(e, hipFree(e->d_slot_base));
+        if (e->d_touched) HIPCHK(e, hipFree(e->d_touched));
+        e->slot_base_cap = std::max<int32_t>(64, n * 2);
+        HIPCHK(e, hipMalloc(&e->d_slot_base, sizeof(void*) * e->slot_base_cap));
+        HIPCHK(e, hipMalloc(&e->d_touched, sizeof(int32_t) * e->slot_base_cap));
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_slot_base, e->slot_ptr.data(), sizeof(void*) * n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->d_touched, e->touched.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
+    return FWA_OK;
+}
+
+int alloc_slice(fwa_engine* e, int64_t q) {
+    if (e->live.count(q)) return FWA_OK;
+    if (e->free_slots.empty()) {
+        int rc = grow_slots(e, std::max<int32_t>(4, (int32_t)e->slot_ptr.size() / 2));
+        if (rc) return rc;
+    }
+    const int32_t s = e->free_slots.back();
+    e->free_slots.pop_back();
+    e->live[q] = s;
+    return FWA_OK;
+}
+
+int release_slot(fwa_engine* e, int32_t slot) {
+    if (e->touched[slot]) {  // restore identities (untouched slots are still clean)
+        const size_t col_bytes = (size_t)e->stride * 8;
+        unsigned long long* base = e->slot_ptr[slot];
+        for (int c = 0; c < e->nacc; ++c) {
+            const int v = (c > 0 && e->ec.acc_kind[c] == ACC_MIN_ORD) ? 0xFF : 0;
+            HIPCHK(e, hipMemsetAsync(base + (int64_t)c * e->stride, v, col_bytes, e->stream));
+        }
+        e->touched[slot] = 0;
+        HIPCHK(e, hipMemsetAsync(e->d_touched + slot, 0, sizeof(int32_t), e->stream));
+    }
+    e->free_slots.push_back(slot);
+    return FWA_OK;
+}
+
+// Publish the directory: every allocated slice (with slot) plus a negative entry for nothing else.
+int publish_dir(fwa_engine* e) {
+    uint32_t need = 256;
+    while (need < 2 * (e->live.size() + e->negative.size() + 16)) need <<= 1;
+    if (need > e->dir_cap) {
+        if (e->d_dir) HIPCHK(e, hipFree(e->d_dir));
+        HIPCHK(e, hipMalloc(&e->d_dir, sizeof(DirEntry) * need));
+        e->dir_cap = need;
+    }
+    std::vector<DirEntry> h(e->dir_cap);
+    memset(h.data(), 0, sizeof(DirEntry) * h.size());
+    for (auto& kv : e->live) {
+        uint32_t i = (uint32_t)jm::mix64((uint64_t)kv.first) & (e->dir_cap - 1);
+        while (h[i].flags & 1) i = (i + 1) & (e->dir_cap - 1);
+        DirEntry& d = h[i];
+        d.q = kv.first;
+        d.slot = kv.second;
+        bool always;
+        accept_threshold(e, kv.first, &d.thr, &always);
+        d.flags = 1 | (always ? 2 : 0);
+        d.first_maxts = jm::wsub(first_window_end(e, kv.first), 1);
+    }
+    for (int64_t q : e->negative) {
+        uint32_t i = (uint32_t)jm::mix64((uint64_t)q) & (e->dir_cap - 1);
+        while (h[i].flags & 1) i = (i + 1) & (e->dir_cap - 1);
+        DirEntry& d = h[i];
+        d.q = q;
+        d.slot = -1;
+        bool always;
+        accept_threshold(e, q, &d.thr, &always);
+        d.flags = 1 | (always ? 2 : 0);
+        d.first_maxts = LONG_MAX_J;
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_dir, h.data(), sizeof(DirEntry) * h.size(), hipMemcpyHostToDevice, e->stream));
+    return FWA_OK;
+}
+
+int ensure_out(fwa_engine* e, int64_t rows) {
+    if (rows <= e->out_cap) return FWA_OK;
+    const int64_t cap = std::max<int64_t>(rows + rows / 4, 1024);
+    for (void* p : {(void*)e->o_key, (void*)e->o_start, (void*)e->o_end}) if (p) HIPCHK(e, hipFree(p));
+    for (int j = 0; j < FWA_MAX_AGGS; ++j) { if (e->o_agg[j]) HIPCHK(e, hipFree(e->o_agg[j])); e->o_agg[j] = nullptr; }
+    HIPCHK(e, hipMalloc(&e->o_key, 8 * cap));
+    HIPCHK(e, hipMalloc(&e->o_start, 8 * cap));
+    HIPCHK(e, hipMalloc(&e->o_end, 8 * cap));
+    for (int j = 0; j < e->cfg.num_aggs; ++j) HIPCHK(e, hipMalloc(&e->o_agg[j], 8 * cap));
+    e->out_cap = cap;
+    return FWA_OK;
+}
+
+int sync_status(fwa_engine* e) {
+    HIPCHK(e, hipMemcpyAsync(e->h_st, e->d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return FWA_OK;
+}
+
+int reset_push_status(fwa_engine* e) {
+    // zero everything but n_keys / rows; min_q starts at ~0
+    DevStatus z;
+    memset(&z, 0, sizeof(z));
+    HIPCHK(e, hipMemsetAsync(e->d_st, 0, offsetof(DevStatus, n_keys), e->stream));
+    HIPCHK(e, hipMemsetAsync(&e->d_st->late_fire, 0, 8, e->stream));
+    HIPCHK(e, hipMemsetAsync(&e->d_st->max_q, 0, 8, e->stream));
+    HIPCHK(e, hipMemsetAsync(&e->d_st->min_q, 0xFF, 8, e->stream));
+    return FWA_OK;
+}
+
+}  // namespace
+
+// ==================================================================================================
+// C-ABI
+
+extern "C" {
+
+const char* fwa_version(void) { return "flink_amd 0.1 (gfx950)"; }
+
+const char* fwa_last_error(const fwa_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+void fwa_destroy(fwa_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->cfg.device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
+                    e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots};
+    for (void* p : bufs) if (p) (void)hipFree(p);
+    for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
+    for (void* p : e->chunks) (void)hipFree(p);
+    if (e->h_st) (void)hipHostFree(e->h_st);
+    for (hipEvent_t ev : e->ev) if (ev) (void)hipEventDestroy(ev);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+int fwa_create(const fwa_config* cfg, fwa_engine** out) {
+    if (!cfg || !out) return FWA_E_ARG;
+    *out = nullptr;
+    const int v = validate(cfg);
+    if (v) return v;
+    fwa_engine* e = new fwa_engine();
+    e->cfg = *cfg;
+    e->kind = cfg->window_kind;
+    e->sem = cfg->semantics;
+    e->size = cfg->size_ms;
+    e->slide = cfg->slide_ms;
+    e->lateness = cfg->semantics == FWA_SEM_DATASTREAM ? cfg->allowed_lateness_ms : 0;
+    if (e->kind == FWA_TUMBLE) {
+        e->g = cfg->size_ms;
+        e->off = cfg->offset_ms % cfg->size_ms;  // (globalOffset + staggerOffset) % size, ALIGNED stagger
+    } else if (e->kind == FWA_SLIDE) {
+        e->g = gcd64(cfg->size_ms, cfg->slide_ms);
+        e->off = cfg->offset_ms;
+    } else {
+        e->g = cfg->slide_ms;
+        e->off = cfg->offset_ms;
+    }
+    e->slide_div = jm::udiv64_make((uint64_t)(e->slide > 0 ? e->slide : 1));
+    e->size_div = jm::udiv64_make((uint64_t)e->size);
+    EngineConst& c = e->ec;
+    memset(&c, 0, sizeof(c));
+    c.g_div = jm::udiv64_make((uint64_t)e->g);
+    c.g = e->g;
+    c.off = e->off;
+    c.sem = e->sem;
+    c.lateness_pos = e->lateness > 0;
+    c.key_kind = cfg->key_kind;
+    c.max_par = cfg->max_parallelism;
+    c.kg_lo = cfg->kg_start;
+    c.kg_hi = cfg->kg_end;
+    c.naggs = cfg->num_aggs;
+    c.nacc = 1;
+    c.acc_kind[0] = ACC_ADD_I64;
+    for (int j = 0; j < cfg->num_aggs; ++j) {
+        AggDesc& d = c.agg[j];
+        d.kind = cfg->aggs[j].kind;
+        d.col = cfg->aggs[j].col;
+        d.acc_kind = acc_kind_of(d.kind);
+        if (d.acc_kind == ACC_NONE) { d.acc = 0; continue; }
+        d.acc = c.nacc;
+        c.acc_kind[c.nacc] = d.acc_kind;
+        c.nacc++;
+    }
+    e->nacc = c.nacc;
+    if (hipSetDevice(cfg->device) != hipSuccess) { delete e; return FWA_E_DEVICE; }
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return FWA_E_DEVICE; }
+    const int64_t kc = cfg->key_capacity > 0 ? cfg->key_capacity : (1 << 20);
+    int64_t cap = 1024;
+    while (cap < 2 * kc) cap <<= 1;
+    e->capacity = cap;
+    e->stride = ((cap + 1 + 63) / 64) * 64;
+    int rc = FWA_OK;
+    do {
+        if (hipMalloc(&e->d_ec, sizeof(EngineConst)) != hipSuccess) { rc = FWA_E_OOM; break; }
+        if (hipMemcpy(e->d_ec, &c, sizeof(EngineConst), hipMemcpyHostToDevice) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        if (hipMalloc(&e->d_keys, sizeof(unsigned long long) * (cap + 1)) != hipSuccess) { rc = FWA_E_OOM; break; }
+        fill_u64_kernel<<<grid_for(cap), kBlock, 0, e->stream>>>(e->d_keys, kEmptyKey, cap);
+        if (hipMemsetAsync(e->d_keys + cap, 0, 8, e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        if (hipMalloc(&e->d_st, sizeof(DevStatus)) != hipSuccess) { rc = FWA_E_OOM; break; }
+        if (hipHostMalloc(&e->h_st, sizeof(DevStatus)) != hipSuccess) { rc = FWA_E_OOM; break; }
+        if (hipMemsetAsync(e->d_st, 0, sizeof(DevStatus), e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        bool evok = true;
+        for (hipEvent_t& ev : e->ev) evok = evok && hipEventCreate(&ev) == hipSuccess;
+        if (!evok) { rc = FWA_E_DEVICE; break; }
+        if (hipMalloc(&e->d_want, sizeof(unsigned long long) * kWantCap) != hipSuccess) { rc = FWA_E_OOM; break; }
+        size_t fr = 0, tot = 0;
+        (void)hipMemGetInfo(&fr, &tot);
+        e->mem_budget = fr / 2;
+        if ((rc = grow_slots(e, 4))) break;
+        if ((rc = publish_dir(e))) break;
+        if (hipStreamSynchronize(e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+    } while (0);
+    if (rc) { fwa_destroy(e); return rc; }
+    *out = e;
+    return FWA_OK;
+}
+
+static int stage_inputs(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* cols,
+                        const int32_t* kh, int64_t n, IngestArgs& a) {
+    size_t need = (size_t)n * 16 + (kh ? (size_t)n * 4 : 0) + 4096;
+    for (int j = 0; j < e->cfg.num_aggs; ++j) need += (size_t)n * 8 + 256;
+    if (need > e->d_in_bytes) {
+        if (e->d_in) HIPCHK(e, hipFree(e->d_in));
+        HIPCHK(e, hipMalloc(&e->d_in, need));
+        e->d_in_bytes = need;
+    }
+    char* p = (char*)e->d_in;
+    hipError_t err = hipSuccess;
+    auto put = [&](const void* src, size_t bytes) -> const void* {
+        void* dst = p;
+        hipError_t r = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream);
+        if (r != hipSuccess) err = r;
+        p += (bytes + 255) / 256 * 256;
+        return dst;
+    };
+    a.keys = (const int64_t*)put(keys, (size_t)n * 8);
+    a.ts = (const int64_t*)put(ts, (size_t)n * 8);
+    a.key_hash = kh ? (const int32_t*)put(kh, (size_t)n * 4) : nullptr;
+    for (int c = 0; c < FWA_MAX_COLS; ++c) a.cols[c] = nullptr;
+    for (int j = 0; j < e->cfg.num_aggs; ++j) {
+        const fwa_agg_spec& s = e->cfg.aggs[j];
+        if (s.kind == FWA_COUNT || a.cols[s.col]) continue;
+        if (!cols || !cols[s.col]) return fail(e, FWA_E_ARG, "missing value column");
+        a.cols[s.col] = put(cols[s.col], (size_t)n * type_size(s.kind));
+    }
+    HIPCHK(e, err);
+    return FWA_OK;
+}
+
+static int launch_ingest(fwa_engine* e, IngestArgs& a, bool replay) {
+    a.key_table = e->d_keys;
+    a.key_mask = (uint64_t)e->capacity - 1;
+    a.dir = e->d_dir;
+    a.dir_mask = e->dir_cap - 1;
+    a.want = e->d_want;
+    a.spill = e->d_spill;
+    a.touched = e->d_touched;
+    a.slot_base = e->d_slot_base;
+    a.stride = e->stride;
+    a.st = e->d_st;
+    HIPCHK(e, hipMemsetAsync(e->d_want, 0, sizeof(unsigned long long) * kWantCap, e->stream));
+    const int grid = grid_for(a.n, 256 * 32);
+    HIPCHK(e, hipEventRecord(e->ev[0], e->stream));
+    if (replay) ingest_kernel<true><<<grid, kBlock, 0, e->stream>>>(a, e->d_ec);
+    else ingest_kernel<false><<<grid, kBlock, 0, e->stream>>>(a, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->ev[1], e->stream));
+    e->ingest_launches++;
+    e->ingest_records += a.n;
+    return FWA_OK;
+}
+
+static int account_ingest(fwa_engine* e) {  // after the stream was synchronised
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+    e->ingest_ms += ms;
+    return FWA_OK;
+}
+
+int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
+             const int32_t* key_hash, int64_t n, int32_t flags, int64_t* late_dropped_out) {
+    if (!e) return FWA_E_STATE;
+    if (n < 0 || (n > 0 && (!keys || !ts))) return fail(e, FWA_E_ARG, "null input column");
+    if (e->cfg.key_kind == FWA_KEY_PREHASHED && n > 0 && !key_hash) return fail(e, FWA_E_ARG, "PREHASHED keys need key_hash");
+    if (n > INT32_MAX) return fail(e, FWA_E_ARG, "batch too large (max 2^31-1 records)");
+    if (late_dropped_out) *late_dropped_out = 0;
+    if (n == 0) return FWA_OK;
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    IngestArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n = n;
+    a.wm = e->wm;
+    if (flags & FWA_PUSH_DEVICE_PTRS) {
+        a.keys = keys;
+        a.ts = ts;
+        a.key_hash = key_hash;
+        for (int j = 0; j < e->cfg.num_aggs; ++j) {
+            const fwa_agg_spec& s = e->cfg.aggs[j];
+            if (s.kind == FWA_COUNT) continue;
+            if (!val_cols || !val_cols[s.col]) return fail(e, FWA_E_ARG, "missing value column");
+            a.cols[s.col] = val_cols[s.col];
+        }
+    } else {
+        int rc = stage_inputs(e, keys, ts, val_cols, key_hash, n, a);
+        if (rc) return rc;
+    }
+    if (n > e->spill_cap) {
+        if (e->d_spill) HIPCHK(e, hipFree(e->d_spill));
+        if (e->d_replay) HIPCHK(e, hipFree(e->d_replay));
+        e->spill_cap = std::max<int64_t>(n, 1 << 16);
+        HIPCHK(e, hipMalloc(&e->d_spill, sizeof(int32_t) * e->spill_cap));
+        HIPCHK(e, hipMalloc(&e->d_replay, sizeof(int32_t) * e->spill_cap));
+    }
+    int rc = reset_push_status(e);
+    if (rc) return rc;
+    rc = launch_ingest(e, a, false);
+    if (rc) return rc;
+    int64_t dropped = 0;
+    int64_t qmin = LONG_MAX_J, qmax = LONG_MIN_J;
+    for (int round = 0;; ++round) {
+        rc = sync_status(e);
+        if (rc) return rc;
+        rc = account_ingest(e);
+        if (rc) return rc;
+        const DevStatus st = *e->h_st;
+        if (st.error) {
+            const char* m = st.error == FWA_E_KEYGROUP ? "Key group is not in the owned KeyGroupRange (StateTable.getMapForKeyGroup)"
+                          : st.error == FWA_E_TS_MIN ? "Record has Long.MIN_VALUE timestamp (= no timestamp marker)."
+                          : st.error == FWA_E_OOM ? (st.key_full ? "key table full: raise fwa_config.key_capacity" : "slice want-set overflow")
+                                                  : "device error";
+            return fail(e, st.error, m);
+        }
+        if (st.late_fire) return fail(e, FWA_E_UNSUPPORTED, "late firing within allowed lateness is not on the GPU path");
+        dropped += (int64_t)st.dropped;
+        if (st.max_q) qmax = std::max<int64_t>(qmax, jm::unord_i64(st.max_q));
+        if (st.min_q != ~0ull) qmin = std::min<int64_t>(qmin, jm::unord_i64(st.min_q));
+        if (st.spill_n == 0) break;
+        if (round > 64) return fail(e, FWA_E_STATE, "miss replay did not converge");
+        // allocate the wanted slices, republish, replay the missed records
+        std::vector<unsigned long long> want(kWantCap);
+        HIPCHK(e, hipMemcpy(want.data(), e->d_want, sizeof(unsigned long long) * kWantCap, hipMemcpyDeviceToHost));
+        for (unsigned long long w : want) {
+            if (!w) continue;
+            const int64_t q = jm::unord_i64(w - 1ull);
+            int64_t thr;
+            bool always;
+            accept_threshold(e, q, &thr, &always);
+            if (always || e->wm < thr) { rc = alloc_slice(e, q); if (rc) return rc; }
+            else e->negative.insert(q);  // late slice: the replay drops its records
+        }
+        rc = publish_dir(e);
+        if (rc) return rc;
+        HIPCHK(e, hipMemcpyAsync(e->d_replay, e->d_spill, sizeof(int32_t) * st.spill_n, hipMemcpyDeviceToDevice, e->stream));
+        rc = reset_push_status(e);
+        if (rc) return rc;
+        IngestArgs b = a;
+        b.idx = e->d_replay;
+        b.n = st.spill_n;
+        rc = launch_ingest(e, b, true);
+        if (rc) return rc;
+    }
+    if (!e->negative.empty()) { e->negative.clear(); rc = publish_dir(e); if (rc) return rc; }
+    // mirror touched flags; extend the lookahead so ordered streams rarely miss
+    HIPCHK(e, hipMemcpy(e->touched.data(), e->d_touched, sizeof(int32_t) * e->touched.size(), hipMemcpyDeviceToHost));
+    if (qmax != LONG_MIN_J) {
+        const int64_t span = qmax - qmin + 1;
+        e->lookahead = std::min<int64_t>(std::max<int64_t>(e->lookahead, 2 * span), 256);
+        if (!e->have_q || qmax > e->max_q) e->max_q = qmax;
+        e->have_q = true;
+        const size_t slot_bytes = (size_t)e->stride * 8 * e->nacc;
+        int64_t budget_slots = (int64_t)(e->mem_budget / std::max<size_t>(slot_bytes, 1));
+        int64_t la = std::min<int64_t>(e->lookahead, std::max<int64_t>(0, budget_slots - (int64_t)e->live.size()));
+        bool changed = false;
+        for (int64_t q = e->max_q + 1; q <= e->max_q + la; ++q)
+            if (!e->live.count(q)) { rc = alloc_slice(e, q); if (rc) return rc; changed = true; }
+        if (changed) { rc = publish_dir(e); if (rc) return rc; }
+    }
+    e->records_in += n;
+    e->late_dropped += dropped;
+    if (late_dropped_out) *late_dropped_out = dropped;
+    return FWA_OK;
+}
+
+int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
+    if (!e) return FWA_E_STATE;
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (out) memset(out, 0, sizeof(*out));
+    int64_t nrows = 0;
+    if (wm > e->wm) {
+        const int64_t prev = e->wm;
+        // windows of touched slices that fire now: prev < end-1 <= wm  (EventTimeTrigger / isWindowFired)
+        std::set<std::pair<int64_t, int64_t>> wins;  // (end, start)
+        std::vector<std::pair<int64_t, int64_t>> tmp;
+        for (auto& kv : e->live) {
+            if (!e->touched[kv.second]) continue;
+            tmp.clear();
+            windows_of_slice(e, kv.first, tmp);
+            for (auto& w : tmp) {
+                const int64_t mt = jm::wsub(w.second, 1);
+                if (mt > prev && mt <= wm) wins.insert({w.second, w.first});
+            }
+        }
+        std::vector<FireWindow> hw;
+        std::vector<int32_t> hs;
+        for (auto& w : wins) {
+            FireWindow f;
+            f.end = w.first;
+            f.start = w.second;
+            f.slot_off = (int32_t)hs.size();
+            const int64_t q0 = slice_q(e, f.start);
+            const int64_t q1 = slice_q(e, jm::wsub(f.end, 1));
+            for (int64_t q = q0; q <= q1; ++q) {
+                auto it = e->live.find(q);
+                if (it != e->live.end() && e->touched[it->second]) hs.push_back(it->second);
+            }
+            f.nslots = (int32_t)hs.size() - f.slot_off;
+            if (f.nslots > 0) hw.push_back(f);
+        }
+        if (!hw.empty()) {
+            if ((int32_t)hw.size() > e->win_cap) {
+                if (e->d_win) HIPCHK(e, hipFree(e->d_win));
+                e->win_cap = (int32_t)hw.size() * 2;
+                HIPCHK(e, hipMalloc(&e->d_win, sizeof(FireWindow) * e->win_cap));
+            }
+            if ((int32_t)hs.size() > e->win_slots_cap) {
+                if (e->d_win_slots) HIPCHK(e, hipFree(e->d_win_slots));
+                e->win_slots_cap = (int32_t)hs.size() * 2;
+                HIPCHK(e, hipMalloc(&e->d_win_slots, sizeof(int32_t) * e->win_slots_cap));
+            }
+            HIPCHK(e, hipMemcpyAsync(e->d_win, hw.data(), sizeof(FireWindow) * hw.size(), hipMemcpyHostToDevice, e->stream));
+            HIPCHK(e, hipMemcpyAsync(e->d_win_slots, hs.data(), sizeof(int32_t) * hs.size(), hipMemcpyHostToDevice, e->stream));
+            int rc = sync_status(e);
+            if (rc) return rc;
+            const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
+            rc = ensure_out(e, (int64_t)hw.size() * nkeys);
+            if (rc) return rc;
+            HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
+            FireArgs f;
+            memset(&f, 0, sizeof(f));
+            f.key_table = e->d_keys;
+            f.capacity = e->capacity;
+            f.stride = e->stride;
+            f.slot_base = e->d_slot_base;
+            f.win = e->d_win;
+            f.win_slots = e->d_win_slots;
+            f.nwin = (int32_t)hw.size();
+            const int64_t key_blocks = (e->capacity + 1 + kBlock - 1) / kBlock;
+            const int64_t want_blocks = std::max<int64_t>(1, 4096 / (int64_t)hw.size());
+            f.blocks_per_win = (int32_t)std::max<int64_t>(1, std::min<int64_t>(key_blocks, want_blocks));
+            f.o_key = e->o_key;
+            f.o_start = e->o_start;
+            f.o_end = e->o_end;
+            for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
+            f.st = e->d_st;
+            const int64_t grid = (int64_t)f.blocks_per_win * (int64_t)hw.size();
+            HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
+            fire_kernel<<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
+            rc = sync_status(e);
+            if (rc) return rc;
+            nrows = (int64_t)e->h_st->rows;
+            float ms = 0.f;
+            HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+            e->fire_ms += ms;
+            e->fire_launches++;
+            e->fire_rows += nrows;
+        }
+        // free slices whose every window is past cleanup (last window: cleanupTime <= wm)
+        std::vector<int64_t> dead;
+        for (auto& kv : e->live) {
+            int64_t thr;
+            bool always;
+            accept_threshold(e, kv.first, &thr, &always);
+            if (!always && wm >= thr) dead.push_back(kv.first);
+        }
+        for (int64_t q : dead) {
+            int rc = release_slot(e, e->live[q]);
+            if (rc) return rc;
+            e->live.erase(q);
+        }
+        if (!dead.empty()) { int rc = publish_dir(e); if (rc) return rc; }
+        e->wm = wm;
+    }
+    e->rows_out += nrows;
+    if (out) {
+        out->n_rows = nrows;
+        out->num_aggs = e->cfg.num_aggs;
+        if (e->cfg.output_on_device) {
+            out->on_device = 1;
+            out->key = e->o_key;
+            out->win_start = e->o_start;
+            out->win_end = e->o_end;
+            for (int j = 0; j < e->cfg.num_aggs; ++j) out->agg[j] = e->o_agg[j];
+        } else {
+            out->on_device = 0;
+            e->h_out.resize(std::max<size_t>((size_t)nrows * 8 * (3 + e->cfg.num_aggs), 8));
+            char* p = e->h_out.data();
+            hipError_t err = hipSuccess;
+            auto get = [&](const void* src, size_t bytes) -> const void* {
+                if (bytes) { hipError_t r = hipMemcpy(p, src, bytes, hipMemcpyDeviceToHost); if (r != hipSuccess) err = r; }
+                const void* r = p;
+                p += bytes;
+                return r;
+            };
+            out->key = (const int64_t*)get(e->o_key, 8 * nrows);
+            out->win_start = (const int64_t*)get(e->o_start, 8 * nrows);
+            out->win_end = (const int64_t*)get(e->o_end, 8 * nrows);
+            for (int j = 0; j < e->cfg.num_aggs; ++j) out->agg[j] = get(e->o_agg[j], type_size(e->cfg.aggs[j].kind) * nrows);
+            HIPCHK(e, err);
+        }
+    }
+    return FWA_OK;
+}
+
+int fwa_flush(fwa_engine* e) {
+    if (!e) return FWA_E_STATE;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return FWA_OK;
+}
+
+int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
+    if (!e || !s) return FWA_E_ARG;
+    int rc = sync_status(e);
+    if (rc) return rc;
+    s->records_in = e->records_in;
+    s->late_dropped = e->late_dropped;
+    s->rows_out = e->rows_out;
+    s->live_keys = (int64_t)e->h_st->n_keys;
+    s->live_slices = (int64_t)e->live.size();
+    s->current_watermark = e->wm;
+    s->ingest_launches = e->ingest_launches;
+    s->ingest_ms = e->ingest_ms;
+    s->ingest_records = e->ingest_records;
+    s->fire_launches = e->fire_launches;
+    s->fire_ms = e->fire_ms;
+    s->fire_rows = e->fire_rows;
+    return FWA_OK;
+}
+
+int fwa_reset_timers(fwa_engine* e) {
+    if (!e) return FWA_E_ARG;
+    e->ingest_launches = e->ingest_records = e->fire_launches = e->fire_rows = 0;
+    e->ingest_ms = e->fire_ms = 0;
+    return FWA_OK;
+}
+
+int fwa_key_groups(const int64_t* keys, const int32_t* key_hash, int64_t n, int32_t key_kind, int32_t max_par,
+                   int32_t par, int32_t* kg_out, int32_t* op_out, int32_t flags, int32_t device) {
+    if (n < 0 || max_par <= 0 || par <= 0 || par > max_par || key_kind < 0 || key_kind > 2) return FWA_E_ARG;
+    if (key_kind == FWA_KEY_PREHASHED && n > 0 && !key_hash) return FWA_E_ARG;
+    if (n == 0) return FWA_OK;
+    if (hipSetDevice(device) != hipSuccess) return FWA_E_DEVICE;
+    if (flags & FWA_PUSH_DEVICE_PTRS) {
+        key_groups_kernel<<<grid_for(n), kBlock>>>(keys, key_hash, n, key_kind, max_par, par, kg_out, op_out);
+        return hipDeviceSynchronize() == hipSuccess ? FWA_OK : FWA_E_DEVICE;
+    }
+    int64_t* dk = nullptr;
+    int32_t *dh = nullptr, *dkg = nullptr, *dop = nullptr;
+    int rc = FWA_OK;
+    do {
+        if (hipMalloc(&dk, 8 * n) != hipSuccess || hipMalloc(&dkg, 4 * n) != hipSuccess) { rc = FWA_E_OOM; break; }
+        if (key_hash && hipMalloc(&dh, 4 * n) != hipSuccess) { rc = FWA_E_OOM; break; }
+        if (op_out && hipMalloc(&dop, 4 * n) != hipSuccess) { rc = FWA_E_OOM; break; }
+        if (hipMemcpy(dk, keys, 8 * n, hipMemcpyHostToDevice) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        if (dh && hipMemcpy(dh, key_hash, 4 * n, hipMemcpyHostToDevice) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        key_groups_kernel<<<grid_for(n), kBlock>>>(dk, dh, n, key_kind, max_par, par, dkg, dop);
+        if (hipMemcpy(kg_out, dkg, 4 * n, hipMemcpyDeviceToHost) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        if (op_out && hipMemcpy(op_out, dop, 4 * n, hipMemcpyDeviceToHost) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+    } while (0);
+    for (void* p : {(void*)dk, (void*)dh, (void*)dkg, (void*)dop}) if (p) (void)hipFree(p);
+    return rc;
+}
+
+int fwa_generate(const fwa_gen_params* p, int64_t n, int64_t* keys, int64_t* ts, int64_t* v_i64, float* v_f32,
+                 double* v_f64, int32_t device, void* stream) {
+    if (!p || n < 0 || p->total_records <= 0 || p->num_keys <= 0 || p->max_delay_ms < 0) return FWA_E_ARG;
+    if (p->key_dist == 1 && !p->zipf_cdf) return FWA_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return FWA_E_DEVICE;
+    if (n == 0) return FWA_OK;
+    generate_kernel<<<grid_for(n, 256 * 64), kBlock, 0, (hipStream_t)stream>>>(*p, n, keys, ts, v_i64, v_f32, v_f64);
+    return hipGetLastError() == hipSuccess ? FWA_OK : FWA_E_DEVICE;
+}
+
+}  // extern "C"

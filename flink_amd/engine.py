@@ -1,0 +1,207 @@
+"""ctypes binding of libflink_amd.so (the HIP engine behind include/flink_amd.h).
+
+`WindowAggregator` is the thin host handle the operator facades (flink_amd.operators) sit on. Inputs
+may be numpy arrays (host; staged by the engine) or torch CUDA tensors (device pointers, zero copy).
+There is no CPU fallback: if the HIP library is missing this module raises at import/first use.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi as A
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libflink_amd.so")
+_LIB = None
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (A.STATUS.get(code, code), msg))
+        self.code = code
+
+
+def lib():
+    """Load libflink_amd.so (built by `make -C flink_amd/csrc` / __graft_entry__.build())."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libflink_amd.so not built (%s): run `make -C flink_amd/csrc`; "
+                           "there is no CPU fallback for the engine" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    A.bind_common(L, "fwa_")
+    L.fwa_push.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                           C.c_int32, C.POINTER(C.c_int64)]
+    L.fwa_push.restype = C.c_int
+    L.fwa_flush.argtypes = [C.c_void_p]
+    L.fwa_flush.restype = C.c_int
+    L.fwa_version.restype = C.c_char_p
+    L.fwa_reset_timers.argtypes = [C.c_void_p]
+    L.fwa_reset_timers.restype = C.c_int
+    L.fwa_key_groups.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                 C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
+    L.fwa_key_groups.restype = C.c_int
+    L.fwa_generate.argtypes = [C.POINTER(A.GenParams), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                               C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+    L.fwa_generate.restype = C.c_int
+    _LIB = L
+    return L
+
+
+def _is_torch_cuda(x):
+    return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if _is_torch_cuda(x):
+        return C.c_void_p(x.data_ptr())
+    return x.ctypes.data_as(C.c_void_p)
+
+
+def _check(rc, h=None, what=""):
+    if rc:
+        msg = lib().fwa_last_error(h).decode() if h else what
+        raise EngineError(rc, msg or what)
+
+
+class WindowAggregator:
+    """One engine handle = one Flink subtask's window operator state (single-threaded)."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.names = A.agg_names(cfg)
+        self.h = C.c_void_p()
+        rc = lib().fwa_create(C.byref(cfg), C.byref(self.h))
+        if rc:
+            raise EngineError(rc, "fwa_create")
+
+    # -- processElement (batched) --
+    def push(self, keys, ts, cols=(), key_hash=None, sync=True):
+        """Push a columnar batch; returns the number of late records dropped in it."""
+        device = _is_torch_cuda(keys)
+        if not device:
+            keys = np.ascontiguousarray(keys, np.int64)
+            ts = np.ascontiguousarray(ts, np.int64)
+            cols = [np.ascontiguousarray(c) for c in cols]
+            if key_hash is not None:
+                key_hash = np.ascontiguousarray(key_hash, np.int32)
+        n = int(keys.shape[0])
+        arr = (C.c_void_p * max(1, len(cols)))(*[_ptr(c).value for c in cols])
+        flags = A.PUSH_DEVICE_PTRS if device else 0
+        dropped = C.c_int64(0)
+        rc = lib().fwa_push(self.h, _ptr(keys), _ptr(ts), arr, _ptr(key_hash), n, flags, C.byref(dropped))
+        _check(rc, self.h)
+        return dropped.value
+
+    # -- processWatermark --
+    def advance_watermark_raw(self, wm):
+        out = A.Out()
+        rc = lib().fwa_advance_watermark(self.h, int(wm), C.byref(out))
+        _check(rc, self.h)
+        return out
+
+    def advance_watermark(self, wm):
+        """Fire every window with maxTimestamp <= wm; returns the fired rows as numpy columns."""
+        out = self.advance_watermark_raw(wm)
+        n = out.n_rows
+        conv = _dev_to_np if out.on_device else _host_to_np
+        res = {f: conv(getattr(out, f), n, np.dtype("i8")) for f in ("key", "win_start", "win_end")}
+        for j, name in enumerate(self.names):
+            res["agg%d" % j] = conv(out.agg[j], n, np.dtype(A.AGG_RESULT_DTYPE[name]))
+        return res
+
+    def advance_watermark_device(self, wm):
+        """Same, but returns zero-copy torch CUDA views of the engine-owned output columns
+        (valid until the next call on this handle). Requires output_on_device=1."""
+        out = self.advance_watermark_raw(wm)
+        n = out.n_rows
+        res = {f: dev_view(getattr(out, f), n, np.dtype("i8")) for f in ("key", "win_start", "win_end")}
+        for j, name in enumerate(self.names):
+            res["agg%d" % j] = dev_view(out.agg[j], n, np.dtype(A.AGG_RESULT_DTYPE[name]))
+        return res
+
+    def flush(self):
+        _check(lib().fwa_flush(self.h), self.h)
+
+    def stats(self):
+        st = A.Stats()
+        _check(lib().fwa_get_stats(self.h, C.byref(st)), self.h)
+        return st
+
+    def reset_timers(self):
+        _check(lib().fwa_reset_timers(self.h), self.h)
+
+    def close(self):
+        if self.h:
+            lib().fwa_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _host_to_np(p, n, dt):
+    if n == 0 or not p:
+        return np.zeros(0, dt)
+    buf = (C.c_char * (n * dt.itemsize)).from_address(p)
+    return np.frombuffer(buf, dtype=dt, count=n).copy()
+
+
+class _CudaArray:
+    def __init__(self, p, n, dt):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": dt.str, "data": (int(p), False),
+                                         "version": 3}
+
+
+def dev_view(p, n, dt):
+    """Zero-copy torch view of engine-owned device memory."""
+    import torch
+    if n == 0 or not p:
+        return torch.zeros(0, dtype=getattr(torch, {"i8": "int64", "f4": "float32", "f8": "float64"}[dt.str[1:]]),
+                           device="cuda")
+    return torch.as_tensor(_CudaArray(p, n, dt), device="cuda")
+
+
+def _dev_to_np(p, n, dt):
+    if n == 0 or not p:
+        return np.zeros(0, dt)
+    return dev_view(p, n, dt).cpu().numpy().copy()
+
+
+def key_groups(keys, max_parallelism=128, parallelism=1, key_kind=A.KEY_JAVA_LONG, key_hash=None, device=0):
+    """KeyGroupRangeAssignment on the GPU: (key_group, operator_index) int32 arrays."""
+    dev = _is_torch_cuda(keys)
+    if dev:
+        import torch
+        n = keys.shape[0]
+        kg = torch.empty(n, dtype=torch.int32, device=keys.device)
+        op = torch.empty(n, dtype=torch.int32, device=keys.device)
+    else:
+        keys = np.ascontiguousarray(keys, np.int64)
+        n = keys.shape[0]
+        kg = np.empty(n, np.int32)
+        op = np.empty(n, np.int32)
+        if key_hash is not None:
+            key_hash = np.ascontiguousarray(key_hash, np.int32)
+    rc = lib().fwa_key_groups(_ptr(keys), _ptr(key_hash), n, key_kind, max_parallelism, parallelism,
+                              _ptr(kg), _ptr(op), A.PUSH_DEVICE_PTRS if dev else 0, device)
+    _check(rc, None, "fwa_key_groups")
+    return kg, op
+
+
+def generate(params, n, keys=None, ts=None, v_i64=None, v_f32=None, v_f64=None, device=0, stream=None):
+    """Fill torch CUDA tensors with the synthetic stream of SURVEY.md §8(d) (device generator)."""
+    rc = lib().fwa_generate(C.byref(params), n, _ptr(keys), _ptr(ts), _ptr(v_i64), _ptr(v_f32),
+                            _ptr(v_f64), device, stream)
+    _check(rc, None, "fwa_generate")
+
+
+def version():
+    return lib().fwa_version().decode()

@@ -140,7 +140,15 @@ typedef struct fwa_stats {
     int64_t live_keys;
     int64_t live_slices;
     int64_t current_watermark;
+    /* device time of the engine's kernels, measured with HIP events on the handle's stream */
+    int64_t ingest_launches;
+    double ingest_ms;            /* sum over ingest-kernel launches */
+    int64_t ingest_records;      /* records processed by those launches (replays included) */
+    int64_t fire_launches;
+    double fire_ms;
+    int64_t fire_rows;
 } fwa_stats;
+
 
 typedef struct fwa_engine fwa_engine;
 
@@ -166,6 +174,9 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out);
 int fwa_flush(fwa_engine* e);
 
 int fwa_get_stats(fwa_engine* e, fwa_stats* out);
+
+/* Reset the kernel timing counters of fwa_stats (bench warm-up). */
+int fwa_reset_timers(fwa_engine* e);
 
 /* Stateless key-group assignment of n keys (device or host pointers per flags):
  * kg_out[i] = murmurHash(hash(key_i)) % max_parallelism; op_out[i] = kg*parallelism/max_parallelism.
