@@ -163,6 +163,7 @@ def main():
         },
         "end_to_end_hbm_frac": e2e_bytes / elapsed / 1e9 / HBM_PEAK_GBPS / world,
         "fire": {"launches": st.fire_launches, "ms": st.fire_ms, "rows": st.fire_rows},
+        "ingest_split_ms": {"partition": st.partition_ms, "combine": st.combine_ms, "total": st.ingest_ms},
         "rows_emitted": rows_all,
         "late_dropped": dropped,
     }

@@ -64,6 +64,8 @@ struct DevStatus {
     unsigned long long rows;    // fire kernel output counter
     unsigned long long max_q;   // ord-encoded max / min slice number accepted this push
     unsigned long long min_q;
+    int32_t pad;                // host-side scratch (straggler count copy)
+    int32_t pad2;
 };
 
 enum AccKind : int32_t { ACC_NONE = 0, ACC_ADD_I64 = 1, ACC_ADD_F64 = 2, ACC_MIN_ORD = 3, ACC_MAX_ORD = 4 };
@@ -73,6 +75,8 @@ struct AggDesc {
     int32_t col;                // input column
     int32_t acc;                // accumulator column (>=1) or 0 for COUNT
     int32_t acc_kind;
+    int32_t vslot;              // partitioned path: which carried value column feeds this aggregate
+    int32_t pad;
 };
 
 struct EngineConst {
@@ -256,6 +260,355 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
 }
 
 // ------------------------------------------------------------------------------------------------
+// v2 ingest: two phases, no global atomics on the accumulators.
+//
+// Phase P (partition_kernel): per tile of kTileP records: Java key-group check, slice + lateness via
+//   the read-only directory, key-table lookup/insert -> kid, then a counting sort of the tile in LDS
+//   by partition p = kid >> seg_log and one global cursor reservation per (tile, partition), so each
+//   bucket run is written as contiguous coalesced stores. Record = meta (u32: local kid | rel << 16)
+//   + up to 2 carried 8-byte value columns.
+// Phase A (combine_kernel): one workgroup owns one partition (SEG consecutive kids) and streams its
+//   bucket once, accumulating into an LDS window of kSL slices with LDS atomics (Flink's
+//   LocalSlicingWindowAggOperator/GlobalAggCombiner split, done on-chip); a slice leaving the window is
+//   merged into HBM with plain coalesced read-modify-write (the workgroup exclusively owns those kids).
+//   Records older than the window ("stragglers") go to a list applied by straggler_kernel with atomics.
+
+constexpr int kThreadsP = 512;
+constexpr int kMaxPart = 1024;
+constexpr int kRelCap = 4096;                      // slice numbers relative to q_base carried in 12..16 bits
+constexpr int kThreadsA = 1024;
+constexpr int kItemsA = 4;
+
+struct PartArgs {
+    const int64_t* keys;
+    const int64_t* ts;
+    const void* cols[FWA_MAX_COLS];
+    const int32_t* key_hash;
+    int64_t n;
+    int64_t wm;
+    unsigned long long* key_table;
+    uint64_t key_mask;
+    const DirEntry* dir;
+    uint32_t dir_mask;
+    unsigned long long* want;
+    int32_t* spill;
+    int32_t* touched;
+    int64_t q_base;
+    uint32_t* b_meta;                  // [np][capb]
+    unsigned long long* b_val0;        // [np][capb]
+    unsigned long long* b_val1;
+    uint32_t* b_cnt;                   // [np]
+    int64_t capb;
+    int32_t seg_log, np;
+    int32_t nv;                        // carried value columns (0..2)
+    int32_t vcol[2];
+    int32_t vsize[2];                  // 4 or 8 bytes
+    DevStatus* st;
+};
+
+__device__ __forceinline__ unsigned long long load_raw(const void* col, int64_t i, int size) {
+    return size == 4 ? (unsigned long long)((const uint32_t*)col)[i] : ((const unsigned long long*)col)[i];
+}
+
+// Block-wide exclusive scan of hist[0..np) into toff (np <= kMaxPart = 2 * kThreadsP).
+__device__ __forceinline__ void block_scan_np(const uint32_t* hist, uint32_t* toff, uint32_t* wsum, int np, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t a0 = (2 * tid < np) ? hist[2 * tid] : 0u;
+    const uint32_t a1 = (2 * tid + 1 < np) ? hist[2 * tid + 1] : 0u;
+    uint32_t x = a0 + a1, incl = x;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int w = 0; w < kThreadsP / 64; ++w) { const uint32_t t = wsum[w]; wsum[w] = run; run += t; }
+        *total = run;
+    }
+    __syncthreads();
+    const uint32_t excl = wsum[wid] + incl - x;
+    if (2 * tid < np) toff[2 * tid] = excl;
+    if (2 * tid + 1 < np) toff[2 * tid + 1] = excl + a0;
+}
+
+template <int NV, int ITEMS>
+__global__ void __launch_bounds__(kThreadsP) partition_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
+    constexpr int kTileP = kThreadsP * ITEMS;
+    constexpr int kItemsP = ITEMS;
+    const EngineConst& c = *cp;
+    __shared__ uint32_t hist[kMaxPart];
+    __shared__ uint32_t toff[kMaxPart];
+    __shared__ uint32_t gbase[kMaxPart];
+    __shared__ uint32_t s_meta[kTileP];
+    __shared__ uint16_t s_part[kTileP];
+    __shared__ unsigned long long s_val[NV > 0 ? NV : 1][NV > 0 ? kTileP : 1];
+    __shared__ uint32_t wsum[kThreadsP / 64];
+    __shared__ uint32_t s_total;
+    __shared__ int s_overflow;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t seg_mask = (1u << a.seg_log) - 1u;
+    unsigned dropped = 0;
+    const int64_t ntiles = (a.n + kTileP - 1) / kTileP;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        for (int i = tid; i < a.np; i += kThreadsP) hist[i] = 0;
+        if (tid == 0) s_overflow = 0;
+        __syncthreads();
+        uint32_t r_meta[kItemsP];
+        uint32_t r_pos[kItemsP];     // (p << 16 | rank) or ~0u when the record does not go to a bucket
+        unsigned long long r_v0[kItemsP], r_v1[kItemsP];
+        const int64_t t0 = tile * kTileP;
+#pragma unroll
+        for (int j = 0; j < kItemsP; ++j) {
+            r_pos[j] = ~0u;
+            const int64_t i = t0 + (int64_t)j * kThreadsP + tid;
+            if (i >= a.n) continue;
+            const int64_t key = a.keys[i];
+            const int64_t ts = a.ts[i];
+            r_v0[j] = NV > 0 ? load_raw(a.cols[a.vcol[0]], i, a.vsize[0]) : 0ull;
+            r_v1[j] = NV > 1 ? load_raw(a.cols[a.vcol[1]], i, a.vsize[1]) : 0ull;
+            const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0), c.max_par);
+            if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }
+            if (c.sem == FWA_SEM_DATASTREAM && ts == LONG_MIN_J) { raise_error(a.st, FWA_E_TS_MIN); continue; }
+            const int64_t d = jm::wsub(ts, c.off);
+            const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
+            const uint64_t uq = jm::udiv64(ud, c.g_div);
+            const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
+            const DirEntry* e = dir_find(a.dir, a.dir_mask, q);
+            bool to_spill = false;
+            if (e == nullptr) { want_insert(a.want, a.st, q); to_spill = true; }
+            else {
+                const bool accepted = (e->flags & 2) || a.wm < e->thr;
+                if (!accepted) { ++dropped; continue; }
+                if (c.lateness_pos && a.wm >= e->first_maxts) atomicAdd(&a.st->late_fire, 1ull);
+                if (e->slot < 0) { want_insert(a.want, a.st, q); to_spill = true; }
+            }
+            const uint64_t rel = (uint64_t)(q - a.q_base);
+            if (!to_spill && rel >= (uint64_t)kRelCap) to_spill = true;     // far slice: slow path
+            if (!to_spill && (uint64_t)key == kEmptyKey) to_spill = true;   // side-slot key: slow path
+            if (to_spill) {
+                const int32_t si = atomicAdd(&a.st->spill_n, 1);
+                a.spill[si] = (int32_t)i;
+                continue;
+            }
+            const int64_t kid = key_slot(a.key_table, a.key_mask, key, a.st);
+            if (kid < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
+            if (a.touched[e->slot] == 0) a.touched[e->slot] = 1;
+            const uint32_t p = (uint32_t)(kid >> a.seg_log);
+            r_meta[j] = ((uint32_t)kid & seg_mask) | ((uint32_t)rel << 16);
+            r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
+        }
+        __syncthreads();
+        block_scan_np(hist, toff, wsum, a.np, &s_total);
+        __syncthreads();
+        for (int p = tid; p < a.np; p += kThreadsP)
+            gbase[p] = hist[p] ? atomicAdd(&a.b_cnt[p], hist[p]) : 0u;
+#pragma unroll
+        for (int j = 0; j < kItemsP; ++j) {
+            if (r_pos[j] == ~0u) continue;
+            const uint32_t p = r_pos[j] >> 16;
+            const uint32_t s = toff[p] + (r_pos[j] & 0xffffu);
+            s_meta[s] = r_meta[j];
+            s_part[s] = (uint16_t)p;
+            if (NV > 0) s_val[0][s] = r_v0[j];
+            if (NV > 1) s_val[NV > 1 ? 1 : 0][s] = r_v1[j];
+        }
+        __syncthreads();
+        const uint32_t total = s_total;
+        for (uint32_t s = tid; s < total; s += kThreadsP) {
+            const uint32_t p = s_part[s];
+            const uint64_t dst = (uint64_t)gbase[p] + (s - toff[p]);
+            if (dst >= (uint64_t)a.capb) { s_overflow = 1; continue; }
+            const uint64_t o = (uint64_t)p * (uint64_t)a.capb + dst;
+            a.b_meta[o] = s_meta[s];
+            if (NV > 0) a.b_val0[o] = s_val[0][s];
+            if (NV > 1) a.b_val1[o] = s_val[NV > 1 ? 1 : 0][s];
+        }
+        __syncthreads();
+        if (tid == 0 && s_overflow) atomicOr(&a.st->key_full, 2);    // bucket overflow: host reruns on the v1 path
+    }
+    for (int s = 32; s >= 1; s >>= 1) dropped += __shfl_xor(dropped, s);
+    if (lane == 0 && dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
+}
+
+struct CombineArgs {
+    const uint32_t* b_meta;
+    const unsigned long long* b_val0;
+    const unsigned long long* b_val1;
+    const uint32_t* b_cnt;
+    int64_t capb;
+    int32_t seg_log, np, sl;           // sl: LDS slice window
+    const int32_t* rel2slot;           // [kRelCap]
+    unsigned long long* const* slot_base;
+    int64_t stride;
+    uint32_t* strag;                   // straggler (p << 32 | idx) list as pairs
+    int32_t* strag_n;
+    int64_t strag_cap;
+    DevStatus* st;
+};
+
+__device__ __forceinline__ unsigned long long ident_of(int acc_kind) { return acc_kind == ACC_MIN_ORD ? ~0ull : 0ull; }
+
+__device__ __forceinline__ unsigned long long carried_ord(unsigned long long raw, int kind) {
+    switch (kind) {
+        case FWA_MIN_I64: case FWA_MAX_I64: return jm::ord_i64((int64_t)raw);
+        case FWA_MIN_F32: case FWA_MAX_F32:
+            return jm::ord_bits64((uint64_t)__double_as_longlong((double)__uint_as_float((uint32_t)raw)));
+        default: return jm::ord_bits64(raw);
+    }
+}
+
+__device__ __forceinline__ double carried_f64(unsigned long long raw, int kind) {
+    return (kind == FWA_SUM_F32 || kind == FWA_AVG_F32) ? (double)__uint_as_float((uint32_t)raw)
+                                                         : __longlong_as_double((long long)raw);
+}
+
+// LDS layout: count u32 [sl][SEG], then (nacc-1) columns of u64 [sl][SEG]
+__global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const EngineConst& c = *cp;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int p = blockIdx.x;
+    const int seg = 1 << a.seg_log;
+    const int sl = a.sl;
+    uint32_t* lcnt = (uint32_t*)smem;
+    const size_t cnt_bytes = ((size_t)sl * seg * 4 + 15) & ~(size_t)15;
+    unsigned long long* lacc = (unsigned long long*)(smem + cnt_bytes);
+    int* s_mm = (int*)(smem + cnt_bytes + (size_t)(c.nacc - 1) * sl * seg * 8);
+    int& s_min = s_mm[0];
+    int& s_max = s_mm[1];
+    // identities
+    for (int i = tid; i < sl * seg; i += kThreadsA) {
+        lcnt[i] = 0;
+        for (int cc = 1; cc < c.nacc; ++cc) lacc[(size_t)(cc - 1) * sl * seg + i] = ident_of(c.acc_kind[cc]);
+    }
+    const int64_t cnt = min((int64_t)a.b_cnt[p], a.capb);
+    const uint32_t* meta = a.b_meta + (int64_t)p * a.capb;
+    const unsigned long long* v0 = a.b_val0 ? a.b_val0 + (int64_t)p * a.capb : nullptr;
+    const unsigned long long* v1 = a.b_val1 ? a.b_val1 + (int64_t)p * a.capb : nullptr;
+    int lo = 0x7fffffff;   // lowest relative slice held in the window (block-uniform)
+    auto flush = [&](int rel) {
+        const int w = rel % sl;
+        const int32_t slot = a.rel2slot[rel];
+        unsigned long long* base = slot >= 0 ? a.slot_base[slot] : nullptr;
+        for (int i = tid; i < seg; i += kThreadsA) {
+            const uint32_t k = lcnt[w * seg + i];
+            if (k == 0) continue;
+            lcnt[w * seg + i] = 0;
+            const int64_t g = ((int64_t)p << a.seg_log) + i;
+            if (!base) continue;   // cannot happen: records were accepted into this slice
+            base[g] += k;
+            for (int cc = 1; cc < c.nacc; ++cc) {
+                unsigned long long* lp = &lacc[(size_t)(cc - 1) * sl * seg + (size_t)w * seg + i];
+                const unsigned long long x = *lp;
+                *lp = ident_of(c.acc_kind[cc]);
+                unsigned long long* gp = &base[(int64_t)cc * a.stride + g];
+                switch (c.acc_kind[cc]) {
+                    case ACC_ADD_I64: *gp += x; break;
+                    case ACC_ADD_F64: *(double*)gp += __longlong_as_double((long long)x); break;
+                    case ACC_MIN_ORD: if (x < *gp) *gp = x; break;
+                    case ACC_MAX_ORD: if (x > *gp) *gp = x; break;
+                    default: break;
+                }
+            }
+        }
+    };
+    __syncthreads();
+    const int64_t chunk = (int64_t)kThreadsA * kItemsA;
+    for (int64_t cb = 0; cb < cnt; cb += chunk) {
+        uint32_t m[kItemsA];
+        unsigned long long x0[kItemsA], x1[kItemsA];
+        int rmin = 0x7fffffff, rmax = -1;
+#pragma unroll
+        for (int j = 0; j < kItemsA; ++j) {
+            const int64_t i = cb + (int64_t)j * kThreadsA + tid;
+            m[j] = ~0u;
+            if (i >= cnt) continue;
+            m[j] = meta[i];
+            x0[j] = v0 ? v0[i] : 0ull;
+            x1[j] = v1 ? v1[i] : 0ull;
+            const int rel = (int)(m[j] >> 16);
+            rmin = min(rmin, rel);
+            rmax = max(rmax, rel);
+        }
+        for (int s = 32; s >= 1; s >>= 1) { rmin = min(rmin, __shfl_xor(rmin, s)); rmax = max(rmax, __shfl_xor(rmax, s)); }
+        if (tid == 0) { s_min = 0x7fffffff; s_max = -1; }
+        __syncthreads();
+        if (lane == 0) { atomicMin(&s_min, rmin); atomicMax(&s_max, rmax); }
+        __syncthreads();
+        const int cmin = s_min, cmax = s_max;
+        if (lo == 0x7fffffff) lo = cmin;
+        while (cmax >= lo + sl) {       // slide the window forward: merge the oldest slice into HBM
+            flush(lo);
+            ++lo;
+            __syncthreads();
+        }
+#pragma unroll
+        for (int j = 0; j < kItemsA; ++j) {
+            if (m[j] == ~0u) continue;
+            const int rel = (int)(m[j] >> 16);
+            const int i = (int)(m[j] & ((1u << a.seg_log) - 1u));
+            if (rel < lo) {             // older than the window: straggler list (applied with atomics)
+                const int32_t si = atomicAdd(a.strag_n, 1);
+                if (si < a.strag_cap) { a.strag[2 * si] = (uint32_t)p; a.strag[2 * si + 1] = (uint32_t)(cb + (int64_t)j * kThreadsA + tid); }
+                else atomicOr(&a.st->key_full, 4);
+                continue;
+            }
+            const int w = rel % sl;
+            atomicAdd(&lcnt[w * seg + i], 1u);
+            for (int jj = 0; jj < c.naggs; ++jj) {
+                const AggDesc d = c.agg[jj];
+                if (d.acc == 0) continue;
+                unsigned long long* lp = &lacc[(size_t)(d.acc - 1) * sl * seg + (size_t)w * seg + i];
+                const unsigned long long raw = d.vslot == 0 ? x0[j] : x1[j];
+                switch (d.acc_kind) {
+                    case ACC_ADD_I64: atomicAdd(lp, raw); break;
+                    case ACC_ADD_F64: atomicAdd((double*)lp, carried_f64(raw, d.kind)); break;
+                    case ACC_MIN_ORD: atomicMin(lp, carried_ord(raw, d.kind)); break;
+                    case ACC_MAX_ORD: atomicMax(lp, carried_ord(raw, d.kind)); break;
+                    default: break;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (lo != 0x7fffffff)
+        for (int r = lo; r < lo + sl && r < kRelCap; ++r) { flush(r); __syncthreads(); }
+}
+
+// Stragglers: bucket entries older than their combiner's window, applied with global atomics.
+__global__ void straggler_kernel(CombineArgs a, const EngineConst* __restrict__ cp, int32_t n) {
+    const EngineConst& c = *cp;
+    for (int32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        const int64_t p = a.strag[2 * t];
+        const int64_t idx = a.strag[2 * t + 1];
+        const int64_t o = p * a.capb + idx;
+        const uint32_t m = a.b_meta[o];
+        const int32_t slot = a.rel2slot[m >> 16];
+        if (slot < 0) continue;
+        const int64_t g = (p << a.seg_log) + (m & ((1u << a.seg_log) - 1u));
+        unsigned long long* base = a.slot_base[slot];
+        atomicAdd(&base[g], 1ull);
+        for (int jj = 0; jj < c.naggs; ++jj) {
+            const AggDesc d = c.agg[jj];
+            if (d.acc == 0) continue;
+            const unsigned long long raw = d.vslot == 0 ? a.b_val0[o] : a.b_val1[o];
+            unsigned long long* gp = base + (int64_t)d.acc * a.stride + g;
+            switch (d.acc_kind) {
+                case ACC_ADD_I64: atomicAdd(gp, raw); break;
+                case ACC_ADD_F64: atomicAdd((double*)gp, carried_f64(raw, d.kind)); break;
+                case ACC_MIN_ORD: atomicMin(gp, carried_ord(raw, d.kind)); break;
+                case ACC_MAX_ORD: atomicMax(gp, carried_ord(raw, d.kind)); break;
+                default: break;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // fire
 
 struct FireWindow {
@@ -279,78 +632,103 @@ struct FireArgs {
     DevStatus* st;
 };
 
+constexpr int kFireJ = 16;                         // keys per thread per block: 4096-key chunks
+
+__device__ __forceinline__ void emit_row(const FireArgs& f, const EngineConst& c, const FireWindow& win, int64_t k,
+                                         unsigned long long kv, uint64_t cnt, int64_t row) {
+    f.o_key[row] = (k < f.capacity) ? (int64_t)kv : LONG_MIN_J;
+    f.o_start[row] = win.start;
+    f.o_end[row] = win.end;
+    for (int j = 0; j < c.naggs; ++j) {
+        const AggDesc d = c.agg[j];
+        int64_t iv = 0;
+        double dv = 0.0;
+        uint64_t ov = (d.acc_kind == ACC_MIN_ORD) ? ~0ull : 0ull;
+        for (int s = 0; s < win.nslots; ++s) {
+            const unsigned long long x = f.slot_base[f.win_slots[win.slot_off + s]][(int64_t)d.acc * f.stride + k];
+            switch (d.acc_kind) {
+                case ACC_ADD_I64: iv = jm::wadd(iv, (int64_t)x); break;
+                case ACC_ADD_F64: dv += __longlong_as_double((long long)x); break;
+                case ACC_MIN_ORD: ov = x < ov ? x : ov; break;
+                case ACC_MAX_ORD: ov = x > ov ? x : ov; break;
+                default: break;
+            }
+        }
+        void* out = f.o_agg[j];
+        switch (d.kind) {
+            case FWA_COUNT: ((int64_t*)out)[row] = (int64_t)cnt; break;
+            case FWA_SUM_I64: ((int64_t*)out)[row] = iv; break;
+            case FWA_SUM_F32: ((float*)out)[row] = (float)dv; break;
+            case FWA_SUM_F64: ((double*)out)[row] = dv; break;
+            case FWA_AVG_I64: {
+                const int64_t n = (int64_t)cnt;  // AvgAggFunction: sum / count (Java long division)
+                ((int64_t*)out)[row] = (n == -1 && iv == LONG_MIN_J) ? LONG_MIN_J : iv / n;
+                break;
+            }
+            case FWA_AVG_F32: ((float*)out)[row] = (float)(dv / (double)(int64_t)cnt); break;
+            case FWA_AVG_F64: ((double*)out)[row] = dv / (double)(int64_t)cnt; break;
+            case FWA_MIN_I64: case FWA_MAX_I64: ((int64_t*)out)[row] = jm::unord_i64(ov); break;
+            case FWA_MIN_F32: case FWA_MAX_F32:
+                ((float*)out)[row] = (float)__longlong_as_double((long long)jm::unord_bits64(ov));
+                break;
+            case FWA_MIN_F64: case FWA_MAX_F64:
+                ((double*)out)[row] = __longlong_as_double((long long)jm::unord_bits64(ov));
+                break;
+            default: break;
+        }
+    }
+}
+
+// One block = one window x one chunk of kBlock*kFireJ consecutive kids. Pass 1 sums COUNT over the
+// window's slices and ballots the emitting keys; one atomic reserves the block's rows; pass 2 writes
+// rows j-major so every wave store is contiguous.
 __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
     const int32_t w = blockIdx.x / f.blocks_per_win;
-    const int32_t chunk = blockIdx.x % f.blocks_per_win;
+    const int64_t chunk = blockIdx.x % f.blocks_per_win;
     const FireWindow win = f.win[w];
     const int64_t nk = f.capacity + 1;
-    const int64_t per = (int64_t)f.blocks_per_win * blockDim.x;
-    const int lane = threadIdx.x & 63;
-    // every lane of a wave walks the same number of iterations (ballot below needs full waves)
-    const int64_t kbeg = (int64_t)chunk * blockDim.x + threadIdx.x;
-    const int64_t iters = (nk - ((int64_t)chunk * blockDim.x) + per - 1) / per;
-    for (int64_t it = 0; it < iters; ++it) {
-        const int64_t k = kbeg + it * per;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int kWaves = kBlock / 64;
+    __shared__ uint32_t woff[kFireJ][kWaves];
+    __shared__ unsigned long long s_base;
+    const int64_t k0 = chunk * (int64_t)kBlock * kFireJ;
+    uint64_t cnt[kFireJ];
+    unsigned long long kvs[kFireJ];
+    unsigned long long masks[kFireJ];
+#pragma unroll
+    for (int j = 0; j < kFireJ; ++j) {
+        const int64_t k = k0 + (int64_t)j * kBlock + tid;
         bool present = false;
         unsigned long long kv = 0;
         if (k < nk) {
             kv = f.key_table[k];
             present = (k < f.capacity) ? (kv != kEmptyKey) : (kv == 1ull);
         }
-        uint64_t cnt = 0;
+        uint64_t cc = 0;
         if (present)
-            for (int s = 0; s < win.nslots; ++s) cnt += f.slot_base[f.win_slots[win.slot_off + s]][k];
-        const bool emit = present && cnt != 0;
-        const unsigned long long mask = __ballot(emit);
-        if (mask == 0) continue;
-        const int leader = __ffsll((long long)mask) - 1;
-        unsigned long long base_row = 0;
-        if (lane == leader) base_row = atomicAdd(&f.st->rows, (unsigned long long)__popcll(mask));
-        base_row = __shfl(base_row, leader);
-        if (!emit) continue;
-        const int64_t row = (int64_t)base_row + __popcll(mask & ((1ull << lane) - 1));
-        f.o_key[row] = (k < f.capacity) ? (int64_t)kv : LONG_MIN_J;
-        f.o_start[row] = win.start;
-        f.o_end[row] = win.end;
-        for (int j = 0; j < c.naggs; ++j) {
-            const AggDesc d = c.agg[j];
-            int64_t iv = 0;
-            double dv = 0.0;
-            uint64_t ov = (d.acc_kind == ACC_MIN_ORD) ? ~0ull : 0ull;
-            for (int s = 0; s < win.nslots; ++s) {
-                const unsigned long long x = f.slot_base[f.win_slots[win.slot_off + s]][(int64_t)d.acc * f.stride + k];
-                switch (d.acc_kind) {
-                    case ACC_ADD_I64: iv = jm::wadd(iv, (int64_t)x); break;
-                    case ACC_ADD_F64: dv += __longlong_as_double((long long)x); break;
-                    case ACC_MIN_ORD: ov = x < ov ? x : ov; break;
-                    case ACC_MAX_ORD: ov = x > ov ? x : ov; break;
-                    default: break;
-                }
-            }
-            void* out = f.o_agg[j];
-            switch (d.kind) {
-                case FWA_COUNT: ((int64_t*)out)[row] = (int64_t)cnt; break;
-                case FWA_SUM_I64: ((int64_t*)out)[row] = iv; break;
-                case FWA_SUM_F32: ((float*)out)[row] = (float)dv; break;
-                case FWA_SUM_F64: ((double*)out)[row] = dv; break;
-                case FWA_AVG_I64: {
-                    const int64_t n = (int64_t)cnt;  // AvgAggFunction: sum / count (Java long division)
-                    ((int64_t*)out)[row] = (n == -1 && iv == LONG_MIN_J) ? LONG_MIN_J : iv / n;
-                    break;
-                }
-                case FWA_AVG_F32: ((float*)out)[row] = (float)(dv / (double)(int64_t)cnt); break;
-                case FWA_AVG_F64: ((double*)out)[row] = dv / (double)(int64_t)cnt; break;
-                case FWA_MIN_I64: case FWA_MAX_I64: ((int64_t*)out)[row] = jm::unord_i64(ov); break;
-                case FWA_MIN_F32: case FWA_MAX_F32:
-                    ((float*)out)[row] = (float)__longlong_as_double((long long)jm::unord_bits64(ov));
-                    break;
-                case FWA_MIN_F64: case FWA_MAX_F64:
-                    ((double*)out)[row] = __longlong_as_double((long long)jm::unord_bits64(ov));
-                    break;
-                default: break;
-            }
-        }
+            for (int s = 0; s < win.nslots; ++s) cc += f.slot_base[f.win_slots[win.slot_off + s]][k];
+        cnt[j] = cc;
+        kvs[j] = kv;
+        const unsigned long long m = __ballot(present && cc != 0);
+        masks[j] = m;
+        if (lane == 0) woff[j][wid] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int j = 0; j < kFireJ; ++j)
+            for (int v = 0; v < kWaves; ++v) { const uint32_t t = woff[j][v]; woff[j][v] = run; run += t; }
+        s_base = run ? atomicAdd(&f.st->rows, (unsigned long long)run) : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int j = 0; j < kFireJ; ++j) {
+        if (!((masks[j] >> lane) & 1ull)) continue;
+        const int64_t k = k0 + (int64_t)j * kBlock + tid;
+        const int64_t row = (int64_t)s_base + woff[j][wid] + __popcll(masks[j] & lt);
+        emit_row(f, c, win, k, kvs[j], cnt[j], row);
     }
 }
 
@@ -472,8 +850,22 @@ struct fwa_engine {
     int64_t wm = LONG_MIN_J;
     int64_t records_in = 0, late_dropped = 0, rows_out = 0;
     size_t mem_budget = 0;
+    // v2 (two-phase) ingest
+    bool v2 = false;
+    int32_t seg_log = 12, np = 0, sl = 2, nv = 0, vcol[2] = {0, 0}, vsize[2] = {8, 8};
+    int64_t capb = 0;
+    uint32_t* d_bmeta = nullptr;
+    unsigned long long* d_bval[2] = {nullptr, nullptr};
+    uint32_t* d_bcnt = nullptr;
+    int32_t* d_rel2slot = nullptr;
+    uint32_t* d_strag = nullptr;
+    int64_t strag_cap = 0;
+    int32_t* d_strag_n = nullptr;
+    size_t combine_lds = 0;
+    int32_t partition_grid = 256;
     // kernel timing (HIP events on this handle's stream)
-    hipEvent_t ev[4] = {};
+    hipEvent_t ev[8] = {};
+    double partition_ms = 0, combine_ms = 0;
     int64_t ingest_launches = 0, ingest_records = 0, fire_launches = 0, fire_rows = 0;
     double ingest_ms = 0, fire_ms = 0;
 };
@@ -745,7 +1137,8 @@ void fwa_destroy(fwa_engine* e) {
     (void)hipSetDevice(e->cfg.device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
-                    e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots};
+                    e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bmeta,
+                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
     for (void* p : e->chunks) (void)hipFree(p);
@@ -804,6 +1197,48 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         c.nacc++;
     }
     e->nacc = c.nacc;
+    // v2 eligibility: <= 2 distinct carried value columns, LDS window of >= 2 slices, <= kMaxPart partitions
+    {
+        int cols[2] = {-1, -1}, sizes[2] = {8, 8}, nv = 0;
+        bool ok = true;
+        for (int j = 0; j < cfg->num_aggs; ++j) {
+            AggDesc& d = c.agg[j];
+            if (d.acc == 0) continue;
+            int slot = -1;
+            for (int v = 0; v < nv; ++v) if (cols[v] == d.col) slot = v;
+            if (slot < 0) {
+                if (nv == 2) { ok = false; break; }
+                slot = nv;
+                cols[nv] = d.col;
+                sizes[nv] = (int)type_size(d.kind);
+                nv++;
+            } else if (sizes[slot] != (int)type_size(d.kind)) ok = false;
+            d.vslot = slot;
+        }
+        const int64_t kc0 = cfg->key_capacity > 0 ? cfg->key_capacity : (1 << 20);
+        int64_t cap0 = 1024;
+        while (cap0 < 2 * kc0) cap0 <<= 1;
+        int seg_log = 12;
+        if (const char* sv = getenv("FWA_SEG_LOG")) seg_log = atoi(sv);
+        const int64_t bps = 4 + 8 * (int64_t)(c.nacc - 1);
+        while (seg_log > 8 && 2 * bps * ((int64_t)1 << seg_log) + 64 > 160 * 1024) --seg_log;
+        int64_t np = cap0 >> seg_log;
+        if (np < 1) np = 1;
+        int sl = (int)std::min<int64_t>(8, (160 * 1024 - 64) / (bps * ((int64_t)1 << seg_log)));
+        if (const char* sv = getenv("FWA_SL")) sl = std::min(sl, atoi(sv));
+        const char* force = getenv("FWA_INGEST");
+        ok = ok && np <= kMaxPart && sl >= 2 && (1 << seg_log) <= 65536 && !(force && !strcmp(force, "v1"));
+        e->v2 = ok;
+        if (ok) {
+            e->seg_log = seg_log;
+            e->np = (int32_t)np;
+            e->sl = sl;
+            e->nv = nv;
+            for (int v = 0; v < 2; ++v) { e->vcol[v] = cols[v] < 0 ? 0 : cols[v]; e->vsize[v] = sizes[v]; }
+            e->combine_lds = (((size_t)sl * ((size_t)1 << seg_log) * 4 + 15) & ~(size_t)15) +
+                             (size_t)(c.nacc - 1) * sl * ((size_t)1 << seg_log) * 8 + 16;
+        }
+    }
     if (hipSetDevice(cfg->device) != hipSuccess) { delete e; return FWA_E_DEVICE; }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return FWA_E_DEVICE; }
     const int64_t kc = cfg->key_capacity > 0 ? cfg->key_capacity : (1 << 20);
@@ -899,6 +1334,125 @@ static int account_ingest(fwa_engine* e) {  // after the stream was synchronised
     return FWA_OK;
 }
 
+static int ensure_v2_buffers(fwa_engine* e, int64_t n) {
+    const int64_t capb = (n / e->np) + (n / e->np) / 4 + 16384;
+    if (capb > e->capb) {
+        for (void* p : {(void*)e->d_bmeta, (void*)e->d_bval[0], (void*)e->d_bval[1]}) if (p) HIPCHK(e, hipFree(p));
+        e->d_bmeta = nullptr;
+        e->d_bval[0] = e->d_bval[1] = nullptr;
+        HIPCHK(e, hipMalloc(&e->d_bmeta, sizeof(uint32_t) * capb * e->np));
+        for (int v = 0; v < e->nv; ++v) HIPCHK(e, hipMalloc(&e->d_bval[v], 8 * capb * e->np));
+        e->capb = capb;
+    }
+    if (!e->d_bcnt) {
+        HIPCHK(e, hipMalloc(&e->d_bcnt, sizeof(uint32_t) * kMaxPart));
+        HIPCHK(e, hipMalloc(&e->d_rel2slot, sizeof(int32_t) * kRelCap));
+        HIPCHK(e, hipMalloc(&e->d_strag_n, 16));
+    }
+    const int64_t scap = std::max<int64_t>(n / 8, 1 << 16);
+    if (scap > e->strag_cap) {
+        if (e->d_strag) HIPCHK(e, hipFree(e->d_strag));
+        HIPCHK(e, hipMalloc(&e->d_strag, sizeof(uint32_t) * 2 * scap));
+        e->strag_cap = scap;
+    }
+    return FWA_OK;
+}
+
+// Two-phase ingest. Sets *ran = false (and leaves no state change besides key insertions) when the
+// batch must take the v1 path instead (bucket overflow on skewed keys).
+static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
+    *ran = false;
+    int rc = ensure_v2_buffers(e, a.n);
+    if (rc) return rc;
+    const int64_t q_base = e->live.empty() ? 0 : e->live.begin()->first;
+    std::vector<int32_t> r2s(kRelCap, -1);
+    for (auto& kv : e->live) {
+        const int64_t rel = kv.first - q_base;
+        if (rel >= 0 && rel < kRelCap) r2s[rel] = kv.second;
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_rel2slot, r2s.data(), sizeof(int32_t) * kRelCap, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_bcnt, 0, sizeof(uint32_t) * kMaxPart, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_strag_n, 0, 16, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_want, 0, sizeof(unsigned long long) * kWantCap, e->stream));
+    PartArgs pa;
+    memset(&pa, 0, sizeof(pa));
+    pa.keys = a.keys;
+    pa.ts = a.ts;
+    for (int c = 0; c < FWA_MAX_COLS; ++c) pa.cols[c] = a.cols[c];
+    pa.key_hash = a.key_hash;
+    pa.n = a.n;
+    pa.wm = a.wm;
+    pa.key_table = e->d_keys;
+    pa.key_mask = (uint64_t)e->capacity - 1;
+    pa.dir = e->d_dir;
+    pa.dir_mask = e->dir_cap - 1;
+    pa.want = e->d_want;
+    pa.spill = e->d_spill;
+    pa.touched = e->d_touched;
+    pa.q_base = q_base;
+    pa.b_meta = e->d_bmeta;
+    pa.b_val0 = e->d_bval[0];
+    pa.b_val1 = e->d_bval[1];
+    pa.b_cnt = e->d_bcnt;
+    pa.capb = e->capb;
+    pa.seg_log = e->seg_log;
+    pa.np = e->np;
+    pa.nv = e->nv;
+    for (int v = 0; v < 2; ++v) { pa.vcol[v] = e->vcol[v]; pa.vsize[v] = e->vsize[v]; }
+    pa.st = e->d_st;
+    HIPCHK(e, hipEventRecord(e->ev[4], e->stream));
+    const int64_t tile = (e->nv == 2 ? 8 : 16) * (int64_t)kThreadsP;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, e->nv == 0 ? 512 : 256));
+    if (e->nv == 0) partition_kernel<0, 16><<<grid, kThreadsP, 0, e->stream>>>(pa, e->d_ec);
+    else if (e->nv == 1) partition_kernel<1, 16><<<grid, kThreadsP, 0, e->stream>>>(pa, e->d_ec);
+    else partition_kernel<2, 8><<<grid, kThreadsP, 0, e->stream>>>(pa, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->ev[5], e->stream));
+    rc = sync_status(e);
+    if (rc) return rc;
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[4], e->ev[5]));
+    e->partition_ms += ms;
+    e->ingest_ms += ms;
+    if (e->h_st->error) { *ran = true; return FWA_OK; }   // reported by the caller's status loop
+    if (e->h_st->key_full & 2) return FWA_OK;             // bucket overflow: caller reruns on v1
+    CombineArgs ca;
+    memset(&ca, 0, sizeof(ca));
+    ca.b_meta = e->d_bmeta;
+    ca.b_val0 = e->d_bval[0];
+    ca.b_val1 = e->d_bval[1];
+    ca.b_cnt = e->d_bcnt;
+    ca.capb = e->capb;
+    ca.seg_log = e->seg_log;
+    ca.np = e->np;
+    ca.sl = e->sl;
+    ca.rel2slot = e->d_rel2slot;
+    ca.slot_base = e->d_slot_base;
+    ca.stride = e->stride;
+    ca.strag = e->d_strag;
+    ca.strag_n = e->d_strag_n;
+    ca.strag_cap = e->strag_cap;
+    ca.st = e->d_st;
+    HIPCHK(e, hipEventRecord(e->ev[6], e->stream));
+    combine_kernel<<<e->np, kThreadsA, e->combine_lds, e->stream>>>(ca, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    int32_t nstrag = 0;
+    HIPCHK(e, hipMemcpyAsync(&e->h_st->pad, e->d_strag_n, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    nstrag = std::min<int64_t>(e->h_st->pad, e->strag_cap);
+    if (nstrag > 0) straggler_kernel<<<grid_for(nstrag), kBlock, 0, e->stream>>>(ca, e->d_ec, nstrag);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->ev[7], e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[6], e->ev[7]));
+    e->combine_ms += ms;
+    e->ingest_ms += ms;
+    e->ingest_launches++;
+    e->ingest_records += a.n;
+    *ran = true;
+    return FWA_OK;
+}
+
 int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
              const int32_t* key_hash, int64_t n, int32_t flags, int64_t* late_dropped_out) {
     if (!e) return FWA_E_STATE;
@@ -935,15 +1489,23 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
     }
     int rc = reset_push_status(e);
     if (rc) return rc;
-    rc = launch_ingest(e, a, false);
-    if (rc) return rc;
+    bool ran_v2 = false;
+    if (e->v2) {
+        rc = push_v2(e, a, &ran_v2);
+        if (rc) return rc;
+    }
+    if (!ran_v2) {
+        rc = reset_push_status(e);
+        if (rc) return rc;
+        rc = launch_ingest(e, a, false);
+        if (rc) return rc;
+    }
     int64_t dropped = 0;
     int64_t qmin = LONG_MAX_J, qmax = LONG_MIN_J;
     for (int round = 0;; ++round) {
         rc = sync_status(e);
         if (rc) return rc;
-        rc = account_ingest(e);
-        if (rc) return rc;
+        if (!ran_v2 || round > 0) { rc = account_ingest(e); if (rc) return rc; }
         const DevStatus st = *e->h_st;
         if (st.error) {
             const char* m = st.error == FWA_E_KEYGROUP ? "Key group is not in the owned KeyGroupRange (StateTable.getMapForKeyGroup)"
@@ -1066,9 +1628,7 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
             f.win = e->d_win;
             f.win_slots = e->d_win_slots;
             f.nwin = (int32_t)hw.size();
-            const int64_t key_blocks = (e->capacity + 1 + kBlock - 1) / kBlock;
-            const int64_t want_blocks = std::max<int64_t>(1, 4096 / (int64_t)hw.size());
-            f.blocks_per_win = (int32_t)std::max<int64_t>(1, std::min<int64_t>(key_blocks, want_blocks));
+            f.blocks_per_win = (int32_t)((e->capacity + 1 + (int64_t)kBlock * kFireJ - 1) / ((int64_t)kBlock * kFireJ));
             f.o_key = e->o_key;
             f.o_start = e->o_start;
             f.o_end = e->o_end;
@@ -1157,13 +1717,15 @@ int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
     s->fire_launches = e->fire_launches;
     s->fire_ms = e->fire_ms;
     s->fire_rows = e->fire_rows;
+    s->partition_ms = e->partition_ms;
+    s->combine_ms = e->combine_ms;
     return FWA_OK;
 }
 
 int fwa_reset_timers(fwa_engine* e) {
     if (!e) return FWA_E_ARG;
     e->ingest_launches = e->ingest_records = e->fire_launches = e->fire_rows = 0;
-    e->ingest_ms = e->fire_ms = 0;
+    e->ingest_ms = e->fire_ms = e->partition_ms = e->combine_ms = 0;
     return FWA_OK;
 }
 

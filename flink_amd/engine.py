@@ -27,6 +27,7 @@ def lib():
     global _LIB
     if _LIB is not None:
         return _LIB
+    _init_torch_runtime_first()
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libflink_amd.so not built (%s): run `make -C flink_amd/csrc`; "
                            "there is no CPU fallback for the engine" % LIB_PATH)
@@ -48,6 +49,17 @@ def lib():
     L.fwa_generate.restype = C.c_int
     _LIB = L
     return L
+
+
+def _init_torch_runtime_first():
+    """torch bundles its own HIP runtime; if libflink_amd.so's (/opt/rocm) runtime initialises first,
+    torch's later sees no GPU. Initialise torch's runtime first when torch and a GPU are present."""
+    try:
+        import torch
+        if torch.cuda.device_count() > 0:
+            torch.cuda.init()
+    except Exception:
+        pass
 
 
 def _is_torch_cuda(x):

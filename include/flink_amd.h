@@ -147,6 +147,8 @@ typedef struct fwa_stats {
     int64_t fire_launches;
     double fire_ms;
     int64_t fire_rows;
+    double partition_ms;         /* two-phase ingest split: phase P (key lookup + partition) */
+    double combine_ms;           /* phase A (LDS combine + HBM merge) */
 } fwa_stats;
 
 
