@@ -99,6 +99,7 @@ struct IngestArgs {
     int64_t wm;
     unsigned long long* key_table;
     uint64_t key_mask;          // capacity-1 (power of two); side slot at capacity
+    int32_t seg_log, part_bits; // key-table segmentation (see key_slot)
     const DirEntry* dir;
     uint32_t dir_mask;
     unsigned long long* want;   // open-addressing set of ord(q), kWantCap entries, 0 = empty
@@ -111,16 +112,24 @@ struct IngestArgs {
 
 __device__ __forceinline__ void raise_error(DevStatus* st, int code) { atomicCAS(&st->error, 0, code); }
 
-// Key table: open addressing, linear probing, CAS insert. Returns kid or -1 when full.
+// Key table: SEGMENTED open addressing. h = mix64(key); segment p = top part_bits of h (the v2
+// combiner's partition), probe linearly inside the segment from h & (SEG-1); CAS insert.
 // A stale EMPTY read only sends us to the CAS, which returns the winner's key: no hand-off needed.
-__device__ __forceinline__ int64_t key_slot(unsigned long long* table, uint64_t mask, int64_t key, DevStatus* st) {
+__device__ __forceinline__ uint64_t seg_base(uint64_t h, int seg_log, int part_bits) {
+    return part_bits ? ((h >> (64 - part_bits)) << seg_log) : 0ull;
+}
+__device__ __forceinline__ int64_t key_slot(unsigned long long* table, uint64_t mask, int seg_log, int part_bits,
+                                            int64_t key, DevStatus* st) {
     if ((uint64_t)key == kEmptyKey) {
         const unsigned long long side = mask + 1;
         if (table[side] != 1ull && atomicCAS(&table[side], 0ull, 1ull) == 0ull) atomicAdd(&st->n_keys, 1ull);
         return (int64_t)side;
     }
-    uint64_t i = jm::mix64((uint64_t)key) & mask;
-    for (uint64_t probe = 0; probe <= mask; ++probe) {
+    const uint64_t h = jm::mix64((uint64_t)key);
+    const uint64_t base = seg_base(h, seg_log, part_bits);
+    const uint64_t smask = ((uint64_t)1 << seg_log) - 1;
+    for (uint64_t probe = 0; probe <= smask; ++probe) {
+        const uint64_t i = base | ((h + probe) & smask);
         const unsigned long long cur = table[i];
         if (cur == (unsigned long long)key) return (int64_t)i;
         if (cur == kEmptyKey) {
@@ -131,7 +140,6 @@ __device__ __forceinline__ int64_t key_slot(unsigned long long* table, uint64_t 
             }
             if (old == (unsigned long long)key) return (int64_t)i;
         }
-        i = (i + 1) & mask;
     }
     return -1;
 }
@@ -217,7 +225,7 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         const uint64_t oq = jm::ord_i64(q);
         qmax = oq > qmax ? oq : qmax;
         qmin = oq < qmin ? oq : qmin;
-        const int64_t kid = key_slot(a.key_table, a.key_mask, key, a.st);
+        const int64_t kid = key_slot(a.key_table, a.key_mask, a.seg_log, a.part_bits, key, a.st);
         if (kid < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
         const int32_t slot = e->slot;
         unsigned long long* base = a.slot_base[slot];
@@ -260,22 +268,23 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
 }
 
 // ------------------------------------------------------------------------------------------------
-// v2 ingest: two phases, no global atomics on the accumulators.
+// v2 ingest: two phases, no global atomics -- Flink's LocalSlicingWindowAggOperator /
+// GlobalAggCombiner split (TwoStageOptimizedWindowAggregateRule.java:88-103) done on-chip.
 //
-// Phase P (partition_kernel): per tile of kTileP records: Java key-group check, slice + lateness via
-//   the read-only directory, key-table lookup/insert -> kid, then a counting sort of the tile in LDS
-//   by partition p = kid >> seg_log and one global cursor reservation per (tile, partition), so each
-//   bucket run is written as contiguous coalesced stores. Record = meta (u32: local kid | rel << 16)
-//   + up to 2 carried 8-byte value columns.
-// Phase A (combine_kernel): one workgroup owns one partition (SEG consecutive kids) and streams its
-//   bucket once, accumulating into an LDS window of kSL slices with LDS atomics (Flink's
-//   LocalSlicingWindowAggOperator/GlobalAggCombiner split, done on-chip); a slice leaving the window is
-//   merged into HBM with plain coalesced read-modify-write (the workgroup exclusively owns those kids).
-//   Records older than the window ("stragglers") go to a list applied by straggler_kernel with atomics.
+// Phase P (partition_kernel): a pure streaming pass. Per tile of records: Java key-group check,
+//   slice number + lateness via the read-only directory, partition p = top bits of mix64(key) (= the
+//   key-table segment that will hold the key), LDS counting sort of the tile by p, one global cursor
+//   reservation per (tile, partition), coalesced stores of the bucket runs. Carried record (SoA):
+//   key u64, up to 2 raw 8-byte value columns, rel u16 (slice number - q_base).
+// Phase A (combine_kernel): one workgroup owns one partition = one SEG-slot key-table segment. It
+//   loads the segment into LDS, streams its bucket once, finds/inserts keys in LDS (ds_cmpst_b64),
+//   accumulates into an LDS window of `sl` slices with LDS atomics, and merges a slice that leaves
+//   the window into HBM with plain coalesced read-modify-write (exclusive ownership: no atomics).
+//   Records older than the window ("stragglers") are applied afterwards by straggler_kernel.
 
 constexpr int kThreadsP = 512;
 constexpr int kMaxPart = 1024;
-constexpr int kRelCap = 4096;                      // slice numbers relative to q_base carried in 12..16 bits
+constexpr int kRelCap = 4096;                      // slice numbers relative to q_base
 constexpr int kThreadsA = 1024;
 constexpr int kItemsA = 4;
 
@@ -286,21 +295,19 @@ struct PartArgs {
     const int32_t* key_hash;
     int64_t n;
     int64_t wm;
-    unsigned long long* key_table;
-    uint64_t key_mask;
     const DirEntry* dir;
     uint32_t dir_mask;
     unsigned long long* want;
     int32_t* spill;
     int32_t* touched;
     int64_t q_base;
-    uint32_t* b_meta;                  // [np][capb]
-    unsigned long long* b_val0;        // [np][capb]
+    unsigned long long* b_key;         // [np][capb]
+    unsigned long long* b_val0;
     unsigned long long* b_val1;
+    uint16_t* b_rel;
     uint32_t* b_cnt;                   // [np]
     int64_t capb;
-    int32_t seg_log, np;
-    int32_t nv;                        // carried value columns (0..2)
+    int32_t part_bits, np;
     int32_t vcol[2];
     int32_t vsize[2];                  // 4 or 8 bytes
     DevStatus* st;
@@ -315,7 +322,8 @@ __device__ __forceinline__ void block_scan_np(const uint32_t* hist, uint32_t* to
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t a0 = (2 * tid < np) ? hist[2 * tid] : 0u;
     const uint32_t a1 = (2 * tid + 1 < np) ? hist[2 * tid + 1] : 0u;
-    uint32_t x = a0 + a1, incl = x;
+    const uint32_t x = a0 + a1;
+    uint32_t incl = x;
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(incl, d);
         if (lane >= d) incl += y;
@@ -335,38 +343,39 @@ __device__ __forceinline__ void block_scan_np(const uint32_t* hist, uint32_t* to
 
 template <int NV, int ITEMS>
 __global__ void __launch_bounds__(kThreadsP) partition_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
-    constexpr int kTileP = kThreadsP * ITEMS;
-    constexpr int kItemsP = ITEMS;
+    constexpr int kTile = kThreadsP * ITEMS;
     const EngineConst& c = *cp;
     __shared__ uint32_t hist[kMaxPart];
     __shared__ uint32_t toff[kMaxPart];
     __shared__ uint32_t gbase[kMaxPart];
-    __shared__ uint32_t s_meta[kTileP];
-    __shared__ uint16_t s_part[kTileP];
-    __shared__ unsigned long long s_val[NV > 0 ? NV : 1][NV > 0 ? kTileP : 1];
+    __shared__ unsigned long long s_key[kTile];
+    __shared__ unsigned long long s_val[NV > 0 ? NV : 1][NV > 0 ? kTile : 1];
+    __shared__ uint16_t s_rel[kTile];
+    __shared__ uint16_t s_part[kTile];
     __shared__ uint32_t wsum[kThreadsP / 64];
     __shared__ uint32_t s_total;
     __shared__ int s_overflow;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const uint32_t seg_mask = (1u << a.seg_log) - 1u;
     unsigned dropped = 0;
-    const int64_t ntiles = (a.n + kTileP - 1) / kTileP;
+    unsigned long long qmax = 0, qmin = ~0ull;
+    const int64_t ntiles = (a.n + kTile - 1) / kTile;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         for (int i = tid; i < a.np; i += kThreadsP) hist[i] = 0;
         if (tid == 0) s_overflow = 0;
         __syncthreads();
-        uint32_t r_meta[kItemsP];
-        uint32_t r_pos[kItemsP];     // (p << 16 | rank) or ~0u when the record does not go to a bucket
-        unsigned long long r_v0[kItemsP], r_v1[kItemsP];
-        const int64_t t0 = tile * kTileP;
+        unsigned long long r_key[ITEMS], r_v0[ITEMS], r_v1[ITEMS];
+        uint32_t r_pos[ITEMS];   // (p << 16 | rank) or ~0u when the record does not go to a bucket
+        uint16_t r_rel[ITEMS];
+        const int64_t t0 = tile * kTile;
 #pragma unroll
-        for (int j = 0; j < kItemsP; ++j) {
+        for (int j = 0; j < ITEMS; ++j) {
             r_pos[j] = ~0u;
             const int64_t i = t0 + (int64_t)j * kThreadsP + tid;
             if (i >= a.n) continue;
             const int64_t key = a.keys[i];
             const int64_t ts = a.ts[i];
+            r_key[j] = (unsigned long long)key;
             r_v0[j] = NV > 0 ? load_raw(a.cols[a.vcol[0]], i, a.vsize[0]) : 0ull;
             r_v1[j] = NV > 1 ? load_raw(a.cols[a.vcol[1]], i, a.vsize[1]) : 0ull;
             const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0), c.max_par);
@@ -393,11 +402,13 @@ __global__ void __launch_bounds__(kThreadsP) partition_kernel(PartArgs a, const 
                 a.spill[si] = (int32_t)i;
                 continue;
             }
-            const int64_t kid = key_slot(a.key_table, a.key_mask, key, a.st);
-            if (kid < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
             if (a.touched[e->slot] == 0) a.touched[e->slot] = 1;
-            const uint32_t p = (uint32_t)(kid >> a.seg_log);
-            r_meta[j] = ((uint32_t)kid & seg_mask) | ((uint32_t)rel << 16);
+            const uint64_t oq = jm::ord_i64(q);
+            qmax = oq > qmax ? oq : qmax;
+            qmin = oq < qmin ? oq : qmin;
+            const uint64_t h = jm::mix64((uint64_t)key);
+            const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
+            r_rel[j] = (uint16_t)rel;
             r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
         }
         __syncthreads();
@@ -406,44 +417,64 @@ __global__ void __launch_bounds__(kThreadsP) partition_kernel(PartArgs a, const 
         for (int p = tid; p < a.np; p += kThreadsP)
             gbase[p] = hist[p] ? atomicAdd(&a.b_cnt[p], hist[p]) : 0u;
 #pragma unroll
-        for (int j = 0; j < kItemsP; ++j) {
+        for (int j = 0; j < ITEMS; ++j) {
             if (r_pos[j] == ~0u) continue;
             const uint32_t p = r_pos[j] >> 16;
-            const uint32_t s = toff[p] + (r_pos[j] & 0xffffu);
-            s_meta[s] = r_meta[j];
-            s_part[s] = (uint16_t)p;
-            if (NV > 0) s_val[0][s] = r_v0[j];
-            if (NV > 1) s_val[NV > 1 ? 1 : 0][s] = r_v1[j];
+            const uint32_t sidx = toff[p] + (r_pos[j] & 0xffffu);
+            s_key[sidx] = r_key[j];
+            s_rel[sidx] = r_rel[j];
+            s_part[sidx] = (uint16_t)p;
+            if (NV > 0) s_val[0][sidx] = r_v0[j];
+            if (NV > 1) s_val[NV > 1 ? 1 : 0][sidx] = r_v1[j];
         }
         __syncthreads();
         const uint32_t total = s_total;
-        for (uint32_t s = tid; s < total; s += kThreadsP) {
-            const uint32_t p = s_part[s];
-            const uint64_t dst = (uint64_t)gbase[p] + (s - toff[p]);
+        for (uint32_t sidx = tid; sidx < total; sidx += kThreadsP) {
+            const uint32_t p = s_part[sidx];
+            const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
             if (dst >= (uint64_t)a.capb) { s_overflow = 1; continue; }
             const uint64_t o = (uint64_t)p * (uint64_t)a.capb + dst;
-            a.b_meta[o] = s_meta[s];
-            if (NV > 0) a.b_val0[o] = s_val[0][s];
-            if (NV > 1) a.b_val1[o] = s_val[NV > 1 ? 1 : 0][s];
+            a.b_key[o] = s_key[sidx];
+            a.b_rel[o] = s_rel[sidx];
+            if (NV > 0) a.b_val0[o] = s_val[0][sidx];
+            if (NV > 1) a.b_val1[o] = s_val[NV > 1 ? 1 : 0][sidx];
         }
         __syncthreads();
         if (tid == 0 && s_overflow) atomicOr(&a.st->key_full, 2);    // bucket overflow: host reruns on the v1 path
     }
-    for (int s = 32; s >= 1; s >>= 1) dropped += __shfl_xor(dropped, s);
-    if (lane == 0 && dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        dropped += __shfl_xor(dropped, sh);
+        const unsigned long long x = __shfl_xor(qmax, sh);
+        qmax = x > qmax ? x : qmax;
+        const unsigned long long y = __shfl_xor(qmin, sh);
+        qmin = y < qmin ? y : qmin;
+    }
+    if (lane == 0) {
+        if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
+        if (qmax) atomicMax(&a.st->max_q, qmax);
+        if (qmin != ~0ull) atomicMin(&a.st->min_q, qmin);
+    }
 }
 
+struct StragEntry {
+    uint64_t o;                        // bucket offset (p * capb + idx)
+    uint32_t g;                        // global kid (key-table slot)
+    uint32_t pad;
+};
+
 struct CombineArgs {
-    const uint32_t* b_meta;
+    const unsigned long long* b_key;
     const unsigned long long* b_val0;
     const unsigned long long* b_val1;
+    const uint16_t* b_rel;
     const uint32_t* b_cnt;
     int64_t capb;
     int32_t seg_log, np, sl;           // sl: LDS slice window
     const int32_t* rel2slot;           // [kRelCap]
+    unsigned long long* key_table;
     unsigned long long* const* slot_base;
     int64_t stride;
-    uint32_t* strag;                   // straggler (p << 32 | idx) list as pairs
+    StragEntry* strag;
     int32_t* strag_n;
     int64_t strag_cap;
     DevStatus* st;
@@ -465,7 +496,7 @@ __device__ __forceinline__ double carried_f64(unsigned long long raw, int kind) 
                                                          : __longlong_as_double((long long)raw);
 }
 
-// LDS layout: count u32 [sl][SEG], then (nacc-1) columns of u64 [sl][SEG]
+// LDS layout: keys u64 [SEG] | count u32 [sl][SEG] | (nacc-1) x u64 [sl][SEG] | 2 ints + flags
 __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const EngineConst& c = *cp;
@@ -473,38 +504,41 @@ __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const
     const int lane = tid & 63;
     const int p = blockIdx.x;
     const int seg = 1 << a.seg_log;
+    const uint32_t smask = (uint32_t)seg - 1u;
     const int sl = a.sl;
-    uint32_t* lcnt = (uint32_t*)smem;
+    unsigned long long* lkey = (unsigned long long*)smem;
+    uint32_t* lcnt = (uint32_t*)(smem + (size_t)seg * 8);
     const size_t cnt_bytes = ((size_t)sl * seg * 4 + 15) & ~(size_t)15;
-    unsigned long long* lacc = (unsigned long long*)(smem + cnt_bytes);
-    int* s_mm = (int*)(smem + cnt_bytes + (size_t)(c.nacc - 1) * sl * seg * 8);
+    unsigned long long* lacc = (unsigned long long*)(smem + (size_t)seg * 8 + cnt_bytes);
+    int* s_mm = (int*)(smem + (size_t)seg * 8 + cnt_bytes + (size_t)(c.nacc - 1) * sl * seg * 8);
     int& s_min = s_mm[0];
     int& s_max = s_mm[1];
-    // identities
+    int& s_new = s_mm[2];
+    unsigned long long* gkeys = a.key_table + ((int64_t)p << a.seg_log);
+    for (int i = tid; i < seg; i += kThreadsA) lkey[i] = gkeys[i];
     for (int i = tid; i < sl * seg; i += kThreadsA) {
         lcnt[i] = 0;
         for (int cc = 1; cc < c.nacc; ++cc) lacc[(size_t)(cc - 1) * sl * seg + i] = ident_of(c.acc_kind[cc]);
     }
+    if (tid == 0) s_new = 0;
     const int64_t cnt = min((int64_t)a.b_cnt[p], a.capb);
-    const uint32_t* meta = a.b_meta + (int64_t)p * a.capb;
-    const unsigned long long* v0 = a.b_val0 ? a.b_val0 + (int64_t)p * a.capb : nullptr;
-    const unsigned long long* v1 = a.b_val1 ? a.b_val1 + (int64_t)p * a.capb : nullptr;
+    const int64_t boff = (int64_t)p * a.capb;
     int lo = 0x7fffffff;   // lowest relative slice held in the window (block-uniform)
     auto flush = [&](int rel) {
         const int w = rel % sl;
-        const int32_t slot = a.rel2slot[rel];
+        const int32_t slot = (rel >= 0 && rel < kRelCap) ? a.rel2slot[rel] : -1;
         unsigned long long* base = slot >= 0 ? a.slot_base[slot] : nullptr;
         for (int i = tid; i < seg; i += kThreadsA) {
             const uint32_t k = lcnt[w * seg + i];
             if (k == 0) continue;
             lcnt[w * seg + i] = 0;
             const int64_t g = ((int64_t)p << a.seg_log) + i;
-            if (!base) continue;   // cannot happen: records were accepted into this slice
-            base[g] += k;
+            if (base) base[g] += k;
             for (int cc = 1; cc < c.nacc; ++cc) {
                 unsigned long long* lp = &lacc[(size_t)(cc - 1) * sl * seg + (size_t)w * seg + i];
                 const unsigned long long x = *lp;
                 *lp = ident_of(c.acc_kind[cc]);
+                if (!base) continue;
                 unsigned long long* gp = &base[(int64_t)cc * a.stride + g];
                 switch (c.acc_kind[cc]) {
                     case ACC_ADD_I64: *gp += x; break;
@@ -519,22 +553,22 @@ __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const
     __syncthreads();
     const int64_t chunk = (int64_t)kThreadsA * kItemsA;
     for (int64_t cb = 0; cb < cnt; cb += chunk) {
-        uint32_t m[kItemsA];
-        unsigned long long x0[kItemsA], x1[kItemsA];
+        unsigned long long kk[kItemsA], x0[kItemsA], x1[kItemsA];
+        int rel[kItemsA];
         int rmin = 0x7fffffff, rmax = -1;
 #pragma unroll
         for (int j = 0; j < kItemsA; ++j) {
             const int64_t i = cb + (int64_t)j * kThreadsA + tid;
-            m[j] = ~0u;
+            rel[j] = -1;
             if (i >= cnt) continue;
-            m[j] = meta[i];
-            x0[j] = v0 ? v0[i] : 0ull;
-            x1[j] = v1 ? v1[i] : 0ull;
-            const int rel = (int)(m[j] >> 16);
-            rmin = min(rmin, rel);
-            rmax = max(rmax, rel);
+            kk[j] = a.b_key[boff + i];
+            x0[j] = a.b_val0 ? a.b_val0[boff + i] : 0ull;
+            x1[j] = a.b_val1 ? a.b_val1[boff + i] : 0ull;
+            rel[j] = a.b_rel[boff + i];
+            rmin = min(rmin, rel[j]);
+            rmax = max(rmax, rel[j]);
         }
-        for (int s = 32; s >= 1; s >>= 1) { rmin = min(rmin, __shfl_xor(rmin, s)); rmax = max(rmax, __shfl_xor(rmax, s)); }
+        for (int sh = 32; sh >= 1; sh >>= 1) { rmin = min(rmin, __shfl_xor(rmin, sh)); rmax = max(rmax, __shfl_xor(rmax, sh)); }
         if (tid == 0) { s_min = 0x7fffffff; s_max = -1; }
         __syncthreads();
         if (lane == 0) { atomicMin(&s_min, rmin); atomicMax(&s_max, rmax); }
@@ -548,21 +582,39 @@ __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const
         }
 #pragma unroll
         for (int j = 0; j < kItemsA; ++j) {
-            if (m[j] == ~0u) continue;
-            const int rel = (int)(m[j] >> 16);
-            const int i = (int)(m[j] & ((1u << a.seg_log) - 1u));
-            if (rel < lo) {             // older than the window: straggler list (applied with atomics)
+            if (rel[j] < 0) continue;
+            // find / insert the key in the LDS segment
+            const unsigned long long key = kk[j];
+            const uint64_t h = jm::mix64(key);
+            uint32_t pos = (uint32_t)h & smask;
+            int32_t local = -1;
+            for (int probe = 0; probe < seg; ++probe) {
+                const unsigned long long cur = lkey[pos];
+                if (cur == key) { local = (int32_t)pos; break; }
+                if (cur == kEmptyKey) {
+                    const unsigned long long old = atomicCAS(&lkey[pos], kEmptyKey, key);
+                    if (old == kEmptyKey) { local = (int32_t)pos; atomicAdd(&s_new, 1); break; }
+                    if (old == key) { local = (int32_t)pos; break; }
+                }
+                pos = (pos + 1) & smask;
+            }
+            if (local < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
+            if (rel[j] < lo) {          // older than the window: applied later with atomics
                 const int32_t si = atomicAdd(a.strag_n, 1);
-                if (si < a.strag_cap) { a.strag[2 * si] = (uint32_t)p; a.strag[2 * si + 1] = (uint32_t)(cb + (int64_t)j * kThreadsA + tid); }
-                else atomicOr(&a.st->key_full, 4);
+                if (si < a.strag_cap) {
+                    a.strag[si].o = (uint64_t)(boff + cb + (int64_t)j * kThreadsA + tid);
+                    a.strag[si].g = (uint32_t)(((int64_t)p << a.seg_log) + local);
+                } else {
+                    atomicOr(&a.st->key_full, 4);
+                }
                 continue;
             }
-            const int w = rel % sl;
-            atomicAdd(&lcnt[w * seg + i], 1u);
+            const int w = rel[j] % sl;
+            atomicAdd(&lcnt[w * seg + local], 1u);
             for (int jj = 0; jj < c.naggs; ++jj) {
                 const AggDesc d = c.agg[jj];
                 if (d.acc == 0) continue;
-                unsigned long long* lp = &lacc[(size_t)(d.acc - 1) * sl * seg + (size_t)w * seg + i];
+                unsigned long long* lp = &lacc[(size_t)(d.acc - 1) * sl * seg + (size_t)w * seg + local];
                 const unsigned long long raw = d.vslot == 0 ? x0[j] : x1[j];
                 switch (d.acc_kind) {
                     case ACC_ADD_I64: atomicAdd(lp, raw); break;
@@ -576,27 +628,27 @@ __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const
         __syncthreads();
     }
     if (lo != 0x7fffffff)
-        for (int r = lo; r < lo + sl && r < kRelCap; ++r) { flush(r); __syncthreads(); }
+        for (int r = lo; r < lo + sl; ++r) { flush(r); __syncthreads(); }
+    if (s_new) {                        // publish newly inserted keys (exclusive owner of this segment)
+        for (int i = tid; i < seg; i += kThreadsA) gkeys[i] = lkey[i];
+        if (tid == 0) atomicAdd(&a.st->n_keys, (unsigned long long)s_new);
+    }
 }
 
 // Stragglers: bucket entries older than their combiner's window, applied with global atomics.
 __global__ void straggler_kernel(CombineArgs a, const EngineConst* __restrict__ cp, int32_t n) {
     const EngineConst& c = *cp;
     for (int32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-        const int64_t p = a.strag[2 * t];
-        const int64_t idx = a.strag[2 * t + 1];
-        const int64_t o = p * a.capb + idx;
-        const uint32_t m = a.b_meta[o];
-        const int32_t slot = a.rel2slot[m >> 16];
+        const StragEntry se = a.strag[t];
+        const int32_t slot = a.rel2slot[a.b_rel[se.o]];
         if (slot < 0) continue;
-        const int64_t g = (p << a.seg_log) + (m & ((1u << a.seg_log) - 1u));
         unsigned long long* base = a.slot_base[slot];
-        atomicAdd(&base[g], 1ull);
+        atomicAdd(&base[se.g], 1ull);
         for (int jj = 0; jj < c.naggs; ++jj) {
             const AggDesc d = c.agg[jj];
             if (d.acc == 0) continue;
-            const unsigned long long raw = d.vslot == 0 ? a.b_val0[o] : a.b_val1[o];
-            unsigned long long* gp = base + (int64_t)d.acc * a.stride + g;
+            const unsigned long long raw = d.vslot == 0 ? a.b_val0[se.o] : a.b_val1[se.o];
+            unsigned long long* gp = base + (int64_t)d.acc * a.stride + se.g;
             switch (d.acc_kind) {
                 case ACC_ADD_I64: atomicAdd(gp, raw); break;
                 case ACC_ADD_F64: atomicAdd((double*)gp, carried_f64(raw, d.kind)); break;
@@ -852,13 +904,14 @@ struct fwa_engine {
     size_t mem_budget = 0;
     // v2 (two-phase) ingest
     bool v2 = false;
-    int32_t seg_log = 12, np = 0, sl = 2, nv = 0, vcol[2] = {0, 0}, vsize[2] = {8, 8};
+    int32_t seg_log = 12, part_bits = 0, np = 0, sl = 2, nv = 0, vcol[2] = {0, 0}, vsize[2] = {8, 8};
     int64_t capb = 0;
-    uint32_t* d_bmeta = nullptr;
+    unsigned long long* d_bkey = nullptr;
+    uint16_t* d_brel = nullptr;
     unsigned long long* d_bval[2] = {nullptr, nullptr};
     uint32_t* d_bcnt = nullptr;
     int32_t* d_rel2slot = nullptr;
-    uint32_t* d_strag = nullptr;
+    StragEntry* d_strag = nullptr;
     int64_t strag_cap = 0;
     int32_t* d_strag_n = nullptr;
     size_t combine_lds = 0;
@@ -1137,7 +1190,7 @@ void fwa_destroy(fwa_engine* e) {
     (void)hipSetDevice(e->cfg.device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
-                    e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bmeta,
+                    e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
@@ -1197,8 +1250,17 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         c.nacc++;
     }
     e->nacc = c.nacc;
-    // v2 eligibility: <= 2 distinct carried value columns, LDS window of >= 2 slices, <= kMaxPart partitions
+    // key-table segmentation (all paths) and v2 eligibility: <= 2 distinct carried value columns,
+    // an LDS window of >= 2 slices next to the SEG-key LDS segment, <= kMaxPart partitions
     {
+        const int64_t kc0 = cfg->key_capacity > 0 ? cfg->key_capacity : (1 << 20);
+        int cap_log = 10;
+        while (((int64_t)1 << cap_log) < 2 * kc0) ++cap_log;
+        int seg_log = 12;
+        if (const char* sv = getenv("FWA_SEG_LOG")) seg_log = atoi(sv);
+        seg_log = std::max(6, std::min(seg_log, cap_log));
+        e->seg_log = seg_log;
+        e->part_bits = cap_log - seg_log;
         int cols[2] = {-1, -1}, sizes[2] = {8, 8}, nv = 0;
         bool ok = true;
         for (int j = 0; j < cfg->num_aggs; ++j) {
@@ -1215,28 +1277,22 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
             } else if (sizes[slot] != (int)type_size(d.kind)) ok = false;
             d.vslot = slot;
         }
-        const int64_t kc0 = cfg->key_capacity > 0 ? cfg->key_capacity : (1 << 20);
-        int64_t cap0 = 1024;
-        while (cap0 < 2 * kc0) cap0 <<= 1;
-        int seg_log = 12;
-        if (const char* sv = getenv("FWA_SEG_LOG")) seg_log = atoi(sv);
+        const int64_t seg = (int64_t)1 << seg_log;
         const int64_t bps = 4 + 8 * (int64_t)(c.nacc - 1);
-        while (seg_log > 8 && 2 * bps * ((int64_t)1 << seg_log) + 64 > 160 * 1024) --seg_log;
-        int64_t np = cap0 >> seg_log;
-        if (np < 1) np = 1;
-        int sl = (int)std::min<int64_t>(8, (160 * 1024 - 64) / (bps * ((int64_t)1 << seg_log)));
+        const int64_t avail = 160 * 1024 - 64 - seg * 8;
+        int sl = (int)std::min<int64_t>(8, avail > 0 ? avail / (bps * seg) : 0);
         if (const char* sv = getenv("FWA_SL")) sl = std::min(sl, atoi(sv));
+        const int64_t np = (int64_t)1 << e->part_bits;
         const char* force = getenv("FWA_INGEST");
-        ok = ok && np <= kMaxPart && sl >= 2 && (1 << seg_log) <= 65536 && !(force && !strcmp(force, "v1"));
+        ok = ok && np <= kMaxPart && sl >= 2 && !(force && !strcmp(force, "v1"));
         e->v2 = ok;
         if (ok) {
-            e->seg_log = seg_log;
             e->np = (int32_t)np;
             e->sl = sl;
             e->nv = nv;
             for (int v = 0; v < 2; ++v) { e->vcol[v] = cols[v] < 0 ? 0 : cols[v]; e->vsize[v] = sizes[v]; }
-            e->combine_lds = (((size_t)sl * ((size_t)1 << seg_log) * 4 + 15) & ~(size_t)15) +
-                             (size_t)(c.nacc - 1) * sl * ((size_t)1 << seg_log) * 8 + 16;
+            e->combine_lds = (size_t)seg * 8 + (((size_t)sl * seg * 4 + 15) & ~(size_t)15) +
+                             (size_t)(c.nacc - 1) * sl * seg * 8 + 16;
         }
     }
     if (hipSetDevice(cfg->device) != hipSuccess) { delete e; return FWA_E_DEVICE; }
@@ -1307,6 +1363,8 @@ static int stage_inputs(fwa_engine* e, const int64_t* keys, const int64_t* ts, c
 static int launch_ingest(fwa_engine* e, IngestArgs& a, bool replay) {
     a.key_table = e->d_keys;
     a.key_mask = (uint64_t)e->capacity - 1;
+    a.seg_log = e->seg_log;
+    a.part_bits = e->part_bits;
     a.dir = e->d_dir;
     a.dir_mask = e->dir_cap - 1;
     a.want = e->d_want;
@@ -1337,10 +1395,12 @@ static int account_ingest(fwa_engine* e) {  // after the stream was synchronised
 static int ensure_v2_buffers(fwa_engine* e, int64_t n) {
     const int64_t capb = (n / e->np) + (n / e->np) / 4 + 16384;
     if (capb > e->capb) {
-        for (void* p : {(void*)e->d_bmeta, (void*)e->d_bval[0], (void*)e->d_bval[1]}) if (p) HIPCHK(e, hipFree(p));
-        e->d_bmeta = nullptr;
+        for (void* p : {(void*)e->d_bkey, (void*)e->d_brel, (void*)e->d_bval[0], (void*)e->d_bval[1]}) if (p) HIPCHK(e, hipFree(p));
+        e->d_bkey = nullptr;
+        e->d_brel = nullptr;
         e->d_bval[0] = e->d_bval[1] = nullptr;
-        HIPCHK(e, hipMalloc(&e->d_bmeta, sizeof(uint32_t) * capb * e->np));
+        HIPCHK(e, hipMalloc(&e->d_bkey, 8 * capb * e->np));
+        HIPCHK(e, hipMalloc(&e->d_brel, 2 * capb * e->np));
         for (int v = 0; v < e->nv; ++v) HIPCHK(e, hipMalloc(&e->d_bval[v], 8 * capb * e->np));
         e->capb = capb;
     }
@@ -1352,7 +1412,7 @@ static int ensure_v2_buffers(fwa_engine* e, int64_t n) {
     const int64_t scap = std::max<int64_t>(n / 8, 1 << 16);
     if (scap > e->strag_cap) {
         if (e->d_strag) HIPCHK(e, hipFree(e->d_strag));
-        HIPCHK(e, hipMalloc(&e->d_strag, sizeof(uint32_t) * 2 * scap));
+        HIPCHK(e, hipMalloc(&e->d_strag, sizeof(StragEntry) * scap));
         e->strag_cap = scap;
     }
     return FWA_OK;
@@ -1382,29 +1442,27 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.key_hash = a.key_hash;
     pa.n = a.n;
     pa.wm = a.wm;
-    pa.key_table = e->d_keys;
-    pa.key_mask = (uint64_t)e->capacity - 1;
     pa.dir = e->d_dir;
     pa.dir_mask = e->dir_cap - 1;
     pa.want = e->d_want;
     pa.spill = e->d_spill;
     pa.touched = e->d_touched;
     pa.q_base = q_base;
-    pa.b_meta = e->d_bmeta;
+    pa.b_key = e->d_bkey;
+    pa.b_rel = e->d_brel;
     pa.b_val0 = e->d_bval[0];
     pa.b_val1 = e->d_bval[1];
     pa.b_cnt = e->d_bcnt;
     pa.capb = e->capb;
-    pa.seg_log = e->seg_log;
+    pa.part_bits = e->part_bits;
     pa.np = e->np;
-    pa.nv = e->nv;
     for (int v = 0; v < 2; ++v) { pa.vcol[v] = e->vcol[v]; pa.vsize[v] = e->vsize[v]; }
     pa.st = e->d_st;
     HIPCHK(e, hipEventRecord(e->ev[4], e->stream));
-    const int64_t tile = (e->nv == 2 ? 8 : 16) * (int64_t)kThreadsP;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, e->nv == 0 ? 512 : 256));
+    const int64_t tile = (e->nv == 2 ? 8 : (e->nv == 1 ? 12 : 16)) * (int64_t)kThreadsP;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256));
     if (e->nv == 0) partition_kernel<0, 16><<<grid, kThreadsP, 0, e->stream>>>(pa, e->d_ec);
-    else if (e->nv == 1) partition_kernel<1, 16><<<grid, kThreadsP, 0, e->stream>>>(pa, e->d_ec);
+    else if (e->nv == 1) partition_kernel<1, 12><<<grid, kThreadsP, 0, e->stream>>>(pa, e->d_ec);
     else partition_kernel<2, 8><<<grid, kThreadsP, 0, e->stream>>>(pa, e->d_ec);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[5], e->stream));
@@ -1418,7 +1476,9 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     if (e->h_st->key_full & 2) return FWA_OK;             // bucket overflow: caller reruns on v1
     CombineArgs ca;
     memset(&ca, 0, sizeof(ca));
-    ca.b_meta = e->d_bmeta;
+    ca.b_key = e->d_bkey;
+    ca.b_rel = e->d_brel;
+    ca.key_table = e->d_keys;
     ca.b_val0 = e->d_bval[0];
     ca.b_val1 = e->d_bval[1];
     ca.b_cnt = e->d_bcnt;
