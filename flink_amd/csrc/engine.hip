@@ -282,11 +282,10 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
 //   the window into HBM with plain coalesced read-modify-write (exclusive ownership: no atomics).
 //   Records older than the window ("stragglers") are applied afterwards by straggler_kernel.
 
-constexpr int kThreadsP = 512;
 constexpr int kMaxPart = 1024;
 constexpr int kRelCap = 4096;                      // slice numbers relative to q_base
 constexpr int kThreadsA = 1024;
-constexpr int kItemsA = 4;
+constexpr int kSub = 16;                           // sub-buckets per partition (spread cursor contention)
 
 struct PartArgs {
     const int64_t* keys;
@@ -317,12 +316,15 @@ __device__ __forceinline__ unsigned long long load_raw(const void* col, int64_t 
     return size == 4 ? (unsigned long long)((const uint32_t*)col)[i] : ((const unsigned long long*)col)[i];
 }
 
-// Block-wide exclusive scan of hist[0..np) into toff (np <= kMaxPart = 2 * kThreadsP).
+// Block-wide exclusive scan of hist[0..np) into toff (np <= kMaxPart, kMaxPart % THREADS == 0).
+template <int THREADS>
 __device__ __forceinline__ void block_scan_np(const uint32_t* hist, uint32_t* toff, uint32_t* wsum, int np, uint32_t* total) {
+    constexpr int PER = kMaxPart / THREADS;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t a0 = (2 * tid < np) ? hist[2 * tid] : 0u;
-    const uint32_t a1 = (2 * tid + 1 < np) ? hist[2 * tid + 1] : 0u;
-    const uint32_t x = a0 + a1;
+    uint32_t v[PER];
+    uint32_t x = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) { v[q] = (PER * tid + q < np) ? hist[PER * tid + q] : 0u; x += v[q]; }
     uint32_t incl = x;
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(incl, d);
@@ -332,17 +334,18 @@ __device__ __forceinline__ void block_scan_np(const uint32_t* hist, uint32_t* to
     __syncthreads();
     if (tid == 0) {
         uint32_t run = 0;
-        for (int w = 0; w < kThreadsP / 64; ++w) { const uint32_t t = wsum[w]; wsum[w] = run; run += t; }
+        for (int w = 0; w < THREADS / 64; ++w) { const uint32_t t = wsum[w]; wsum[w] = run; run += t; }
         *total = run;
     }
     __syncthreads();
-    const uint32_t excl = wsum[wid] + incl - x;
-    if (2 * tid < np) toff[2 * tid] = excl;
-    if (2 * tid + 1 < np) toff[2 * tid + 1] = excl + a0;
+    uint32_t excl = wsum[wid] + incl - x;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) { if (PER * tid + q < np) toff[PER * tid + q] = excl; excl += v[q]; }
 }
 
-template <int NV, int ITEMS>
-__global__ void __launch_bounds__(kThreadsP) partition_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
+template <int NV, int ITEMS, int THREADS>
+__global__ void __launch_bounds__(THREADS) partition_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
+    constexpr int kThreadsP = THREADS;
     constexpr int kTile = kThreadsP * ITEMS;
     const EngineConst& c = *cp;
     __shared__ uint32_t hist[kMaxPart];
@@ -359,6 +362,11 @@ __global__ void __launch_bounds__(kThreadsP) partition_kernel(PartArgs a, const 
     const int lane = tid & 63;
     unsigned dropped = 0;
     unsigned long long qmax = 0, qmin = ~0ull;
+    int64_t m_q = LONG_MIN_J;            // memoised directory entry; q = LONG_MIN needs g == 1 and ts - off == LONG_MIN
+    bool m_init = false;
+    bool m_found = false;
+    int32_t m_slot = -1, m_flags = 0;
+    int64_t m_thr = 0, m_first = 0;
     const int64_t ntiles = (a.n + kTile - 1) / kTile;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         for (int i = tid; i < a.np; i += kThreadsP) hist[i] = 0;
@@ -368,31 +376,55 @@ __global__ void __launch_bounds__(kThreadsP) partition_kernel(PartArgs a, const 
         uint32_t r_pos[ITEMS];   // (p << 16 | rank) or ~0u when the record does not go to a bucket
         uint16_t r_rel[ITEMS];
         const int64_t t0 = tile * kTile;
+        int64_t r_ts[ITEMS];
+        int32_t r_kh[ITEMS];
+        // 1) issue every load of the tile first (no control flow between them)
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const int64_t i = t0 + (int64_t)j * kThreadsP + tid;
+            const bool ok = i < a.n;
+            r_key[j] = ok ? (unsigned long long)a.keys[i] : 0ull;
+            r_ts[j] = ok ? a.ts[i] : 0;
+            r_v0[j] = (NV > 0 && ok) ? load_raw(a.cols[a.vcol[0]], i, a.vsize[0]) : 0ull;
+            r_v1[j] = (NV > 1 && ok) ? load_raw(a.cols[a.vcol[1]], i, a.vsize[1]) : 0ull;
+            r_kh[j] = (a.key_hash && ok) ? a.key_hash[i] : 0;
+        }
+        // 2) compute; the directory entry of the previous record's slice is memoised (ordered
+        //    streams put a tile into one or two slices, so the dependent directory walk is rare)
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             r_pos[j] = ~0u;
             const int64_t i = t0 + (int64_t)j * kThreadsP + tid;
             if (i >= a.n) continue;
-            const int64_t key = a.keys[i];
-            const int64_t ts = a.ts[i];
-            r_key[j] = (unsigned long long)key;
-            r_v0[j] = NV > 0 ? load_raw(a.cols[a.vcol[0]], i, a.vsize[0]) : 0ull;
-            r_v1[j] = NV > 1 ? load_raw(a.cols[a.vcol[1]], i, a.vsize[1]) : 0ull;
-            const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0), c.max_par);
+            const int64_t key = (int64_t)r_key[j];
+            const int64_t ts = r_ts[j];
+            const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, r_kh[j]), c.max_par);
             if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }
             if (c.sem == FWA_SEM_DATASTREAM && ts == LONG_MIN_J) { raise_error(a.st, FWA_E_TS_MIN); continue; }
             const int64_t d = jm::wsub(ts, c.off);
             const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
             const uint64_t uq = jm::udiv64(ud, c.g_div);
             const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
-            const DirEntry* e = dir_find(a.dir, a.dir_mask, q);
+            if (!m_init || q != m_q) {
+                m_init = true;
+                m_q = q;
+                const DirEntry* e = dir_find(a.dir, a.dir_mask, q);
+                m_found = e != nullptr;
+                if (m_found) {
+                    m_slot = e->slot;
+                    m_flags = e->flags;
+                    m_thr = e->thr;
+                    m_first = e->first_maxts;
+                    if (m_slot >= 0 && a.touched[m_slot] == 0) a.touched[m_slot] = 1;
+                }
+            }
             bool to_spill = false;
-            if (e == nullptr) { want_insert(a.want, a.st, q); to_spill = true; }
+            if (!m_found) { want_insert(a.want, a.st, q); to_spill = true; }
             else {
-                const bool accepted = (e->flags & 2) || a.wm < e->thr;
+                const bool accepted = (m_flags & 2) || a.wm < m_thr;
                 if (!accepted) { ++dropped; continue; }
-                if (c.lateness_pos && a.wm >= e->first_maxts) atomicAdd(&a.st->late_fire, 1ull);
-                if (e->slot < 0) { want_insert(a.want, a.st, q); to_spill = true; }
+                if (c.lateness_pos && a.wm >= m_first) atomicAdd(&a.st->late_fire, 1ull);
+                if (m_slot < 0) { want_insert(a.want, a.st, q); to_spill = true; }
             }
             const uint64_t rel = (uint64_t)(q - a.q_base);
             if (!to_spill && rel >= (uint64_t)kRelCap) to_spill = true;     // far slice: slow path
@@ -402,7 +434,6 @@ __global__ void __launch_bounds__(kThreadsP) partition_kernel(PartArgs a, const 
                 a.spill[si] = (int32_t)i;
                 continue;
             }
-            if (a.touched[e->slot] == 0) a.touched[e->slot] = 1;
             const uint64_t oq = jm::ord_i64(q);
             qmax = oq > qmax ? oq : qmax;
             qmin = oq < qmin ? oq : qmin;
@@ -412,10 +443,11 @@ __global__ void __launch_bounds__(kThreadsP) partition_kernel(PartArgs a, const 
             r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
         }
         __syncthreads();
-        block_scan_np(hist, toff, wsum, a.np, &s_total);
+        block_scan_np<THREADS>(hist, toff, wsum, a.np, &s_total);
         __syncthreads();
+        const int sub = blockIdx.x % kSub;
         for (int p = tid; p < a.np; p += kThreadsP)
-            gbase[p] = hist[p] ? atomicAdd(&a.b_cnt[p], hist[p]) : 0u;
+            gbase[p] = hist[p] ? atomicAdd(&a.b_cnt[p * kSub + sub], hist[p]) : 0u;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             if (r_pos[j] == ~0u) continue;
@@ -433,7 +465,7 @@ __global__ void __launch_bounds__(kThreadsP) partition_kernel(PartArgs a, const 
             const uint32_t p = s_part[sidx];
             const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
             if (dst >= (uint64_t)a.capb) { s_overflow = 1; continue; }
-            const uint64_t o = (uint64_t)p * (uint64_t)a.capb + dst;
+            const uint64_t o = ((uint64_t)p * kSub + (blockIdx.x % kSub)) * (uint64_t)a.capb + dst;
             a.b_key[o] = s_key[sidx];
             a.b_rel[o] = s_rel[sidx];
             if (NV > 0) a.b_val0[o] = s_val[0][sidx];
@@ -497,6 +529,7 @@ __device__ __forceinline__ double carried_f64(unsigned long long raw, int kind) 
 }
 
 // LDS layout: keys u64 [SEG] | count u32 [sl][SEG] | (nacc-1) x u64 [sl][SEG] | 2 ints + flags
+template <int kItemsA, bool kPrefetch>
 __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const EngineConst& c = *cp;
@@ -521,8 +554,16 @@ __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const
         for (int cc = 1; cc < c.nacc; ++cc) lacc[(size_t)(cc - 1) * sl * seg + i] = ident_of(c.acc_kind[cc]);
     }
     if (tid == 0) s_new = 0;
-    const int64_t cnt = min((int64_t)a.b_cnt[p], a.capb);
-    const int64_t boff = (int64_t)p * a.capb;
+    // sub-bucket s of partition p: records [0, cnt_s) at ((p*kSub + s) * capb); wave w reads sub
+    // w / (waves per sub); the subs advance in lockstep so each chunk spans ~one event-time range
+    constexpr int kLanesPerSub = kThreadsA / kSub;
+    const int my_sub = tid / kLanesPerSub;
+    const int my_li = tid % kLanesPerSub;
+    const int64_t my_cnt = min((int64_t)a.b_cnt[p * kSub + my_sub], a.capb);
+    const int64_t boff = ((int64_t)p * kSub + my_sub) * a.capb;
+    int64_t maxcnt = 0;
+    for (int s2 = 0; s2 < kSub; ++s2) maxcnt = max(maxcnt, min((int64_t)a.b_cnt[p * kSub + s2], a.capb));
+    const int64_t cnt = maxcnt;
     int lo = 0x7fffffff;   // lowest relative slice held in the window (block-uniform)
     auto flush = [&](int rel) {
         const int w = rel % sl;
@@ -551,23 +592,36 @@ __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const
         }
     };
     __syncthreads();
-    const int64_t chunk = (int64_t)kThreadsA * kItemsA;
+    const int64_t chunk = (int64_t)kLanesPerSub * kItemsA;      // records per sub per chunk
+    // software pipeline: the next chunk's bucket loads are in flight while this chunk is combined
+    unsigned long long nk_[kItemsA], nx0[kItemsA], nx1[kItemsA];
+    int nrel[kItemsA];
+    auto load_chunk = [&](int64_t cb) {
+#pragma unroll
+        for (int j = 0; j < kItemsA; ++j) {
+            const int64_t i = cb + (int64_t)j * kLanesPerSub + my_li;
+            const bool ok = i < my_cnt;
+            nk_[j] = ok ? a.b_key[boff + i] : 0ull;
+            nx0[j] = (ok && a.b_val0) ? a.b_val0[boff + i] : 0ull;
+            nx1[j] = (ok && a.b_val1) ? a.b_val1[boff + i] : 0ull;
+            nrel[j] = ok ? (int)a.b_rel[boff + i] : -1;
+        }
+    };
+    if (kPrefetch) load_chunk(0);
     for (int64_t cb = 0; cb < cnt; cb += chunk) {
+        if (!kPrefetch) load_chunk(cb);
         unsigned long long kk[kItemsA], x0[kItemsA], x1[kItemsA];
         int rel[kItemsA];
         int rmin = 0x7fffffff, rmax = -1;
 #pragma unroll
         for (int j = 0; j < kItemsA; ++j) {
-            const int64_t i = cb + (int64_t)j * kThreadsA + tid;
-            rel[j] = -1;
-            if (i >= cnt) continue;
-            kk[j] = a.b_key[boff + i];
-            x0[j] = a.b_val0 ? a.b_val0[boff + i] : 0ull;
-            x1[j] = a.b_val1 ? a.b_val1[boff + i] : 0ull;
-            rel[j] = a.b_rel[boff + i];
-            rmin = min(rmin, rel[j]);
-            rmax = max(rmax, rel[j]);
+            kk[j] = nk_[j];
+            x0[j] = nx0[j];
+            x1[j] = nx1[j];
+            rel[j] = nrel[j];
+            if (rel[j] >= 0) { rmin = min(rmin, rel[j]); rmax = max(rmax, rel[j]); }
         }
+        if (kPrefetch && cb + chunk < cnt) load_chunk(cb + chunk);
         for (int sh = 32; sh >= 1; sh >>= 1) { rmin = min(rmin, __shfl_xor(rmin, sh)); rmax = max(rmax, __shfl_xor(rmax, sh)); }
         if (tid == 0) { s_min = 0x7fffffff; s_max = -1; }
         __syncthreads();
@@ -602,7 +656,7 @@ __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const
             if (rel[j] < lo) {          // older than the window: applied later with atomics
                 const int32_t si = atomicAdd(a.strag_n, 1);
                 if (si < a.strag_cap) {
-                    a.strag[si].o = (uint64_t)(boff + cb + (int64_t)j * kThreadsA + tid);
+                    a.strag[si].o = (uint64_t)(boff + cb + (int64_t)j * kLanesPerSub + my_li);
                     a.strag[si].g = (uint32_t)(((int64_t)p << a.seg_log) + local);
                 } else {
                     atomicOr(&a.st->key_full, 4);
@@ -1393,19 +1447,20 @@ static int account_ingest(fwa_engine* e) {  // after the stream was synchronised
 }
 
 static int ensure_v2_buffers(fwa_engine* e, int64_t n) {
-    const int64_t capb = (n / e->np) + (n / e->np) / 4 + 16384;
+    const int64_t per = n / ((int64_t)e->np * kSub);                 // expected records per sub-bucket
+    const int64_t capb = per + per / 4 + 2048;
     if (capb > e->capb) {
         for (void* p : {(void*)e->d_bkey, (void*)e->d_brel, (void*)e->d_bval[0], (void*)e->d_bval[1]}) if (p) HIPCHK(e, hipFree(p));
         e->d_bkey = nullptr;
         e->d_brel = nullptr;
         e->d_bval[0] = e->d_bval[1] = nullptr;
-        HIPCHK(e, hipMalloc(&e->d_bkey, 8 * capb * e->np));
-        HIPCHK(e, hipMalloc(&e->d_brel, 2 * capb * e->np));
-        for (int v = 0; v < e->nv; ++v) HIPCHK(e, hipMalloc(&e->d_bval[v], 8 * capb * e->np));
+        HIPCHK(e, hipMalloc(&e->d_bkey, 8 * capb * e->np * kSub));
+        HIPCHK(e, hipMalloc(&e->d_brel, 2 * capb * e->np * kSub));
+        for (int v = 0; v < e->nv; ++v) HIPCHK(e, hipMalloc(&e->d_bval[v], 8 * capb * e->np * kSub));
         e->capb = capb;
     }
     if (!e->d_bcnt) {
-        HIPCHK(e, hipMalloc(&e->d_bcnt, sizeof(uint32_t) * kMaxPart));
+        HIPCHK(e, hipMalloc(&e->d_bcnt, sizeof(uint32_t) * kMaxPart * kSub));
         HIPCHK(e, hipMalloc(&e->d_rel2slot, sizeof(int32_t) * kRelCap));
         HIPCHK(e, hipMalloc(&e->d_strag_n, 16));
     }
@@ -1431,7 +1486,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         if (rel >= 0 && rel < kRelCap) r2s[rel] = kv.second;
     }
     HIPCHK(e, hipMemcpyAsync(e->d_rel2slot, r2s.data(), sizeof(int32_t) * kRelCap, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_bcnt, 0, sizeof(uint32_t) * kMaxPart, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_bcnt, 0, sizeof(uint32_t) * kMaxPart * kSub, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_strag_n, 0, 16, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_want, 0, sizeof(unsigned long long) * kWantCap, e->stream));
     PartArgs pa;
@@ -1459,11 +1514,25 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     for (int v = 0; v < 2; ++v) { pa.vcol[v] = e->vcol[v]; pa.vsize[v] = e->vsize[v]; }
     pa.st = e->d_st;
     HIPCHK(e, hipEventRecord(e->ev[4], e->stream));
-    const int64_t tile = (e->nv == 2 ? 8 : (e->nv == 1 ? 12 : 16)) * (int64_t)kThreadsP;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256));
-    if (e->nv == 0) partition_kernel<0, 16><<<grid, kThreadsP, 0, e->stream>>>(pa, e->d_ec);
-    else if (e->nv == 1) partition_kernel<1, 12><<<grid, kThreadsP, 0, e->stream>>>(pa, e->d_ec);
-    else partition_kernel<2, 8><<<grid, kThreadsP, 0, e->stream>>>(pa, e->d_ec);
+    // tile shape variants (FWA_PVAR): 0 = 512 thr x 12 items, 1 = 1024 x 6, 2 = 512 x 8 (2 WG/CU), 3 = 256 x 12
+    static const int pvar = getenv("FWA_PVAR") ? atoi(getenv("FWA_PVAR")) : 1;
+    int threads = 512, items = 12, per_cu = 1;
+    if (e->nv == 2) items = 8;
+    if (e->nv == 0) items = 16;
+    if (pvar == 1) { threads = 1024; items /= 2; }
+    if (pvar == 2) { items = e->nv == 2 ? 4 : (e->nv == 1 ? 6 : 8); per_cu = 2; }
+    if (pvar == 3) { threads = 256; items = e->nv == 2 ? 12 : (e->nv == 1 ? 16 : 24); per_cu = 1; }
+    const int64_t tile = (int64_t)items * threads;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256 * per_cu));
+#define PLAUNCH(NV, IT, TH) partition_kernel<NV, IT, TH><<<grid, TH, 0, e->stream>>>(pa, e->d_ec)
+    if (e->nv == 0) {
+        if (pvar == 1) PLAUNCH(0, 8, 1024); else if (pvar == 2) PLAUNCH(0, 8, 512); else if (pvar == 3) PLAUNCH(0, 24, 256); else PLAUNCH(0, 16, 512);
+    } else if (e->nv == 1) {
+        if (pvar == 1) PLAUNCH(1, 6, 1024); else if (pvar == 2) PLAUNCH(1, 6, 512); else if (pvar == 3) PLAUNCH(1, 16, 256); else PLAUNCH(1, 12, 512);
+    } else {
+        if (pvar == 1) PLAUNCH(2, 4, 1024); else if (pvar == 2) PLAUNCH(2, 4, 512); else if (pvar == 3) PLAUNCH(2, 12, 256); else PLAUNCH(2, 8, 512);
+    }
+#undef PLAUNCH
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[5], e->stream));
     rc = sync_status(e);
@@ -1494,7 +1563,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.strag_cap = e->strag_cap;
     ca.st = e->d_st;
     HIPCHK(e, hipEventRecord(e->ev[6], e->stream));
-    combine_kernel<<<e->np, kThreadsA, e->combine_lds, e->stream>>>(ca, e->d_ec);
+    static const int avar = getenv("FWA_AVAR") ? atoi(getenv("FWA_AVAR")) : 1;
+    if (avar == 1) combine_kernel<8, false><<<e->np, kThreadsA, e->combine_lds, e->stream>>>(ca, e->d_ec);
+    else if (avar == 2) combine_kernel<2, true><<<e->np, kThreadsA, e->combine_lds, e->stream>>>(ca, e->d_ec);
+    else combine_kernel<4, true><<<e->np, kThreadsA, e->combine_lds, e->stream>>>(ca, e->d_ec);
     HIPCHK(e, hipGetLastError());
     int32_t nstrag = 0;
     HIPCHK(e, hipMemcpyAsync(&e->h_st->pad, e->d_strag_n, 4, hipMemcpyDeviceToHost, e->stream));

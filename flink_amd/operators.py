@@ -1,0 +1,136 @@
+"""Operator facades mirroring the reference's operator interfaces over the GPU engine.
+
+DataStream  WindowOperator.processElement / processWatermark / close
+            flink-streaming-java/.../runtime/operators/windowing/WindowOperator.java:278-481
+Table       SlicingWindowProcessor.open/initializeWatermark/processElement/advanceProgress/
+            prepareCheckpoint/fireWindow/clearWindow/close
+            flink-table-runtime/.../window/slicing/SlicingWindowProcessor.java:33-126
+
+Records are buffered columnar and handed to the engine in batches (the engine's unit of work);
+every buffered record is pushed before a watermark is applied, so the observable results equal
+per-record processing. Emission order among windows with the same end is
+unspecified in the reference too (TimerHeapInternalTimer orders by timestamp only).
+"""
+import numpy as np
+
+from . import _abi as A
+from .assigners import WindowSpec
+
+
+class _Batcher:
+    def __init__(self, ncols, batch):
+        self.ncols, self.batch = ncols, batch
+        self.reset()
+
+    def reset(self):
+        self.keys, self.ts = [], []
+        self.cols = [[] for _ in range(self.ncols)]
+
+    def __len__(self):
+        return len(self.keys)
+
+    def add(self, key, ts, values):
+        self.keys.append(key)
+        self.ts.append(ts)
+        for c, v in zip(self.cols, values):
+            c.append(v)
+
+    def arrays(self, dtypes):
+        return (np.asarray(self.keys, np.int64), np.asarray(self.ts, np.int64),
+                [np.asarray(c, dt) for c, dt in zip(self.cols, dtypes)])
+
+
+def _col_dtypes(aggs, ncols):
+    dts = ["i8"] * ncols
+    for name, col in aggs:
+        if A.AGG_INPUT_DTYPE[name]:
+            dts[col] = A.AGG_INPUT_DTYPE[name]
+    return dts
+
+
+class _Base:
+    def __init__(self, spec: WindowSpec, aggs, batch_size=1 << 20, engine_factory=None, **cfg_kw):
+        if engine_factory is None:
+            from .engine import WindowAggregator
+            engine_factory = WindowAggregator
+        self.aggs = list(aggs)
+        self.ncols = max([c + 1 for n, c in self.aggs if A.AGG_INPUT_DTYPE[n]] + [0])
+        self.dtypes = _col_dtypes(self.aggs, self.ncols)
+        self.cfg = A.make_config(aggs=self.aggs, **spec.config_kwargs(), **cfg_kw)
+        self.engine = engine_factory(self.cfg)
+        self.buf = _Batcher(self.ncols, batch_size)
+        self.num_late_records_dropped = 0
+        self.current_watermark = A.LONG_MIN
+
+    def _push(self):
+        if len(self.buf):
+            k, t, c = self.buf.arrays(self.dtypes)
+            self.num_late_records_dropped += self.engine.push(k, t, c)
+            self.buf.reset()
+
+    def _add(self, key, ts, values):
+        self.buf.add(key, ts, values)
+        if len(self.buf) >= self.buf.batch:
+            self._push()
+
+    def _rows(self, res):
+        names = A.agg_names(self.cfg)
+        out = []
+        for i in range(len(res["key"])):
+            out.append((int(res["key"][i]), int(res["win_start"][i]), int(res["win_end"][i]),
+                        tuple(res["agg%d" % j][i].item() for j in range(len(names)))))
+        return out
+
+    def close(self):
+        self.engine.close()
+
+
+class WindowOperator(_Base):
+    """DataStream window operator (event time, EventTimeTrigger, AggregateFunction/ReduceFunction
+    restricted to the engine's built-in aggregates). Emits (key, window_start, window_end, aggs)
+    with record timestamp window.maxTimestamp() = window_end - 1 (WindowOperator.java:552-557)."""
+
+    def __init__(self, assigner: WindowSpec, aggs, allowed_lateness_ms=0, **kw):
+        super().__init__(assigner, aggs, allowed_lateness_ms=allowed_lateness_ms, **kw)
+
+    def process_element(self, key, value_columns, timestamp):
+        self._add(key, timestamp, value_columns)
+
+    def process_watermark(self, wm):
+        self._push()
+        if wm > self.current_watermark:
+            self.current_watermark = wm
+        return [(r, r[2] - 1) for r in self._rows(self.engine.advance_watermark(wm))]
+
+
+class SlicingWindowProcessor(_Base):
+    """Table window-TVF processor: one GPU processor replaces Slice{Shared,Unshared}WindowAggProcessor.
+    Output rows are key ++ aggs ++ [window_start, window_end] (AbstractWindowAggProcessor.java:230-233)."""
+
+    def open(self):
+        return self
+
+    def initialize_watermark(self, wm):
+        self.current_watermark = wm
+
+    def process_element(self, key, row_values, rowtime):
+        """Returns False: drops are reported per batch through num_late_records_dropped."""
+        self._add(key, rowtime, row_values)
+        return False
+
+    def advance_progress(self, progress):
+        self._push()
+        if progress <= self.current_watermark:
+            return []                                     # SlicingWindowOperator.java:231
+        self.current_watermark = progress
+        return [(k, *aggs, ws, we) for (k, ws, we, aggs) in self._rows(self.engine.advance_watermark(progress))]
+
+    def prepare_checkpoint(self):
+        self._push()
+        self.engine.flush()
+
+    def fire_window(self, window_end):
+        """No-op: the GPU processor fires every due window inside advance_progress."""
+
+    def clear_window(self, window_end):
+        """No-op: slices are released by the engine when their last window fired."""

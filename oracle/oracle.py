@@ -123,6 +123,9 @@ class Oracle:
             raise OracleError(rc, lib().or_last_error(self.h).decode())
         return rows_from_out(out, self.names)
 
+    def flush(self):
+        """The oracle applies every record immediately; nothing is buffered."""
+
     def stats(self):
         st = A.Stats()
         lib().or_get_stats(self.h, C.byref(st))

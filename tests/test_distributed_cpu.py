@@ -1,0 +1,93 @@
+"""world_size-2 gloo test of the key-group-partitioned pipeline (flink_amd.distributed): the keyBy
+all-to-all + MIN-watermark protocol must give exactly the single-operator result. The per-rank
+engine is the oracle here (no GPU in this container); on the GPU box it is the HIP engine."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from flink_amd import _abi as A
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _stream(seed, n):
+    rng = np.random.default_rng(seed)
+    keys = rng.integers(0, 5000, n).astype(np.int64)
+    ts = np.sort(rng.integers(0, 100_000, n)).astype(np.int64) - rng.integers(0, 2000, n)
+    vals = rng.integers(-1000, 1000, n).astype(np.int64)
+    return keys, ts, vals
+
+
+def _worker(rank, world, port, outdir):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from flink_amd.distributed import KeyedWindowPipeline
+    from oracle import oracle as O
+    L = O.lib()
+
+    def router(keys):  # KeyGroupStreamPartitioner.selectChannel restated through the oracle
+        return torch.tensor([L.or_operator_index(128, world, L.or_key_group(int(k), 0, 0, 128)) for k in keys.tolist()],
+                            dtype=torch.int64)
+
+    pipe = KeyedWindowPipeline(rank, world, engine_factory=O.Oracle, router=router,
+                               window_kind="TUMBLE", size_ms=5000, aggs=[("COUNT", 0), ("SUM_I64", 0)])
+    keys, ts, vals = _stream(42 + rank, 6000)   # each rank is one source subtask
+    rows = []
+    nb = 4
+    for b in range(nb + 1):
+        if b < nb:
+            sl = slice(b * 1500, (b + 1) * 1500)
+            pipe.push(torch.from_numpy(keys[sl]), torch.from_numpy(ts[sl]), [torch.from_numpy(vals[sl])])
+            local_wm = int(ts[: (b + 1) * 1500].max()) - 2001
+        else:
+            local_wm = A.LONG_MAX
+        r = pipe.advance_watermark(local_wm)
+        rows.append(np.stack([r["key"], r["win_start"], r["win_end"], r["agg0"], r["agg1"]], axis=1))
+    np.save(os.path.join(outdir, "rank%d.npy" % rank), np.concatenate(rows))
+    pipe.close()
+    dist.destroy_process_group()
+
+
+def test_two_rank_keyby_pipeline_matches_single_operator(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = np.concatenate([np.load(tmp_path / ("rank%d.npy" % r)) for r in range(world)])
+    # reference: one operator over the union of both sources, watermark = min over sources per step
+    from oracle.oracle import Oracle
+    cfg = A.make_config(window_kind="TUMBLE", size_ms=5000, aggs=[("COUNT", 0), ("SUM_I64", 0)])
+    o = Oracle(cfg)
+    streams = [_stream(42 + r, 6000) for r in range(world)]
+    exp = []
+    for b in range(5):
+        if b < 4:
+            for k, t, v in streams:
+                sl = slice(b * 1500, (b + 1) * 1500)
+                o.push(k[sl], t[sl], [v[sl]])
+            wm = min(int(t[: (b + 1) * 1500].max()) - 2001 for k, t, v in streams)
+        else:
+            wm = A.LONG_MAX
+        r = o.advance_watermark(wm)
+        exp.append(np.stack([r["key"], r["win_start"], r["win_end"], r["agg0"], r["agg1"]], axis=1))
+    exp = np.concatenate(exp)
+    key = lambda a: a[np.lexsort(a.T[::-1])]
+    assert got.shape == exp.shape
+    assert np.array_equal(key(got), key(exp))
+    # every key's rows live on exactly the rank owning its key group
+    ranks = [np.load(tmp_path / ("rank%d.npy" % r)) for r in range(world)]
+    assert not (set(ranks[0][:, 0].tolist()) & set(ranks[1][:, 0].tolist()))
