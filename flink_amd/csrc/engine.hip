@@ -286,6 +286,10 @@ constexpr int kMaxPart = 1024;
 constexpr int kRelCap = 4096;                      // slice numbers relative to q_base
 constexpr int kThreadsA = 1024;
 constexpr int kSub = 16;                           // sub-buckets per partition (spread cursor contention)
+// Phase P's per-launch verdict for a relative slice (built by the host from the directory and the
+// watermark): accept into a bucket, count as late-dropped, or hand to the v1 replay (directory miss,
+// slice without slot, late firing within allowed lateness, errors -- everything rare).
+constexpr uint8_t kCodeSlow = 0, kCodeAccept = 1, kCodeDrop = 2;
 
 struct PartArgs {
     const int64_t* keys;
@@ -294,11 +298,8 @@ struct PartArgs {
     const int32_t* key_hash;
     int64_t n;
     int64_t wm;
-    const DirEntry* dir;
-    uint32_t dir_mask;
-    unsigned long long* want;
+    const uint8_t* relcode;            // [kRelCap] per relative slice: kCodeAccept / kCodeDrop / kCodeSlow
     int32_t* spill;
-    int32_t* touched;
     int64_t q_base;
     unsigned long long* b_key;         // [np][capb]
     unsigned long long* b_val0;
@@ -309,6 +310,7 @@ struct PartArgs {
     int32_t part_bits, np;
     int32_t vcol[2];
     int32_t vsize[2];                  // 4 or 8 bytes
+    int32_t abl;                       // ablation bits (timing experiments only; 0 in production)
     DevStatus* st;
 };
 
@@ -343,8 +345,8 @@ __device__ __forceinline__ void block_scan_np(const uint32_t* hist, uint32_t* to
     for (int q = 0; q < PER; ++q) { if (PER * tid + q < np) toff[PER * tid + q] = excl; excl += v[q]; }
 }
 
-template <int NV, int ITEMS, int THREADS>
-__global__ void __launch_bounds__(THREADS) partition_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
+template <int NV, int ITEMS, int THREADS, int MINW = 1>
+__global__ void __launch_bounds__(THREADS, MINW) partition_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
     constexpr int kThreadsP = THREADS;
     constexpr int kTile = kThreadsP * ITEMS;
     const EngineConst& c = *cp;
@@ -358,15 +360,14 @@ __global__ void __launch_bounds__(THREADS) partition_kernel(PartArgs a, const En
     __shared__ uint32_t wsum[kThreadsP / 64];
     __shared__ uint32_t s_total;
     __shared__ int s_overflow;
+    __shared__ uint8_t s_code[kRelCap];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     unsigned dropped = 0;
-    unsigned long long qmax = 0, qmin = ~0ull;
-    int64_t m_q = LONG_MIN_J;            // memoised directory entry; q = LONG_MIN needs g == 1 and ts - off == LONG_MIN
-    bool m_init = false;
-    bool m_found = false;
-    int32_t m_slot = -1, m_flags = 0;
-    int64_t m_thr = 0, m_first = 0;
+    uint32_t relmax = 0, relmin = ~0u;   // accepted records' relative slice range (lookahead, touched)
+    const bool kg_all = c.kg_lo == 0 && c.kg_hi == c.max_par - 1;   // whole range owned: no check needed
+    const bool ds = c.sem == FWA_SEM_DATASTREAM;
+    for (int r = tid; r < kRelCap / 4; r += kThreadsP) ((uint32_t*)s_code)[r] = ((const uint32_t*)a.relcode)[r];
     const int64_t ntiles = (a.n + kTile - 1) / kTile;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         for (int i = tid; i < a.np; i += kThreadsP) hist[i] = 0;
@@ -389,65 +390,51 @@ __global__ void __launch_bounds__(THREADS) partition_kernel(PartArgs a, const En
             r_v1[j] = (NV > 1 && ok) ? load_raw(a.cols[a.vcol[1]], i, a.vsize[1]) : 0ull;
             r_kh[j] = (a.key_hash && ok) ? a.key_hash[i] : 0;
         }
-        // 2) compute; the directory entry of the previous record's slice is memoised (ordered
-        //    streams put a tile into one or two slices, so the dependent directory walk is rare)
+        // 2) compute: straight-line fast path; every rare case goes to the spill list (v1 replay)
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-            r_pos[j] = ~0u;
             const int64_t i = t0 + (int64_t)j * kThreadsP + tid;
-            if (i >= a.n) continue;
             const int64_t key = (int64_t)r_key[j];
             const int64_t ts = r_ts[j];
-            const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, r_kh[j]), c.max_par);
-            if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }
-            if (c.sem == FWA_SEM_DATASTREAM && ts == LONG_MIN_J) { raise_error(a.st, FWA_E_TS_MIN); continue; }
             const int64_t d = jm::wsub(ts, c.off);
             const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
             const uint64_t uq = jm::udiv64(ud, c.g_div);
             const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
-            if (!m_init || q != m_q) {
-                m_init = true;
-                m_q = q;
-                const DirEntry* e = dir_find(a.dir, a.dir_mask, q);
-                m_found = e != nullptr;
-                if (m_found) {
-                    m_slot = e->slot;
-                    m_flags = e->flags;
-                    m_thr = e->thr;
-                    m_first = e->first_maxts;
-                    if (m_slot >= 0 && a.touched[m_slot] == 0) a.touched[m_slot] = 1;
-                }
-            }
-            bool to_spill = false;
-            if (!m_found) { want_insert(a.want, a.st, q); to_spill = true; }
-            else {
-                const bool accepted = (m_flags & 2) || a.wm < m_thr;
-                if (!accepted) { ++dropped; continue; }
-                if (c.lateness_pos && a.wm >= m_first) atomicAdd(&a.st->late_fire, 1ull);
-                if (m_slot < 0) { want_insert(a.want, a.st, q); to_spill = true; }
-            }
             const uint64_t rel = (uint64_t)(q - a.q_base);
-            if (!to_spill && rel >= (uint64_t)kRelCap) to_spill = true;     // far slice: slow path
-            if (!to_spill && (uint64_t)key == kEmptyKey) to_spill = true;   // side-slot key: slow path
-            if (to_spill) {
-                const int32_t si = atomicAdd(&a.st->spill_n, 1);
-                a.spill[si] = (int32_t)i;
-                continue;
+            uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
+            if (!kg_all) {
+                const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, r_kh[j]), c.max_par);
+                if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;     // the replay raises FWA_E_KEYGROUP
             }
-            const uint64_t oq = jm::ord_i64(q);
-            qmax = oq > qmax ? oq : qmax;
-            qmin = oq < qmin ? oq : qmin;
-            const uint64_t h = jm::mix64((uint64_t)key);
-            const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
-            r_rel[j] = (uint16_t)rel;
-            r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
+            if (ds && ts == LONG_MIN_J) code = kCodeSlow;                // the replay raises FWA_E_TS_MIN
+            if ((uint64_t)key == kEmptyKey) code = kCodeSlow;            // side-slot key
+            if (i >= a.n) code = 0xff;
+            dropped += code == kCodeDrop;
+            const bool slow = code == kCodeSlow;
+            const unsigned long long mk = __ballot(slow);
+            if (mk) {                                                    // wave-aggregated spill append
+                const int leader = __ffsll((long long)mk) - 1;
+                int32_t sb = 0;
+                if (lane == leader) sb = atomicAdd(&a.st->spill_n, __popcll(mk));
+                sb = __shfl(sb, leader);
+                if (slow) a.spill[sb + __popcll(mk & ((1ull << lane) - 1))] = (int32_t)i;
+            }
+            r_pos[j] = ~0u;
+            if (code == kCodeAccept) {
+                relmax = max(relmax, (uint32_t)rel);
+                relmin = min(relmin, (uint32_t)rel);
+                const uint64_t h = jm::mix64((uint64_t)key);
+                const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
+                r_rel[j] = (uint16_t)rel;
+                r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
+            }
         }
         __syncthreads();
         block_scan_np<THREADS>(hist, toff, wsum, a.np, &s_total);
         __syncthreads();
         const int sub = blockIdx.x % kSub;
         for (int p = tid; p < a.np; p += kThreadsP)
-            gbase[p] = hist[p] ? atomicAdd(&a.b_cnt[p * kSub + sub], hist[p]) : 0u;
+            gbase[p] = (a.abl & 1) ? (uint32_t)((tile * 7) & 1023) : (hist[p] ? atomicAdd(&a.b_cnt[p * kSub + sub], hist[p]) : 0u);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             if (r_pos[j] == ~0u) continue;
@@ -465,6 +452,7 @@ __global__ void __launch_bounds__(THREADS) partition_kernel(PartArgs a, const En
             const uint32_t p = s_part[sidx];
             const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
             if (dst >= (uint64_t)a.capb) { s_overflow = 1; continue; }
+            if (a.abl & 2) { if (s_key[sidx] == 0x1234567ull) a.b_key[0] = 1; continue; }
             const uint64_t o = ((uint64_t)p * kSub + (blockIdx.x % kSub)) * (uint64_t)a.capb + dst;
             a.b_key[o] = s_key[sidx];
             a.b_rel[o] = s_rel[sidx];
@@ -476,15 +464,15 @@ __global__ void __launch_bounds__(THREADS) partition_kernel(PartArgs a, const En
     }
     for (int sh = 32; sh >= 1; sh >>= 1) {
         dropped += __shfl_xor(dropped, sh);
-        const unsigned long long x = __shfl_xor(qmax, sh);
-        qmax = x > qmax ? x : qmax;
-        const unsigned long long y = __shfl_xor(qmin, sh);
-        qmin = y < qmin ? y : qmin;
+        relmax = max(relmax, (uint32_t)__shfl_xor((int)relmax, sh));
+        relmin = min(relmin, (uint32_t)__shfl_xor((int)relmin, sh));
     }
     if (lane == 0) {
         if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
-        if (qmax) atomicMax(&a.st->max_q, qmax);
-        if (qmin != ~0ull) atomicMin(&a.st->min_q, qmin);
+        if (relmin != ~0u) {
+            atomicMax(&a.st->max_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmax));
+            atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
+        }
     }
 }
 
@@ -509,6 +497,7 @@ struct CombineArgs {
     StragEntry* strag;
     int32_t* strag_n;
     int64_t strag_cap;
+    int32_t abl;                       // ablation bits (timing experiments only)
     DevStatus* st;
 };
 
@@ -634,15 +623,23 @@ __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const
             ++lo;
             __syncthreads();
         }
+        // first probes of all records issued back to back (independent LDS reads in flight)
+        uint32_t pos0[kItemsA];
+        unsigned long long cur0[kItemsA];
+#pragma unroll
+        for (int j = 0; j < kItemsA; ++j) {
+            pos0[j] = (uint32_t)jm::mix64(kk[j]) & smask;
+            cur0[j] = lkey[pos0[j]];
+        }
 #pragma unroll
         for (int j = 0; j < kItemsA; ++j) {
             if (rel[j] < 0) continue;
             // find / insert the key in the LDS segment
             const unsigned long long key = kk[j];
-            const uint64_t h = jm::mix64(key);
-            uint32_t pos = (uint32_t)h & smask;
-            int32_t local = -1;
-            for (int probe = 0; probe < seg; ++probe) {
+            uint32_t pos = pos0[j];
+            int32_t local = (cur0[j] == key) ? (int32_t)pos : -1;
+            if (a.abl & 1) local = (int32_t)pos;   // ablation: no LDS probe
+            for (int probe = 0; probe < seg && local < 0; ++probe) {
                 const unsigned long long cur = lkey[pos];
                 if (cur == key) { local = (int32_t)pos; break; }
                 if (cur == kEmptyKey) {
@@ -664,6 +661,7 @@ __global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const
                 continue;
             }
             const int w = rel[j] % sl;
+            if (a.abl & 2) { if (key == 0x1234567ull) lcnt[0] = 1; continue; }   // ablation: no LDS atomics
             atomicAdd(&lcnt[w * seg + local], 1u);
             for (int jj = 0; jj < c.naggs; ++jj) {
                 const AggDesc d = c.agg[jj];
@@ -1333,7 +1331,7 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         }
         const int64_t seg = (int64_t)1 << seg_log;
         const int64_t bps = 4 + 8 * (int64_t)(c.nacc - 1);
-        const int64_t avail = 160 * 1024 - 64 - seg * 8;
+        const int64_t avail = 160 * 1024 - 256 - seg * 8;
         int sl = (int)std::min<int64_t>(8, avail > 0 ? avail / (bps * seg) : 0);
         if (const char* sv = getenv("FWA_SL")) sl = std::min(sl, atoi(sv));
         const int64_t np = (int64_t)1 << e->part_bits;
@@ -1461,7 +1459,7 @@ static int ensure_v2_buffers(fwa_engine* e, int64_t n) {
     }
     if (!e->d_bcnt) {
         HIPCHK(e, hipMalloc(&e->d_bcnt, sizeof(uint32_t) * kMaxPart * kSub));
-        HIPCHK(e, hipMalloc(&e->d_rel2slot, sizeof(int32_t) * kRelCap));
+        HIPCHK(e, hipMalloc(&e->d_rel2slot, (sizeof(int32_t) + 1) * kRelCap));   // rel2slot | relcode
         HIPCHK(e, hipMalloc(&e->d_strag_n, 16));
     }
     const int64_t scap = std::max<int64_t>(n / 8, 1 << 16);
@@ -1480,12 +1478,24 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     int rc = ensure_v2_buffers(e, a.n);
     if (rc) return rc;
     const int64_t q_base = e->live.empty() ? 0 : e->live.begin()->first;
-    std::vector<int32_t> r2s(kRelCap, -1);
+    // rel2slot (combine) and relcode (partition): the directory restricted to [q_base, q_base + kRelCap)
+    // with each slice's acceptance under the current watermark (WindowOperator.isWindowLate /
+    // SlicingWindowOperator lateness, as in ingest_kernel)
+    std::vector<int32_t> r2s(kRelCap + kRelCap / 4, -1);
+    uint8_t* code = (uint8_t*)(r2s.data() + kRelCap);
+    memset(code, kCodeSlow, kRelCap);
     for (auto& kv : e->live) {
         const int64_t rel = kv.first - q_base;
-        if (rel >= 0 && rel < kRelCap) r2s[rel] = kv.second;
+        if (rel < 0 || rel >= kRelCap) continue;
+        r2s[rel] = kv.second;
+        int64_t thr;
+        bool always;
+        accept_threshold(e, kv.first, &thr, &always);
+        if (!always && !(a.wm < thr)) code[rel] = kCodeDrop;
+        else if (e->lateness > 0 && a.wm >= jm::wsub(first_window_end(e, kv.first), 1)) code[rel] = kCodeSlow;
+        else code[rel] = kCodeAccept;
     }
-    HIPCHK(e, hipMemcpyAsync(e->d_rel2slot, r2s.data(), sizeof(int32_t) * kRelCap, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->d_rel2slot, r2s.data(), (sizeof(int32_t) + 1) * kRelCap, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_bcnt, 0, sizeof(uint32_t) * kMaxPart * kSub, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_strag_n, 0, 16, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_want, 0, sizeof(unsigned long long) * kWantCap, e->stream));
@@ -1497,11 +1507,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.key_hash = a.key_hash;
     pa.n = a.n;
     pa.wm = a.wm;
-    pa.dir = e->d_dir;
-    pa.dir_mask = e->dir_cap - 1;
-    pa.want = e->d_want;
+    pa.relcode = (const uint8_t*)(e->d_rel2slot + kRelCap);
     pa.spill = e->d_spill;
-    pa.touched = e->d_touched;
     pa.q_base = q_base;
     pa.b_key = e->d_bkey;
     pa.b_rel = e->d_brel;
@@ -1513,6 +1520,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.np = e->np;
     for (int v = 0; v < 2; ++v) { pa.vcol[v] = e->vcol[v]; pa.vsize[v] = e->vsize[v]; }
     pa.st = e->d_st;
+    static const int pabl = getenv("FWA_PABL") ? atoi(getenv("FWA_PABL")) : 0;
+    pa.abl = pabl;
     HIPCHK(e, hipEventRecord(e->ev[4], e->stream));
     // tile shape variants (FWA_PVAR): 0 = 512 thr x 12 items, 1 = 1024 x 6, 2 = 512 x 8 (2 WG/CU), 3 = 256 x 12
     static const int pvar = getenv("FWA_PVAR") ? atoi(getenv("FWA_PVAR")) : 1;
@@ -1521,16 +1530,21 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     if (e->nv == 0) items = 16;
     if (pvar == 1) { threads = 1024; items /= 2; }
     if (pvar == 2) { items = e->nv == 2 ? 4 : (e->nv == 1 ? 6 : 8); per_cu = 2; }
+    if (pvar == 4) { threads = 1024; items = e->nv == 2 ? 2 : (e->nv == 1 ? 3 : 4); per_cu = 2; }
     if (pvar == 3) { threads = 256; items = e->nv == 2 ? 12 : (e->nv == 1 ? 16 : 24); per_cu = 1; }
     const int64_t tile = (int64_t)items * threads;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256 * per_cu));
-#define PLAUNCH(NV, IT, TH) partition_kernel<NV, IT, TH><<<grid, TH, 0, e->stream>>>(pa, e->d_ec)
+#define PLAUNCH(NV, IT, TH, MW) partition_kernel<NV, IT, TH, MW><<<grid, TH, 0, e->stream>>>(pa, e->d_ec)
+    // pvar 2 / 4: two workgroups per CU (LDS <= 80 KB, VGPR <= 128) so one loads while the other computes
     if (e->nv == 0) {
-        if (pvar == 1) PLAUNCH(0, 8, 1024); else if (pvar == 2) PLAUNCH(0, 8, 512); else if (pvar == 3) PLAUNCH(0, 24, 256); else PLAUNCH(0, 16, 512);
+        if (pvar == 1) PLAUNCH(0, 8, 1024, 1); else if (pvar == 2) PLAUNCH(0, 8, 512, 4); else if (pvar == 3) PLAUNCH(0, 24, 256, 1);
+        else if (pvar == 4) PLAUNCH(0, 4, 1024, 2); else PLAUNCH(0, 16, 512, 1);
     } else if (e->nv == 1) {
-        if (pvar == 1) PLAUNCH(1, 6, 1024); else if (pvar == 2) PLAUNCH(1, 6, 512); else if (pvar == 3) PLAUNCH(1, 16, 256); else PLAUNCH(1, 12, 512);
+        if (pvar == 1) PLAUNCH(1, 6, 1024, 1); else if (pvar == 2) PLAUNCH(1, 6, 512, 4); else if (pvar == 3) PLAUNCH(1, 16, 256, 1);
+        else if (pvar == 4) PLAUNCH(1, 3, 1024, 2); else PLAUNCH(1, 12, 512, 1);
     } else {
-        if (pvar == 1) PLAUNCH(2, 4, 1024); else if (pvar == 2) PLAUNCH(2, 4, 512); else if (pvar == 3) PLAUNCH(2, 12, 256); else PLAUNCH(2, 8, 512);
+        if (pvar == 1) PLAUNCH(2, 4, 1024, 1); else if (pvar == 2) PLAUNCH(2, 4, 512, 4); else if (pvar == 3) PLAUNCH(2, 12, 256, 1);
+        else if (pvar == 4) PLAUNCH(2, 2, 1024, 2); else PLAUNCH(2, 8, 512, 1);
     }
 #undef PLAUNCH
     HIPCHK(e, hipGetLastError());
@@ -1543,6 +1557,14 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     e->ingest_ms += ms;
     if (e->h_st->error) { *ran = true; return FWA_OK; }   // reported by the caller's status loop
     if (e->h_st->key_full & 2) return FWA_OK;             // bucket overflow: caller reruns on v1
+    if (e->h_st->min_q != ~0ull) {                        // slices that received records (over-marking is harmless)
+        bool changed = false;
+        const int64_t q0 = jm::unord_i64(e->h_st->min_q), q1 = jm::unord_i64(e->h_st->max_q);
+        for (auto it = e->live.lower_bound(q0); it != e->live.end() && it->first <= q1; ++it)
+            if (!e->touched[it->second]) { e->touched[it->second] = 1; changed = true; }
+        if (changed)
+            HIPCHK(e, hipMemcpyAsync(e->d_touched, e->touched.data(), sizeof(int32_t) * e->touched.size(), hipMemcpyHostToDevice, e->stream));
+    }
     CombineArgs ca;
     memset(&ca, 0, sizeof(ca));
     ca.b_key = e->d_bkey;
@@ -1562,6 +1584,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.strag_n = e->d_strag_n;
     ca.strag_cap = e->strag_cap;
     ca.st = e->d_st;
+    static const int aabl = getenv("FWA_AABL") ? atoi(getenv("FWA_AABL")) : 0;
+    ca.abl = aabl;
     HIPCHK(e, hipEventRecord(e->ev[6], e->stream));
     static const int avar = getenv("FWA_AVAR") ? atoi(getenv("FWA_AVAR")) : 1;
     if (avar == 1) combine_kernel<8, false><<<e->np, kThreadsA, e->combine_lds, e->stream>>>(ca, e->d_ec);
