@@ -83,7 +83,7 @@ def main():
     wms[-1] = A.LONG_MAX                           # final watermark flushes every window
 
     cfg_kw = dict(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=args.window_ms,
-                  aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=args.keys,
+                  aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=int(args.keys * float(os.environ.get("FWA_KCAP", "1"))),
                   output_on_device=1, device=local_rank)
     if world > 1:
         from flink_amd.distributed import KeyedWindowPipeline

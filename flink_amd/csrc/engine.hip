@@ -40,6 +40,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr uint64_t kEmptyKey = 0x8000000000000000ull;  // key-table sentinel (INT64_MIN); that key uses a side slot
+constexpr int kBucket = 8;                              // key-table probe bucket: 8 slots = 64 B
 constexpr int32_t kWantCap = 1 << 14;                   // distinct missing slices reported per launch
 
 // ------------------------------------------------------------------------------------------------
@@ -113,7 +114,11 @@ struct IngestArgs {
 __device__ __forceinline__ void raise_error(DevStatus* st, int code) { atomicCAS(&st->error, 0, code); }
 
 // Key table: SEGMENTED open addressing. h = mix64(key); segment p = top part_bits of h (the v2
-// combiner's partition), probe linearly inside the segment from h & (SEG-1); CAS insert.
+// combiner's partition), probe linearly inside the segment from the kBucket-aligned home
+// (h & (SEG-1)) & ~(kBucket-1); CAS insert. The aligned home lets the combiner read a key's whole
+// home bucket (64 B) with one LDS round instead of walking the probe sequence slot by slot: linear
+// probing's displacement tail (~20 slots at load 0.5 over a 4096-slot segment) made a wave's probe
+// loop run for the worst of its 256 records (r01 clock64 profile: 75 % of combine time).
 // A stale EMPTY read only sends us to the CAS, which returns the winner's key: no hand-off needed.
 __device__ __forceinline__ uint64_t seg_base(uint64_t h, int seg_log, int part_bits) {
     return part_bits ? ((h >> (64 - part_bits)) << seg_log) : 0ull;
@@ -128,8 +133,9 @@ __device__ __forceinline__ int64_t key_slot(unsigned long long* table, uint64_t 
     const uint64_t h = jm::mix64((uint64_t)key);
     const uint64_t base = seg_base(h, seg_log, part_bits);
     const uint64_t smask = ((uint64_t)1 << seg_log) - 1;
+    const uint64_t home = h & smask & ~(uint64_t)(kBucket - 1);   // probing starts at a bucket boundary
     for (uint64_t probe = 0; probe <= smask; ++probe) {
-        const uint64_t i = base | ((h + probe) & smask);
+        const uint64_t i = base | ((home + probe) & smask);
         const unsigned long long cur = table[i];
         if (cur == (unsigned long long)key) return (int64_t)i;
         if (cur == kEmptyKey) {
@@ -284,7 +290,6 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
 
 constexpr int kMaxPart = 1024;
 constexpr int kRelCap = 4096;                      // slice numbers relative to q_base
-constexpr int kThreadsA = 1024;
 constexpr int kSub = 16;                           // sub-buckets per partition (spread cursor contention)
 // Phase P's per-launch verdict for a relative slice (built by the host from the directory and the
 // watermark): accept into a bucket, count as late-dropped, or hand to the v1 replay (directory miss,
@@ -499,6 +504,7 @@ struct CombineArgs {
     int64_t strag_cap;
     int32_t abl;                       // ablation bits (timing experiments only)
     DevStatus* st;
+    long long* prof;                   // optional per-block phase cycle counters (FWA_APROF)
 };
 
 __device__ __forceinline__ unsigned long long ident_of(int acc_kind) { return acc_kind == ACC_MIN_ORD ? ~0ull : 0ull; }
@@ -517,174 +523,258 @@ __device__ __forceinline__ double carried_f64(unsigned long long raw, int kind) 
                                                          : __longlong_as_double((long long)raw);
 }
 
-// LDS layout: keys u64 [SEG] | count u32 [sl][SEG] | (nacc-1) x u64 [sl][SEG] | 2 ints + flags
-template <int kItemsA, bool kPrefetch>
-__global__ void __launch_bounds__(kThreadsA) combine_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
+// ------------------------------------------------------------------------------------------------
+// combine3: the Phase A combiner, restructured for latency tolerance (DESIGN.md §4, r01 clock64
+// profile: the v2 combiner spent 43 % of its time in serialised flat RMWs / scalar-load waits).
+//  * wave w streams sub-bucket w (64 lanes, coalesced); the next chunk's loads are issued before the
+//    current chunk is combined (register double buffer);
+//  * ONE barrier per chunk: each wave publishes its chunk's slice range into a double-buffered LDS
+//    slot, the block range is read back after the barrier (no LDS atomics, no second barrier);
+//  * aggregate descriptors are hoisted into registers once; the inner loop has no scalar loads;
+//  * the slice flush reads LDS into registers, then issues every HBM load of the flush before any
+//    add/store (one exposed latency per flush instead of one per slot and column), through
+//    address-space-1 pointers (global_load/store, not flat).
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+typedef const __attribute__((address_space(1))) unsigned long long* gc_u64_ptr;
+
+// LAYOUT: the accumulator columns, fixed at compile time for the common shapes so the per-record
+// path has no descriptor switch (a runtime switch over 8 columns cost ~1000 scalar instructions per
+// record from SGPR spills): 1 = COUNT + one ADD_I64 fed by value slot 0 (SUM/AVG over BIGINT);
+// 2 = COUNT only; 0 = generic (descriptor table in LDS, one column per loop trip).
+template <int IT, int SL, int NV, int TH, int LAYOUT>
+__global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int kWaves = TH / 64;
+    constexpr int LPS = TH / kSub;     // lanes per sub-bucket (64: one wave per sub; 32: two subs per wave)
+    static_assert(LPS == 32 || LPS == 64, "sub-bucket lane mapping");
     const EngineConst& c = *cp;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int sub = tid / LPS, li = tid % LPS;
     const int p = blockIdx.x;
     const int seg = 1 << a.seg_log;
     const uint32_t smask = (uint32_t)seg - 1u;
-    const int sl = a.sl;
+    const int nacc = LAYOUT == 1 ? 2 : (LAYOUT == 2 ? 1 : c.nacc);
+    __shared__ int s_desc[FWA_MAX_AGGS + 1];   // generic layout: per column kind | vslot << 8 | input kind << 16
+    if (LAYOUT == 0 && tid == 0) {
+        for (int j = 0; j < c.naggs; ++j)
+            if (c.agg[j].acc > 0) s_desc[c.agg[j].acc] = c.agg[j].acc_kind | (c.agg[j].vslot << 8) | (c.agg[j].kind << 16);
+    }
     unsigned long long* lkey = (unsigned long long*)smem;
     uint32_t* lcnt = (uint32_t*)(smem + (size_t)seg * 8);
-    const size_t cnt_bytes = ((size_t)sl * seg * 4 + 15) & ~(size_t)15;
-    unsigned long long* lacc = (unsigned long long*)(smem + (size_t)seg * 8 + cnt_bytes);
-    int* s_mm = (int*)(smem + (size_t)seg * 8 + cnt_bytes + (size_t)(c.nacc - 1) * sl * seg * 8);
-    int& s_min = s_mm[0];
-    int& s_max = s_mm[1];
-    int& s_new = s_mm[2];
+    unsigned long long* lacc = (unsigned long long*)(smem + (size_t)seg * 8 + (size_t)SL * seg * 4);
+    int* s_mm = (int*)(smem + (size_t)seg * 8 + (size_t)SL * seg * 4 + (size_t)(nacc - 1) * SL * seg * 8);
+    // s_mm: [2][kWaves] mins, [2][kWaves] maxs, s_new
+    int* s_min = s_mm;
+    int* s_max = s_mm + 2 * kWaves;
+    int* s_new = s_mm + 4 * kWaves;
+    long long pt = clock64();
+    long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
     unsigned long long* gkeys = a.key_table + ((int64_t)p << a.seg_log);
-    for (int i = tid; i < seg; i += kThreadsA) lkey[i] = gkeys[i];
-    for (int i = tid; i < sl * seg; i += kThreadsA) {
+    for (int i = tid; i < seg; i += TH) lkey[i] = gkeys[i];
+    for (int i = tid; i < SL * seg; i += TH) {
         lcnt[i] = 0;
-        for (int cc = 1; cc < c.nacc; ++cc) lacc[(size_t)(cc - 1) * sl * seg + i] = ident_of(c.acc_kind[cc]);
     }
-    if (tid == 0) s_new = 0;
-    // sub-bucket s of partition p: records [0, cnt_s) at ((p*kSub + s) * capb); wave w reads sub
-    // w / (waves per sub); the subs advance in lockstep so each chunk spans ~one event-time range
-    constexpr int kLanesPerSub = kThreadsA / kSub;
-    const int my_sub = tid / kLanesPerSub;
-    const int my_li = tid % kLanesPerSub;
-    const int64_t my_cnt = min((int64_t)a.b_cnt[p * kSub + my_sub], a.capb);
-    const int64_t boff = ((int64_t)p * kSub + my_sub) * a.capb;
-    int64_t maxcnt = 0;
-    for (int s2 = 0; s2 < kSub; ++s2) maxcnt = max(maxcnt, min((int64_t)a.b_cnt[p * kSub + s2], a.capb));
-    const int64_t cnt = maxcnt;
-    int lo = 0x7fffffff;   // lowest relative slice held in the window (block-uniform)
-    auto flush = [&](int rel) {
-        const int w = rel % sl;
+    if (tid == 0) *s_new = 0;
+    __syncthreads();
+    for (int cc = 1; cc < nacc; ++cc) {
+        const unsigned long long id = LAYOUT == 1 ? 0ull : ident_of(s_desc[cc] & 0xff);
+        for (int i = tid; i < SL * seg; i += TH) lacc[(size_t)(cc - 1) * SL * seg + i] = id;
+    }
+    const int64_t my_cnt = min((int64_t)a.b_cnt[p * kSub + sub], a.capb);
+    const int64_t boff = ((int64_t)p * kSub + sub) * a.capb;
+    int64_t cnt = 0;
+    for (int s2 = 0; s2 < kSub; ++s2) cnt = max(cnt, min((int64_t)a.b_cnt[p * kSub + s2], a.capb));
+    const gc_u64_ptr bk = (const gc_u64_ptr)(a.b_key + boff);
+    const gc_u64_ptr bv0 = a.b_val0 ? (const gc_u64_ptr)(a.b_val0 + boff) : nullptr;
+    const gc_u64_ptr bv1 = a.b_val1 ? (const gc_u64_ptr)(a.b_val1 + boff) : nullptr;
+    const __attribute__((address_space(1))) uint16_t* br = (const __attribute__((address_space(1))) uint16_t*)(a.b_rel + boff);
+    int lo = 0x7fffffff;
+    auto flush = [&](int rel) {   // merge window slice `rel` into HBM; every thread owns seg/TH slots
+        constexpr int kPer = 4096 / TH;   // seg <= 4096
+        const int w = rel & (SL - 1);
         const int32_t slot = (rel >= 0 && rel < kRelCap) ? a.rel2slot[rel] : -1;
-        unsigned long long* base = slot >= 0 ? a.slot_base[slot] : nullptr;
-        for (int i = tid; i < seg; i += kThreadsA) {
-            const uint32_t k = lcnt[w * seg + i];
-            if (k == 0) continue;
-            lcnt[w * seg + i] = 0;
-            const int64_t g = ((int64_t)p << a.seg_log) + i;
-            if (base) base[g] += k;
-            for (int cc = 1; cc < c.nacc; ++cc) {
-                unsigned long long* lp = &lacc[(size_t)(cc - 1) * sl * seg + (size_t)w * seg + i];
-                const unsigned long long x = *lp;
-                *lp = ident_of(c.acc_kind[cc]);
-                if (!base) continue;
-                unsigned long long* gp = &base[(int64_t)cc * a.stride + g];
-                switch (c.acc_kind[cc]) {
-                    case ACC_ADD_I64: *gp += x; break;
-                    case ACC_ADD_F64: *(double*)gp += __longlong_as_double((long long)x); break;
-                    case ACC_MIN_ORD: if (x < *gp) *gp = x; break;
-                    case ACC_MAX_ORD: if (x > *gp) *gp = x; break;
+        g_u64* base = slot >= 0 ? (g_u64*)a.slot_base[slot] : nullptr;
+        uint32_t k[kPer];
+        int64_t g[kPer];
+#pragma unroll
+        for (int m = 0; m < kPer; ++m) {
+            const int i = tid + m * TH;
+            k[m] = 0;
+            g[m] = ((int64_t)p << a.seg_log) + i;
+            if (i < seg) { k[m] = lcnt[w * seg + i]; lcnt[w * seg + i] = 0; }
+        }
+        if (base) {
+            unsigned long long old[kPer];
+#pragma unroll
+            for (int m = 0; m < kPer; ++m) old[m] = k[m] ? base[g[m]] : 0ull;
+#pragma unroll
+            for (int m = 0; m < kPer; ++m) if (k[m]) base[g[m]] = old[m] + k[m];
+        }
+        for (int cc = 1; cc < nacc; ++cc) {
+            const int akc = LAYOUT == 1 ? ACC_ADD_I64 : (s_desc[cc] & 0xff);
+            unsigned long long x[kPer], old[kPer];
+            const unsigned long long id = ident_of(akc);
+#pragma unroll
+            for (int m = 0; m < kPer; ++m) {
+                const int i = tid + m * TH;
+                x[m] = id;
+                if (k[m]) {
+                    unsigned long long* lp = &lacc[(size_t)(cc - 1) * SL * seg + (size_t)w * seg + i];
+                    x[m] = *lp;
+                    *lp = id;
+                }
+            }
+            if (!base) continue;
+            g_u64* col = base + (int64_t)cc * a.stride;
+#pragma unroll
+            for (int m = 0; m < kPer; ++m) old[m] = k[m] ? col[g[m]] : 0ull;
+#pragma unroll
+            for (int m = 0; m < kPer; ++m) {
+                if (!k[m]) continue;
+                unsigned long long r = old[m];
+                switch (akc) {
+                    case ACC_ADD_I64: r = old[m] + x[m]; break;
+                    case ACC_ADD_F64: r = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)old[m]) + __longlong_as_double((long long)x[m])); break;
+                    case ACC_MIN_ORD: r = x[m] < old[m] ? x[m] : old[m]; break;
+                    case ACC_MAX_ORD: r = x[m] > old[m] ? x[m] : old[m]; break;
                     default: break;
                 }
+                col[g[m]] = r;
             }
         }
     };
     __syncthreads();
-    const int64_t chunk = (int64_t)kLanesPerSub * kItemsA;      // records per sub per chunk
-    // software pipeline: the next chunk's bucket loads are in flight while this chunk is combined
-    unsigned long long nk_[kItemsA], nx0[kItemsA], nx1[kItemsA];
-    int nrel[kItemsA];
+    // register double buffer: n* = chunk in flight, c* = chunk being combined
+    unsigned long long nkey[IT], nx0[IT], nx1[IT];
+    int nrel[IT];
     auto load_chunk = [&](int64_t cb) {
 #pragma unroll
-        for (int j = 0; j < kItemsA; ++j) {
-            const int64_t i = cb + (int64_t)j * kLanesPerSub + my_li;
+        for (int j = 0; j < IT; ++j) {
+            const int64_t i = cb + (int64_t)j * LPS + li;
             const bool ok = i < my_cnt;
-            nk_[j] = ok ? a.b_key[boff + i] : 0ull;
-            nx0[j] = (ok && a.b_val0) ? a.b_val0[boff + i] : 0ull;
-            nx1[j] = (ok && a.b_val1) ? a.b_val1[boff + i] : 0ull;
-            nrel[j] = ok ? (int)a.b_rel[boff + i] : -1;
+            nkey[j] = ok ? bk[i] : 0ull;
+            nx0[j] = (NV > 0 && ok) ? bv0[i] : 0ull;
+            nx1[j] = (NV > 1 && ok) ? bv1[i] : 0ull;
+            nrel[j] = ok ? (int)br[i] : -1;
         }
     };
-    if (kPrefetch) load_chunk(0);
-    for (int64_t cb = 0; cb < cnt; cb += chunk) {
-        if (!kPrefetch) load_chunk(cb);
-        unsigned long long kk[kItemsA], x0[kItemsA], x1[kItemsA];
-        int rel[kItemsA];
+    constexpr int64_t kChunk = (int64_t)IT * LPS;
+    load_chunk(0);
+    PMARK(0);
+    int it = 0;
+    for (int64_t cb = 0; cb < cnt; cb += kChunk, ++it) {
+        unsigned long long key[IT], x0[IT], x1[IT];
+        int rel[IT];
         int rmin = 0x7fffffff, rmax = -1;
 #pragma unroll
-        for (int j = 0; j < kItemsA; ++j) {
-            kk[j] = nk_[j];
-            x0[j] = nx0[j];
-            x1[j] = nx1[j];
-            rel[j] = nrel[j];
+        for (int j = 0; j < IT; ++j) {
+            key[j] = nkey[j]; x0[j] = nx0[j]; x1[j] = nx1[j]; rel[j] = nrel[j];
             if (rel[j] >= 0) { rmin = min(rmin, rel[j]); rmax = max(rmax, rel[j]); }
         }
-        if (kPrefetch && cb + chunk < cnt) load_chunk(cb + chunk);
+        PMARK(1);
+        if (cb + kChunk < cnt) load_chunk(cb + kChunk);
         for (int sh = 32; sh >= 1; sh >>= 1) { rmin = min(rmin, __shfl_xor(rmin, sh)); rmax = max(rmax, __shfl_xor(rmax, sh)); }
-        if (tid == 0) { s_min = 0x7fffffff; s_max = -1; }
+        const int buf = it & 1;
+        if (lane == 0) { s_min[buf * kWaves + wv] = rmin; s_max[buf * kWaves + wv] = rmax; }
+        // first probes in flight across the barrier
+        uint32_t pos[IT];
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            pos[j] = (uint32_t)jm::mix64(key[j]) & smask;
+        }
+        PMARK(2);
         __syncthreads();
-        if (lane == 0) { atomicMin(&s_min, rmin); atomicMax(&s_max, rmax); }
-        __syncthreads();
-        const int cmin = s_min, cmax = s_max;
+        PMARK(3);
+        int cmin = 0x7fffffff, cmax = -1;
+#pragma unroll
+        for (int v = 0; v < kWaves; ++v) { cmin = min(cmin, s_min[buf * kWaves + v]); cmax = max(cmax, s_max[buf * kWaves + v]); }
+        if (cmax < 0) continue;
         if (lo == 0x7fffffff) lo = cmin;
-        while (cmax >= lo + sl) {       // slide the window forward: merge the oldest slice into HBM
-            flush(lo);
-            ++lo;
+        if (cmax >= lo + SL) {
+            while (cmax >= lo + SL) { if (!(a.abl & 4)) flush(lo); ++lo; }
             __syncthreads();
         }
-        // first probes of all records issued back to back (independent LDS reads in flight)
-        uint32_t pos0[kItemsA];
-        unsigned long long cur0[kItemsA];
+        PMARK(4);
+        // bucket probing: read the key's 8-slot home bucket (4 x ds_read_b128), compare all 8; only
+        // keys displaced past their bucket (a few %) take another round
+        int32_t loc[IT];
 #pragma unroll
-        for (int j = 0; j < kItemsA; ++j) {
-            pos0[j] = (uint32_t)jm::mix64(kk[j]) & smask;
-            cur0[j] = lkey[pos0[j]];
+        for (int j = 0; j < IT; ++j) {
+            loc[j] = -2;
+            if (rel[j] < 0) continue;
+            if (a.abl & 1) { loc[j] = (int32_t)pos[j]; continue; }
+            const unsigned long long kk = key[j];
+            uint32_t b = pos[j] & ~(uint32_t)(kBucket - 1);
+            int32_t found = -1;
+            for (int round = 0; round <= (seg >> 3) && found < 0; ++round) {
+                const ulonglong2* bp = (const ulonglong2*)&lkey[b];
+                const ulonglong2 q0 = bp[0], q1 = bp[1], q2 = bp[2], q3 = bp[3];
+                const unsigned long long v[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+                uint32_t eq = 0, em = 0;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) { eq |= (uint32_t)(v[t] == kk) << t; em |= (uint32_t)(v[t] == kEmptyKey) << t; }
+                if (eq) { found = (int32_t)(b + __builtin_ctz(eq)); break; }
+                if (em) {                       // absent: insert at the first empty slot (CAS vs other lanes)
+                    const uint32_t sidx = b + __builtin_ctz(em);
+                    const unsigned long long old = atomicCAS(&lkey[sidx], kEmptyKey, kk);
+                    if (old == kEmptyKey) { found = (int32_t)sidx; atomicAdd(s_new, 1); break; }
+                    if (old == kk) { found = (int32_t)sidx; break; }
+                    continue;                   // lost the slot to another key: re-read this bucket
+                }
+                b = (b + kBucket) & smask;
+                if (a.prof && lane == 0) pacc[7]++;
+            }
+            loc[j] = found;
         }
 #pragma unroll
-        for (int j = 0; j < kItemsA; ++j) {
+        for (int j = 0; j < IT; ++j) {
             if (rel[j] < 0) continue;
-            // find / insert the key in the LDS segment
-            const unsigned long long key = kk[j];
-            uint32_t pos = pos0[j];
-            int32_t local = (cur0[j] == key) ? (int32_t)pos : -1;
-            if (a.abl & 1) local = (int32_t)pos;   // ablation: no LDS probe
-            for (int probe = 0; probe < seg && local < 0; ++probe) {
-                const unsigned long long cur = lkey[pos];
-                if (cur == key) { local = (int32_t)pos; break; }
-                if (cur == kEmptyKey) {
-                    const unsigned long long old = atomicCAS(&lkey[pos], kEmptyKey, key);
-                    if (old == kEmptyKey) { local = (int32_t)pos; atomicAdd(&s_new, 1); break; }
-                    if (old == key) { local = (int32_t)pos; break; }
-                }
-                pos = (pos + 1) & smask;
-            }
+            const int32_t local = loc[j];
             if (local < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
-            if (rel[j] < lo) {          // older than the window: applied later with atomics
+            if (rel[j] < lo) {          // older than the window: applied after the kernel with atomics
+                if (a.prof) pacc[6] += 1000000;
                 const int32_t si = atomicAdd(a.strag_n, 1);
                 if (si < a.strag_cap) {
-                    a.strag[si].o = (uint64_t)(boff + cb + (int64_t)j * kLanesPerSub + my_li);
+                    a.strag[si].o = (uint64_t)(boff + cb + (int64_t)j * LPS + li);
                     a.strag[si].g = (uint32_t)(((int64_t)p << a.seg_log) + local);
                 } else {
                     atomicOr(&a.st->key_full, 4);
                 }
                 continue;
             }
-            const int w = rel[j] % sl;
-            if (a.abl & 2) { if (key == 0x1234567ull) lcnt[0] = 1; continue; }   // ablation: no LDS atomics
+            const int w = rel[j] & (SL - 1);
+            if (a.abl & 2) { if (x0[j] == 0x123456789ull) lcnt[0] = 1; continue; }
             atomicAdd(&lcnt[w * seg + local], 1u);
-            for (int jj = 0; jj < c.naggs; ++jj) {
-                const AggDesc d = c.agg[jj];
-                if (d.acc == 0) continue;
-                unsigned long long* lp = &lacc[(size_t)(d.acc - 1) * sl * seg + (size_t)w * seg + local];
-                const unsigned long long raw = d.vslot == 0 ? x0[j] : x1[j];
-                switch (d.acc_kind) {
-                    case ACC_ADD_I64: atomicAdd(lp, raw); break;
-                    case ACC_ADD_F64: atomicAdd((double*)lp, carried_f64(raw, d.kind)); break;
-                    case ACC_MIN_ORD: atomicMin(lp, carried_ord(raw, d.kind)); break;
-                    case ACC_MAX_ORD: atomicMax(lp, carried_ord(raw, d.kind)); break;
-                    default: break;
+            if constexpr (LAYOUT == 1) {
+                atomicAdd(&lacc[(size_t)w * seg + local], x0[j]);
+            } else if constexpr (LAYOUT == 0) {
+                for (int cc = 1; cc < nacc; ++cc) {
+                    const int d = s_desc[cc];
+                    unsigned long long* lp = &lacc[(size_t)(cc - 1) * SL * seg + (size_t)w * seg + local];
+                    const unsigned long long raw = (NV > 1 && ((d >> 8) & 0xff) != 0) ? x1[j] : x0[j];
+                    const int ik = d >> 16;
+                    switch (d & 0xff) {
+                        case ACC_ADD_I64: atomicAdd(lp, raw); break;
+                        case ACC_ADD_F64: atomicAdd((double*)lp, carried_f64(raw, ik)); break;
+                        case ACC_MIN_ORD: atomicMin(lp, carried_ord(raw, ik)); break;
+                        case ACC_MAX_ORD: atomicMax(lp, carried_ord(raw, ik)); break;
+                        default: break;
+                    }
                 }
             }
         }
-        __syncthreads();
+        PMARK(5);
     }
+    __syncthreads();
     if (lo != 0x7fffffff)
-        for (int r = lo; r < lo + sl; ++r) { flush(r); __syncthreads(); }
-    if (s_new) {                        // publish newly inserted keys (exclusive owner of this segment)
-        for (int i = tid; i < seg; i += kThreadsA) gkeys[i] = lkey[i];
-        if (tid == 0) atomicAdd(&a.st->n_keys, (unsigned long long)s_new);
+        for (int r = lo; r < lo + SL; ++r) flush(r);
+    if (*s_new) {                       // publish newly inserted keys (exclusive owner of this segment)
+        for (int i = tid; i < seg; i += TH) gkeys[i] = lkey[i];
+        if (tid == 0) atomicAdd(&a.st->n_keys, (unsigned long long)*s_new);
     }
+    if (a.prof && tid == 0) for (int q = 0; q < 8; ++q) a.prof[(int64_t)p * 8 + q] = pacc[q];
+#undef PMARK
 }
 
 // Stragglers: bucket entries older than their combiner's window, applied with global atomics.
@@ -1586,11 +1676,29 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.st = e->d_st;
     static const int aabl = getenv("FWA_AABL") ? atoi(getenv("FWA_AABL")) : 0;
     ca.abl = aabl;
+    static const int aprof = getenv("FWA_APROF") ? atoi(getenv("FWA_APROF")) : 0;
+    static long long* d_prof = nullptr;
+    if (aprof && !d_prof) HIPCHK(e, hipMalloc(&d_prof, sizeof(long long) * 8 * kMaxPart));
+    ca.prof = aprof ? d_prof : nullptr;
     HIPCHK(e, hipEventRecord(e->ev[6], e->stream));
-    static const int avar = getenv("FWA_AVAR") ? atoi(getenv("FWA_AVAR")) : 1;
-    if (avar == 1) combine_kernel<8, false><<<e->np, kThreadsA, e->combine_lds, e->stream>>>(ca, e->d_ec);
-    else if (avar == 2) combine_kernel<2, true><<<e->np, kThreadsA, e->combine_lds, e->stream>>>(ca, e->d_ec);
-    else combine_kernel<4, true><<<e->np, kThreadsA, e->combine_lds, e->stream>>>(ca, e->d_ec);
+    static const int avar = getenv("FWA_AVAR") ? atoi(getenv("FWA_AVAR")) : 4;
+    const size_t seg3 = (size_t)1 << e->seg_log;
+    const size_t lds3 = seg3 * 8 + 2 * seg3 * 4 + (size_t)(e->nacc - 1) * 2 * seg3 * 8 + 4 * 4 * kSub + 16;
+    int layout = 0;
+    if (e->nacc == 1) layout = 2;
+    else if (e->nacc == 2 && e->ec.acc_kind[1] == ACC_ADD_I64) {
+        for (int j = 0; j < e->cfg.num_aggs; ++j)
+            if (e->ec.agg[j].acc == 1 && e->ec.agg[j].vslot == 0) layout = 1;
+    }
+#define C3L(IT, TH, NV) do { \
+        if (layout == 1) combine3_kernel<IT, 2, NV, TH, 1><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); \
+        else if (layout == 2) combine3_kernel<IT, 2, NV, TH, 2><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); \
+        else combine3_kernel<IT, 2, NV, TH, 0><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); } while (0)
+#define C3LAUNCH(IT, TH) do { if (e->nv == 0) C3L(IT, TH, 0); else if (e->nv == 1) C3L(IT, TH, 1); else C3L(IT, TH, 2); } while (0)
+    if (avar == 1) C3LAUNCH(8, 512);
+    else if (avar == 4) C3LAUNCH(4, 1024);
+    else if (avar == 6) C3LAUNCH(4, 512);
+
     HIPCHK(e, hipGetLastError());
     int32_t nstrag = 0;
     HIPCHK(e, hipMemcpyAsync(&e->h_st->pad, e->d_strag_n, 4, hipMemcpyDeviceToHost, e->stream));
@@ -1601,6 +1709,14 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     HIPCHK(e, hipEventRecord(e->ev[7], e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipEventElapsedTime(&ms, e->ev[6], e->ev[7]));
+    if (aprof) {
+        std::vector<long long> hp(8 * e->np);
+        HIPCHK(e, hipMemcpy(hp.data(), d_prof, sizeof(long long) * 8 * e->np, hipMemcpyDeviceToHost));
+        double tot[8] = {0};
+        for (int b = 0; b < e->np; ++b) for (int k = 0; k < 8; ++k) tot[k] += (double)hp[b * 8 + k] / e->np;
+        fprintf(stderr, "[aprof] kernel %.3f ms; per-block avg cycles: %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n",
+                ms, tot[0], tot[1], tot[2], tot[3], tot[4], tot[5], tot[6], tot[7]);
+    }
     e->combine_ms += ms;
     e->ingest_ms += ms;
     e->ingest_launches++;
