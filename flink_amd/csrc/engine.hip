@@ -20,6 +20,7 @@
 // it that has not fired when it arrives; it is dropped (numLateRecordsDropped) iff that set is
 // empty; a window is emitted for a key iff at least one record contributed to it.
 #include <hip/hip_runtime.h>
+#include <hipcub/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -67,6 +68,7 @@ struct DevStatus {
     unsigned long long min_q;
     int32_t pad;                // host-side scratch (straggler count copy)
     int32_t pad2;
+    unsigned long long sess_live;  // sessions: in-flight sessions (rows a fire can emit at most)
 };
 
 enum AccKind : int32_t { ACC_NONE = 0, ACC_ADD_I64 = 1, ACC_ADD_F64 = 2, ACC_MIN_ORD = 3, ACC_MAX_ORD = 4 };
@@ -96,6 +98,7 @@ struct IngestArgs {
     const void* cols[FWA_MAX_COLS];
     const int32_t* key_hash;
     const int32_t* idx;         // optional index list (miss replay)
+    const unsigned long long* pcount;  // partial accumulators (fwa_push_partials): COUNT per row; cols[j] = acc of agg j
     int64_t n;
     int64_t wm;
     unsigned long long* key_table;
@@ -186,13 +189,26 @@ __device__ __forceinline__ uint64_t load_ord(const void* col, int64_t i, int kin
     }
 }
 
+// One input value in its accumulator domain (i64 bits, f64 bits, or ordered key).
+__device__ __forceinline__ unsigned long long acc_input(const AggDesc& d, const void* col, int64_t i) {
+    switch (d.acc_kind) {
+        case ACC_ADD_I64: return ((const unsigned long long*)col)[i];
+        case ACC_ADD_F64: {
+            const double v = (d.kind == FWA_SUM_F32 || d.kind == FWA_AVG_F32) ? (double)((const float*)col)[i]
+                                                                               : ((const double*)col)[i];
+            return (unsigned long long)__double_as_longlong(v);
+        }
+        default: return load_ord(col, i, d.kind);
+    }
+}
+
 template <bool kIdx>
 __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
     const int lane = threadIdx.x & 63;
     const int64_t stride_grid = (int64_t)gridDim.x * blockDim.x;
     unsigned long long qmax = 0, qmin = ~0ull;
-    unsigned dropped = 0;
+    unsigned long long dropped = 0;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.n; t += stride_grid) {
         const int64_t i = kIdx ? (int64_t)a.idx[t] : t;
         const int64_t key = a.keys[i];
@@ -219,8 +235,9 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
             a.spill[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)i;
             continue;
         }
+        const unsigned long long cadd = a.pcount ? a.pcount[i] : 1ull;   // records this row stands for
         const bool accepted = (e->flags & 2) || a.wm < e->thr;
-        if (!accepted) { ++dropped; continue; }
+        if (!accepted) { dropped += cadd; continue; }
         if (c.lateness_pos && a.wm >= e->first_maxts) atomicAdd(&a.st->late_fire, 1ull);
         if (e->slot < 0) {                                      // known slice without slot: replay
             want_insert(a.want, a.st, q);
@@ -236,24 +253,20 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         const int32_t slot = e->slot;
         unsigned long long* base = a.slot_base[slot];
         if (a.touched[slot] == 0) a.touched[slot] = 1;
-        atomicAdd(&base[kid], 1ull);                            // COUNT(*)
+        atomicAdd(&base[kid], cadd);                            // COUNT(*)
 #pragma unroll
         for (int j = 0; j < FWA_MAX_AGGS; ++j) {
             if (j >= c.naggs) break;
             const AggDesc dsc = c.agg[j];
             if (dsc.acc == 0) continue;
             unsigned long long* col = base + (int64_t)dsc.acc * a.stride + kid;
-            const void* in = a.cols[dsc.col];
+            const unsigned long long x = a.pcount ? ((const unsigned long long*)a.cols[j])[i]   // accumulator
+                                                  : acc_input(dsc, a.cols[dsc.col], i);
             switch (dsc.acc_kind) {
-                case ACC_ADD_I64: atomicAdd(col, (unsigned long long)((const int64_t*)in)[i]); break;
-                case ACC_ADD_F64: {
-                    const double v = (dsc.kind == FWA_SUM_F32 || dsc.kind == FWA_AVG_F32)
-                                         ? (double)((const float*)in)[i] : ((const double*)in)[i];
-                    atomicAdd((double*)col, v);
-                    break;
-                }
-                case ACC_MIN_ORD: atomicMin(col, (unsigned long long)load_ord(in, i, dsc.kind)); break;
-                case ACC_MAX_ORD: atomicMax(col, (unsigned long long)load_ord(in, i, dsc.kind)); break;
+                case ACC_ADD_I64: atomicAdd(col, x); break;
+                case ACC_ADD_F64: atomicAdd((double*)col, __longlong_as_double((long long)x)); break;
+                case ACC_MIN_ORD: atomicMin(col, x); break;
+                case ACC_MAX_ORD: atomicMax(col, x); break;
                 default: break;
             }
         }
@@ -823,53 +836,70 @@ struct FireArgs {
     int64_t* o_start;
     int64_t* o_end;
     void* o_agg[FWA_MAX_AGGS];
+    int64_t* o_count;           // partial mode: COUNT(*) per row
+    int32_t raw;                // 1: emit accumulators (fwa_drain_partials), not results
     DevStatus* st;
 };
 
-constexpr int kFireJ = 16;                         // keys per thread per block: 4096-key chunks
+constexpr int kFireJ = 16;                        // keys per thread per block: 4096-key chunks
+
+// Final value of one aggregate (AggregateFunction.getResult / SQL getValueExpression) from its
+// accumulator column value x (i64 sum bits, f64 sum bits or an ordered MIN/MAX key) and COUNT.
+__device__ __forceinline__ void write_agg(const AggDesc& d, uint64_t cnt, unsigned long long x, void* out, int64_t row) {
+    const int64_t iv = (int64_t)x;
+    const double dv = __longlong_as_double((long long)x);
+    switch (d.kind) {
+        case FWA_COUNT: ((int64_t*)out)[row] = (int64_t)cnt; break;
+        case FWA_SUM_I64: ((int64_t*)out)[row] = iv; break;
+        case FWA_SUM_F32: ((float*)out)[row] = (float)dv; break;
+        case FWA_SUM_F64: ((double*)out)[row] = dv; break;
+        case FWA_AVG_I64: {
+            const int64_t n = (int64_t)cnt;  // AvgAggFunction: sum / count (Java long division)
+            ((int64_t*)out)[row] = (n == -1 && iv == LONG_MIN_J) ? LONG_MIN_J : iv / n;
+            break;
+        }
+        case FWA_AVG_F32: ((float*)out)[row] = (float)(dv / (double)(int64_t)cnt); break;
+        case FWA_AVG_F64: ((double*)out)[row] = dv / (double)(int64_t)cnt; break;
+        case FWA_MIN_I64: case FWA_MAX_I64: ((int64_t*)out)[row] = jm::unord_i64(x); break;
+        case FWA_MIN_F32: case FWA_MAX_F32:
+            ((float*)out)[row] = (float)__longlong_as_double((long long)jm::unord_bits64(x));
+            break;
+        case FWA_MIN_F64: case FWA_MAX_F64:
+            ((double*)out)[row] = __longlong_as_double((long long)jm::unord_bits64(x));
+            break;
+        default: break;
+    }
+}
+
+// Accumulator algebra: combine two accumulator values of one column (AggregateFunction.merge).
+__device__ __forceinline__ unsigned long long acc_combine(int acc_kind, unsigned long long x, unsigned long long y) {
+    switch (acc_kind) {
+        case ACC_ADD_I64: return x + y;
+        case ACC_ADD_F64:
+            return (unsigned long long)__double_as_longlong(__longlong_as_double((long long)x) + __longlong_as_double((long long)y));
+        case ACC_MIN_ORD: return y < x ? y : x;
+        case ACC_MAX_ORD: return y > x ? y : x;
+        default: return x;
+    }
+}
 
 __device__ __forceinline__ void emit_row(const FireArgs& f, const EngineConst& c, const FireWindow& win, int64_t k,
                                          unsigned long long kv, uint64_t cnt, int64_t row) {
     f.o_key[row] = (k < f.capacity) ? (int64_t)kv : LONG_MIN_J;
     f.o_start[row] = win.start;
     f.o_end[row] = win.end;
+    if (f.o_count) f.o_count[row] = (int64_t)cnt;
     for (int j = 0; j < c.naggs; ++j) {
         const AggDesc d = c.agg[j];
-        int64_t iv = 0;
-        double dv = 0.0;
-        uint64_t ov = (d.acc_kind == ACC_MIN_ORD) ? ~0ull : 0ull;
-        for (int s = 0; s < win.nslots; ++s) {
-            const unsigned long long x = f.slot_base[f.win_slots[win.slot_off + s]][(int64_t)d.acc * f.stride + k];
-            switch (d.acc_kind) {
-                case ACC_ADD_I64: iv = jm::wadd(iv, (int64_t)x); break;
-                case ACC_ADD_F64: dv += __longlong_as_double((long long)x); break;
-                case ACC_MIN_ORD: ov = x < ov ? x : ov; break;
-                case ACC_MAX_ORD: ov = x > ov ? x : ov; break;
-                default: break;
-            }
+        unsigned long long x = ident_of(d.acc_kind);
+        if (d.acc > 0)
+            for (int s = 0; s < win.nslots; ++s)
+                x = acc_combine(d.acc_kind, x, f.slot_base[f.win_slots[win.slot_off + s]][(int64_t)d.acc * f.stride + k]);
+        if (f.raw) {   // partial accumulators (fwa_drain_partials): the accumulator value itself
+            ((unsigned long long*)f.o_agg[j])[row] = d.acc > 0 ? x : cnt;
+            continue;
         }
-        void* out = f.o_agg[j];
-        switch (d.kind) {
-            case FWA_COUNT: ((int64_t*)out)[row] = (int64_t)cnt; break;
-            case FWA_SUM_I64: ((int64_t*)out)[row] = iv; break;
-            case FWA_SUM_F32: ((float*)out)[row] = (float)dv; break;
-            case FWA_SUM_F64: ((double*)out)[row] = dv; break;
-            case FWA_AVG_I64: {
-                const int64_t n = (int64_t)cnt;  // AvgAggFunction: sum / count (Java long division)
-                ((int64_t*)out)[row] = (n == -1 && iv == LONG_MIN_J) ? LONG_MIN_J : iv / n;
-                break;
-            }
-            case FWA_AVG_F32: ((float*)out)[row] = (float)(dv / (double)(int64_t)cnt); break;
-            case FWA_AVG_F64: ((double*)out)[row] = dv / (double)(int64_t)cnt; break;
-            case FWA_MIN_I64: case FWA_MAX_I64: ((int64_t*)out)[row] = jm::unord_i64(ov); break;
-            case FWA_MIN_F32: case FWA_MAX_F32:
-                ((float*)out)[row] = (float)__longlong_as_double((long long)jm::unord_bits64(ov));
-                break;
-            case FWA_MIN_F64: case FWA_MAX_F64:
-                ((double*)out)[row] = __longlong_as_double((long long)jm::unord_bits64(ov));
-                break;
-            default: break;
-        }
+        write_agg(d, cnt, x, f.o_agg[j], row);
     }
 }
 
@@ -924,6 +954,200 @@ __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineCo
         const int64_t row = (int64_t)s_base + woff[j][wid] + __popcll(masks[j] & lt);
         emit_row(f, c, win, k, kvs[j], cnt[j], row);
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// sessions (merging windows, DataStream EventTimeSessionWindows with EventTimeTrigger)
+//
+// State per key (kid): up to kMaxSess in-flight sessions {start, end, accumulators} in HBM, SoA by
+// (kid * kMaxSess + s). Semantics restated from MergingWindowSet.addWindow (MergingWindowSet.java:
+// 153-236), TimeWindow.intersects/cover/mergeWindows (TimeWindow.java:116-124, 208-254) and the merging
+// branch of WindowOperator.processElement (WindowOperator.java:288-389):
+//  * a record opens the window [ts, ts + gap) (EventTimeSessionWindows.assignWindows :61-63);
+//  * it merges with every in-flight session that intersects it (touching windows merge); in-flight
+//    sessions never intersect each other, so the merge set is exactly those sessions;
+//  * if nothing merged and the new window is late (maxTimestamp <= wm, allowed lateness 0) the window
+//    is retired and the record dropped (counted iff ts <= wm, isElementLate :597-601);
+//  * a session fires (and is cleared) when wm >= end - 1 (EventTimeTrigger.onEventTime, cleanup timer).
+// Whether a late record survives depends on the sessions in flight when it arrives, so the records
+// of a key are applied in ARRIVAL order: a stable radix sort by kid groups them, one thread walks a
+// key's run sequentially. Keys are independent, so the parallelism is over keys.
+
+constexpr int kMaxSess = 16;
+
+struct SessArgs {
+    const int64_t* keys;
+    const int64_t* ts;
+    const void* cols[FWA_MAX_COLS];
+    const int32_t* key_hash;
+    int64_t n;
+    int64_t wm;
+    int64_t gap;
+    unsigned long long* key_table;
+    uint64_t key_mask;
+    int32_t seg_log, part_bits;
+    uint32_t* kid;              // [n] key-table slot per record, arrival order
+    uint32_t* idx;              // [n] 0..n-1 (sort values)
+    const uint32_t* skid;       // [n] kids, stably sorted
+    const uint32_t* sidx;       // [n] record index of skid[i]
+    int32_t* s_cnt;             // [cap+1] in-flight sessions per kid
+    int64_t* s_start;           // [(cap+1) * kMaxSess]
+    int64_t* s_end;
+    unsigned long long* s_acc;  // [nacc][(cap+1) * kMaxSess]; column 0 = COUNT
+    int64_t sstride;
+    DevStatus* st;
+};
+
+__global__ void __launch_bounds__(kBlock) sess_key_kernel(SessArgs a, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t key = a.keys[i];
+        a.idx[i] = (uint32_t)i;
+        a.kid[i] = 0xffffffffu;
+        const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0), c.max_par);
+        if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }   // StateTable :300-307
+        if (a.ts[i] == LONG_MIN_J) { raise_error(a.st, FWA_E_TS_MIN); continue; }
+        const int64_t kid = key_slot(a.key_table, a.key_mask, a.seg_log, a.part_bits, key, a.st);
+        if (kid < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
+        a.kid[i] = (uint32_t)kid;
+    }
+}
+
+__device__ __forceinline__ void sess_copy(const SessArgs& a, int nacc, int64_t dst, int64_t src) {
+    a.s_start[dst] = a.s_start[src];
+    a.s_end[dst] = a.s_end[src];
+    for (int cc = 0; cc < nacc; ++cc) a.s_acc[cc * a.sstride + dst] = a.s_acc[cc * a.sstride + src];
+}
+
+__global__ void __launch_bounds__(kBlock) sess_process_kernel(SessArgs a, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    const int nacc = c.nacc;
+    unsigned long long dropped = 0;
+    long long live_delta = 0;
+    bool overflow = false;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.n; t += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t k = a.skid[t];
+        if (t > 0 && a.skid[t - 1] == k) continue;          // not the head of this key's run
+        const int64_t base = (int64_t)k * kMaxSess;
+        int ns = a.s_cnt[k];
+        for (int64_t j = t; j < a.n && a.skid[j] == k; ++j) {
+            const int64_t i = a.sidx[j];
+            const int64_t ts = a.ts[i];
+            const int64_t ws = ts, we = jm::wadd(ts, a.gap);
+            int64_t cs = ws, ce = we;
+            int first = -1;
+            for (int s = 0; s < ns; ++s) {
+                const int64_t ss = a.s_start[base + s], se = a.s_end[base + s];
+                if (!(ss <= we && se >= ws)) continue;          // TimeWindow.intersects
+                cs = ss < cs ? ss : cs;                         // TimeWindow.cover
+                ce = se > ce ? se : ce;
+                if (first < 0) { first = s; continue; }
+                for (int cc = 0; cc < nacc; ++cc) {             // mergeNamespaces -> AggregateFunction.merge
+                    unsigned long long* pf = &a.s_acc[cc * a.sstride + base + first];
+                    *pf = acc_combine(c.acc_kind[cc], *pf, a.s_acc[cc * a.sstride + base + s]);
+                }
+                --ns;
+                --live_delta;
+                if (s != ns) sess_copy(a, nacc, base + s, base + ns);
+                --s;                                            // re-examine the session moved into s
+            }
+            if (first < 0) {
+                if (jm::wsub(we, 1) <= a.wm) {                  // isWindowLate -> retireWindow; record skipped
+                    if (ts <= a.wm) ++dropped;                  // isElementLate
+                    continue;
+                }
+                if (ns == kMaxSess) { overflow = true; continue; }
+                first = ns++;
+                ++live_delta;
+                a.s_acc[base + first] = 0;
+                for (int cc = 1; cc < nacc; ++cc) a.s_acc[cc * a.sstride + base + first] = ident_of(c.acc_kind[cc]);
+            }
+            a.s_start[base + first] = cs;
+            a.s_end[base + first] = ce;
+            a.s_acc[base + first] += 1ull;                      // COUNT(*)
+            for (int jj = 0; jj < c.naggs; ++jj) {              // AggregateFunction.add
+                const AggDesc d = c.agg[jj];
+                if (d.acc == 0) continue;
+                unsigned long long* p = &a.s_acc[d.acc * a.sstride + base + first];
+                *p = acc_combine(d.acc_kind, *p, acc_input(d, a.cols[d.col], i));
+            }
+        }
+        a.s_cnt[k] = ns;
+    }
+    if (overflow) { a.st->key_full |= 8; raise_error(a.st, FWA_E_OOM); }
+    if (dropped) atomicAdd(&a.st->dropped, dropped);
+    if (live_delta) atomicAdd(&a.st->sess_live, (unsigned long long)live_delta);
+}
+
+struct SessFireArgs {
+    const unsigned long long* key_table;
+    int64_t capacity;
+    int64_t wm;
+    int32_t* s_cnt;
+    int64_t* s_start;
+    int64_t* s_end;
+    unsigned long long* s_acc;
+    int64_t sstride;
+    int64_t* o_key;
+    int64_t* o_start;
+    int64_t* o_end;
+    void* o_agg[FWA_MAX_AGGS];
+    DevStatus* st;
+};
+
+// Fire every in-flight session with end - 1 <= wm (EventTimeTrigger.onEventTime + clearAllState),
+// compacting the survivors; one reservation atomic per wave for the emitted rows.
+__global__ void __launch_bounds__(kBlock) sess_fire_kernel(SessFireArgs f, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    const int lane = threadIdx.x & 63;
+    const int64_t nk = f.capacity + 1;
+    long long fired_total = 0;
+    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < nk; k0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = k0 + threadIdx.x;
+        const int ns = k < nk ? f.s_cnt[k] : 0;
+        const int64_t base = k * kMaxSess;
+        uint32_t fm = 0;                                        // bit s: session s fires
+        for (int s = 0; s < ns; ++s)
+            if (jm::wsub(f.s_end[base + s], 1) <= f.wm) fm |= 1u << s;
+        const uint32_t nf = __popc(fm);
+        uint32_t incl = nf;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d);
+            if (lane >= d) incl += y;
+        }
+        unsigned long long wbase = 0;
+        if (lane == 63 && incl) wbase = atomicAdd(&f.st->rows, (unsigned long long)incl);
+        wbase = __shfl(wbase, 63);
+        if (!nf) continue;
+        int64_t row = (int64_t)wbase + incl - nf;
+        const int64_t kv = k < f.capacity ? (int64_t)f.key_table[k] : LONG_MIN_J;
+        int keep = 0;
+        for (int s = 0; s < ns; ++s) {
+            const int64_t src = base + s;
+            if (fm & (1u << s)) {
+                f.o_key[row] = kv;
+                f.o_start[row] = f.s_start[src];
+                f.o_end[row] = f.s_end[src];
+                const uint64_t cnt = f.s_acc[src];
+                for (int j = 0; j < c.naggs; ++j) {
+                    const AggDesc d = c.agg[j];
+                    write_agg(d, cnt, d.acc > 0 ? f.s_acc[d.acc * f.sstride + src] : 0ull, f.o_agg[j], row);
+                }
+                ++row;
+            } else {
+                if (keep != s) {
+                    f.s_start[base + keep] = f.s_start[src];
+                    f.s_end[base + keep] = f.s_end[src];
+                    for (int cc = 0; cc < c.nacc; ++cc) f.s_acc[cc * f.sstride + base + keep] = f.s_acc[cc * f.sstride + src];
+                }
+                ++keep;
+            }
+        }
+        f.s_cnt[k] = keep;
+        fired_total += nf;
+    }
+    for (int d = 32; d >= 1; d >>= 1) fired_total += __shfl_xor(fired_total, d);
+    if (lane == 0 && fired_total) atomicAdd(&f.st->sess_live, (unsigned long long)(-fired_total));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1063,6 +1287,19 @@ struct fwa_engine {
     double partition_ms = 0, combine_ms = 0;
     int64_t ingest_launches = 0, ingest_records = 0, fire_launches = 0, fire_rows = 0;
     double ingest_ms = 0, fire_ms = 0;
+    // sessions (merging windows)
+    int32_t* d_scnt = nullptr;
+    int64_t* d_sstart = nullptr;
+    int64_t* d_send = nullptr;
+    unsigned long long* d_sacc = nullptr;
+    int64_t sstride = 0;
+    uint32_t* d_sess_sort = nullptr;   // kid | idx | skid | sidx, 4 x sess_sort_cap
+    int64_t sess_sort_cap = 0;
+    void* d_sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    int32_t kid_bits = 0;
+    // partial accumulators (fwa_drain_partials)
+    int64_t* o_count = nullptr;
 };
 
 namespace {
@@ -1119,8 +1356,11 @@ int validate(const fwa_config* c) {
             if (c->semantics != FWA_SEM_TABLE || c->size_ms <= 0 || c->slide_ms <= 0 || c->size_ms % c->slide_ms)
                 return FWA_E_ARG;
             break;
-        case FWA_SESSION:
-            return FWA_E_UNSUPPORTED;  // merging windows are a later row
+        case FWA_SESSION:                                                    // EventTimeSessionWindows.java:45-50
+            if (c->gap_ms <= 0) return FWA_E_ARG;
+            if (c->semantics != FWA_SEM_DATASTREAM) return FWA_E_UNSUPPORTED;   // legacy Table SESSION: not on this path
+            if (c->allowed_lateness_ms != 0) return FWA_E_UNSUPPORTED;         // late firings of merged windows
+            break;
         default:
             return FWA_E_ARG;
     }
@@ -1234,7 +1474,7 @@ int alloc_slice(fwa_engine* e, int64_t q) {
     return FWA_OK;
 }
 
-int release_slot(fwa_engine* e, int32_t slot) {
+int reset_slot(fwa_engine* e, int32_t slot) {
     if (e->touched[slot]) {  // restore identities (untouched slots are still clean)
         const size_t col_bytes = (size_t)e->stride * 8;
         unsigned long long* base = e->slot_ptr[slot];
@@ -1245,6 +1485,12 @@ int release_slot(fwa_engine* e, int32_t slot) {
         e->touched[slot] = 0;
         HIPCHK(e, hipMemsetAsync(e->d_touched + slot, 0, sizeof(int32_t), e->stream));
     }
+    return FWA_OK;
+}
+
+int release_slot(fwa_engine* e, int32_t slot) {
+    int rc = reset_slot(e, slot);
+    if (rc) return rc;
     e->free_slots.push_back(slot);
     return FWA_OK;
 }
@@ -1295,6 +1541,8 @@ int ensure_out(fwa_engine* e, int64_t rows) {
     HIPCHK(e, hipMalloc(&e->o_start, 8 * cap));
     HIPCHK(e, hipMalloc(&e->o_end, 8 * cap));
     for (int j = 0; j < e->cfg.num_aggs; ++j) HIPCHK(e, hipMalloc(&e->o_agg[j], 8 * cap));
+    if (e->o_count) HIPCHK(e, hipFree(e->o_count));
+    HIPCHK(e, hipMalloc(&e->o_count, 8 * cap));
     e->out_cap = cap;
     return FWA_OK;
 }
@@ -1333,7 +1581,8 @@ void fwa_destroy(fwa_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel,
-                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n};
+                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n,
+                    e->d_scnt, e->d_sstart, e->d_send, e->d_sacc, e->d_sess_sort, e->d_sort_tmp, e->o_count};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
     for (void* p : e->chunks) (void)hipFree(p);
@@ -1361,9 +1610,12 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
     } else if (e->kind == FWA_SLIDE) {
         e->g = gcd64(cfg->size_ms, cfg->slide_ms);
         e->off = cfg->offset_ms;
-    } else {
+    } else if (e->kind == FWA_CUMULATE) {
         e->g = cfg->slide_ms;
         e->off = cfg->offset_ms;
+    } else {                                     // SESSION: no slices
+        e->g = 1;
+        e->off = 0;
     }
     e->slide_div = jm::udiv64_make((uint64_t)(e->slide > 0 ? e->slide : 1));
     e->size_div = jm::udiv64_make((uint64_t)e->size);
@@ -1426,7 +1678,7 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         if (const char* sv = getenv("FWA_SL")) sl = std::min(sl, atoi(sv));
         const int64_t np = (int64_t)1 << e->part_bits;
         const char* force = getenv("FWA_INGEST");
-        ok = ok && np <= kMaxPart && sl >= 2 && !(force && !strcmp(force, "v1"));
+        ok = ok && np <= kMaxPart && sl >= 2 && !(force && !strcmp(force, "v1")) && e->kind != FWA_SESSION;
         e->v2 = ok;
         if (ok) {
             e->np = (int32_t)np;
@@ -1461,8 +1713,19 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         size_t fr = 0, tot = 0;
         (void)hipMemGetInfo(&fr, &tot);
         e->mem_budget = fr / 2;
-        if ((rc = grow_slots(e, 4))) break;
-        if ((rc = publish_dir(e))) break;
+        if (e->kind == FWA_SESSION) {            // per-key in-flight session lists
+            e->sstride = (cap + 1) * kMaxSess;
+            e->kid_bits = 1;
+            while (((int64_t)1 << e->kid_bits) < cap + 1) ++e->kid_bits;
+            if (hipMalloc(&e->d_scnt, sizeof(int32_t) * (cap + 1)) != hipSuccess) { rc = FWA_E_OOM; break; }
+            if (hipMalloc(&e->d_sstart, 8 * e->sstride) != hipSuccess) { rc = FWA_E_OOM; break; }
+            if (hipMalloc(&e->d_send, 8 * e->sstride) != hipSuccess) { rc = FWA_E_OOM; break; }
+            if (hipMalloc(&e->d_sacc, 8 * e->sstride * e->nacc) != hipSuccess) { rc = FWA_E_OOM; break; }
+            if (hipMemsetAsync(e->d_scnt, 0, sizeof(int32_t) * (cap + 1), e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        } else {
+            if ((rc = grow_slots(e, 4))) break;
+            if ((rc = publish_dir(e))) break;
+        }
         if (hipStreamSynchronize(e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
     } while (0);
     if (rc) { fwa_destroy(e); return rc; }
@@ -1725,44 +1988,142 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     return FWA_OK;
 }
 
-int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
-             const int32_t* key_hash, int64_t n, int32_t flags, int64_t* late_dropped_out) {
-    if (!e) return FWA_E_STATE;
-    if (n < 0 || (n > 0 && (!keys || !ts))) return fail(e, FWA_E_ARG, "null input column");
-    if (e->cfg.key_kind == FWA_KEY_PREHASHED && n > 0 && !key_hash) return fail(e, FWA_E_ARG, "PREHASHED keys need key_hash");
-    if (n > INT32_MAX) return fail(e, FWA_E_ARG, "batch too large (max 2^31-1 records)");
-    if (late_dropped_out) *late_dropped_out = 0;
-    if (n == 0) return FWA_OK;
-    HIPCHK(e, hipSetDevice(e->cfg.device));
-    IngestArgs a;
-    memset(&a, 0, sizeof(a));
-    a.n = n;
-    a.wm = e->wm;
-    if (flags & FWA_PUSH_DEVICE_PTRS) {
-        a.keys = keys;
-        a.ts = ts;
-        a.key_hash = key_hash;
-        for (int j = 0; j < e->cfg.num_aggs; ++j) {
-            const fwa_agg_spec& s = e->cfg.aggs[j];
-            if (s.kind == FWA_COUNT) continue;
-            if (!val_cols || !val_cols[s.col]) return fail(e, FWA_E_ARG, "missing value column");
-            a.cols[s.col] = val_cols[s.col];
+// Sessions: key lookup, stable radix sort of the batch by kid (arrival order kept inside a key),
+// then one sequential MergingWindowSet walk per key (sess_process_kernel).
+static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
+    const int64_t n = a.n;
+    if (n > e->sess_sort_cap) {
+        if (e->d_sess_sort) HIPCHK(e, hipFree(e->d_sess_sort));
+        e->d_sess_sort = nullptr;
+        const int64_t cap = std::max<int64_t>(n, 1 << 16);
+        HIPCHK(e, hipMalloc(&e->d_sess_sort, sizeof(uint32_t) * 4 * cap));
+        e->sess_sort_cap = cap;
+        size_t bytes = 0;
+        HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap, 0,
+                                                     e->kid_bits, e->stream));
+        if (bytes > e->sort_tmp_bytes) {
+            if (e->d_sort_tmp) HIPCHK(e, hipFree(e->d_sort_tmp));
+            e->d_sort_tmp = nullptr;
+            HIPCHK(e, hipMalloc(&e->d_sort_tmp, bytes));
+            e->sort_tmp_bytes = bytes;
         }
-    } else {
-        int rc = stage_inputs(e, keys, ts, val_cols, key_hash, n, a);
-        if (rc) return rc;
     }
-    if (n > e->spill_cap) {
-        if (e->d_spill) HIPCHK(e, hipFree(e->d_spill));
-        if (e->d_replay) HIPCHK(e, hipFree(e->d_replay));
-        e->spill_cap = std::max<int64_t>(n, 1 << 16);
-        HIPCHK(e, hipMalloc(&e->d_spill, sizeof(int32_t) * e->spill_cap));
-        HIPCHK(e, hipMalloc(&e->d_replay, sizeof(int32_t) * e->spill_cap));
+    uint32_t* kid = e->d_sess_sort;
+    uint32_t* idx = kid + e->sess_sort_cap;
+    uint32_t* skid = idx + e->sess_sort_cap;
+    uint32_t* sidx = skid + e->sess_sort_cap;
+    SessArgs s;
+    memset(&s, 0, sizeof(s));
+    s.keys = a.keys;
+    s.ts = a.ts;
+    for (int c = 0; c < FWA_MAX_COLS; ++c) s.cols[c] = a.cols[c];
+    s.key_hash = a.key_hash;
+    s.n = n;
+    s.wm = e->wm;
+    s.gap = e->cfg.gap_ms;
+    s.key_table = e->d_keys;
+    s.key_mask = (uint64_t)e->capacity - 1;
+    s.seg_log = e->seg_log;
+    s.part_bits = e->part_bits;
+    s.kid = kid;
+    s.idx = idx;
+    s.skid = skid;
+    s.sidx = sidx;
+    s.s_cnt = e->d_scnt;
+    s.s_start = e->d_sstart;
+    s.s_end = e->d_send;
+    s.s_acc = e->d_sacc;
+    s.sstride = e->sstride;
+    s.st = e->d_st;
+    int rc = reset_push_status(e);
+    if (rc) return rc;
+    HIPCHK(e, hipEventRecord(e->ev[0], e->stream));
+    sess_key_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(s, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    rc = sync_status(e);
+    if (rc) return rc;
+    if (e->h_st->error) return FWA_OK;               // reported by the caller
+    size_t bytes = e->sort_tmp_bytes;
+    HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(e->d_sort_tmp, bytes, (const uint32_t*)kid, skid, (const uint32_t*)idx,
+                                                 sidx, (int)n, 0, e->kid_bits, e->stream));
+    sess_process_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(s, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->ev[1], e->stream));
+    rc = sync_status(e);
+    if (rc) return rc;
+    rc = account_ingest(e);
+    if (rc) return rc;
+    e->ingest_launches++;
+    e->ingest_records += n;
+    *dropped_out = (int64_t)e->h_st->dropped;
+    return FWA_OK;
+}
+
+// Fire kernel over a list of windows (each a union of slots). raw = 1 emits the accumulators and
+// COUNT(*) instead of the final aggregate values (fwa_drain_partials).
+static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const std::vector<int32_t>& hs, int raw,
+                       int64_t* nrows) {
+    if ((int32_t)hw.size() > e->win_cap) {
+        if (e->d_win) HIPCHK(e, hipFree(e->d_win));
+        e->d_win = nullptr;
+        e->win_cap = (int32_t)hw.size() * 2;
+        HIPCHK(e, hipMalloc(&e->d_win, sizeof(FireWindow) * e->win_cap));
     }
+    if ((int32_t)hs.size() > e->win_slots_cap) {
+        if (e->d_win_slots) HIPCHK(e, hipFree(e->d_win_slots));
+        e->d_win_slots = nullptr;
+        e->win_slots_cap = (int32_t)hs.size() * 2;
+        HIPCHK(e, hipMalloc(&e->d_win_slots, sizeof(int32_t) * e->win_slots_cap));
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_win, hw.data(), sizeof(FireWindow) * hw.size(), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->d_win_slots, hs.data(), sizeof(int32_t) * hs.size(), hipMemcpyHostToDevice, e->stream));
+    int rc = sync_status(e);
+    if (rc) return rc;
+    const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
+    rc = ensure_out(e, (int64_t)hw.size() * nkeys);
+    if (rc) return rc;
+    HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
+    FireArgs f;
+    memset(&f, 0, sizeof(f));
+    f.key_table = e->d_keys;
+    f.capacity = e->capacity;
+    f.stride = e->stride;
+    f.slot_base = e->d_slot_base;
+    f.win = e->d_win;
+    f.win_slots = e->d_win_slots;
+    f.nwin = (int32_t)hw.size();
+    f.blocks_per_win = (int32_t)((e->capacity + 1 + (int64_t)kBlock * kFireJ - 1) / ((int64_t)kBlock * kFireJ));
+    f.o_key = e->o_key;
+    f.o_start = e->o_start;
+    f.o_end = e->o_end;
+    for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
+    f.o_count = raw ? e->o_count : nullptr;
+    f.raw = raw;
+    f.st = e->d_st;
+    const int64_t grid = (int64_t)f.blocks_per_win * (int64_t)hw.size();
+    HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
+    fire_kernel<<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
+    rc = sync_status(e);
+    if (rc) return rc;
+    *nrows = (int64_t)e->h_st->rows;
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+    e->fire_ms += ms;
+    e->fire_launches++;
+    e->fire_rows += *nrows;
+    return FWA_OK;
+}
+
+// Shared ingest driver: two-phase path when allowed, else the v1 kernel; slice-miss replays;
+// lookahead slice allocation; stats.
+static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, int64_t* late_dropped_out) {
     int rc = reset_push_status(e);
     if (rc) return rc;
     bool ran_v2 = false;
-    if (e->v2) {
+    if (e->v2 && allow_v2) {
         rc = push_v2(e, a, &ran_v2);
         if (rc) return rc;
     }
@@ -1837,12 +2198,211 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
     return FWA_OK;
 }
 
+int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
+             const int32_t* key_hash, int64_t n, int32_t flags, int64_t* late_dropped_out) {
+    if (!e) return FWA_E_STATE;
+    if (n < 0 || (n > 0 && (!keys || !ts))) return fail(e, FWA_E_ARG, "null input column");
+    if (e->cfg.key_kind == FWA_KEY_PREHASHED && n > 0 && !key_hash) return fail(e, FWA_E_ARG, "PREHASHED keys need key_hash");
+    if (n > INT32_MAX) return fail(e, FWA_E_ARG, "batch too large (max 2^31-1 records)");
+    if (late_dropped_out) *late_dropped_out = 0;
+    if (n == 0) return FWA_OK;
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    IngestArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n = n;
+    a.wm = e->wm;
+    if (flags & FWA_PUSH_DEVICE_PTRS) {
+        a.keys = keys;
+        a.ts = ts;
+        a.key_hash = key_hash;
+        for (int j = 0; j < e->cfg.num_aggs; ++j) {
+            const fwa_agg_spec& s = e->cfg.aggs[j];
+            if (s.kind == FWA_COUNT) continue;
+            if (!val_cols || !val_cols[s.col]) return fail(e, FWA_E_ARG, "missing value column");
+            a.cols[s.col] = val_cols[s.col];
+        }
+    } else {
+        int rc = stage_inputs(e, keys, ts, val_cols, key_hash, n, a);
+        if (rc) return rc;
+    }
+    if (n > e->spill_cap) {
+        if (e->d_spill) HIPCHK(e, hipFree(e->d_spill));
+        if (e->d_replay) HIPCHK(e, hipFree(e->d_replay));
+        e->spill_cap = std::max<int64_t>(n, 1 << 16);
+        HIPCHK(e, hipMalloc(&e->d_spill, sizeof(int32_t) * e->spill_cap));
+        HIPCHK(e, hipMalloc(&e->d_replay, sizeof(int32_t) * e->spill_cap));
+    }
+    if (e->kind == FWA_SESSION) {
+        int64_t dropped = 0;
+        int rc = push_session(e, a, &dropped);
+        if (rc) return rc;
+        if (e->h_st->error) {
+            const int err = e->h_st->error;
+            return fail(e, err, err == FWA_E_KEYGROUP ? "Key group is not in the owned KeyGroupRange (StateTable.getMapForKeyGroup)"
+                              : err == FWA_E_TS_MIN ? "Record has Long.MIN_VALUE timestamp (= no timestamp marker)."
+                              : (e->h_st->key_full & 8) ? "more than 16 in-flight sessions for one key"
+                                                         : "key table full: raise fwa_config.key_capacity");
+        }
+        e->records_in += n;
+        e->late_dropped += dropped;
+        if (late_dropped_out) *late_dropped_out = dropped;
+        return FWA_OK;
+    }
+    return push_common(e, a, n, true, late_dropped_out);
+}
+
+int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_ts, const int64_t* count,
+                      const void* const* acc, int64_t n, int32_t flags, int64_t* late_dropped_out) {
+    if (!e) return FWA_E_STATE;
+    if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
+    if (n < 0 || (n > 0 && (!keys || !slice_ts || !count))) return fail(e, FWA_E_ARG, "null input column");
+    if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "partials need a computable key hash");
+    if (n > INT32_MAX) return fail(e, FWA_E_ARG, "batch too large (max 2^31-1 records)");
+    if (late_dropped_out) *late_dropped_out = 0;
+    if (n == 0) return FWA_OK;
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    IngestArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n = n;
+    a.wm = e->wm;
+    const void* src[3 + FWA_MAX_AGGS] = {keys, slice_ts, count};
+    int nsrc = 3;
+    for (int j = 0; j < e->cfg.num_aggs; ++j) {
+        if (e->ec.agg[j].acc == 0) continue;
+        if (!acc || !acc[j]) return fail(e, FWA_E_ARG, "missing accumulator column");
+        src[nsrc++] = acc[j];
+    }
+    const void* dev[3 + FWA_MAX_AGGS];
+    if (flags & FWA_PUSH_DEVICE_PTRS) {
+        for (int c = 0; c < nsrc; ++c) dev[c] = src[c];
+    } else {                                   // stage host columns (8 bytes each) into the input buffer
+        const size_t colb = ((size_t)n * 8 + 255) / 256 * 256;
+        if (colb * nsrc > e->d_in_bytes) {
+            if (e->d_in) HIPCHK(e, hipFree(e->d_in));
+            e->d_in = nullptr;
+            HIPCHK(e, hipMalloc(&e->d_in, colb * nsrc));
+            e->d_in_bytes = colb * nsrc;
+        }
+        for (int c = 0; c < nsrc; ++c) {
+            dev[c] = (char*)e->d_in + colb * c;
+            HIPCHK(e, hipMemcpyAsync((void*)dev[c], src[c], (size_t)n * 8, hipMemcpyHostToDevice, e->stream));
+        }
+    }
+    a.keys = (const int64_t*)dev[0];
+    a.ts = (const int64_t*)dev[1];
+    a.pcount = (const unsigned long long*)dev[2];
+    for (int j = 0, c = 3; j < e->cfg.num_aggs; ++j)
+        if (e->ec.agg[j].acc > 0) a.cols[j] = dev[c++];
+    if (n > e->spill_cap) {
+        if (e->d_spill) HIPCHK(e, hipFree(e->d_spill));
+        if (e->d_replay) HIPCHK(e, hipFree(e->d_replay));
+        e->spill_cap = std::max<int64_t>(n, 1 << 16);
+        HIPCHK(e, hipMalloc(&e->d_spill, sizeof(int32_t) * e->spill_cap));
+        HIPCHK(e, hipMalloc(&e->d_replay, sizeof(int32_t) * e->spill_cap));
+    }
+    return push_common(e, a, n, false, late_dropped_out);
+}
+
+// Export every (key, slice) accumulator that received records since the last drain and reset those
+// slices (the local half of LocalSlicingWindowAggOperator -> GlobalAggCombiner).
+int fwa_drain_partials(fwa_engine* e, fwa_partials* out) {
+    if (!e || !out) return FWA_E_ARG;
+    if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    memset(out, 0, sizeof(*out));
+    std::vector<FireWindow> hw;
+    std::vector<int32_t> hs;
+    for (auto& kv : e->live) {
+        if (!e->touched[kv.second]) continue;
+        FireWindow f;
+        f.start = slice_start(e, kv.first);
+        f.end = jm::wadd(f.start, e->g);
+        f.slot_off = (int32_t)hs.size();
+        f.nslots = 1;
+        hs.push_back(kv.second);
+        hw.push_back(f);
+    }
+    int64_t nrows = 0;
+    if (!hw.empty()) {
+        int rc = launch_fire(e, hw, hs, 1, &nrows);
+        if (rc) return rc;
+        for (int32_t slot : hs) {
+            rc = reset_slot(e, slot);
+            if (rc) return rc;
+        }
+    }
+    out->n = nrows;
+    out->num_aggs = e->cfg.num_aggs;
+    out->on_device = e->cfg.output_on_device ? 1 : 0;
+    const int64_t* cols[3] = {e->o_key, e->o_start, e->o_count};
+    const void* accs[FWA_MAX_AGGS] = {};
+    for (int j = 0; j < e->cfg.num_aggs; ++j) accs[j] = e->o_agg[j];
+    if (e->cfg.output_on_device) {
+        out->key = cols[0];
+        out->slice_start = cols[1];
+        out->count = cols[2];
+        for (int j = 0; j < e->cfg.num_aggs; ++j) out->acc[j] = accs[j];
+        return FWA_OK;
+    }
+    e->h_out.resize(std::max<size_t>((size_t)nrows * 8 * (3 + e->cfg.num_aggs), 8));
+    char* p = e->h_out.data();
+    auto get = [&](const void* d) -> const void* {
+        if (nrows) { hipError_t r = hipMemcpy(p, d, 8 * nrows, hipMemcpyDeviceToHost); if (r != hipSuccess) return nullptr; }
+        const void* r = p;
+        p += 8 * nrows;
+        return r;
+    };
+    out->key = (const int64_t*)get(cols[0]);
+    out->slice_start = (const int64_t*)get(cols[1]);
+    out->count = (const int64_t*)get(cols[2]);
+    for (int j = 0; j < e->cfg.num_aggs; ++j) out->acc[j] = get(accs[j]);
+    if (!out->key || !out->slice_start || !out->count) return fail(e, FWA_E_DEVICE, "partials copy failed");
+    return FWA_OK;
+}
+
 int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
     if (!e) return FWA_E_STATE;
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (out) memset(out, 0, sizeof(*out));
     int64_t nrows = 0;
-    if (wm > e->wm) {
+    if (wm > e->wm && e->kind == FWA_SESSION) {
+        int rc = sync_status(e);
+        if (rc) return rc;
+        const int64_t live = (int64_t)e->h_st->sess_live;
+        if (live > 0) {
+            rc = ensure_out(e, live);
+            if (rc) return rc;
+            HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
+            SessFireArgs f;
+            memset(&f, 0, sizeof(f));
+            f.key_table = e->d_keys;
+            f.capacity = e->capacity;
+            f.wm = wm;
+            f.s_cnt = e->d_scnt;
+            f.s_start = e->d_sstart;
+            f.s_end = e->d_send;
+            f.s_acc = e->d_sacc;
+            f.sstride = e->sstride;
+            f.o_key = e->o_key;
+            f.o_start = e->o_start;
+            f.o_end = e->o_end;
+            for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
+            f.st = e->d_st;
+            HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
+            sess_fire_kernel<<<grid_for(e->capacity + 1, 256 * 16), kBlock, 0, e->stream>>>(f, e->d_ec);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
+            rc = sync_status(e);
+            if (rc) return rc;
+            nrows = (int64_t)e->h_st->rows;
+            float ms = 0.f;
+            HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+            e->fire_ms += ms;
+            e->fire_launches++;
+            e->fire_rows += nrows;
+        }
+        e->wm = wm;
+    } else if (wm > e->wm) {
         const int64_t prev = e->wm;
         // windows of touched slices that fire now: prev < end-1 <= wm  (EventTimeTrigger / isWindowFired)
         std::set<std::pair<int64_t, int64_t>> wins;  // (end, start)
@@ -1873,52 +2433,8 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
             if (f.nslots > 0) hw.push_back(f);
         }
         if (!hw.empty()) {
-            if ((int32_t)hw.size() > e->win_cap) {
-                if (e->d_win) HIPCHK(e, hipFree(e->d_win));
-                e->win_cap = (int32_t)hw.size() * 2;
-                HIPCHK(e, hipMalloc(&e->d_win, sizeof(FireWindow) * e->win_cap));
-            }
-            if ((int32_t)hs.size() > e->win_slots_cap) {
-                if (e->d_win_slots) HIPCHK(e, hipFree(e->d_win_slots));
-                e->win_slots_cap = (int32_t)hs.size() * 2;
-                HIPCHK(e, hipMalloc(&e->d_win_slots, sizeof(int32_t) * e->win_slots_cap));
-            }
-            HIPCHK(e, hipMemcpyAsync(e->d_win, hw.data(), sizeof(FireWindow) * hw.size(), hipMemcpyHostToDevice, e->stream));
-            HIPCHK(e, hipMemcpyAsync(e->d_win_slots, hs.data(), sizeof(int32_t) * hs.size(), hipMemcpyHostToDevice, e->stream));
-            int rc = sync_status(e);
+            int rc = launch_fire(e, hw, hs, 0, &nrows);
             if (rc) return rc;
-            const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
-            rc = ensure_out(e, (int64_t)hw.size() * nkeys);
-            if (rc) return rc;
-            HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
-            FireArgs f;
-            memset(&f, 0, sizeof(f));
-            f.key_table = e->d_keys;
-            f.capacity = e->capacity;
-            f.stride = e->stride;
-            f.slot_base = e->d_slot_base;
-            f.win = e->d_win;
-            f.win_slots = e->d_win_slots;
-            f.nwin = (int32_t)hw.size();
-            f.blocks_per_win = (int32_t)((e->capacity + 1 + (int64_t)kBlock * kFireJ - 1) / ((int64_t)kBlock * kFireJ));
-            f.o_key = e->o_key;
-            f.o_start = e->o_start;
-            f.o_end = e->o_end;
-            for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
-            f.st = e->d_st;
-            const int64_t grid = (int64_t)f.blocks_per_win * (int64_t)hw.size();
-            HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
-            fire_kernel<<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
-            HIPCHK(e, hipGetLastError());
-            HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
-            rc = sync_status(e);
-            if (rc) return rc;
-            nrows = (int64_t)e->h_st->rows;
-            float ms = 0.f;
-            HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
-            e->fire_ms += ms;
-            e->fire_launches++;
-            e->fire_rows += nrows;
         }
         // free slices whose every window is past cleanup (last window: cleanupTime <= wm)
         std::vector<int64_t> dead;
@@ -1981,7 +2497,7 @@ int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
     s->late_dropped = e->late_dropped;
     s->rows_out = e->rows_out;
     s->live_keys = (int64_t)e->h_st->n_keys;
-    s->live_slices = (int64_t)e->live.size();
+    s->live_slices = e->kind == FWA_SESSION ? (int64_t)e->h_st->sess_live : (int64_t)e->live.size();
     s->current_watermark = e->wm;
     s->ingest_launches = e->ingest_launches;
     s->ingest_ms = e->ingest_ms;

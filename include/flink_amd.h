@@ -22,6 +22,9 @@
  *                            -> fireWindow/clearWindow (SliceSharedWindowAggProcessor.java:64-118,
  *                               SliceUnsharedWindowAggProcessor.java:46-55)
  *   fwa_flush              SlicingWindowProcessor.prepareCheckpoint (RecordsWindowBuffer.flush :107-118)
+ *   fwa_drain_partials     LocalSlicingWindowAggOperator -> RecordsWindowBuffer.flush (local half of two-phase)
+ *                            LocalSlicingWindowAggOperator.java:111-137
+ *   fwa_push_partials      GlobalAggCombiner.combine (global half)  GlobalAggCombiner.java:77-110
  *   fwa_key_groups         KeyGroupRangeAssignment.assignToKeyGroup + computeOperatorIndexForKeyGroup
  *                            flink-runtime/.../state/KeyGroupRangeAssignment.java:63-127
  *                          (the keyBy partitioner KeyGroupStreamPartitioner.selectChannel :55-65)
@@ -176,6 +179,34 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out);
 int fwa_flush(fwa_engine* e);
 
 int fwa_get_stats(fwa_engine* e, fwa_stats* out);
+
+/* ---- two-phase (local / global) aggregation ----
+ * Flink's two-phase window plan (TwoStageOptimizedWindowAggregateRule.java:88-103):
+ *   LocalSlicingWindowAggOperator (LocalSlicingWindowAggOperator.java:111-131) pre-aggregates each
+ *   source subtask's records per (key, slice) and emits partial accumulators, which are shuffled by key
+ *   group to GlobalAggCombiner (GlobalAggCombiner.java:77-110), which merges them into the window state.
+ * Used by the multi-GPU keyBy exchange to ship per-(key, slice) partials instead of raw records.
+ * Not available for SESSION windows (FWA_E_UNSUPPORTED). */
+typedef struct fwa_partials {
+    int64_t n;
+    int32_t on_device;           /* pointers below are device pointers if 1 */
+    int32_t num_aggs;
+    const int64_t* key;
+    const int64_t* slice_start;  /* start timestamp of the (key, slice) accumulator */
+    const int64_t* count;        /* COUNT(*) of the records it holds */
+    const void* acc[FWA_MAX_AGGS]; /* 8-byte accumulator of agg j: i64 sum, f64 sum bits, or the engine's
+                                      order-preserving MIN/MAX key; COUNT aggregates repeat count */
+} fwa_partials;
+
+/* Export every (key, slice) accumulator that received records since the last drain, and reset those
+ * slices (the engine stays a pure pre-aggregator when it is drained after every push). */
+int fwa_drain_partials(fwa_engine* e, fwa_partials* out);
+
+/* Merge partial accumulators (as produced by fwa_drain_partials on another handle with the same
+ * window and aggregate configuration) into this handle's state. slice_ts may be any timestamp inside
+ * the slice. Late partials are dropped like records (their counts are added to late_dropped_out). */
+int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_ts, const int64_t* count,
+                      const void* const* acc, int64_t n, int32_t flags, int64_t* late_dropped_out);
 
 /* Reset the kernel timing counters of fwa_stats (bench warm-up). */
 int fwa_reset_timers(fwa_engine* e);

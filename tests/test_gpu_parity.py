@@ -32,8 +32,7 @@ def eng_mod():
     return engine
 
 
-@pytest.mark.parametrize("case", [c for c in KATS["operators"] if c["window_kind"] != "SESSION"],
-                         ids=lambda c: c["name"].split(" ")[0])
+@pytest.mark.parametrize("case", KATS["operators"], ids=lambda c: c["name"].split(" ")[0])
 def test_reference_kats_on_gpu(eng_mod, case):
     replay_kat(case, eng_mod.WindowAggregator)
 
@@ -50,6 +49,8 @@ CONFIGS = [
     dict(window_kind="SLIDE", semantics="DATASTREAM", size_ms=5000, slide_ms=2000, offset_ms=300),
     dict(window_kind="SLIDE", semantics="TABLE", size_ms=4000, slide_ms=1000),
     dict(window_kind="CUMULATE", semantics="TABLE", size_ms=3000, slide_ms=1000),
+    dict(window_kind="SESSION", semantics="DATASTREAM", gap_ms=700),
+    dict(window_kind="SESSION", semantics="DATASTREAM", gap_ms=2500),
 ]
 
 
@@ -246,3 +247,46 @@ def test_c2_scaled_properties(eng_mod):
     assert tot_cnt + dropped == n
     assert dropped == 0  # bounded out-of-orderness D: nothing is late
     assert tot_sum == int(vh.astype(object).sum())
+
+
+def test_session_edge_cases(eng_mod):
+    """Touching windows merge (TimeWindow.intersects is inclusive), a late record survives only when it
+    touches an in-flight session, a fired session is retired (a later touching record opens a new one),
+    the INT64_MIN key and window-end overflow (ts + gap wraps) behave as in the reference."""
+    from oracle.oracle import Oracle
+    cfg = A.make_config(window_kind="SESSION", gap_ms=1000, aggs=[("COUNT", 0), ("SUM_I64", 0), ("MAX_I64", 0)],
+                        key_capacity=1024)
+    L = A.LONG_MAX
+    steps = [
+        ([(1, 0), (1, 1000), (1, 2000), (2, 5), (-2**63, 7)], 500),      # 1: [0,3000) via touching merges
+        ([(1, 100), (2, 6000), (1, 2999)], 1500),                          # late 100 merges into in-flight session
+        ([(2, 100), (1, 5000), (2, 4000), (5, 2500)], 2998),               # key 2 @100: late, alone -> dropped
+        ([(1, 2500), (1, 3000), (3, L - 10), (5, 1600), (6, 1600)], 4000), # late 5@1600 touches in-flight -> kept
+        ([(1, 4100), (1, 3999), (3, L - 5)], L),                           # 1@3999: fired session retired -> new
+    ]
+    g, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
+    for recs, wm in steps:
+        k = np.array([r[0] for r in recs], np.int64)
+        t = np.array([r[1] for r in recs], np.int64)
+        v = np.arange(len(recs), dtype=np.int64) * 7 + 3
+        assert g.push(k, t, [v]) == o.push(k, t, [v])
+        assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), A.agg_names(cfg), ctx="wm=%d" % wm)
+    assert g.stats().late_dropped == o.stats().late_dropped
+
+
+def test_session_hot_key_many_records(eng_mod):
+    """One key with thousands of records in a batch (a long sequential run) plus many short keys."""
+    from oracle.oracle import Oracle
+    rng = np.random.default_rng(3)
+    n = 20_000
+    k = np.where(rng.random(n) < 0.3, 42, rng.integers(0, 3000, n)).astype(np.int64)
+    t = np.sort(rng.integers(0, 200_000, n)).astype(np.int64) - rng.integers(0, 3000, n)
+    v = rng.integers(-1000, 1000, n).astype(np.int64)
+    cfg = A.make_config(window_kind="SESSION", gap_ms=300, aggs=[("COUNT", 0), ("SUM_I64", 0), ("MIN_I64", 0)],
+                        key_capacity=4096)
+    g, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
+    for b in range(4):
+        sl = slice(b * n // 4, (b + 1) * n // 4)
+        assert g.push(k[sl], t[sl], [v[sl]]) == o.push(k[sl], t[sl], [v[sl]])
+        wm = int(t[: (b + 1) * n // 4].max()) - 3001 if b < 3 else A.LONG_MAX
+        assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), A.agg_names(cfg), ctx="b=%d" % b)
