@@ -69,6 +69,14 @@ class Out(C.Structure):
     ]
 
 
+class Partials(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("on_device", C.c_int32), ("num_aggs", C.c_int32),
+        ("key", C.c_void_p), ("slice_start", C.c_void_p), ("count", C.c_void_p),
+        ("acc", C.c_void_p * FWA_MAX_AGGS),
+    ]
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("records_in", C.c_int64), ("late_dropped", C.c_int64), ("rows_out", C.c_int64),

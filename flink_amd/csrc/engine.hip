@@ -317,6 +317,8 @@ struct PartArgs {
     int64_t n;
     int64_t wm;
     const uint8_t* relcode;            // [kRelCap] per relative slice: kCodeAccept / kCodeDrop / kCodeSlow
+    const int32_t* rel2slot;           // [kRelCap] slot of each relative slice (touched marking)
+    int32_t* touched;                  // per slot
     int32_t* spill;
     int64_t q_base;
     unsigned long long* b_key;         // [np][capb]
@@ -375,9 +377,9 @@ __global__ void __launch_bounds__(THREADS, MINW) partition_kernel(PartArgs a, co
     __shared__ unsigned long long s_val[NV > 0 ? NV : 1][NV > 0 ? kTile : 1];
     __shared__ uint16_t s_rel[kTile];
     __shared__ uint16_t s_part[kTile];
+    __shared__ uint16_t s_src[kTile];   // position of the record inside the tile (bucket-overflow spill)
     __shared__ uint32_t wsum[kThreadsP / 64];
     __shared__ uint32_t s_total;
-    __shared__ int s_overflow;
     __shared__ uint8_t s_code[kRelCap];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -389,7 +391,6 @@ __global__ void __launch_bounds__(THREADS, MINW) partition_kernel(PartArgs a, co
     const int64_t ntiles = (a.n + kTile - 1) / kTile;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         for (int i = tid; i < a.np; i += kThreadsP) hist[i] = 0;
-        if (tid == 0) s_overflow = 0;
         __syncthreads();
         unsigned long long r_key[ITEMS], r_v0[ITEMS], r_v1[ITEMS];
         uint32_t r_pos[ITEMS];   // (p << 16 | rank) or ~0u when the record does not go to a bucket
@@ -461,6 +462,7 @@ __global__ void __launch_bounds__(THREADS, MINW) partition_kernel(PartArgs a, co
             s_key[sidx] = r_key[j];
             s_rel[sidx] = r_rel[j];
             s_part[sidx] = (uint16_t)p;
+            s_src[sidx] = (uint16_t)(j * kThreadsP + tid);
             if (NV > 0) s_val[0][sidx] = r_v0[j];
             if (NV > 1) s_val[NV > 1 ? 1 : 0][sidx] = r_v1[j];
         }
@@ -469,7 +471,10 @@ __global__ void __launch_bounds__(THREADS, MINW) partition_kernel(PartArgs a, co
         for (uint32_t sidx = tid; sidx < total; sidx += kThreadsP) {
             const uint32_t p = s_part[sidx];
             const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
-            if (dst >= (uint64_t)a.capb) { s_overflow = 1; continue; }
+            if (dst >= (uint64_t)a.capb) {      // sub-bucket full (skewed keys): the v1 replay takes it
+                a.spill[atomicAdd(&a.st->spill_n, 1)] = (int32_t)(t0 + s_src[sidx]);
+                continue;
+            }
             if (a.abl & 2) { if (s_key[sidx] == 0x1234567ull) a.b_key[0] = 1; continue; }
             const uint64_t o = ((uint64_t)p * kSub + (blockIdx.x % kSub)) * (uint64_t)a.capb + dst;
             a.b_key[o] = s_key[sidx];
@@ -478,7 +483,6 @@ __global__ void __launch_bounds__(THREADS, MINW) partition_kernel(PartArgs a, co
             if (NV > 1) a.b_val1[o] = s_val[NV > 1 ? 1 : 0][sidx];
         }
         __syncthreads();
-        if (tid == 0 && s_overflow) atomicOr(&a.st->key_full, 2);    // bucket overflow: host reruns on the v1 path
     }
     for (int sh = 32; sh >= 1; sh >>= 1) {
         dropped += __shfl_xor(dropped, sh);
@@ -492,6 +496,13 @@ __global__ void __launch_bounds__(THREADS, MINW) partition_kernel(PartArgs a, co
             atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
         }
     }
+    // mark the slots of the accepted slice range touched (over-marking is harmless: a touched slot
+    // without records emits nothing and is merely re-cleared)
+    if (relmin != ~0u)
+        for (uint32_t r = relmin + (uint32_t)lane; r <= relmax; r += 64) {
+            const int32_t slot = a.rel2slot[r];
+            if (slot >= 0 && a.touched[slot] == 0) a.touched[slot] = 1;
+        }
 }
 
 struct StragEntry {
@@ -791,8 +802,9 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
 }
 
 // Stragglers: bucket entries older than their combiner's window, applied with global atomics.
-__global__ void straggler_kernel(CombineArgs a, const EngineConst* __restrict__ cp, int32_t n) {
+__global__ void straggler_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
+    const int32_t n = (int32_t)min((int64_t)*a.strag_n, a.strag_cap);
     for (int32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
         const StragEntry se = a.strag[t];
         const int32_t slot = a.rel2slot[a.b_rel[se.o]];
@@ -1153,6 +1165,21 @@ __global__ void __launch_bounds__(kBlock) sess_fire_kernel(SessFireArgs f, const
 // ------------------------------------------------------------------------------------------------
 // utility kernels
 
+// Per-push reset of the device status (all but n_keys / rows; min_q = ~0), the want-set and, for the
+// two-phase path, the bucket cursors and straggler count: one launch instead of a string of memsets.
+__global__ void push_reset_kernel(DevStatus* st, unsigned long long* want, int32_t nwant, uint32_t* bcnt, int32_t nbcnt,
+                                  int32_t* strag_n) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int32_t nt = gridDim.x * blockDim.x;
+    if (t == 0) {
+        st->error = 0; st->spill_n = 0; st->want_n = 0; st->key_full = 0;
+        st->dropped = 0; st->late_fire = 0; st->max_q = 0; st->min_q = ~0ull;
+        if (strag_n) strag_n[0] = 0;
+    }
+    for (int32_t i = t; i < nwant; i += nt) want[i] = 0ull;
+    for (int32_t i = t; i < nbcnt; i += nt) bcnt[i] = 0u;
+}
+
 __global__ void fill_u64_kernel(unsigned long long* p, unsigned long long v, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -1280,6 +1307,7 @@ struct fwa_engine {
     StragEntry* d_strag = nullptr;
     int64_t strag_cap = 0;
     int32_t* d_strag_n = nullptr;
+    bool v2_timing_pending = false;   // Phase P / A events recorded, read after the next sync
     size_t combine_lds = 0;
     int32_t partition_grid = 256;
     // kernel timing (HIP events on this handle's stream)
@@ -1300,9 +1328,18 @@ struct fwa_engine {
     int32_t kid_bits = 0;
     // partial accumulators (fwa_drain_partials)
     int64_t* o_count = nullptr;
+    // pinned upload arena: small host->device uploads (directory, code table, fire lists) are copied into
+    // it and enqueued without a host sync; it is recycled at every stream synchronisation
+    char* h_arena = nullptr;
+    size_t arena_cap = 0, arena_used = 0;
+    int32_t* h_touched = nullptr;     // pinned landing buffer of the touched-flag mirror
+    int32_t h_touched_cap = 0;
 };
 
 namespace {
+
+int upload(fwa_engine* e, void* dst, const void* src, size_t bytes);
+int stream_sync(fwa_engine* e);
 
 int fail(fwa_engine* e, int code, const std::string& msg) {
     if (e) e->err = msg;
@@ -1457,9 +1494,9 @@ int grow_slots(fwa_engine* e, int32_t add) {
         HIPCHK(e, hipMalloc(&e->d_slot_base, sizeof(void*) * e->slot_base_cap));
         HIPCHK(e, hipMalloc(&e->d_touched, sizeof(int32_t) * e->slot_base_cap));
     }
-    HIPCHK(e, hipMemcpyAsync(e->d_slot_base, e->slot_ptr.data(), sizeof(void*) * n, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->d_touched, e->touched.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
-    return FWA_OK;
+    int rc = upload(e, e->d_slot_base, e->slot_ptr.data(), sizeof(void*) * n);
+    if (rc) return rc;
+    return upload(e, e->d_touched, e->touched.data(), sizeof(int32_t) * n);
 }
 
 int alloc_slice(fwa_engine* e, int64_t q) {
@@ -1528,8 +1565,7 @@ int publish_dir(fwa_engine* e) {
         d.flags = 1 | (always ? 2 : 0);
         d.first_maxts = LONG_MAX_J;
     }
-    HIPCHK(e, hipMemcpyAsync(e->d_dir, h.data(), sizeof(DirEntry) * h.size(), hipMemcpyHostToDevice, e->stream));
-    return FWA_OK;
+    return upload(e, e->d_dir, h.data(), sizeof(DirEntry) * h.size());
 }
 
 int ensure_out(fwa_engine* e, int64_t rows) {
@@ -1547,20 +1583,62 @@ int ensure_out(fwa_engine* e, int64_t rows) {
     return FWA_OK;
 }
 
-int sync_status(fwa_engine* e) {
-    HIPCHK(e, hipMemcpyAsync(e->h_st, e->d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, e->stream));
+int stream_sync(fwa_engine* e) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->arena_used = 0;
     return FWA_OK;
 }
 
-int reset_push_status(fwa_engine* e) {
-    // zero everything but n_keys / rows; min_q starts at ~0
-    DevStatus z;
-    memset(&z, 0, sizeof(z));
-    HIPCHK(e, hipMemsetAsync(e->d_st, 0, offsetof(DevStatus, n_keys), e->stream));
-    HIPCHK(e, hipMemsetAsync(&e->d_st->late_fire, 0, 8, e->stream));
-    HIPCHK(e, hipMemsetAsync(&e->d_st->max_q, 0, 8, e->stream));
-    HIPCHK(e, hipMemsetAsync(&e->d_st->min_q, 0xFF, 8, e->stream));
+// The one host synchronisation of a push / fire: device status + touched-flag mirror in one round trip.
+int sync_status(fwa_engine* e) {
+    HIPCHK(e, hipMemcpyAsync(e->h_st, e->d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, e->stream));
+    const int32_t ns = (int32_t)e->touched.size();
+    if (ns > 0 && e->d_touched) {
+        if (ns > e->h_touched_cap) {
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            if (e->h_touched) HIPCHK(e, hipHostFree(e->h_touched));
+            e->h_touched = nullptr;
+            e->h_touched_cap = std::max<int32_t>(256, ns * 2);
+            HIPCHK(e, hipHostMalloc(&e->h_touched, sizeof(int32_t) * e->h_touched_cap));
+        }
+        HIPCHK(e, hipMemcpyAsync(e->h_touched, e->d_touched, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, e->stream));
+    }
+    int rc = stream_sync(e);
+    if (rc) return rc;
+    if (ns > 0 && e->d_touched) memcpy(e->touched.data(), e->h_touched, sizeof(int32_t) * ns);
+    return FWA_OK;
+}
+
+// Enqueue a host->device copy of a small host buffer through the pinned arena (no host sync; the
+// source may be reused as soon as this returns).
+int upload(fwa_engine* e, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return FWA_OK;
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (need > e->arena_cap) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (e->h_arena) HIPCHK(e, hipHostFree(e->h_arena));
+        e->h_arena = nullptr;
+        e->arena_cap = std::max<size_t>(need * 2, (size_t)4 << 20);
+        HIPCHK(e, hipHostMalloc((void**)&e->h_arena, e->arena_cap));
+        e->arena_used = 0;
+    }
+    if (e->arena_used + need > e->arena_cap) {   // arena exhausted before a sync: drain the stream
+        int rc = stream_sync(e);
+        if (rc) return rc;
+    }
+    char* p = e->h_arena + e->arena_used;
+    memcpy(p, src, bytes);
+    HIPCHK(e, hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, e->stream));
+    e->arena_used += need;
+    return FWA_OK;
+}
+
+int reset_push_status(fwa_engine* e, bool v2bufs = false) {
+    // zero everything but n_keys / rows; min_q starts at ~0; want-set; v2: bucket cursors, stragglers
+    push_reset_kernel<<<64, kBlock, 0, e->stream>>>(e->d_st, e->d_want, e->d_want ? kWantCap : 0,
+                                                    v2bufs ? e->d_bcnt : nullptr, v2bufs ? kMaxPart * kSub : 0,
+                                                    v2bufs ? e->d_strag_n : nullptr);
+    HIPCHK(e, hipGetLastError());
     return FWA_OK;
 }
 
@@ -1587,6 +1665,8 @@ void fwa_destroy(fwa_engine* e) {
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
     for (void* p : e->chunks) (void)hipFree(p);
     if (e->h_st) (void)hipHostFree(e->h_st);
+    if (e->h_arena) (void)hipHostFree(e->h_arena);
+    if (e->h_touched) (void)hipHostFree(e->h_touched);
     for (hipEvent_t ev : e->ev) if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -1778,7 +1858,6 @@ static int launch_ingest(fwa_engine* e, IngestArgs& a, bool replay) {
     a.slot_base = e->d_slot_base;
     a.stride = e->stride;
     a.st = e->d_st;
-    HIPCHK(e, hipMemsetAsync(e->d_want, 0, sizeof(unsigned long long) * kWantCap, e->stream));
     const int grid = grid_for(a.n, 256 * 32);
     HIPCHK(e, hipEventRecord(e->ev[0], e->stream));
     if (replay) ingest_kernel<true><<<grid, kBlock, 0, e->stream>>>(a, e->d_ec);
@@ -1848,10 +1927,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else if (e->lateness > 0 && a.wm >= jm::wsub(first_window_end(e, kv.first), 1)) code[rel] = kCodeSlow;
         else code[rel] = kCodeAccept;
     }
-    HIPCHK(e, hipMemcpyAsync(e->d_rel2slot, r2s.data(), (sizeof(int32_t) + 1) * kRelCap, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_bcnt, 0, sizeof(uint32_t) * kMaxPart * kSub, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_strag_n, 0, 16, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_want, 0, sizeof(unsigned long long) * kWantCap, e->stream));
+    rc = upload(e, e->d_rel2slot, r2s.data(), (sizeof(int32_t) + 1) * kRelCap);
+    if (rc) return rc;
+    rc = reset_push_status(e, true);
+    if (rc) return rc;
     PartArgs pa;
     memset(&pa, 0, sizeof(pa));
     pa.keys = a.keys;
@@ -1861,6 +1940,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.n = a.n;
     pa.wm = a.wm;
     pa.relcode = (const uint8_t*)(e->d_rel2slot + kRelCap);
+    pa.rel2slot = e->d_rel2slot;
+    pa.touched = e->d_touched;
     pa.spill = e->d_spill;
     pa.q_base = q_base;
     pa.b_key = e->d_bkey;
@@ -1902,22 +1983,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
 #undef PLAUNCH
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[5], e->stream));
-    rc = sync_status(e);
-    if (rc) return rc;
-    float ms = 0.f;
-    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[4], e->ev[5]));
-    e->partition_ms += ms;
-    e->ingest_ms += ms;
-    if (e->h_st->error) { *ran = true; return FWA_OK; }   // reported by the caller's status loop
-    if (e->h_st->key_full & 2) return FWA_OK;             // bucket overflow: caller reruns on v1
-    if (e->h_st->min_q != ~0ull) {                        // slices that received records (over-marking is harmless)
-        bool changed = false;
-        const int64_t q0 = jm::unord_i64(e->h_st->min_q), q1 = jm::unord_i64(e->h_st->max_q);
-        for (auto it = e->live.lower_bound(q0); it != e->live.end() && it->first <= q1; ++it)
-            if (!e->touched[it->second]) { e->touched[it->second] = 1; changed = true; }
-        if (changed)
-            HIPCHK(e, hipMemcpyAsync(e->d_touched, e->touched.data(), sizeof(int32_t) * e->touched.size(), hipMemcpyHostToDevice, e->stream));
-    }
+    // no host round trip between the phases: Phase P marks touched slots itself, spills bucket
+    // overflow to the v1 replay list, and the straggler pass reads its count on the device
     CombineArgs ca;
     memset(&ca, 0, sizeof(ca));
     ca.b_key = e->d_bkey;
@@ -1963,16 +2030,14 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     else if (avar == 6) C3LAUNCH(4, 512);
 
     HIPCHK(e, hipGetLastError());
-    int32_t nstrag = 0;
-    HIPCHK(e, hipMemcpyAsync(&e->h_st->pad, e->d_strag_n, 4, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    nstrag = std::min<int64_t>(e->h_st->pad, e->strag_cap);
-    if (nstrag > 0) straggler_kernel<<<grid_for(nstrag), kBlock, 0, e->stream>>>(ca, e->d_ec, nstrag);
+    straggler_kernel<<<256, kBlock, 0, e->stream>>>(ca, e->d_ec);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[7], e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[6], e->ev[7]));
+    e->v2_timing_pending = true;
     if (aprof) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        float ms = 0.f;
+        HIPCHK(e, hipEventElapsedTime(&ms, e->ev[6], e->ev[7]));
         std::vector<long long> hp(8 * e->np);
         HIPCHK(e, hipMemcpy(hp.data(), d_prof, sizeof(long long) * 8 * e->np, hipMemcpyDeviceToHost));
         double tot[8] = {0};
@@ -1980,8 +2045,6 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         fprintf(stderr, "[aprof] kernel %.3f ms; per-block avg cycles: %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n",
                 ms, tot[0], tot[1], tot[2], tot[3], tot[4], tot[5], tot[6], tot[7]);
     }
-    e->combine_ms += ms;
-    e->ingest_ms += ms;
     e->ingest_launches++;
     e->ingest_records += a.n;
     *ran = true;
@@ -2076,10 +2139,11 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
         e->win_slots_cap = (int32_t)hs.size() * 2;
         HIPCHK(e, hipMalloc(&e->d_win_slots, sizeof(int32_t) * e->win_slots_cap));
     }
-    HIPCHK(e, hipMemcpyAsync(e->d_win, hw.data(), sizeof(FireWindow) * hw.size(), hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->d_win_slots, hs.data(), sizeof(int32_t) * hs.size(), hipMemcpyHostToDevice, e->stream));
-    int rc = sync_status(e);
+    int rc = upload(e, e->d_win, hw.data(), sizeof(FireWindow) * hw.size());
     if (rc) return rc;
+    rc = upload(e, e->d_win_slots, hs.data(), sizeof(int32_t) * hs.size());
+    if (rc) return rc;
+    // rows <= windows x distinct keys; n_keys is current: every push ends with a status sync
     const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
     rc = ensure_out(e, (int64_t)hw.size() * nkeys);
     if (rc) return rc;
@@ -2120,8 +2184,7 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
 // Shared ingest driver: two-phase path when allowed, else the v1 kernel; slice-miss replays;
 // lookahead slice allocation; stats.
 static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, int64_t* late_dropped_out) {
-    int rc = reset_push_status(e);
-    if (rc) return rc;
+    int rc = FWA_OK;
     bool ran_v2 = false;
     if (e->v2 && allow_v2) {
         rc = push_v2(e, a, &ran_v2);
@@ -2135,9 +2198,20 @@ static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, i
     }
     int64_t dropped = 0;
     int64_t qmin = LONG_MAX_J, qmax = LONG_MIN_J;
+    bool republish = false;
     for (int round = 0;; ++round) {
         rc = sync_status(e);
         if (rc) return rc;
+        if (e->v2_timing_pending) {
+            float ms = 0.f;
+            HIPCHK(e, hipEventElapsedTime(&ms, e->ev[4], e->ev[5]));
+            e->partition_ms += ms;
+            e->ingest_ms += ms;
+            HIPCHK(e, hipEventElapsedTime(&ms, e->ev[6], e->ev[7]));
+            e->combine_ms += ms;
+            e->ingest_ms += ms;
+            e->v2_timing_pending = false;
+        }
         if (!ran_v2 || round > 0) { rc = account_ingest(e); if (rc) return rc; }
         const DevStatus st = *e->h_st;
         if (st.error) {
@@ -2176,9 +2250,8 @@ static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, i
         rc = launch_ingest(e, b, true);
         if (rc) return rc;
     }
-    if (!e->negative.empty()) { e->negative.clear(); rc = publish_dir(e); if (rc) return rc; }
-    // mirror touched flags; extend the lookahead so ordered streams rarely miss
-    HIPCHK(e, hipMemcpy(e->touched.data(), e->d_touched, sizeof(int32_t) * e->touched.size(), hipMemcpyDeviceToHost));
+    if (!e->negative.empty()) { e->negative.clear(); republish = true; }
+    // (touched flags were mirrored by the last sync) extend the lookahead so ordered streams rarely miss
     if (qmax != LONG_MIN_J) {
         const int64_t span = qmax - qmin + 1;
         e->lookahead = std::min<int64_t>(std::max<int64_t>(e->lookahead, 2 * span), 256);
@@ -2187,11 +2260,10 @@ static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, i
         const size_t slot_bytes = (size_t)e->stride * 8 * e->nacc;
         int64_t budget_slots = (int64_t)(e->mem_budget / std::max<size_t>(slot_bytes, 1));
         int64_t la = std::min<int64_t>(e->lookahead, std::max<int64_t>(0, budget_slots - (int64_t)e->live.size()));
-        bool changed = false;
         for (int64_t q = e->max_q + 1; q <= e->max_q + la; ++q)
-            if (!e->live.count(q)) { rc = alloc_slice(e, q); if (rc) return rc; changed = true; }
-        if (changed) { rc = publish_dir(e); if (rc) return rc; }
+            if (!e->live.count(q)) { rc = alloc_slice(e, q); if (rc) return rc; republish = true; }
     }
+    if (republish) { rc = publish_dir(e); if (rc) return rc; }
     e->records_in += n;
     e->late_dropped += dropped;
     if (late_dropped_out) *late_dropped_out = dropped;
@@ -2305,7 +2377,27 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
 
 // Export every (key, slice) accumulator that received records since the last drain and reset those
 // slices (the local half of LocalSlicingWindowAggOperator -> GlobalAggCombiner).
-int fwa_drain_partials(fwa_engine* e, fwa_partials* out) {
+// Free slices whose every window is past cleanup at wm (last window: cleanupTime <= wm).
+static int retire_slices(fwa_engine* e, int64_t wm) {
+    std::vector<int64_t> dead;
+    for (auto& kv : e->live) {
+        int64_t thr;
+        bool always;
+        accept_threshold(e, kv.first, &thr, &always);
+        if (!always && wm >= thr) dead.push_back(kv.first);
+    }
+    for (int64_t q : dead) {
+        int rc = release_slot(e, e->live[q]);
+        if (rc) return rc;
+        e->live.erase(q);
+    }
+    if (!dead.empty()) return publish_dir(e);
+    return FWA_OK;
+}
+
+// Local half of LocalSlicingWindowAggOperator -> GlobalAggCombiner: export the (key, slice)
+// accumulators of every touched slice complete at wm, reset them, forward the watermark.
+int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     if (!e || !out) return FWA_E_ARG;
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
     HIPCHK(e, hipSetDevice(e->cfg.device));
@@ -2317,6 +2409,7 @@ int fwa_drain_partials(fwa_engine* e, fwa_partials* out) {
         FireWindow f;
         f.start = slice_start(e, kv.first);
         f.end = jm::wadd(f.start, e->g);
+        if (wm != LONG_MAX_J && !(jm::wsub(f.end, 1) <= wm)) continue;   // slice not complete at wm
         f.slot_off = (int32_t)hs.size();
         f.nslots = 1;
         hs.push_back(kv.second);
@@ -2330,6 +2423,11 @@ int fwa_drain_partials(fwa_engine* e, fwa_partials* out) {
             rc = reset_slot(e, slot);
             if (rc) return rc;
         }
+    }
+    if (wm > e->wm) {   // forward the watermark: lateness from now on, release slices past cleanup
+        int rc = retire_slices(e, wm);
+        if (rc) return rc;
+        e->wm = wm;
     }
     out->n = nrows;
     out->num_aggs = e->cfg.num_aggs;
@@ -2436,20 +2534,8 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
             int rc = launch_fire(e, hw, hs, 0, &nrows);
             if (rc) return rc;
         }
-        // free slices whose every window is past cleanup (last window: cleanupTime <= wm)
-        std::vector<int64_t> dead;
-        for (auto& kv : e->live) {
-            int64_t thr;
-            bool always;
-            accept_threshold(e, kv.first, &thr, &always);
-            if (!always && wm >= thr) dead.push_back(kv.first);
-        }
-        for (int64_t q : dead) {
-            int rc = release_slot(e, e->live[q]);
-            if (rc) return rc;
-            e->live.erase(q);
-        }
-        if (!dead.empty()) { int rc = publish_dir(e); if (rc) return rc; }
+        int rc = retire_slices(e, wm);
+        if (rc) return rc;
         e->wm = wm;
     }
     e->rows_out += nrows;
@@ -2485,7 +2571,8 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
 
 int fwa_flush(fwa_engine* e) {
     if (!e) return FWA_E_STATE;
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    int rc = stream_sync(e);
+    if (rc) return rc;
     return FWA_OK;
 }
 

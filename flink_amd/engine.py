@@ -36,6 +36,11 @@ def lib():
     L.fwa_push.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                            C.c_int32, C.POINTER(C.c_int64)]
     L.fwa_push.restype = C.c_int
+    L.fwa_drain_partials.argtypes = [C.c_void_p, C.c_int64, C.POINTER(A.Partials)]
+    L.fwa_drain_partials.restype = C.c_int
+    L.fwa_push_partials.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                    C.c_int32, C.POINTER(C.c_int64)]
+    L.fwa_push_partials.restype = C.c_int
     L.fwa_flush.argtypes = [C.c_void_p]
     L.fwa_flush.restype = C.c_int
     L.fwa_version.restype = C.c_char_p
@@ -135,6 +140,40 @@ class WindowAggregator:
         for j, name in enumerate(self.names):
             res["agg%d" % j] = dev_view(out.agg[j], n, np.dtype(A.AGG_RESULT_DTYPE[name]))
         return res
+
+    # -- two-phase aggregation (LocalSlicingWindowAggOperator -> GlobalAggCombiner) --
+    def drain_partials(self, wm):
+        """Local pre-aggregator watermark step: export the (key, slice) accumulators of every slice
+        complete at wm and forward the watermark. Returns dict key/slice_start/count/acc<j> (numpy, or
+        zero-copy torch CUDA views valid until the next call when output_on_device=1)."""
+        out = A.Partials()
+        _check(lib().fwa_drain_partials(self.h, int(wm), C.byref(out)), self.h)
+        n = out.n
+        i8 = np.dtype("i8")
+        if out.on_device:
+            conv = dev_view
+        else:
+            conv = _host_to_np
+        res = {"key": conv(out.key, n, i8), "slice_start": conv(out.slice_start, n, i8), "count": conv(out.count, n, i8)}
+        for j in range(out.num_aggs):
+            res["acc%d" % j] = conv(out.acc[j], n, i8)
+        return res
+
+    def push_partials(self, keys, slice_ts, count, accs):
+        """Merge partial accumulators (from drain_partials on a handle with the same window / aggregate
+        configuration) into this handle's state; returns the number of late records dropped."""
+        device = _is_torch_cuda(keys)
+        if not device:
+            keys = np.ascontiguousarray(keys, np.int64)
+            slice_ts = np.ascontiguousarray(slice_ts, np.int64)
+            count = np.ascontiguousarray(count, np.int64)
+            accs = [np.ascontiguousarray(a).view(np.int64) for a in accs]
+        arr = (C.c_void_p * A.FWA_MAX_AGGS)(*([_ptr(a).value for a in accs] + [None] * (A.FWA_MAX_AGGS - len(accs))))
+        dropped = C.c_int64(0)
+        rc = lib().fwa_push_partials(self.h, _ptr(keys), _ptr(slice_ts), _ptr(count), arr, int(keys.shape[0]),
+                                     A.PUSH_DEVICE_PTRS if device else 0, C.byref(dropped))
+        _check(rc, self.h)
+        return dropped.value
 
     def flush(self):
         _check(lib().fwa_flush(self.h), self.h)

@@ -198,9 +198,13 @@ typedef struct fwa_partials {
                                       order-preserving MIN/MAX key; COUNT aggregates repeat count */
 } fwa_partials;
 
-/* Export every (key, slice) accumulator that received records since the last drain, and reset those
- * slices (the engine stays a pure pre-aggregator when it is drained after every push). */
-int fwa_drain_partials(fwa_engine* e, fwa_partials* out);
+/* Local pre-aggregator watermark step (LocalSlicingWindowAggOperator: flush the buffer, forward the
+ * watermark). Exports, instead of firing, the (key, slice) accumulators of every slice that received
+ * records and is complete at wm (slice end - 1 <= wm; every such slice when wm == INT64_MAX), resets
+ * them, then advances this handle's watermark to wm (records for fired windows are late from then on;
+ * slices past cleanup are released). A handle drained this way never emits window rows itself: the
+ * owner merges the partials with fwa_push_partials before advancing its own watermark to wm. */
+int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out);
 
 /* Merge partial accumulators (as produced by fwa_drain_partials on another handle with the same
  * window and aggregate configuration) into this handle's state. slice_ts may be any timestamp inside

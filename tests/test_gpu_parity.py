@@ -290,3 +290,31 @@ def test_session_hot_key_many_records(eng_mod):
         assert g.push(k[sl], t[sl], [v[sl]]) == o.push(k[sl], t[sl], [v[sl]])
         wm = int(t[: (b + 1) * n // 4].max()) - 3001 if b < 3 else A.LONG_MAX
         assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), A.agg_names(cfg), ctx="b=%d" % b)
+
+
+@pytest.mark.parametrize("ci", [i for i, c in enumerate(CONFIGS) if c["window_kind"] != "SESSION"])
+@pytest.mark.parametrize("aggs", [I64_AGGS, F64_AGGS], ids=["i64", "f64"])
+def test_two_phase_partials_vs_oracle(eng_mod, ci, aggs):
+    """Flink's two-phase plan (TwoStageOptimizedWindowAggregateRule.java:88-103): two local
+    pre-aggregators (LocalSlicingWindowAggOperator) drain (key, slice) partials at every watermark, the
+    owner merges them (GlobalAggCombiner.java:77-110) and fires. Rows and late-drop totals must equal
+    one operator over the union of the streams."""
+    from oracle.oracle import Oracle
+    cfg = A.make_config(aggs=aggs, key_capacity=4096, **CONFIGS[ci])
+    names = A.agg_names(cfg)
+    stream = random_stream(300 + ci, 30_000, 500, 50_000, 1200)
+    loc = [eng_mod.WindowAggregator(cfg) for _ in range(2)]
+    glob, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
+    dropped_g = dropped_o = 0
+    for (k, t, cols, wm) in batches_of(stream, 9, 1200):
+        dropped_o += o.push(k, t, cols)
+        for s in range(2):
+            sl = slice(s, None, 2)
+            dropped_g += loc[s].push(k[sl], t[sl], [c[sl] for c in cols])
+        for s in range(2):
+            p = loc[s].drain_partials(wm)
+            dropped_g += glob.push_partials(p["key"], p["slice_start"], p["count"],
+                                            [p["acc%d" % j] for j in range(len(names))])
+        assert_rows_equal(glob.advance_watermark(wm), o.advance_watermark(wm), names, rtol=tol, ctx="wm=%d" % wm)
+    assert dropped_g == dropped_o and dropped_o > 0
+    assert all(l.stats().rows_out == 0 for l in loc)   # pre-aggregators never fire windows themselves
