@@ -93,7 +93,8 @@ def main():
         fire = lambda b: pipe.advance_watermark(wms[b], device_output=True)  # noqa: E731
     else:
         eng = E.WindowAggregator(A.make_config(**cfg_kw))
-        push = lambda b: eng.push(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], [vals[b * B:(b + 1) * B]])  # noqa: E731
+        push = lambda b: eng.push(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], [vals[b * B:(b + 1) * B]],  # noqa: E731
+                                  sync=False)
         fire = lambda b: eng.advance_watermark_device(wms[b])  # noqa: E731
 
     rows = 0
@@ -165,7 +166,7 @@ def main():
         "fire": {"launches": st.fire_launches, "ms": st.fire_ms, "rows": st.fire_rows},
         "ingest_split_ms": {"partition": st.partition_ms, "combine": st.combine_ms, "total": st.ingest_ms},
         "rows_emitted": rows_all,
-        "late_dropped": dropped,
+        "late_dropped": st.late_dropped if world == 1 else dropped,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, cfg_kw)

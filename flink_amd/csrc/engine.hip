@@ -1308,6 +1308,10 @@ struct fwa_engine {
     int64_t strag_cap = 0;
     int32_t* d_strag_n = nullptr;
     bool v2_timing_pending = false;   // Phase P / A events recorded, read after the next sync
+    // FWA_PUSH_ASYNC: the last push is enqueued but not yet settled (status, miss replay, lookahead)
+    bool pend = false, pend_v2 = false;
+    int64_t pend_n = 0;
+    IngestArgs pend_a;
     size_t combine_lds = 0;
     int32_t partition_grid = 256;
     // kernel timing (HIP events on this handle's stream)
@@ -1590,7 +1594,7 @@ int stream_sync(fwa_engine* e) {
 }
 
 // The one host synchronisation of a push / fire: device status + touched-flag mirror in one round trip.
-int sync_status(fwa_engine* e) {
+int enqueue_status(fwa_engine* e) {
     HIPCHK(e, hipMemcpyAsync(e->h_st, e->d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, e->stream));
     const int32_t ns = (int32_t)e->touched.size();
     if (ns > 0 && e->d_touched) {
@@ -1603,10 +1607,22 @@ int sync_status(fwa_engine* e) {
         }
         HIPCHK(e, hipMemcpyAsync(e->h_touched, e->d_touched, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, e->stream));
     }
+    return FWA_OK;
+}
+
+// Wait for a status copy enqueued by enqueue_status (nothing may resize `touched` in between).
+int wait_status(fwa_engine* e) {
     int rc = stream_sync(e);
     if (rc) return rc;
+    const int32_t ns = (int32_t)e->touched.size();
     if (ns > 0 && e->d_touched) memcpy(e->touched.data(), e->h_touched, sizeof(int32_t) * ns);
     return FWA_OK;
+}
+
+int sync_status(fwa_engine* e) {
+    int rc = enqueue_status(e);
+    if (rc) return rc;
+    return wait_status(e);
 }
 
 // Enqueue a host->device copy of a small host buffer through the pinned arena (no host sync; the
@@ -2183,7 +2199,18 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
 
 // Shared ingest driver: two-phase path when allowed, else the v1 kernel; slice-miss replays;
 // lookahead slice allocation; stats.
-static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, int64_t* late_dropped_out) {
+static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, bool status_enqueued,
+                       int64_t* late_dropped_out);
+
+// Settle an FWA_PUSH_ASYNC push (first thing every stateful entry point does).
+static int settle_pending(fwa_engine* e) {
+    if (!e->pend) return FWA_OK;
+    e->pend = false;
+    IngestArgs a = e->pend_a;
+    return push_settle(e, a, e->pend_n, e->pend_v2, true, nullptr);
+}
+
+static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, bool async, int64_t* late_dropped_out) {
     int rc = FWA_OK;
     bool ran_v2 = false;
     if (e->v2 && allow_v2) {
@@ -2196,11 +2223,28 @@ static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, i
         rc = launch_ingest(e, a, false);
         if (rc) return rc;
     }
+    if (async) {   // settled by the next call on the handle (settle_pending)
+        rc = enqueue_status(e);
+        if (rc) return rc;
+        e->pend = true;
+        e->pend_a = a;
+        e->pend_n = n;
+        e->pend_v2 = ran_v2;
+        return FWA_OK;
+    }
+    return push_settle(e, a, n, ran_v2, false, late_dropped_out);
+}
+
+// Second half of a push: read the device status, replay missed records (allocating their slices),
+// extend the lookahead, account. status_enqueued: the first status copy is already in the stream.
+static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, bool status_enqueued,
+                       int64_t* late_dropped_out) {
+    int rc = FWA_OK;
     int64_t dropped = 0;
     int64_t qmin = LONG_MAX_J, qmax = LONG_MIN_J;
     bool republish = false;
     for (int round = 0;; ++round) {
-        rc = sync_status(e);
+        rc = (round == 0 && status_enqueued) ? wait_status(e) : sync_status(e);
         if (rc) return rc;
         if (e->v2_timing_pending) {
             float ms = 0.f;
@@ -2279,6 +2323,7 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
     if (late_dropped_out) *late_dropped_out = 0;
     if (n == 0) return FWA_OK;
     HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (int rc0 = settle_pending(e)) return rc0;
     IngestArgs a;
     memset(&a, 0, sizeof(a));
     a.n = n;
@@ -2320,7 +2365,7 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
         if (late_dropped_out) *late_dropped_out = dropped;
         return FWA_OK;
     }
-    return push_common(e, a, n, true, late_dropped_out);
+    return push_common(e, a, n, true, (flags & FWA_PUSH_ASYNC) != 0, late_dropped_out);
 }
 
 int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_ts, const int64_t* count,
@@ -2333,6 +2378,7 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
     if (late_dropped_out) *late_dropped_out = 0;
     if (n == 0) return FWA_OK;
     HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (int rc0 = settle_pending(e)) return rc0;
     IngestArgs a;
     memset(&a, 0, sizeof(a));
     a.n = n;
@@ -2372,7 +2418,7 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
         HIPCHK(e, hipMalloc(&e->d_spill, sizeof(int32_t) * e->spill_cap));
         HIPCHK(e, hipMalloc(&e->d_replay, sizeof(int32_t) * e->spill_cap));
     }
-    return push_common(e, a, n, false, late_dropped_out);
+    return push_common(e, a, n, false, (flags & FWA_PUSH_ASYNC) != 0, late_dropped_out);
 }
 
 // Export every (key, slice) accumulator that received records since the last drain and reset those
@@ -2401,6 +2447,7 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     if (!e || !out) return FWA_E_ARG;
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
     HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (int rc0 = settle_pending(e)) return rc0;
     memset(out, 0, sizeof(*out));
     std::vector<FireWindow> hw;
     std::vector<int32_t> hs;
@@ -2461,6 +2508,7 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
 int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
     if (!e) return FWA_E_STATE;
     HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (int rc0 = settle_pending(e)) return rc0;
     if (out) memset(out, 0, sizeof(*out));
     int64_t nrows = 0;
     if (wm > e->wm && e->kind == FWA_SESSION) {
@@ -2571,6 +2619,7 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
 
 int fwa_flush(fwa_engine* e) {
     if (!e) return FWA_E_STATE;
+    if (int rc0 = settle_pending(e)) return rc0;
     int rc = stream_sync(e);
     if (rc) return rc;
     return FWA_OK;
@@ -2578,6 +2627,7 @@ int fwa_flush(fwa_engine* e) {
 
 int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
     if (!e || !s) return FWA_E_ARG;
+    if (int rc0 = settle_pending(e)) return rc0;
     int rc = sync_status(e);
     if (rc) return rc;
     s->records_in = e->records_in;
@@ -2599,6 +2649,7 @@ int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
 
 int fwa_reset_timers(fwa_engine* e) {
     if (!e) return FWA_E_ARG;
+    if (int rc0 = settle_pending(e)) return rc0;
     e->ingest_launches = e->ingest_records = e->fire_launches = e->fire_rows = 0;
     e->ingest_ms = e->fire_ms = e->partition_ms = e->combine_ms = 0;
     return FWA_OK;

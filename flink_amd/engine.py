@@ -98,7 +98,11 @@ class WindowAggregator:
 
     # -- processElement (batched) --
     def push(self, keys, ts, cols=(), key_hash=None, sync=True):
-        """Push a columnar batch; returns the number of late records dropped in it."""
+        """Push a columnar batch; returns the number of late records dropped in it.
+
+        sync=False (device inputs only) enqueues the batch and returns 0 at once (FWA_PUSH_ASYNC): the
+        batch is settled by the next call on the handle, and the device tensors must stay alive until
+        then; late drops are then counted in stats().late_dropped only."""
         device = _is_torch_cuda(keys)
         if not device:
             keys = np.ascontiguousarray(keys, np.int64)
@@ -109,6 +113,8 @@ class WindowAggregator:
         n = int(keys.shape[0])
         arr = (C.c_void_p * max(1, len(cols)))(*[_ptr(c).value for c in cols])
         flags = A.PUSH_DEVICE_PTRS if device else 0
+        if not sync and device:
+            flags |= A.PUSH_ASYNC
         dropped = C.c_int64(0)
         rc = lib().fwa_push(self.h, _ptr(keys), _ptr(ts), arr, _ptr(key_hash), n, flags, C.byref(dropped))
         _check(rc, self.h)

@@ -98,7 +98,11 @@ enum fwa_status {
 
 /* Flags for fwa_push */
 #define FWA_PUSH_DEVICE_PTRS 0x1 /* key/ts/value pointers are device (HBM) pointers */
-#define FWA_PUSH_ASYNC 0x2       /* do not synchronise; late_dropped_out is not written */
+#define FWA_PUSH_ASYNC 0x2       /* enqueue and return without a host synchronisation: the batch is
+                                  * settled (status read, miss replay, lookahead) at the start of the
+                                  * next call on the handle, which also reports its errors. Device
+                                  * input buffers must stay valid until that next call returns;
+                                  * late_dropped_out is not written (see fwa_stats.late_dropped). */
 
 typedef struct fwa_agg_spec {
     int32_t kind; /* enum fwa_agg_kind */
@@ -166,7 +170,7 @@ const char* fwa_version(void);
 
 /* Columnar batch of n records: keys[n], ts[n], val_cols[c][n] (type implied by the aggs reading c).
  * key_hash may be NULL unless key_kind == FWA_KEY_PREHASHED (then int32 key.hashCode() per record).
- * Input buffers are borrowed for the duration of the call only. */
+ * Input buffers are borrowed for the duration of the call only (FWA_PUSH_ASYNC: until the next call). */
 int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
              const int32_t* key_hash, int64_t n, int32_t flags, int64_t* late_dropped_out);
 

@@ -318,3 +318,35 @@ def test_two_phase_partials_vs_oracle(eng_mod, ci, aggs):
         assert_rows_equal(glob.advance_watermark(wm), o.advance_watermark(wm), names, rtol=tol, ctx="wm=%d" % wm)
     assert dropped_g == dropped_o and dropped_o > 0
     assert all(l.stats().rows_out == 0 for l in loc)   # pre-aggregators never fire windows themselves
+
+
+@pytest.mark.parametrize("ci", [0, 3, 6])
+def test_async_push_vs_oracle(eng_mod, ci):
+    """FWA_PUSH_ASYNC: batches are enqueued without a host sync and settled by the next call (a
+    following push or the watermark). Two pushes per watermark, late records and slice misses
+    (replays) included; rows and the late-drop total must equal the oracle's."""
+    import torch
+    from oracle.oracle import Oracle
+    cfg = A.make_config(aggs=I64_AGGS, key_capacity=4096, output_on_device=0, **CONFIGS[ci])
+    names = A.agg_names(cfg)
+    keys, ts, vi, vf, vd = random_stream(300 + ci, 48_000, 600, 60_000, 1500)
+    g = eng_mod.WindowAggregator(cfg)
+    o = Oracle(cfg)
+    n = len(keys)
+    dk, dt, dv = (torch.from_numpy(x).cuda() for x in (keys, ts, vi))
+    nb = 12
+    max_ts = -2**63
+    dropped_o = 0
+    for b in range(nb):
+        sl = slice(b * n // nb, (b + 1) * n // nb)
+        max_ts = max(max_ts, int(ts[sl].max()))
+        assert g.push(dk[sl], dt[sl], [dv[sl]], sync=False) == 0
+        dropped_o += o.push(keys[sl], ts[sl], [vi[sl]])
+        if b % 2 == 1:
+            wm = max_ts - 1500 - 1
+            assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), names, rtol=tol, ctx="wm=%d" % wm)
+    assert_rows_equal(g.advance_watermark(A.LONG_MAX), o.advance_watermark(A.LONG_MAX), names, rtol=tol)
+    st = g.stats()
+    assert dropped_o > 0 and st.late_dropped == dropped_o and st.records_in == n
+    g.close()
+    o.close()
