@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", choices=["partials", "raw"], default="partials",
+                    help="N>1 keyBy plan: two-phase partial accumulators (default) or raw records")
     args = ap.parse_args()
 
     from flink_amd import _abi as A
@@ -86,9 +88,11 @@ def main():
                   aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=int(args.keys * float(os.environ.get("FWA_KCAP", "1"))),
                   output_on_device=1, device=local_rank)
     if world > 1:
-        from flink_amd.distributed import KeyedWindowPipeline
-        pipe = KeyedWindowPipeline(rank, world, **cfg_kw)
-        eng = pipe.engine
+        from flink_amd.distributed import KeyedWindowPipeline, TwoPhaseKeyedWindowPipeline
+        cls = TwoPhaseKeyedWindowPipeline if args.exchange == "partials" else KeyedWindowPipeline
+        pipe = cls(rank, world, **cfg_kw)
+        eng = pipe.local if args.exchange == "partials" else pipe.engine   # the ingest path being measured
+        engines = [pipe.engine] + ([pipe.local] if args.exchange == "partials" else [])
         push = lambda b: pipe.push(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], [vals[b * B:(b + 1) * B]])  # noqa: E731
         fire = lambda b: pipe.advance_watermark(wms[b], device_output=True)  # noqa: E731
     else:
@@ -96,12 +100,14 @@ def main():
         push = lambda b: eng.push(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], [vals[b * B:(b + 1) * B]],  # noqa: E731
                                   sync=False)
         fire = lambda b: eng.advance_watermark_device(wms[b])  # noqa: E731
+        engines = [eng]
 
     rows = 0
     for b in range(args.warmup):
         push(b)
         rows += fire(b)["key"].shape[0]
-    eng.reset_timers()
+    for x in engines:
+        x.reset_timers()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -154,6 +160,8 @@ def main():
                                                         args.steps, B, args.delay_ms),
             "records_per_gpu_timed": args.steps * B, "keys": args.keys, "batch": B,
             "window_ms": args.window_ms, "parallelism": "key-group dp%d" % world,
+            "exchange": ("two-phase partials (local pre-aggregation, RCCL all_to_all)" if args.exchange == "partials"
+                         else "raw records (RCCL all_to_all)") if world > 1 else "none",
         },
         "roofline": {
             "bound": "hbm", "kernel": "ingest_kernel",
@@ -166,7 +174,7 @@ def main():
         "fire": {"launches": st.fire_launches, "ms": st.fire_ms, "rows": st.fire_rows},
         "ingest_split_ms": {"partition": st.partition_ms, "combine": st.combine_ms, "total": st.ingest_ms},
         "rows_emitted": rows_all,
-        "late_dropped": st.late_dropped if world == 1 else dropped,
+        "late_dropped": sum(x.stats().late_dropped for x in engines) if args.exchange == "partials" or world == 1 else dropped,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, cfg_kw)

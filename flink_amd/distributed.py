@@ -7,10 +7,20 @@ Reference structure this replaces:
   ownership       computeKeyGroupRangeForOperatorIndex     RT/state/KeyGroupRangeAssignment.java:93-106
   watermark       StatusWatermarkValve: min over input channels  SJ/runtime/watermarkstatus/StatusWatermarkValve.java:192
 
-Rank r owns key groups key_group_range_for_operator(maxP, world, r). Each push routes every record to
-its owner (dest = kg * world / maxP, computed on the GPU) with one all_to_all_single per column after
-an all_to_all of the counts; the owner's engine then accumulates. Each advance_watermark takes the
-MIN over ranks (the valve), then fires locally. No other collective is on the data path.
+Rank r owns key groups key_group_range_for_operator(maxP, world, r). Two exchange plans:
+
+* KeyedWindowPipeline (raw records, the DataStream keyBy): each push routes every record to its owner
+  (dest = kg * world / maxP, computed on the GPU) with one all_to_all_single of the packed
+  (key, ts, values) rows after an all_to_all of the counts; the owner's engine then accumulates.
+* TwoPhaseKeyedWindowPipeline (Flink's two-phase window plan, TwoStageOptimizedWindowAggregateRule
+  .java:88-103): every rank pre-aggregates its own source records per (key, slice) in a local engine
+  (LocalSlicingWindowAggOperator.java:111-131); at each watermark the complete slices' partial
+  accumulators are drained, exchanged by key group in one all_to_all_single, and merged into the
+  owner's engine (GlobalAggCombiner.java:77-110), which fires. With 1M keys this ships one 32-40 B
+  partial per (key, slice) instead of one 24 B record per input record.
+
+Each advance_watermark takes the MIN over ranks (the valve), then fires locally. No other collective
+is on the data path.
 """
 import numpy as np
 import torch
@@ -25,7 +35,7 @@ def _gpu_router(max_parallelism, world, key_kind):
 
     def route(keys):
         _, op = engine.key_groups(keys, max_parallelism, world, key_kind=key_kind, device=keys.device.index or 0)
-        return op.to(torch.int64)
+        return torch.as_tensor(op).to(torch.int64)
     return route
 
 
@@ -52,17 +62,10 @@ class KeyedWindowPipeline:
 
     def push(self, keys, ts, cols=()):
         """keys/ts/cols: this rank's source records (torch tensors on the rank's device)."""
-        dest = self.route(keys)
-        order = torch.argsort(dest, stable=True)
-        counts = torch.bincount(dest, minlength=self.world)
-        recv_counts = torch.empty_like(counts)
-        dist.all_to_all_single(recv_counts, counts, group=self.group)
-        send = counts.tolist()
-        recv = recv_counts.tolist()
-        k = self._a2a(keys[order], send, recv)
-        t = self._a2a(ts[order], send, recv)
-        c = [self._a2a(x[order], send, recv) for x in cols]
-        self.exchanged += int(sum(send)) - int(send[self.rank])
+        cols = list(cols)
+        recv = exchange_rows(self, keys, [keys, ts] + cols)
+        k, t = recv[:, 0].contiguous(), recv[:, 1].contiguous()
+        c = [unpack_col(recv[:, 2 + j], x.dtype) for j, x in enumerate(cols)]
         if k.is_cuda:
             return self.engine.push(k, t, c)
         return self.engine.push(k.numpy(), t.numpy(), [x.numpy() for x in c])
@@ -81,6 +84,79 @@ class KeyedWindowPipeline:
 
     def close(self):
         self.engine.close()
+
+
+def unpack_col(cell, dtype):
+    """Inverse of exchange_rows' packing for one column."""
+    if dtype.itemsize == 8:
+        return cell.contiguous().view(dtype)
+    return cell.to(torch.int32).view(dtype).contiguous()
+
+
+def exchange_rows(pipe, keys, cols):
+    """keyBy exchange of a row set: route by key group, pack the columns into one int64 [n, m] tensor,
+    one all_to_all of the counts and one all_to_all_single of the rows (RCCL over xGMI). Returns the
+    received rows (int64 [n_recv, m]; 4-byte columns travel zero-extended in their 8-byte cell)."""
+    dest = pipe.route(keys)
+    n = int(keys.shape[0])
+    packed = torch.empty((n, len(cols)), dtype=torch.int64, device=keys.device)
+    for j, x in enumerate(cols):
+        packed[:, j] = x.view(torch.int64) if x.dtype.itemsize == 8 else x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    if pipe.world > 1:
+        order = torch.argsort(dest, stable=True)
+        packed = packed[order]
+    counts = torch.bincount(dest, minlength=pipe.world)
+    recv_counts = torch.empty_like(counts)
+    dist.all_to_all_single(recv_counts, counts, group=pipe.group)
+    send = counts.tolist()
+    recv = recv_counts.tolist()
+    out = torch.empty((sum(recv), len(cols)), dtype=torch.int64, device=keys.device)
+    dist.all_to_all_single(out, packed, recv, send, group=pipe.group)
+    pipe.exchanged += int(sum(send)) - int(send[pipe.rank])
+    return out
+
+
+class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
+    """One Flink subtask per rank in the two-phase plan: a local pre-aggregating engine over this
+    rank's source records (all key groups), then the partial-accumulator keyBy exchange into the
+    engine owning this rank's key groups. Same push / advance_watermark surface as
+    KeyedWindowPipeline; pushes involve no collective."""
+
+    def __init__(self, rank, world, group=None, engine_factory=None, router=None, local_factory=None, **cfg_kw):
+        super().__init__(rank, world, group=group, engine_factory=engine_factory, router=router, **cfg_kw)
+        lkw = dict(cfg_kw)
+        lkw["output_on_device"] = 1 if dist.get_backend(group) == "nccl" else 0
+        self.local_cfg = A.make_config(**lkw)           # the pre-aggregator sees every key group
+        if local_factory is None:
+            from .engine import WindowAggregator
+            local_factory = WindowAggregator
+        self.local = local_factory(self.local_cfg)
+        self.partials_sent = 0
+
+    def push(self, keys, ts, cols=()):
+        if keys.is_cuda:
+            return self.local.push(keys, ts, list(cols), sync=False)
+        return self.local.push(keys.numpy(), ts.numpy(), [x.numpy() for x in cols])
+
+    def advance_watermark(self, local_wm, device_output=False):
+        wm = self.global_watermark(local_wm)
+        p = self.local.drain_partials(wm)
+        na = len(self.names)
+        cols = [p["key"], p["slice_start"], p["count"]] + [p["acc%d" % j] for j in range(na)]
+        cols = [c if isinstance(c, torch.Tensor) else torch.from_numpy(c) for c in cols]
+        recv = exchange_rows(self, cols[0], cols)
+        self.partials_sent += int(cols[0].shape[0])
+        col = [recv[:, j].contiguous() for j in range(recv.shape[1])]
+        if not recv.is_cuda:
+            col = [c.numpy() for c in col]
+        self.engine.push_partials(col[0], col[1], col[2], col[3:])
+        if device_output:
+            return self.engine.advance_watermark_device(wm)
+        return self.engine.advance_watermark(wm)
+
+    def close(self):
+        self.local.close()
+        super().close()
 
 
 def merge_rows(parts, names):

@@ -31,7 +31,65 @@ def _stream(seed, n):
     return keys, ts, vals
 
 
-def _worker(rank, world, port, outdir):
+class _LocalPreAgg:
+    """Test-side CPU stand-in for the GPU pre-aggregator role (fwa_drain_partials semantics, tumbling
+    COUNT + SUM_I64): drops records whose window fired at the current watermark, buffers the rest,
+    drain(wm) emits one (key, slice_start, count, sum) partial per key and complete slice."""
+
+    def __init__(self, cfg):
+        self.size = cfg.size_ms
+        self.wm = A.LONG_MIN
+        self.buf = []
+
+    def push(self, keys, ts, cols=()):
+        start = ts - np.mod(ts, self.size)
+        ok = start + self.size - 1 > self.wm
+        self.buf.append((keys[ok], start[ok], cols[0][ok]))
+        return int((~ok).sum())
+
+    def drain_partials(self, wm):
+        self.wm = max(self.wm, wm)
+        if not self.buf:
+            k = s = v = np.zeros(0, np.int64)
+        else:
+            k, s, v = (np.concatenate(c) for c in zip(*self.buf))
+        done = s + self.size - 1 <= self.wm
+        self.buf = [(k[~done], s[~done], v[~done])]
+        groups = {}
+        for key, st, val in zip(k[done].tolist(), s[done].tolist(), v[done].tolist()):
+            c, t = groups.get((key, st), (0, 0))
+            groups[(key, st)] = (c + 1, t + val)
+        items = sorted(groups.items())
+        arr = lambda f: np.array([f(it) for it in items], dtype=np.int64)  # noqa: E731
+        return {"key": arr(lambda it: it[0][0]), "slice_start": arr(lambda it: it[0][1]),
+                "count": arr(lambda it: it[1][0]), "acc0": arr(lambda it: it[1][0]), "acc1": arr(lambda it: it[1][1])}
+
+    def close(self):
+        pass
+
+
+class _OracleFromPartials:
+    """Test-side global role: merges partials into the oracle by re-expanding each (count c, sum s)
+    partial into c records at slice_start (one carrying s, the rest 0) -- exact for COUNT + SUM."""
+
+    def __init__(self, cfg):
+        from oracle.oracle import Oracle
+        self.o = Oracle(cfg)
+
+    def push_partials(self, keys, slice_ts, count, accs):
+        rep = np.repeat(np.arange(len(keys)), count)
+        first = np.r_[True, rep[1:] != rep[:-1]] if len(rep) else np.zeros(0, bool)
+        vals = np.where(first, np.asarray(accs[1])[rep], 0).astype(np.int64)
+        return self.o.push(np.asarray(keys)[rep], np.asarray(slice_ts)[rep], [vals])
+
+    def advance_watermark(self, wm):
+        return self.o.advance_watermark(wm)
+
+    def close(self):
+        self.o.close()
+
+
+def _worker(rank, world, port, outdir, two_phase=False):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -45,8 +103,13 @@ def _worker(rank, world, port, outdir):
         return torch.tensor([L.or_operator_index(128, world, L.or_key_group(int(k), 0, 0, 128)) for k in keys.tolist()],
                             dtype=torch.int64)
 
-    pipe = KeyedWindowPipeline(rank, world, engine_factory=O.Oracle, router=router,
-                               window_kind="TUMBLE", size_ms=5000, aggs=[("COUNT", 0), ("SUM_I64", 0)])
+    kw = dict(router=router, window_kind="TUMBLE", size_ms=5000, aggs=[("COUNT", 0), ("SUM_I64", 0)])
+    if two_phase:
+        from flink_amd.distributed import TwoPhaseKeyedWindowPipeline
+        pipe = TwoPhaseKeyedWindowPipeline(rank, world, engine_factory=_OracleFromPartials,
+                                           local_factory=_LocalPreAgg, **kw)
+    else:
+        pipe = KeyedWindowPipeline(rank, world, engine_factory=O.Oracle, **kw)
     keys, ts, vals = _stream(42 + rank, 6000)   # each rank is one source subtask
     rows = []
     nb = 4
@@ -64,9 +127,10 @@ def _worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def test_two_rank_keyby_pipeline_matches_single_operator(tmp_path):
+@pytest.mark.parametrize("two_phase", [False, True], ids=["raw_records", "two_phase_partials"])
+def test_two_rank_keyby_pipeline_matches_single_operator(tmp_path, two_phase):
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), two_phase), nprocs=world, join=True)
     got = np.concatenate([np.load(tmp_path / ("rank%d.npy" % r)) for r in range(world)])
     # reference: one operator over the union of both sources, watermark = min over sources per step
     from oracle.oracle import Oracle
