@@ -505,6 +505,151 @@ __global__ void __launch_bounds__(THREADS, MINW) partition_kernel(PartArgs a, co
         }
 }
 
+// partition2: Phase P with the next tile's loads in flight while the current tile is scanned,
+// reserved and stored (r01 ablation: without its bucket stores Phase P still took 0.58 ms per 2^26
+// records, twice the streaming time of its 1.6 GB of input -- one tile in flight per CU left every
+// latency in the tile's chain exposed). The tile is staged in LDS in arrival order (x_*), the
+// counting sort only writes a permutation (s_src) and the store loop gathers through it, so the
+// load registers are free as soon as the tile is classified.
+template <int NV, int ITEMS, int THREADS>
+__global__ void __launch_bounds__(THREADS, 1) partition2_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
+    constexpr int kTile = THREADS * ITEMS;
+    const EngineConst& c = *cp;
+    __shared__ uint32_t hist[kMaxPart];
+    __shared__ uint32_t toff[kMaxPart];
+    __shared__ uint32_t gbase[kMaxPart];
+    __shared__ unsigned long long x_key[kTile];
+    __shared__ unsigned long long x_val[NV > 0 ? NV : 1][NV > 0 ? kTile : 1];
+    __shared__ uint16_t x_rel[kTile];
+    __shared__ uint16_t s_part[kTile];
+    __shared__ uint16_t s_src[kTile];
+    __shared__ uint32_t wsum[THREADS / 64];
+    __shared__ uint32_t s_total;
+    __shared__ uint8_t s_code[kRelCap];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    unsigned dropped = 0;
+    uint32_t relmax = 0, relmin = ~0u;
+    const bool kg_all = c.kg_lo == 0 && c.kg_hi == c.max_par - 1;
+    const bool ds = c.sem == FWA_SEM_DATASTREAM;
+    for (int r = tid; r < kRelCap / 4; r += THREADS) ((uint32_t*)s_code)[r] = ((const uint32_t*)a.relcode)[r];
+    const int64_t ntiles = (a.n + kTile - 1) / kTile;
+    const int sub = blockIdx.x % kSub;
+    unsigned long long r_key[ITEMS], r_v0[ITEMS], r_v1[ITEMS];
+    int64_t r_ts[ITEMS];
+    int32_t r_kh[ITEMS];
+    auto load = [&](int64_t t) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const int64_t i = t * kTile + (int64_t)j * THREADS + tid;
+            const bool ok = i < a.n;
+            r_key[j] = ok ? (unsigned long long)a.keys[i] : 0ull;
+            r_ts[j] = ok ? a.ts[i] : 0;
+            r_v0[j] = (NV > 0 && ok) ? load_raw(a.cols[a.vcol[0]], i, a.vsize[0]) : 0ull;
+            r_v1[j] = (NV > 1 && ok) ? load_raw(a.cols[a.vcol[1]], i, a.vsize[1]) : 0ull;
+            r_kh[j] = (a.key_hash && ok) ? a.key_hash[i] : 0;
+        }
+    };
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) load(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        for (int i = tid; i < a.np; i += THREADS) hist[i] = 0;
+        __syncthreads();
+        const int64_t t0 = tile * kTile;
+        uint32_t r_pos[ITEMS];   // (p << 16 | rank) or ~0u when the record does not go to a bucket
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const int64_t i = t0 + (int64_t)j * THREADS + tid;
+            const int64_t key = (int64_t)r_key[j];
+            const int64_t ts = r_ts[j];
+            const int64_t d = jm::wsub(ts, c.off);
+            const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
+            const uint64_t uq = jm::udiv64(ud, c.g_div);
+            const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
+            const uint64_t rel = (uint64_t)(q - a.q_base);
+            uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
+            if (!kg_all) {
+                const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, r_kh[j]), c.max_par);
+                if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;
+            }
+            if (ds && ts == LONG_MIN_J) code = kCodeSlow;
+            if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
+            if (i >= a.n) code = 0xff;
+            dropped += code == kCodeDrop;
+            const bool slow = code == kCodeSlow;
+            const unsigned long long mk = __ballot(slow);
+            if (mk) {
+                const int leader = __ffsll((long long)mk) - 1;
+                int32_t sb = 0;
+                if (lane == leader) sb = atomicAdd(&a.st->spill_n, __popcll(mk));
+                sb = __shfl(sb, leader);
+                if (slow) a.spill[sb + __popcll(mk & ((1ull << lane) - 1))] = (int32_t)i;
+            }
+            r_pos[j] = ~0u;
+            if (code == kCodeAccept) {
+                relmax = max(relmax, (uint32_t)rel);
+                relmin = min(relmin, (uint32_t)rel);
+                const uint64_t h = jm::mix64((uint64_t)key);
+                const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
+                const int x = j * THREADS + tid;
+                x_key[x] = r_key[j];
+                x_rel[x] = (uint16_t)rel;
+                if (NV > 0) x_val[0][x] = r_v0[j];
+                if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = r_v1[j];
+                r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
+            }
+        }
+        if (tile + gridDim.x < ntiles) load(tile + gridDim.x);   // next tile in flight from here on
+        __syncthreads();
+        block_scan_np<THREADS>(hist, toff, wsum, a.np, &s_total);
+        __syncthreads();
+        for (int p = tid; p < a.np; p += THREADS)
+            gbase[p] = hist[p] ? atomicAdd(&a.b_cnt[p * kSub + sub], hist[p]) : 0u;
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            if (r_pos[j] == ~0u) continue;
+            const uint32_t p = r_pos[j] >> 16;
+            const uint32_t sidx = toff[p] + (r_pos[j] & 0xffffu);
+            s_part[sidx] = (uint16_t)p;
+            s_src[sidx] = (uint16_t)(j * THREADS + tid);
+        }
+        __syncthreads();
+        const uint32_t total = s_total;
+        for (uint32_t sidx = tid; sidx < total; sidx += THREADS) {
+            const uint32_t p = s_part[sidx];
+            const uint32_t x = s_src[sidx];
+            const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
+            if (dst >= (uint64_t)a.capb) {      // sub-bucket full (skewed keys): the v1 replay takes it
+                a.spill[atomicAdd(&a.st->spill_n, 1)] = (int32_t)(t0 + x);
+                continue;
+            }
+            const uint64_t o = ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
+            a.b_key[o] = x_key[x];
+            a.b_rel[o] = x_rel[x];
+            if (NV > 0) a.b_val0[o] = x_val[0][x];
+            if (NV > 1) a.b_val1[o] = x_val[NV > 1 ? 1 : 0][x];
+        }
+        __syncthreads();
+    }
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        dropped += __shfl_xor(dropped, sh);
+        relmax = max(relmax, (uint32_t)__shfl_xor((int)relmax, sh));
+        relmin = min(relmin, (uint32_t)__shfl_xor((int)relmin, sh));
+    }
+    if (lane == 0) {
+        if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
+        if (relmin != ~0u) {
+            atomicMax(&a.st->max_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmax));
+            atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
+        }
+    }
+    if (relmin != ~0u)
+        for (uint32_t r = relmin + (uint32_t)lane; r <= relmax; r += 64) {
+            const int32_t slot = a.rel2slot[r];
+            if (slot >= 0 && a.touched[slot] == 0) a.touched[slot] = 1;
+        }
+}
+
 struct StragEntry {
     uint64_t o;                        // bucket offset (p * capb + idx)
     uint32_t g;                        // global kid (key-table slot)
@@ -918,6 +1063,9 @@ __device__ __forceinline__ void emit_row(const FireArgs& f, const EngineConst& c
 // One block = one window x one chunk of kBlock*kFireJ consecutive kids. Pass 1 sums COUNT over the
 // window's slices and ballots the emitting keys; one atomic reserves the block's rows; pass 2 writes
 // rows j-major so every wave store is contiguous.
+// PRE = 1 (one stateful accumulator column, e.g. COUNT + SUM(long), single-slot windows): pass 1
+// also loads that column, so pass 2 only stores (the generic emit re-reads it behind every store).
+template <int PRE>
 __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
     const int32_t w = blockIdx.x / f.blocks_per_win;
@@ -932,17 +1080,29 @@ __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineCo
     uint64_t cnt[kFireJ];
     unsigned long long kvs[kFireJ];
     unsigned long long masks[kFireJ];
+    unsigned long long xs[PRE ? kFireJ : 1];
+    const unsigned long long* slot0 = PRE ? f.slot_base[f.win_slots[win.slot_off]] : nullptr;
+    if (PRE) {   // issue every load of the chunk before the first use
+#pragma unroll
+        for (int j = 0; j < kFireJ; ++j) {
+            const int64_t k = k0 + (int64_t)j * kBlock + tid;
+            kvs[j] = k < nk ? f.key_table[k] : kEmptyKey;
+            cnt[j] = k < nk ? slot0[k] : 0;
+            xs[PRE ? j : 0] = k < nk ? slot0[f.stride + k] : 0;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < kFireJ; ++j) {
         const int64_t k = k0 + (int64_t)j * kBlock + tid;
         bool present = false;
-        unsigned long long kv = 0;
+        unsigned long long kv = PRE ? kvs[j] : 0;
         if (k < nk) {
-            kv = f.key_table[k];
+            if (!PRE) kv = f.key_table[k];
             present = (k < f.capacity) ? (kv != kEmptyKey) : (kv == 1ull);
         }
         uint64_t cc = 0;
-        if (present)
+        if (PRE) cc = present ? cnt[j] : 0;
+        else if (present)
             for (int s = 0; s < win.nslots; ++s) cc += f.slot_base[f.win_slots[win.slot_off + s]][k];
         cnt[j] = cc;
         kvs[j] = kv;
@@ -964,7 +1124,20 @@ __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineCo
         if (!((masks[j] >> lane) & 1ull)) continue;
         const int64_t k = k0 + (int64_t)j * kBlock + tid;
         const int64_t row = (int64_t)s_base + woff[j][wid] + __popcll(masks[j] & lt);
-        emit_row(f, c, win, k, kvs[j], cnt[j], row);
+        if (PRE) {
+            f.o_key[row] = (k < f.capacity) ? (int64_t)kvs[j] : LONG_MIN_J;
+            f.o_start[row] = win.start;
+            f.o_end[row] = win.end;
+            if (f.o_count) f.o_count[row] = (int64_t)cnt[j];
+            for (int a = 0; a < c.naggs; ++a) {
+                const AggDesc d = c.agg[a];
+                const unsigned long long x = d.acc > 0 ? xs[PRE ? j : 0] : ident_of(d.acc_kind);
+                if (f.raw) ((unsigned long long*)f.o_agg[a])[row] = d.acc > 0 ? x : cnt[j];
+                else write_agg(d, cnt[j], x, f.o_agg[a], row);
+            }
+        } else {
+            emit_row(f, c, win, k, kvs[j], cnt[j], row);
+        }
     }
 }
 
@@ -1180,6 +1353,22 @@ __global__ void push_reset_kernel(DevStatus* st, unsigned long long* want, int32
     for (int32_t i = t; i < nbcnt; i += nt) bcnt[i] = 0u;
 }
 
+// Restore the identities of a list of slots (every accumulator column; MIN columns 0xFF..) and clear
+// their touched flags: one launch for all slices a watermark retires (was 3 memsets per slot).
+__global__ void reset_slots_kernel(unsigned long long* const* slot_base, const int32_t* list, int64_t stride,
+                                   int32_t* touched, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    const int32_t slot = list[blockIdx.y];
+    unsigned long long* base = slot_base[slot];
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int col = 0; col < c.nacc; ++col) {
+        const unsigned long long v = (col > 0 && c.acc_kind[col] == ACC_MIN_ORD) ? ~0ull : 0ull;
+        unsigned long long* p = base + (int64_t)col * stride;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < stride; i += step) p[i] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) touched[slot] = 0;
+}
+
 __global__ void fill_u64_kernel(unsigned long long* p, unsigned long long v, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -1260,6 +1449,9 @@ struct fwa_engine {
     int32_t slot_base_cap = 0;
     std::vector<int32_t> free_slots;
     int32_t* d_touched = nullptr;
+    std::vector<int32_t> pending_reset;   // slots whose identities reset_slots_kernel restores next
+    int32_t* d_reset_list = nullptr;
+    int32_t reset_cap = 0;
     std::vector<int32_t> touched;     // host mirror
     // slice directory
     DirEntry* d_dir = nullptr;
@@ -1515,17 +1707,32 @@ int alloc_slice(fwa_engine* e, int64_t q) {
     return FWA_OK;
 }
 
+// Queue a slot for identity restoration (untouched slots are still clean); flush_resets launches it.
 int reset_slot(fwa_engine* e, int32_t slot) {
-    if (e->touched[slot]) {  // restore identities (untouched slots are still clean)
-        const size_t col_bytes = (size_t)e->stride * 8;
-        unsigned long long* base = e->slot_ptr[slot];
-        for (int c = 0; c < e->nacc; ++c) {
-            const int v = (c > 0 && e->ec.acc_kind[c] == ACC_MIN_ORD) ? 0xFF : 0;
-            HIPCHK(e, hipMemsetAsync(base + (int64_t)c * e->stride, v, col_bytes, e->stream));
-        }
+    if (e->touched[slot]) {
+        e->pending_reset.push_back(slot);
         e->touched[slot] = 0;
-        HIPCHK(e, hipMemsetAsync(e->d_touched + slot, 0, sizeof(int32_t), e->stream));
     }
+    return FWA_OK;
+}
+
+// Enqueue the queued resets (one kernel) before anything can reuse those slots.
+int flush_resets(fwa_engine* e) {
+    const int32_t n = (int32_t)e->pending_reset.size();
+    if (n == 0) return FWA_OK;
+    if (n > e->reset_cap) {
+        if (e->d_reset_list) HIPCHK(e, hipFree(e->d_reset_list));
+        e->d_reset_list = nullptr;
+        e->reset_cap = std::max<int32_t>(64, 2 * n);
+        HIPCHK(e, hipMalloc(&e->d_reset_list, sizeof(int32_t) * e->reset_cap));
+    }
+    int rc = upload(e, e->d_reset_list, e->pending_reset.data(), sizeof(int32_t) * n);
+    if (rc) return rc;
+    const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 1024 / n), (e->stride + 1023) / 1024);
+    reset_slots_kernel<<<dim3((unsigned)blocks, (unsigned)n), 1024, 0, e->stream>>>(e->d_slot_base, e->d_reset_list,
+                                                                                   e->stride, e->d_touched, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    e->pending_reset.clear();
     return FWA_OK;
 }
 
@@ -1675,7 +1882,7 @@ void fwa_destroy(fwa_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel,
-                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n,
+                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n, e->d_reset_list,
                     e->d_scnt, e->d_sstart, e->d_send, e->d_sacc, e->d_sess_sort, e->d_sort_tmp, e->o_count};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
@@ -1974,11 +2181,11 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.abl = pabl;
     HIPCHK(e, hipEventRecord(e->ev[4], e->stream));
     // tile shape variants (FWA_PVAR): 0 = 512 thr x 12 items, 1 = 1024 x 6, 2 = 512 x 8 (2 WG/CU), 3 = 256 x 12
-    static const int pvar = getenv("FWA_PVAR") ? atoi(getenv("FWA_PVAR")) : 1;
+    static const int pvar = getenv("FWA_PVAR") ? atoi(getenv("FWA_PVAR")) : 5;
     int threads = 512, items = 12, per_cu = 1;
     if (e->nv == 2) items = 8;
     if (e->nv == 0) items = 16;
-    if (pvar == 1) { threads = 1024; items /= 2; }
+    if (pvar == 1 || pvar == 5) { threads = 1024; items /= 2; }
     if (pvar == 2) { items = e->nv == 2 ? 4 : (e->nv == 1 ? 6 : 8); per_cu = 2; }
     if (pvar == 4) { threads = 1024; items = e->nv == 2 ? 2 : (e->nv == 1 ? 3 : 4); per_cu = 2; }
     if (pvar == 3) { threads = 256; items = e->nv == 2 ? 12 : (e->nv == 1 ? 16 : 24); per_cu = 1; }
@@ -1986,7 +2193,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256 * per_cu));
 #define PLAUNCH(NV, IT, TH, MW) partition_kernel<NV, IT, TH, MW><<<grid, TH, 0, e->stream>>>(pa, e->d_ec)
     // pvar 2 / 4: two workgroups per CU (LDS <= 80 KB, VGPR <= 128) so one loads while the other computes
-    if (e->nv == 0) {
+#define P2LAUNCH(NV, IT) partition2_kernel<NV, IT, 1024><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec)
+    if (pvar == 5) {   // pipelined (default)
+        if (e->nv == 0) P2LAUNCH(0, 8); else if (e->nv == 1) P2LAUNCH(1, 6); else P2LAUNCH(2, 4);
+    } else if (e->nv == 0) {
         if (pvar == 1) PLAUNCH(0, 8, 1024, 1); else if (pvar == 2) PLAUNCH(0, 8, 512, 4); else if (pvar == 3) PLAUNCH(0, 24, 256, 1);
         else if (pvar == 4) PLAUNCH(0, 4, 1024, 2); else PLAUNCH(0, 16, 512, 1);
     } else if (e->nv == 1) {
@@ -1997,6 +2207,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else if (pvar == 4) PLAUNCH(2, 2, 1024, 2); else PLAUNCH(2, 8, 512, 1);
     }
 #undef PLAUNCH
+#undef P2LAUNCH
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[5], e->stream));
     // no host round trip between the phases: Phase P marks touched slots itself, spills bucket
@@ -2183,7 +2394,10 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     f.st = e->d_st;
     const int64_t grid = (int64_t)f.blocks_per_win * (int64_t)hw.size();
     HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
-    fire_kernel<<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
+    bool single = e->nacc == 2;   // one stateful accumulator column, every window one slot
+    for (const FireWindow& w : hw) single = single && w.nslots == 1;
+    if (single) fire_kernel<1><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
+    else fire_kernel<0><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
     rc = sync_status(e);
@@ -2437,6 +2651,7 @@ static int retire_slices(fwa_engine* e, int64_t wm) {
         if (rc) return rc;
         e->live.erase(q);
     }
+    if (int rc = flush_resets(e)) return rc;
     if (!dead.empty()) return publish_dir(e);
     return FWA_OK;
 }
@@ -2470,6 +2685,8 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
             rc = reset_slot(e, slot);
             if (rc) return rc;
         }
+        rc = flush_resets(e);
+        if (rc) return rc;
     }
     if (wm > e->wm) {   // forward the watermark: lateness from now on, release slices past cleanup
         int rc = retire_slices(e, wm);
