@@ -332,6 +332,7 @@ struct PartArgs {
     int32_t vsize[2];                  // 4 or 8 bytes
     int32_t abl;                       // ablation bits (timing experiments only; 0 in production)
     DevStatus* st;
+    long long* prof;                   // optional per-block phase cycle counters (FWA_PPROF)
 };
 
 __device__ __forceinline__ unsigned long long load_raw(const void* col, int64_t i, int size) {
@@ -511,8 +512,10 @@ __global__ void __launch_bounds__(THREADS, MINW) partition_kernel(PartArgs a, co
 // latency in the tile's chain exposed). The tile is staged in LDS in arrival order (x_*), the
 // counting sort only writes a permutation (s_src) and the store loop gathers through it, so the
 // load registers are free as soon as the tile is classified.
-template <int NV, int ITEMS, int THREADS>
-__global__ void __launch_bounds__(THREADS, 1) partition2_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
+// VW: value-column widths, bit v set = carried value column v is 8 bytes (else 4): a compile-time
+// width keeps the tile's loads branch-free, so none waits for another.
+template <int NV, int ITEMS, int THREADS, int MINW = 1, int VW = 3>
+__global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
     constexpr int kTile = THREADS * ITEMS;
     const EngineConst& c = *cp;
     __shared__ uint32_t hist[kMaxPart];
@@ -538,23 +541,62 @@ __global__ void __launch_bounds__(THREADS, 1) partition2_kernel(PartArgs a, cons
     unsigned long long r_key[ITEMS], r_v0[ITEMS], r_v1[ITEMS];
     int64_t r_ts[ITEMS];
     int32_t r_kh[ITEMS];
+    // Column pointers resolved once (uniform, SGPRs): indexing the kernel-argument array per load
+    // made hipcc fetch the pointer with a vector load and wait vmcnt(0) before every value load,
+    // serialising the tile's loads item by item.
+    const int64_t* __restrict__ pkeys = a.keys;
+    const int64_t* __restrict__ pts = a.ts;
+    const void* pc0 = NV > 0 ? a.cols[a.vcol[0]] : nullptr;
+    const void* pc1 = NV > 1 ? a.cols[a.vcol[1]] : nullptr;
+    constexpr bool w0 = (VW & 1) != 0, w1 = (VW & 2) != 0;
+    const int32_t* __restrict__ pkh = a.key_hash;
+    const int64_t n = a.n;
+    // every load of a tile is issued before any is used; uniform branches sit outside the item loops
+    // (a per-item select between a 4- and an 8-byte load made hipcc wait vmcnt(0) at every join)
     auto load = [&](int64_t t) {
+        int64_t ic[ITEMS];
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const int64_t i = t * kTile + (int64_t)j * THREADS + tid;
-            const bool ok = i < a.n;
-            r_key[j] = ok ? (unsigned long long)a.keys[i] : 0ull;
-            r_ts[j] = ok ? a.ts[i] : 0;
-            r_v0[j] = (NV > 0 && ok) ? load_raw(a.cols[a.vcol[0]], i, a.vsize[0]) : 0ull;
-            r_v1[j] = (NV > 1 && ok) ? load_raw(a.cols[a.vcol[1]], i, a.vsize[1]) : 0ull;
-            r_kh[j] = (a.key_hash && ok) ? a.key_hash[i] : 0;
+            ic[j] = i < n ? i : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) { r_key[j] = (unsigned long long)pkeys[ic[j]]; r_ts[j] = pts[ic[j]]; }
+        if constexpr (NV > 0) {
+            if constexpr (w0) {
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j) r_v0[j] = ((const unsigned long long*)pc0)[ic[j]];
+            } else {
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j) r_v0[j] = ((const uint32_t*)pc0)[ic[j]];
+            }
+        }
+        if constexpr (NV > 1) {
+            if constexpr (w1) {
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j) r_v1[j] = ((const unsigned long long*)pc1)[ic[j]];
+            } else {
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j) r_v1[j] = ((const uint32_t*)pc1)[ic[j]];
+            }
+        }
+        if (pkh) {
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) r_kh[j] = pkh[ic[j]];
+        } else {
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) r_kh[j] = 0;
         }
     };
+    long long pt = clock64();
+    long long pacc[6] = {0, 0, 0, 0, 0, 0};
+#define QMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
     int64_t tile = blockIdx.x;
     if (tile < ntiles) load(tile);
     for (; tile < ntiles; tile += gridDim.x) {
         for (int i = tid; i < a.np; i += THREADS) hist[i] = 0;
         __syncthreads();
+        QMARK(5);
         const int64_t t0 = tile * kTile;
         uint32_t r_pos[ITEMS];   // (p << 16 | rank) or ~0u when the record does not go to a bucket
 #pragma unroll
@@ -599,10 +641,12 @@ __global__ void __launch_bounds__(THREADS, 1) partition2_kernel(PartArgs a, cons
                 r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
             }
         }
+        QMARK(0);
         if (tile + gridDim.x < ntiles) load(tile + gridDim.x);   // next tile in flight from here on
         __syncthreads();
         block_scan_np<THREADS>(hist, toff, wsum, a.np, &s_total);
         __syncthreads();
+        QMARK(1);
         for (int p = tid; p < a.np; p += THREADS)
             gbase[p] = hist[p] ? atomicAdd(&a.b_cnt[p * kSub + sub], hist[p]) : 0u;
 #pragma unroll
@@ -614,6 +658,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition2_kernel(PartArgs a, cons
             s_src[sidx] = (uint16_t)(j * THREADS + tid);
         }
         __syncthreads();
+        QMARK(2);
         const uint32_t total = s_total;
         for (uint32_t sidx = tid; sidx < total; sidx += THREADS) {
             const uint32_t p = s_part[sidx];
@@ -629,8 +674,12 @@ __global__ void __launch_bounds__(THREADS, 1) partition2_kernel(PartArgs a, cons
             if (NV > 0) a.b_val0[o] = x_val[0][x];
             if (NV > 1) a.b_val1[o] = x_val[NV > 1 ? 1 : 0][x];
         }
+        QMARK(3);
         __syncthreads();
+        QMARK(4);
     }
+    if (a.prof && tid == 0) for (int q = 0; q < 6; ++q) a.prof[(int64_t)blockIdx.x * 8 + q] = pacc[q];
+#undef QMARK
     for (int sh = 32; sh >= 1; sh >>= 1) {
         dropped += __shfl_xor(dropped, sh);
         relmax = max(relmax, (uint32_t)__shfl_xor((int)relmax, sh));
@@ -2179,6 +2228,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.st = e->d_st;
     static const int pabl = getenv("FWA_PABL") ? atoi(getenv("FWA_PABL")) : 0;
     pa.abl = pabl;
+    static const int pprof = getenv("FWA_PPROF") ? atoi(getenv("FWA_PPROF")) : 0;
+    static long long* d_pprof = nullptr;
+    if (pprof && !d_pprof) HIPCHK(e, hipMalloc(&d_pprof, sizeof(long long) * 8 * 1024));
+    pa.prof = pprof ? d_pprof : nullptr;
     HIPCHK(e, hipEventRecord(e->ev[4], e->stream));
     // tile shape variants (FWA_PVAR): 0 = 512 thr x 12 items, 1 = 1024 x 6, 2 = 512 x 8 (2 WG/CU), 3 = 256 x 12
     static const int pvar = getenv("FWA_PVAR") ? atoi(getenv("FWA_PVAR")) : 5;
@@ -2193,9 +2246,13 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256 * per_cu));
 #define PLAUNCH(NV, IT, TH, MW) partition_kernel<NV, IT, TH, MW><<<grid, TH, 0, e->stream>>>(pa, e->d_ec)
     // pvar 2 / 4: two workgroups per CU (LDS <= 80 KB, VGPR <= 128) so one loads while the other computes
-#define P2LAUNCH(NV, IT) partition2_kernel<NV, IT, 1024><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec)
+    const int vw = (e->vsize[0] == 8 ? 1 : 0) | (e->vsize[1] == 8 ? 2 : 0);
+#define P2LAUNCH(NV, IT, VW) partition2_kernel<NV, IT, 1024, 1, VW><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec)
     if (pvar == 5) {   // pipelined (default)
-        if (e->nv == 0) P2LAUNCH(0, 8); else if (e->nv == 1) P2LAUNCH(1, 6); else P2LAUNCH(2, 4);
+        if (e->nv == 0) P2LAUNCH(0, 8, 3);
+        else if (e->nv == 1) { if (vw & 1) P2LAUNCH(1, 6, 3); else P2LAUNCH(1, 6, 2); }
+        else if (vw == 3) P2LAUNCH(2, 4, 3); else if (vw == 2) P2LAUNCH(2, 4, 2);
+        else if (vw == 1) P2LAUNCH(2, 4, 1); else P2LAUNCH(2, 4, 0);
     } else if (e->nv == 0) {
         if (pvar == 1) PLAUNCH(0, 8, 1024, 1); else if (pvar == 2) PLAUNCH(0, 8, 512, 4); else if (pvar == 3) PLAUNCH(0, 24, 256, 1);
         else if (pvar == 4) PLAUNCH(0, 4, 1024, 2); else PLAUNCH(0, 16, 512, 1);
@@ -2210,6 +2267,17 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
 #undef P2LAUNCH
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[5], e->stream));
+    if (pprof) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        float ms = 0.f;
+        HIPCHK(e, hipEventElapsedTime(&ms, e->ev[4], e->ev[5]));
+        std::vector<long long> hp(8 * grid);
+        HIPCHK(e, hipMemcpy(hp.data(), d_pprof, sizeof(long long) * 8 * grid, hipMemcpyDeviceToHost));
+        double tot[6] = {0};
+        for (int b = 0; b < grid; ++b) for (int k = 0; k < 6; ++k) tot[k] += (double)hp[b * 8 + k] / grid;
+        fprintf(stderr, "[pprof] kernel %.3f ms; per-block avg cycles: classify %.0f scan %.0f scatter %.0f store %.0f endbar %.0f topbar %.0f\n",
+                ms, tot[0], tot[1], tot[2], tot[3], tot[4], tot[5]);
+    }
     // no host round trip between the phases: Phase P marks touched slots itself, spills bucket
     // overflow to the v1 replay list, and the straggler pass reads its count on the device
     CombineArgs ca;
