@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
+                    help="c2: tumbling 10s COUNT+SUM(long), 1M uniform keys (the metric's workload); "
+                         "c3: HOP 60s/1s (Table slicing), Zipf(1.1) keys over 1M items")
     ap.add_argument("--exchange", choices=["partials", "raw"], default="partials",
                     help="N>1 keyBy plan: two-phase partial accumulators (default) or raw records")
     args = ap.parse_args()
@@ -69,7 +72,11 @@ def main():
     p = A.GenParams(seed_k=0x5eed0001 ^ (rank * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF),
                     seed_t=0x5eed0002 + rank, seed_v=0x5eed0003 + rank, first_index=0, total_records=n_rank,
                     num_keys=args.keys, t0_ms=1_700_000_000_000, span_ms=span, max_delay_ms=args.delay_ms,
-                    key_dist=0, val_kind=0)
+                    key_dist=1 if args.config == "c3" else 0, val_kind=0)
+    if args.config == "c3":   # Zipf(1.1) CDF over the key ids, sampled bit-identically by the device generator
+        w = 1.0 / np.arange(1, args.keys + 1, dtype=np.float64) ** 1.1
+        zcdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
+        p.zipf_cdf = zcdf.data_ptr()
     log("rank %d/%d generating %d records (%.1f GB) in HBM" % (rank, world, n_rank, n_rank * 24 / 1e9))
     keys = torch.empty(n_rank, dtype=torch.int64, device=dev)
     ts = torch.empty_like(keys)
@@ -84,7 +91,10 @@ def main():
         wms.append(m - args.delay_ms - 1)          # BoundedOutOfOrdernessWatermarks.onPeriodicEmit
     wms[-1] = A.LONG_MAX                           # final watermark flushes every window
 
-    cfg_kw = dict(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=args.window_ms,
+    win_kw = dict(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=args.window_ms)
+    if args.config == "c3":
+        win_kw = dict(window_kind="SLIDE", semantics="TABLE", size_ms=60_000, slide_ms=1_000)
+    cfg_kw = dict(**win_kw,
                   aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=int(args.keys * float(os.environ.get("FWA_KCAP", "1"))),
                   output_on_device=1, device=local_rank)
     if world > 1:
@@ -142,8 +152,26 @@ def main():
     alg_bytes_ingest = 24.0 * st.ingest_records       # key + ts + val, read once
     achieved = alg_bytes_ingest / ingest_s / 1e9 if ingest_s > 0 else 0.0
     e2e_bytes = 24.0 * recs_timed + 40.0 * rows_all    # whole-job algorithmic bytes incl. emitted rows
+    # HBM traffic per ingest launch (Phase P + Phase A) from the committed rocprofv3 PMC passes of this
+    # same workload (counters need their own runs: tools/gpu_pmc.sh); null for other shapes
+    traffic, traffic_src = None, None
+    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_c2_v6.json")
+    if args.config == "c2" and os.path.exists(pmc_path):
+        pmc = json.load(open(pmc_path))
+        if pmc["config"]["batch"] == B:
+            traffic = pmc["ingest_bytes_per_launch"]
+            traffic_src = "profiles/r01_pmc_c2_v6.json (FETCH_SIZE x2 + WRITE_SIZE, partition2 + combine3)"
+    if args.config == "c3":
+        metric = "records/sec aggregated (C3: HOP 60s/1s, Zipf(1.1) keys over %d items)" % args.keys
+        workload = ("C3: Table HOP 60s/1s (1s slices) COUNT+SUM(long), Zipf(1.1) over %d keys, %d records/GPU "
+                    "(%d batches of %d), D=%dms" % (args.keys, args.steps * B, args.steps, B, args.delay_ms))
+    else:
+        metric = "records/sec aggregated (1M-key tumbling SUM)"
+        workload = ("C2: event-time tumbling %ds COUNT+SUM(long), %d uniform keys, %d records/GPU "
+                    "(%d batches of %d), D=%dms" % (args.window_ms // 1000, args.keys, args.steps * B,
+                                                    args.steps, B, args.delay_ms))
     out = {
-        "metric": "records/sec aggregated (1M-key tumbling SUM)",
+        "metric": metric,
         "value": value,
         "unit": "records/s",
         "n_gpus": world,
@@ -156,9 +184,7 @@ def main():
         "dtype": "int64",
         "data": "synthetic (splitmix64 counter-based stream, SURVEY.md §8(d)), generated in HBM",
         "config": {
-            "workload": "C2: event-time tumbling %ds COUNT+SUM(long), %d uniform keys, %d records/GPU "
-                        "(%d batches of %d), D=%dms" % (args.window_ms // 1000, args.keys, args.steps * B,
-                                                        args.steps, B, args.delay_ms),
+            "workload": workload,
             "records_per_gpu_timed": args.steps * B, "keys": args.keys, "batch": B,
             "window_ms": args.window_ms, "parallelism": "key-group dp%d" % world,
             "exchange": ("two-phase partials (local pre-aggregation, RCCL all_to_all)" if args.exchange == "partials"
@@ -167,7 +193,8 @@ def main():
         "roofline": {
             "bound": "hbm", "kernel": "ingest_kernel",
             "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+            "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_unit": "bytes per launch",
+            "traffic_source": traffic_src, "alg_bytes_per_launch": 24 * B,
             "alg_bytes_per_record": 24, "launches": st.ingest_launches,
             "avg_launch_ms": st.ingest_ms / max(1, st.ingest_launches),
         },

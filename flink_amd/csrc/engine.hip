@@ -741,6 +741,27 @@ __device__ __forceinline__ double carried_f64(unsigned long long raw, int kind) 
                                                          : __longlong_as_double((long long)raw);
 }
 
+// Apply one bucket entry (offset o, global kid g) to its slice's HBM accumulators with global atomics.
+__device__ __forceinline__ void strag_apply(const CombineArgs& a, const EngineConst& c, uint64_t o, uint32_t g) {
+    const int32_t slot = a.rel2slot[a.b_rel[o]];
+    if (slot < 0) return;
+    unsigned long long* base = a.slot_base[slot];
+    atomicAdd(&base[g], 1ull);
+    for (int jj = 0; jj < c.naggs; ++jj) {
+        const AggDesc d = c.agg[jj];
+        if (d.acc == 0) continue;
+        const unsigned long long raw = d.vslot == 0 ? a.b_val0[o] : a.b_val1[o];
+        unsigned long long* gp = base + (int64_t)d.acc * a.stride + g;
+        switch (d.acc_kind) {
+            case ACC_ADD_I64: atomicAdd(gp, raw); break;
+            case ACC_ADD_F64: atomicAdd((double*)gp, carried_f64(raw, d.kind)); break;
+            case ACC_MIN_ORD: atomicMin(gp, carried_ord(raw, d.kind)); break;
+            case ACC_MAX_ORD: atomicMax(gp, carried_ord(raw, d.kind)); break;
+            default: break;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // combine3: the Phase A combiner, restructured for latency tolerance (DESIGN.md §4, r01 clock64
 // profile: the v2 combiner spent 43 % of its time in serialised flat RMWs / scalar-load waits).
@@ -953,11 +974,13 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
             if (rel[j] < lo) {          // older than the window: applied after the kernel with atomics
                 if (a.prof) pacc[6] += 1000000;
                 const int32_t si = atomicAdd(a.strag_n, 1);
+                const uint64_t so = (uint64_t)(boff + cb + (int64_t)j * LPS + li);
+                const uint32_t sg = (uint32_t)(((int64_t)p << a.seg_log) + local);
                 if (si < a.strag_cap) {
-                    a.strag[si].o = (uint64_t)(boff + cb + (int64_t)j * LPS + li);
-                    a.strag[si].g = (uint32_t)(((int64_t)p << a.seg_log) + local);
-                } else {
-                    atomicOr(&a.st->key_full, 4);
+                    a.strag[si].o = so;
+                    a.strag[si].g = sg;
+                } else {   // list full (skewed, out-of-order input): apply it here; this block owns the
+                    strag_apply(a, c, so, sg);   // kid and has already merged that slice, so atomics suffice
                 }
                 continue;
             }
@@ -1001,23 +1024,7 @@ __global__ void straggler_kernel(CombineArgs a, const EngineConst* __restrict__ 
     const int32_t n = (int32_t)min((int64_t)*a.strag_n, a.strag_cap);
     for (int32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
         const StragEntry se = a.strag[t];
-        const int32_t slot = a.rel2slot[a.b_rel[se.o]];
-        if (slot < 0) continue;
-        unsigned long long* base = a.slot_base[slot];
-        atomicAdd(&base[se.g], 1ull);
-        for (int jj = 0; jj < c.naggs; ++jj) {
-            const AggDesc d = c.agg[jj];
-            if (d.acc == 0) continue;
-            const unsigned long long raw = d.vslot == 0 ? a.b_val0[se.o] : a.b_val1[se.o];
-            unsigned long long* gp = base + (int64_t)d.acc * a.stride + se.g;
-            switch (d.acc_kind) {
-                case ACC_ADD_I64: atomicAdd(gp, raw); break;
-                case ACC_ADD_F64: atomicAdd((double*)gp, carried_f64(raw, d.kind)); break;
-                case ACC_MIN_ORD: atomicMin(gp, carried_ord(raw, d.kind)); break;
-                case ACC_MAX_ORD: atomicMax(gp, carried_ord(raw, d.kind)); break;
-                default: break;
-            }
-        }
+        strag_apply(a, c, se.o, se.g);
     }
 }
 
@@ -1187,6 +1194,122 @@ __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineCo
         } else {
             emit_row(f, c, win, k, kvs[j], cnt[j], row);
         }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// fire_slide: one watermark fires a RUN of consecutive hop windows (HOP 60 s / 1 s over a batch of
+// 67 s of event time fires 67 windows of 60 slices each). The generic fire re-merges every window
+// from its slices (67 x 60 slice reads per key and column); here each key walks the run once with a
+// running sum, S_w = S_{w-1} + (slices entering) - (slices leaving): 2r slice reads per window
+// (r = slide / slice). Only for invertible accumulators -- COUNT and 64-bit integer sums, which wrap
+// exactly like Java long arithmetic, so the running sum equals the direct sum bit for bit; float
+// sums and MIN/MAX keep the generic fire. Rows are emitted window by window with one row
+// reservation per block and window.
+constexpr int kSlideMaxU = 2048;                  // union slices per launch (LDS slot table)
+constexpr int kSlideJ = 8;                        // keys per thread
+constexpr int kSlideAcc = 4;                      // COUNT + up to 3 integer-sum columns
+
+struct FireSlideArgs {
+    const unsigned long long* key_table;
+    int64_t capacity, stride;
+    const unsigned long long* const* upos;   // [m] slot base per union slice (nullptr: no records)
+    int32_t m, nw, L, r;                     // union slices, windows, slices per window, per slide
+    int64_t start0, slide, size;             // first window start, window step, window size
+    int64_t* o_key;
+    int64_t* o_start;
+    int64_t* o_end;
+    void* o_agg[FWA_MAX_AGGS];
+    DevStatus* st;
+};
+
+__global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    constexpr int kWaves = kBlock / 64;
+    __shared__ const unsigned long long* s_u[kSlideMaxU];
+    __shared__ uint32_t woff[kSlideJ][kWaves];
+    __shared__ unsigned long long s_base;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int i = tid; i < f.m; i += kBlock) s_u[i] = f.upos[i];
+    const int nacc = c.nacc;
+    const int64_t nk = f.capacity + 1;
+    const int64_t k0 = (int64_t)blockIdx.x * kBlock * kSlideJ;
+    unsigned long long kv[kSlideJ];
+    bool present[kSlideJ];
+    unsigned long long S[kSlideJ][kSlideAcc];
+#pragma unroll
+    for (int j = 0; j < kSlideJ; ++j) {
+        const int64_t k = k0 + (int64_t)j * kBlock + tid;
+        kv[j] = k < nk ? f.key_table[k] : kEmptyKey;
+        present[j] = k < nk && ((k < f.capacity) ? (kv[j] != kEmptyKey) : (kv[j] == 1ull));
+#pragma unroll
+        for (int a = 0; a < kSlideAcc; ++a) S[j][a] = 0;
+    }
+    __syncthreads();
+    // window 0: the sum of its L slices
+    for (int u = 0; u < f.L; ++u) {
+        const unsigned long long* b = s_u[u];
+        if (!b) continue;
+#pragma unroll
+        for (int j = 0; j < kSlideJ; ++j) {
+            if (!present[j]) continue;
+            const int64_t k = k0 + (int64_t)j * kBlock + tid;
+#pragma unroll
+            for (int a = 0; a < kSlideAcc; ++a) if (a < nacc) S[j][a] += b[(int64_t)a * f.stride + k];
+        }
+    }
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int w = 0; w < f.nw; ++w) {
+        if (w > 0) {
+            for (int t = 0; t < f.r; ++t) {
+                const unsigned long long* bin = s_u[(w - 1) * f.r + f.L + t];
+                const unsigned long long* bout = s_u[(w - 1) * f.r + t];
+#pragma unroll
+                for (int j = 0; j < kSlideJ; ++j) {
+                    if (!present[j]) continue;
+                    const int64_t k = k0 + (int64_t)j * kBlock + tid;
+#pragma unroll
+                    for (int a = 0; a < kSlideAcc; ++a) {
+                        if (a >= nacc) continue;
+                        const unsigned long long xin = bin ? bin[(int64_t)a * f.stride + k] : 0ull;
+                        const unsigned long long xout = bout ? bout[(int64_t)a * f.stride + k] : 0ull;
+                        S[j][a] = S[j][a] + xin - xout;
+                    }
+                }
+            }
+        }
+        unsigned long long masks[kSlideJ];
+#pragma unroll
+        for (int j = 0; j < kSlideJ; ++j) {
+            masks[j] = __ballot(present[j] && S[j][0] != 0);
+            if (lane == 0) woff[j][wid] = (uint32_t)__popcll(masks[j]);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t run = 0;
+            for (int j = 0; j < kSlideJ; ++j)
+                for (int v = 0; v < kWaves; ++v) { const uint32_t t = woff[j][v]; woff[j][v] = run; run += t; }
+            s_base = run ? atomicAdd(&f.st->rows, (unsigned long long)run) : 0ull;
+        }
+        __syncthreads();
+        const int64_t ws = f.start0 + (int64_t)w * f.slide;
+#pragma unroll
+        for (int j = 0; j < kSlideJ; ++j) {
+            if (!((masks[j] >> lane) & 1ull)) continue;
+            const int64_t k = k0 + (int64_t)j * kBlock + tid;
+            const int64_t row = (int64_t)s_base + woff[j][wid] + __popcll(masks[j] & lt);
+            f.o_key[row] = (k < f.capacity) ? (int64_t)kv[j] : LONG_MIN_J;
+            f.o_start[row] = ws;
+            f.o_end[row] = ws + f.size;
+            for (int a = 0; a < c.naggs; ++a) {
+                const AggDesc d = c.agg[a];
+                unsigned long long x = 0;
+#pragma unroll
+                for (int q = 1; q < kSlideAcc; ++q) if (q == d.acc) x = S[j][q];
+                write_agg(d, S[j][0], x, f.o_agg[a], row);
+            }
+        }
+        __syncthreads();   // woff / s_base reuse
     }
 }
 
@@ -1532,6 +1655,7 @@ struct fwa_engine {
     int32_t win_cap = 0;
     int32_t* d_win_slots = nullptr;
     int32_t win_slots_cap = 0;
+    void* d_upos = nullptr;            // fire_slide union slot table
     // watermark / stats
     int64_t wm = LONG_MIN_J;
     int64_t records_in = 0, late_dropped = 0, rows_out = 0;
@@ -1931,7 +2055,7 @@ void fwa_destroy(fwa_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel,
-                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n, e->d_reset_list,
+                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n, e->d_reset_list, e->d_upos,
                     e->d_scnt, e->d_sstart, e->d_send, e->d_sacc, e->d_sess_sort, e->d_sort_tmp, e->o_count};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
@@ -2790,6 +2914,73 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     return FWA_OK;
 }
 
+// A run of consecutive hop windows with invertible accumulators: fire_slide_kernel. *done = false
+// leaves the run to the generic fire.
+static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>& wins, int64_t* nrows, bool* done) {
+    *done = false;
+    if (e->nacc > kSlideAcc) return FWA_OK;
+    for (int c = 1; c < e->nacc; ++c) if (e->ec.acc_kind[c] != ACC_ADD_I64) return FWA_OK;
+    if (e->size % e->g || e->slide % e->g) return FWA_OK;
+    const int64_t L = e->size / e->g, r = e->slide / e->g;
+    const int64_t start0 = wins.begin()->second;
+    int64_t nw = 0;
+    for (auto& w : wins) {   // consecutive hop windows: start_w = start0 + w * slide
+        if (w.second != jm::wadd(start0, (int64_t)((uint64_t)nw * (uint64_t)e->slide)) || w.first != jm::wadd(w.second, e->size))
+            return FWA_OK;
+        ++nw;
+    }
+    const int64_t m = (nw - 1) * r + L;
+    if (m > kSlideMaxU) return FWA_OK;
+    const int64_t q0 = slice_q(e, start0);
+    std::vector<const unsigned long long*> up(m, nullptr);
+    bool any = false;
+    for (int64_t i = 0; i < m; ++i) {
+        auto it = e->live.find(q0 + i);
+        if (it != e->live.end() && e->touched[it->second]) { up[i] = e->slot_ptr[it->second]; any = true; }
+    }
+    *done = true;
+    if (!any) return FWA_OK;
+    if (!e->d_upos) HIPCHK(e, hipMalloc(&e->d_upos, sizeof(void*) * kSlideMaxU));
+    int rc = upload(e, e->d_upos, up.data(), sizeof(void*) * m);
+    if (rc) return rc;
+    const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
+    rc = ensure_out(e, nw * nkeys);
+    if (rc) return rc;
+    HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
+    FireSlideArgs f;
+    memset(&f, 0, sizeof(f));
+    f.key_table = e->d_keys;
+    f.capacity = e->capacity;
+    f.stride = e->stride;
+    f.upos = (const unsigned long long* const*)e->d_upos;
+    f.m = (int32_t)m;
+    f.nw = (int32_t)nw;
+    f.L = (int32_t)L;
+    f.r = (int32_t)r;
+    f.start0 = start0;
+    f.slide = e->slide;
+    f.size = e->size;
+    f.o_key = e->o_key;
+    f.o_start = e->o_start;
+    f.o_end = e->o_end;
+    for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
+    f.st = e->d_st;
+    const int64_t grid = (e->capacity + 1 + (int64_t)kBlock * kSlideJ - 1) / ((int64_t)kBlock * kSlideJ);
+    HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
+    fire_slide_kernel<<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
+    rc = sync_status(e);
+    if (rc) return rc;
+    *nrows = (int64_t)e->h_st->rows;
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+    e->fire_ms += ms;
+    e->fire_launches++;
+    e->fire_rows += *nrows;
+    return FWA_OK;
+}
+
 int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
     if (!e) return FWA_E_STATE;
     HIPCHK(e, hipSetDevice(e->cfg.device));
@@ -2847,9 +3038,15 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
                 if (mt > prev && mt <= wm) wins.insert({w.second, w.first});
             }
         }
+        bool slid = false;
+        static const bool noslide = getenv("FWA_NOSLIDE") != nullptr;   // A/B switch (timing experiments)
+        if (e->kind == FWA_SLIDE && wins.size() >= 2 && !noslide) {
+            int rc = fire_slide(e, wins, &nrows, &slid);
+            if (rc) return rc;
+        }
         std::vector<FireWindow> hw;
         std::vector<int32_t> hs;
-        for (auto& w : wins) {
+        if (!slid) for (auto& w : wins) {
             FireWindow f;
             f.end = w.first;
             f.start = w.second;

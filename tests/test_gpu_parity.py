@@ -350,3 +350,55 @@ def test_async_push_vs_oracle(eng_mod, ci):
     assert dropped_o > 0 and st.late_dropped == dropped_o and st.records_in == n
     g.close()
     o.close()
+
+
+SLIDE_SUM_AGGS = [("COUNT", 0), ("SUM_I64", 0), ("AVG_I64", 0)]
+
+
+@pytest.mark.parametrize("ci", [3, 4, 5])
+def test_slide_running_fire_vs_oracle(eng_mod, ci):
+    """Hop windows with invertible accumulators fire through fire_slide_kernel (running sums over a
+    run of consecutive windows): bit-exact against the oracle, including i64 wrap-around."""
+    from oracle.oracle import Oracle
+    cfg = A.make_config(aggs=SLIDE_SUM_AGGS, key_capacity=4096, **CONFIGS[ci])
+    names = A.agg_names(cfg)
+    stream = random_stream(500 + ci, 40_000, 600, 60_000, 1500)
+    dropped = run_pair(cfg, batches_of(stream, 8, 1500), eng_mod.WindowAggregator, Oracle, names)
+    assert dropped > 0
+
+
+def test_c3_shape_zipf_hop_vs_oracle(eng_mod):
+    """C3 shape at 2^19 records: Table HOP 60 s / 1 s, Zipf(1.1) keys (one key carries ~11 % of the
+    records: bucket overflow and replay), COUNT + SUM(long), device generator, exact equality."""
+    import torch
+    from oracle import oracle as O
+    n, nkeys = 1 << 19, 100_000
+    w = 1.0 / np.arange(1, nkeys + 1, dtype=np.float64) ** 1.1
+    cdf = np.cumsum(w) / w.sum()
+    dcdf = torch.from_numpy(cdf).cuda()
+    p = A.GenParams(seed_k=5, seed_t=6, seed_v=7, first_index=0, total_records=n, num_keys=nkeys, t0_ms=0,
+                    span_ms=200_000, max_delay_ms=1000, key_dist=1, val_kind=0)
+    p.zipf_cdf = dcdf.data_ptr()
+    k = torch.empty(n, dtype=torch.int64, device="cuda")
+    t = torch.empty_like(k)
+    v = torch.empty_like(k)
+    eng_mod.generate(p, n, k, t, v)
+    torch.cuda.synchronize()
+    kh, th, vh = k.cpu().numpy(), t.cpu().numpy(), v.cpu().numpy()
+    assert np.array_equal((kh, th, vh)[0], O.generate(p, n, cdf=cdf)[0])
+    cfg = A.make_config(window_kind="SLIDE", semantics="TABLE", size_ms=60_000, slide_ms=1_000,
+                        aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=nkeys)
+    g = eng_mod.WindowAggregator(cfg)
+    o = O.Oracle(cfg)
+    nb = 4
+    for b in range(nb + 1):
+        if b < nb:
+            sl = slice(b * n // nb, (b + 1) * n // nb)
+            g.push(k[sl], t[sl], [v[sl]])
+            o.push(kh[sl], th[sl], [vh[sl]])
+            wm = int(th[: (b + 1) * n // nb].max()) - 1001
+        else:
+            wm = A.LONG_MAX
+        assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), ["COUNT", "SUM_I64"], ctx="wm=%d" % wm)
+    g.close()
+    o.close()
