@@ -2914,6 +2914,152 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     return FWA_OK;
 }
 
+// ---- snapshot / restore (include/flink_amd.h) ----
+static const uint64_t kSnapMagic = 0x3150414E53415746ull;   // "FWASNAP1"
+enum { kSnapHdr = 32 };                                       // header words
+// header word layout: 0 magic, 1 version, 2 window kind, 3 semantics, 4 size, 5 slide, 6 offset, 7 gap,
+// 8 allowed lateness, 9 max parallelism, 10 key kind, 11 num aggs, 12..19 agg kinds, 20 watermark,
+// 21 entries, 22 kg_start, 23 kg_end of the snapshotting handle, 24..31 reserved (0)
+
+static void snap_header(const fwa_engine* e, int64_t* h, int64_t n) {
+    memset(h, 0, sizeof(int64_t) * kSnapHdr);
+    h[0] = (int64_t)kSnapMagic;
+    h[1] = 1;
+    h[2] = e->cfg.window_kind;
+    h[3] = e->cfg.semantics;
+    h[4] = e->cfg.size_ms;
+    h[5] = e->cfg.slide_ms;
+    h[6] = e->cfg.offset_ms;
+    h[7] = e->cfg.gap_ms;
+    h[8] = e->cfg.allowed_lateness_ms;
+    h[9] = e->cfg.max_parallelism;
+    h[10] = e->cfg.key_kind;
+    h[11] = e->cfg.num_aggs;
+    for (int j = 0; j < e->cfg.num_aggs; ++j) h[12 + j] = e->cfg.aggs[j].kind;
+    h[20] = e->wm;
+    h[21] = n;
+    h[22] = e->cfg.kg_start;
+    h[23] = e->cfg.kg_end;
+}
+
+// Export every (key, slice) accumulator of every live slice (non-destructive raw fire), then bucket
+// the rows by key group on the host (counting sort) into the blob.
+int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
+    if (!e || !out) return FWA_E_ARG;
+    memset(out, 0, sizeof(*out));
+    if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "snapshot of session windows is not supported");
+    if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "snapshot needs a computable key hash");
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (int rc0 = settle_pending(e)) return rc0;
+    std::vector<FireWindow> hw;
+    std::vector<int32_t> hs;
+    for (auto& kv : e->live) {
+        if (!e->touched[kv.second]) continue;
+        FireWindow f;
+        f.start = slice_start(e, kv.first);
+        f.end = jm::wadd(f.start, e->g);
+        f.slot_off = (int32_t)hs.size();
+        f.nslots = 1;
+        hs.push_back(kv.second);
+        hw.push_back(f);
+    }
+    int64_t n = 0;
+    if (!hw.empty()) {
+        const int64_t rows0 = e->fire_rows, launches0 = e->fire_launches;
+        const double ms0 = e->fire_ms;
+        int rc = launch_fire(e, hw, hs, 1, &n);
+        if (rc) return rc;
+        e->fire_rows = rows0;            // a snapshot is not a fire: keep the fire counters clean
+        e->fire_launches = launches0;
+        e->fire_ms = ms0;
+    }
+    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, ncols = 3 + na;
+    std::vector<int64_t> cols((size_t)n * ncols);
+    const void* src[3 + FWA_MAX_AGGS] = {e->o_key, e->o_start, e->o_count};
+    for (int j = 0; j < na; ++j) src[3 + j] = e->o_agg[j];
+    for (int c = 0; c < ncols && n > 0; ++c)
+        HIPCHK(e, hipMemcpy(cols.data() + (size_t)c * n, src[c], 8 * (size_t)n, hipMemcpyDeviceToHost));
+    std::vector<int32_t> kg((size_t)n);
+    std::vector<int64_t> off((size_t)maxp + 1, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        kg[i] = jm::key_group(jm::key_hash(cols[i], e->cfg.key_kind, 0), maxp);
+        off[kg[i] + 1]++;
+    }
+    for (int g = 0; g < maxp; ++g) off[g + 1] += off[g];
+    const size_t words = kSnapHdr + (size_t)maxp + 1 + (size_t)n * ncols;
+    int64_t* b = (int64_t*)malloc(words * 8);
+    if (!b) return fail(e, FWA_E_OOM, "snapshot blob allocation failed");
+    snap_header(e, b, n);
+    memcpy(b + kSnapHdr, off.data(), 8 * ((size_t)maxp + 1));
+    int64_t* body = b + kSnapHdr + maxp + 1;
+    std::vector<int64_t> cur(off.begin(), off.end() - 1);
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t d = cur[kg[i]]++;
+        for (int c = 0; c < ncols; ++c) body[(size_t)c * n + d] = cols[(size_t)c * n + i];
+    }
+    out->data = b;
+    out->size = (int64_t)(words * 8);
+    return FWA_OK;
+}
+
+void fwa_blob_free(fwa_blob* b) {
+    if (!b) return;
+    free(b->data);
+    b->data = nullptr;
+    b->size = 0;
+}
+
+int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, int32_t n_blobs) {
+    if (!e) return FWA_E_STATE;
+    if (n_blobs < 0 || (n_blobs > 0 && (!blobs || !sizes))) return fail(e, FWA_E_ARG, "null snapshot list");
+    if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "restore of session windows is not supported");
+    if (int rc0 = settle_pending(e)) return rc0;
+    if (e->records_in != 0 || e->wm != LONG_MIN_J || !e->live.empty())
+        return fail(e, FWA_E_STATE, "restore needs a fresh handle");
+    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism;
+    int64_t ref[kSnapHdr];
+    snap_header(e, ref, 0);
+    // validate every blob before touching state
+    for (int32_t b = 0; b < n_blobs; ++b) {
+        const int64_t* h = (const int64_t*)blobs[b];
+        if (!h || sizes[b] < (int64_t)(8 * (kSnapHdr + maxp + 1)) || (uint64_t)h[0] != kSnapMagic || h[1] != 1)
+            return fail(e, FWA_E_ARG, "not a flink_amd snapshot (bad magic/version/size)");
+        for (int w = 2; w < 20; ++w)
+            if (h[w] != ref[w]) return fail(e, FWA_E_ARG, "snapshot window/aggregate configuration differs");
+        const int64_t n = h[21];
+        if (n < 0 || sizes[b] != (int64_t)(8 * (kSnapHdr + maxp + 1 + (size_t)n * (3 + na))))
+            return fail(e, FWA_E_ARG, "snapshot size does not match its entry count");
+    }
+    int64_t wm = LONG_MAX_J;
+    bool any = false;
+    for (int32_t b = 0; b < n_blobs; ++b) {
+        const int64_t* h = (const int64_t*)blobs[b];
+        const int64_t n = h[21];
+        wm = std::min<int64_t>(wm, h[20]);
+        any = true;
+        const int64_t* off = h + kSnapHdr;
+        const int64_t lo = off[e->cfg.kg_start], hi = off[e->cfg.kg_end + 1];
+        if (lo < 0 || hi < lo || hi > n) return fail(e, FWA_E_ARG, "corrupt key-group offsets");
+        if (hi == lo) continue;
+        const int64_t* body = off + maxp + 1;
+        const void* acc[FWA_MAX_AGGS] = {};
+        for (int j = 0; j < na; ++j) acc[j] = body + (size_t)(3 + j) * n + lo;
+        int64_t late = 0;
+        int rc = fwa_push_partials(e, body + lo, body + (size_t)n + lo, body + (size_t)2 * n + lo, acc, hi - lo, 0, &late);
+        if (rc) return rc;
+        if (late) return fail(e, FWA_E_STATE, "restored partials were dropped as late");
+    }
+    if (int rc = settle_pending(e)) return rc;
+    e->records_in = 0;   // metrics are not part of the snapshot
+    e->late_dropped = 0;
+    if (any && wm > e->wm) {   // windows with maxTs <= wm fired before the snapshot: no re-fire
+        int rc = retire_slices(e, wm);
+        if (rc) return rc;
+        e->wm = wm;
+    }
+    return FWA_OK;
+}
+
 // A run of consecutive hop windows with invertible accumulators: fire_slide_kernel. *done = false
 // leaves the run to the generic fire.
 static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>& wins, int64_t* nrows, bool* done) {

@@ -22,6 +22,11 @@ class EngineError(RuntimeError):
         self.code = code
 
 
+class Blob(C.Structure):
+    """fwa_blob (include/flink_amd.h): engine-allocated snapshot buffer."""
+    _fields_ = [("data", C.c_void_p), ("size", C.c_int64)]
+
+
 def lib():
     """Load libflink_amd.so (built by `make -C flink_amd/csrc` / __graft_entry__.build())."""
     global _LIB
@@ -41,6 +46,12 @@ def lib():
     L.fwa_push_partials.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                     C.c_int32, C.POINTER(C.c_int64)]
     L.fwa_push_partials.restype = C.c_int
+    L.fwa_snapshot.argtypes = [C.c_void_p, C.POINTER(Blob)]
+    L.fwa_snapshot.restype = C.c_int
+    L.fwa_blob_free.argtypes = [C.POINTER(Blob)]
+    L.fwa_blob_free.restype = None
+    L.fwa_restore.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.c_int32]
+    L.fwa_restore.restype = C.c_int
     L.fwa_flush.argtypes = [C.c_void_p]
     L.fwa_flush.restype = C.c_int
     L.fwa_version.restype = C.c_char_p
@@ -180,6 +191,27 @@ class WindowAggregator:
                                      A.PUSH_DEVICE_PTRS if device else 0, C.byref(dropped))
         _check(rc, self.h)
         return dropped.value
+
+    # -- checkpoint / restore (HeapSnapshotStrategy + SlicingWindowOperator watermark state) --
+    def snapshot(self):
+        """Return the handle's keyed window state + watermark as bytes (key-group-partitioned blob,
+        format in include/flink_amd.h; parse with flink_amd.snapshot.parse)."""
+        b = Blob()
+        _check(lib().fwa_snapshot(self.h, C.byref(b)), self.h)
+        try:
+            return C.string_at(b.data, b.size) if b.size else b""
+        finally:
+            lib().fwa_blob_free(C.byref(b))
+
+    def restore(self, blobs):
+        """Restore a fresh handle from one or more snapshots (only this handle's key groups are read;
+        watermark = min over the snapshots)."""
+        if isinstance(blobs, (bytes, bytearray)):
+            blobs = [blobs]
+        bufs = [C.create_string_buffer(bytes(b), len(b)) for b in blobs]
+        ptrs = (C.c_void_p * max(1, len(bufs)))(*[C.cast(b, C.c_void_p).value for b in bufs])
+        sizes = (C.c_int64 * max(1, len(bufs)))(*[len(b) for b in blobs])
+        _check(lib().fwa_restore(self.h, ptrs, sizes, len(bufs)), self.h)
 
     def flush(self):
         _check(lib().fwa_flush(self.h), self.h)

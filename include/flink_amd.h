@@ -28,6 +28,9 @@
  *   fwa_key_groups         KeyGroupRangeAssignment.assignToKeyGroup + computeOperatorIndexForKeyGroup
  *                            flink-runtime/.../state/KeyGroupRangeAssignment.java:63-127
  *                          (the keyBy partitioner KeyGroupStreamPartitioner.selectChannel :55-65)
+ *   fwa_snapshot           HeapSnapshotStrategy (keyed window state by key group) + the watermark union
+ *                            state of SlicingWindowOperator.snapshotState (:204-209)
+ *   fwa_restore            HeapRestoreOperation / SlicingWindowOperator.initializeState (:186-202)
  *   fwa_destroy            WindowOperator.close / SlicingWindowProcessor.close
  *
  * Status codes mirror the Java exceptions the reference throws.
@@ -215,6 +218,33 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out);
  * the slice. Late partials are dropped like records (their counts are added to late_dropped_out). */
 int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_ts, const int64_t* count,
                       const void* const* acc, int64_t n, int32_t flags, int64_t* late_dropped_out);
+
+/* ---- checkpoint / restore ----
+ * fwa_snapshot replaces the keyed-state half of the operator snapshot: HeapSnapshotStrategy writes the
+ * window state per key group with a KeyGroupRangeOffsets index (HeapSnapshotStrategy.java:154-179,
+ * CopyOnWriteStateMapSnapshot.java:142-147) and SlicingWindowOperator.snapshotState stores the current
+ * watermark in union list state (SlicingWindowOperator.java:204-209). The blob holds, in one buffer
+ * (little-endian int64 words): a header (magic "FWASNAP1", window/aggregate configuration,
+ * watermark, entry count), a key-group offset table off[max_parallelism + 1] (entries of key group g
+ * are [off[g], off[g+1])), then SoA columns key[n], slice_start[n], count[n], acc_j[n] (one per
+ * aggregate, same encoding as fwa_partials). Per-key timers are not stored: the engine's timers are
+ * derived from the live slices and the watermark, as the reference re-registers them from state.
+ * Not available for SESSION windows (FWA_E_UNSUPPORTED). The blob is engine-allocated; free it
+ * with fwa_blob_free. */
+typedef struct fwa_blob {
+    void* data;
+    int64_t size;   /* bytes */
+} fwa_blob;
+
+int fwa_snapshot(fwa_engine* e, fwa_blob* out);
+void fwa_blob_free(fwa_blob* b);
+
+/* Restore a fresh handle (nothing pushed yet) from one or more snapshots of handles with the same
+ * window and aggregate configuration: only the key groups of this handle's [kg_start, kg_end] are
+ * read (rescaling, StateAssignmentOperation / KeyGroupRangeOffsets), and the watermark becomes the
+ * MIN of the snapshots' watermarks (SlicingWindowOperator.initializeState :186-202). Windows that
+ * fired before the snapshot do not fire again. */
+int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, int32_t n_blobs);
 
 /* Reset the kernel timing counters of fwa_stats (bench warm-up). */
 int fwa_reset_timers(fwa_engine* e);
