@@ -43,12 +43,18 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "c5s"], default="c2",
                     help="c2: tumbling 10s COUNT+SUM(long), 1M uniform keys (the metric's workload); "
-                         "c3: HOP 60s/1s (Table slicing), Zipf(1.1) keys over 1M items")
+                         "c3: HOP 60s/1s (Table slicing), Zipf(1.1) keys over 1M items; "
+                         "c4: tumbling 10s COUNT+SUM(long), 100M uniform keys, maxParallelism 128; "
+                         "c5: Table TUMBLE 10s TVF COUNT, SUM(double), AVG(double), MAX(float), MAX(double); "
+                         "c5s: DataStream session windows (gap 5s), same float aggregates")
     ap.add_argument("--exchange", choices=["partials", "raw"], default="partials",
                     help="N>1 keyBy plan: two-phase partial accumulators (default) or raw records")
     args = ap.parse_args()
+    if args.config == "c4" and args.keys == 1_000_000:
+        args.keys = 100_000_000
+    fp = args.config in ("c5", "c5s")   # float value columns (f32 + f64)
 
     from flink_amd import _abi as A
     from flink_amd import engine as E
@@ -72,7 +78,7 @@ def main():
     p = A.GenParams(seed_k=0x5eed0001 ^ (rank * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF),
                     seed_t=0x5eed0002 + rank, seed_v=0x5eed0003 + rank, first_index=0, total_records=n_rank,
                     num_keys=args.keys, t0_ms=1_700_000_000_000, span_ms=span, max_delay_ms=args.delay_ms,
-                    key_dist=1 if args.config == "c3" else 0, val_kind=0)
+                    key_dist=1 if args.config == "c3" else 0, val_kind=1 if fp else 0)
     if args.config == "c3":   # Zipf(1.1) CDF over the key ids, sampled bit-identically by the device generator
         w = 1.0 / np.arange(1, args.keys + 1, dtype=np.float64) ** 1.1
         zcdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
@@ -80,8 +86,13 @@ def main():
     log("rank %d/%d generating %d records (%.1f GB) in HBM" % (rank, world, n_rank, n_rank * 24 / 1e9))
     keys = torch.empty(n_rank, dtype=torch.int64, device=dev)
     ts = torch.empty_like(keys)
-    vals = torch.empty_like(keys)
-    E.generate(p, n_rank, keys, ts, vals, device=local_rank)
+    if fp:
+        vals = torch.empty(n_rank, dtype=torch.float32, device=dev)
+        vals_d = torch.empty(n_rank, dtype=torch.float64, device=dev)
+        E.generate(p, n_rank, keys, ts, None, vals, vals_d, device=local_rank)
+    else:
+        vals = torch.empty_like(keys)
+        E.generate(p, n_rank, keys, ts, vals, device=local_rank)
     torch.cuda.synchronize()
     bmax = ts.view(S, B).max(dim=1).values.cpu().numpy()
     wms = []
@@ -94,20 +105,28 @@ def main():
     win_kw = dict(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=args.window_ms)
     if args.config == "c3":
         win_kw = dict(window_kind="SLIDE", semantics="TABLE", size_ms=60_000, slide_ms=1_000)
+    aggs = [("COUNT", 0), ("SUM_I64", 0)]
+    if fp:   # C5: column 0 = f (FLOAT), column 1 = d (DOUBLE)
+        aggs = [("COUNT", 0), ("SUM_F64", 1), ("AVG_F64", 1), ("MAX_F32", 0), ("MAX_F64", 1)]
+        win_kw = dict(window_kind="TUMBLE", semantics="TABLE", size_ms=args.window_ms)
+        if args.config == "c5s":
+            win_kw = dict(window_kind="SESSION", semantics="DATASTREAM", gap_ms=5_000)
     cfg_kw = dict(**win_kw,
-                  aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=int(args.keys * float(os.environ.get("FWA_KCAP", "1"))),
+                  aggs=aggs, key_capacity=int(args.keys * float(os.environ.get("FWA_KCAP", "1"))),
                   output_on_device=1, device=local_rank)
+    cols_of = (lambda b: [vals[b * B:(b + 1) * B], vals_d[b * B:(b + 1) * B]]) if fp else \
+        (lambda b: [vals[b * B:(b + 1) * B]])
     if world > 1:
         from flink_amd.distributed import KeyedWindowPipeline, TwoPhaseKeyedWindowPipeline
         cls = TwoPhaseKeyedWindowPipeline if args.exchange == "partials" else KeyedWindowPipeline
         pipe = cls(rank, world, **cfg_kw)
         eng = pipe.local if args.exchange == "partials" else pipe.engine   # the ingest path being measured
         engines = [pipe.engine] + ([pipe.local] if args.exchange == "partials" else [])
-        push = lambda b: pipe.push(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], [vals[b * B:(b + 1) * B]])  # noqa: E731
+        push = lambda b: pipe.push(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], cols_of(b))  # noqa: E731
         fire = lambda b: pipe.advance_watermark(wms[b], device_output=True)["key"].shape[0]  # noqa: E731
     else:
         eng = E.WindowAggregator(A.make_config(**cfg_kw))
-        views = [(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], [vals[b * B:(b + 1) * B]]) for b in range(S)]
+        views = [(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], cols_of(b)) for b in range(S)]
         push = lambda b: eng.push(*views[b], sync=False)  # noqa: E731
         # fired rows stay in HBM (engine-owned device columns); only the row count comes back
         fire = lambda b: eng.advance_watermark_raw(wms[b]).n_rows  # noqa: E731
@@ -149,9 +168,11 @@ def main():
 
     # live roofline of the dominant kernel (ingest), HIP events on the engine's stream
     ingest_s = st.ingest_ms / 1e3
-    alg_bytes_ingest = 24.0 * st.ingest_records       # key + ts + val, read once
+    rec_bytes = 28 if fp else 24                      # key + ts + val(s), read once; C5: f32 + f64
+    alg_bytes_ingest = rec_bytes * st.ingest_records
     achieved = alg_bytes_ingest / ingest_s / 1e9 if ingest_s > 0 else 0.0
-    e2e_bytes = 24.0 * recs_timed + 40.0 * rows_all    # whole-job algorithmic bytes incl. emitted rows
+    row_bytes = 24 + 8 * len(aggs)                     # key, start, end + one 8 B column per aggregate
+    e2e_bytes = rec_bytes * recs_timed + row_bytes * rows_all   # whole-job algorithmic bytes incl. emitted rows
     # HBM traffic per ingest launch (Phase P + Phase A) from the committed rocprofv3 PMC passes of this
     # same workload (counters need their own runs: tools/gpu_pmc.sh); null for other shapes
     traffic, traffic_src = None, None
@@ -165,6 +186,17 @@ def main():
         metric = "records/sec aggregated (C3: HOP 60s/1s, Zipf(1.1) keys over %d items)" % args.keys
         workload = ("C3: Table HOP 60s/1s (1s slices) COUNT+SUM(long), Zipf(1.1) over %d keys, %d records/GPU "
                     "(%d batches of %d), D=%dms" % (args.keys, args.steps * B, args.steps, B, args.delay_ms))
+    elif args.config == "c4":
+        metric = "records/sec aggregated (C4: %dM-key tumbling SUM, maxParallelism 128)" % (args.keys // 1_000_000)
+        workload = ("C4: event-time tumbling %ds COUNT+SUM(long), %d uniform keys, %d records/GPU "
+                    "(%d batches of %d), D=%dms" % (args.window_ms // 1000, args.keys, args.steps * B,
+                                                    args.steps, B, args.delay_ms))
+    elif fp:
+        kind = "Table TUMBLE %ds TVF" % (args.window_ms // 1000) if args.config == "c5" else "DataStream SESSION gap 5s"
+        metric = "records/sec aggregated (C5: %s, COUNT/SUM/AVG(double)/MAX(float,double))" % kind
+        workload = ("C5: %s, COUNT, SUM(d), AVG(d), MAX(f), MAX(d) over f32/f64 in [0,1), %d uniform keys, "
+                    "%d records/GPU (%d batches of %d), D=%dms" % (kind, args.keys, args.steps * B, args.steps, B,
+                                                                   args.delay_ms))
     else:
         metric = "records/sec aggregated (1M-key tumbling SUM)"
         workload = ("C2: event-time tumbling %ds COUNT+SUM(long), %d uniform keys, %d records/GPU "
@@ -181,7 +213,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int64",
+        "dtype": "f32+f64" if fp else "int64",
         "data": "synthetic (splitmix64 counter-based stream, SURVEY.md §8(d)), generated in HBM",
         "config": {
             "workload": workload,
@@ -194,8 +226,8 @@ def main():
             "bound": "hbm", "kernel": "ingest_kernel",
             "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_unit": "bytes per launch",
-            "traffic_source": traffic_src, "alg_bytes_per_launch": 24 * B,
-            "alg_bytes_per_record": 24, "launches": st.ingest_launches,
+            "traffic_source": traffic_src, "alg_bytes_per_launch": rec_bytes * B,
+            "alg_bytes_per_record": rec_bytes, "launches": st.ingest_launches,
             "avg_launch_ms": st.ingest_ms / max(1, st.ingest_launches),
         },
         "end_to_end_hbm_frac": e2e_bytes / elapsed / 1e9 / HBM_PEAK_GBPS / world,
@@ -204,7 +236,7 @@ def main():
         "rows_emitted": rows_all,
         "late_dropped": sum(x.stats().late_dropped for x in engines) if args.exchange == "partials" or world == 1 else dropped,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         out["cpu_baseline"] = cpu_baseline(args, cfg_kw)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -79,7 +79,8 @@ struct AggDesc {
     int32_t acc;                // accumulator column (>=1) or 0 for COUNT
     int32_t acc_kind;
     int32_t vslot;              // partitioned path: which carried value column feeds this aggregate
-    int32_t pad;
+    int32_t alias;              // 1: shares the accumulator column of an earlier aggregate (e.g. SUM(d) and
+                                // AVG(d) keep one double sum): read at fire, never updated through it
 };
 
 struct EngineConst {
@@ -258,7 +259,7 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         for (int j = 0; j < FWA_MAX_AGGS; ++j) {
             if (j >= c.naggs) break;
             const AggDesc dsc = c.agg[j];
-            if (dsc.acc == 0) continue;
+            if (dsc.acc == 0 || dsc.alias) continue;
             unsigned long long* col = base + (int64_t)dsc.acc * a.stride + kid;
             const unsigned long long x = a.pcount ? ((const unsigned long long*)a.cols[j])[i]   // accumulator
                                                   : acc_input(dsc, a.cols[dsc.col], i);
@@ -749,7 +750,7 @@ __device__ __forceinline__ void strag_apply(const CombineArgs& a, const EngineCo
     atomicAdd(&base[g], 1ull);
     for (int jj = 0; jj < c.naggs; ++jj) {
         const AggDesc d = c.agg[jj];
-        if (d.acc == 0) continue;
+        if (d.acc == 0 || d.alias) continue;
         const unsigned long long raw = d.vslot == 0 ? a.b_val0[o] : a.b_val1[o];
         unsigned long long* gp = base + (int64_t)d.acc * a.stride + g;
         switch (d.acc_kind) {
@@ -796,7 +797,7 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
     __shared__ int s_desc[FWA_MAX_AGGS + 1];   // generic layout: per column kind | vslot << 8 | input kind << 16
     if (LAYOUT == 0 && tid == 0) {
         for (int j = 0; j < c.naggs; ++j)
-            if (c.agg[j].acc > 0) s_desc[c.agg[j].acc] = c.agg[j].acc_kind | (c.agg[j].vslot << 8) | (c.agg[j].kind << 16);
+            if (c.agg[j].acc > 0 && !c.agg[j].alias) s_desc[c.agg[j].acc] = c.agg[j].acc_kind | (c.agg[j].vslot << 8) | (c.agg[j].kind << 16);
     }
     unsigned long long* lkey = (unsigned long long*)smem;
     uint32_t* lcnt = (uint32_t*)(smem + (size_t)seg * 8);
@@ -1424,7 +1425,7 @@ __global__ void __launch_bounds__(kBlock) sess_process_kernel(SessArgs a, const 
             a.s_acc[base + first] += 1ull;                      // COUNT(*)
             for (int jj = 0; jj < c.naggs; ++jj) {              // AggregateFunction.add
                 const AggDesc d = c.agg[jj];
-                if (d.acc == 0) continue;
+                if (d.acc == 0 || d.alias) continue;
                 unsigned long long* p = &a.s_acc[d.acc * a.sstride + base + first];
                 *p = acc_combine(d.acc_kind, *p, acc_input(d, a.cols[d.col], i));
             }
@@ -1731,6 +1732,14 @@ int acc_kind_of(int kind) {
         case FWA_SUM_F32: case FWA_SUM_F64: case FWA_AVG_F32: case FWA_AVG_F64: return ACC_ADD_F64;
         case FWA_MIN_I64: case FWA_MIN_F32: case FWA_MIN_F64: return ACC_MIN_ORD;
         default: return ACC_MAX_ORD;
+    }
+}
+
+int input_class(int kind) {   // 0: BIGINT input, 1: FLOAT, 2: DOUBLE
+    switch (kind) {
+        case FWA_SUM_F32: case FWA_MIN_F32: case FWA_MAX_F32: case FWA_AVG_F32: return 1;
+        case FWA_SUM_F64: case FWA_MIN_F64: case FWA_MAX_F64: case FWA_AVG_F64: return 2;
+        default: return 0;
     }
 }
 
@@ -2114,7 +2123,14 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         d.kind = cfg->aggs[j].kind;
         d.col = cfg->aggs[j].col;
         d.acc_kind = acc_kind_of(d.kind);
+        d.alias = 0;
         if (d.acc_kind == ACC_NONE) { d.acc = 0; continue; }
+        int share = -1;   // same accumulator kind over the same input column and input type: one column
+        for (int i = 0; i < j && share < 0; ++i)
+            if (c.agg[i].acc > 0 && !c.agg[i].alias && c.agg[i].acc_kind == d.acc_kind && c.agg[i].col == d.col &&
+                input_class(c.agg[i].kind) == input_class(d.kind) && !getenv("FWA_NO_ACC_SHARE"))
+                share = i;
+        if (share >= 0) { d.acc = c.agg[share].acc; d.alias = 1; continue; }
         d.acc = c.nacc;
         c.acc_kind[c.nacc] = d.acc_kind;
         c.nacc++;
@@ -2147,11 +2163,24 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
             } else if (sizes[slot] != (int)type_size(d.kind)) ok = false;
             d.vslot = slot;
         }
+        // segment size: the largest SEG whose LDS key segment + 2-slice accumulator window fits next to
+        // each other in 160 KB (wide aggregate lists, e.g. C5's 4 float accumulators, need SEG < 4096)
+        // while the partition count stays <= kMaxPart
+        auto lds_need = [&](int sg) {
+            const int64_t sgz = (int64_t)1 << sg;
+            return sgz * 8 + 2 * sgz * 4 + (int64_t)(c.nacc - 1) * 2 * sgz * 8 + 4 * 4 * kSub + 16;
+        };
+        while (!getenv("FWA_SEG_LOG") && seg_log > 9 && lds_need(seg_log) > 160 * 1024 &&
+               ((int64_t)1 << (cap_log - seg_log + 1)) <= kMaxPart)
+            --seg_log;
+        e->seg_log = seg_log;
+        e->part_bits = cap_log - seg_log;
         const int64_t seg = (int64_t)1 << seg_log;
         const int64_t bps = 4 + 8 * (int64_t)(c.nacc - 1);
         const int64_t avail = 160 * 1024 - 256 - seg * 8;
         int sl = (int)std::min<int64_t>(8, avail > 0 ? avail / (bps * seg) : 0);
         if (const char* sv = getenv("FWA_SL")) sl = std::min(sl, atoi(sv));
+        if (lds_need(seg_log) > 160 * 1024) sl = 0;
         const int64_t np = (int64_t)1 << e->part_bits;
         const char* force = getenv("FWA_INGEST");
         ok = ok && np <= kMaxPart && sl >= 2 && !(force && !strcmp(force, "v1")) && e->kind != FWA_SESSION;
