@@ -14,8 +14,8 @@
 //   fire kernel   : on a watermark, for every newly fired window (end-1 <= wm) merge its slices per
 //                   key and emit (key, start, end, aggs) for keys with COUNT > 0.
 //
-// Semantics restated (not copied) from WindowOperator.java:278-481 (DataStream, allowed lateness 0:
-// late firings are not on this path) and AbstractWindowAggProcessor.java:142-182 +
+// Semantics restated (not copied) from WindowOperator.java:278-481 (DataStream; late firings within
+// allowed lateness go to late_fire_kernel) and AbstractWindowAggProcessor.java:142-182 +
 // Slice{Shared,Unshared}WindowAggProcessor (Table): a record contributes to every window containing
 // it that has not fired when it arrives; it is dropped (numLateRecordsDropped) iff that set is
 // empty; a window is emitted for a key iff at least one record contributed to it.
@@ -109,6 +109,7 @@ struct IngestArgs {
     uint32_t dir_mask;
     unsigned long long* want;   // open-addressing set of ord(q), kWantCap entries, 0 = empty
     int32_t* spill;
+    int32_t* late;              // DataStream late firings (window fired, within allowed lateness): deferred
     int32_t* touched;           // per slot
     unsigned long long* const* slot_base;
     int64_t stride;             // elements per accumulator column
@@ -239,11 +240,15 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         const unsigned long long cadd = a.pcount ? a.pcount[i] : 1ull;   // records this row stands for
         const bool accepted = (e->flags & 2) || a.wm < e->thr;
         if (!accepted) { dropped += cadd; continue; }
-        if (c.lateness_pos && a.wm >= e->first_maxts) atomicAdd(&a.st->late_fire, 1ull);
         if (e->slot < 0) {                                      // known slice without slot: replay
             want_insert(a.want, a.st, q);
             int32_t si = atomicAdd(&a.st->spill_n, 1);
             a.spill[si] = (int32_t)i;
+            continue;
+        }
+        if (c.lateness_pos && a.wm >= e->first_maxts) {        // some window of the slice fired already:
+            const unsigned long long li = atomicAdd(&a.st->late_fire, 1ull);   // EventTimeTrigger.onElement
+            a.late[li] = (int32_t)i;                            // FIRE -> late_fire_kernel, in arrival order
             continue;
         }
         const uint64_t oq = jm::ord_i64(q);
@@ -1512,6 +1517,90 @@ __global__ void __launch_bounds__(kBlock) sess_fire_kernel(SessFireArgs f, const
 // utility kernels
 
 // Per-push reset of the device status (all but n_keys / rows; min_q = ~0), the want-set and, for the
+// Late firings (DataStream, allowed lateness > 0): WindowOperator.processElement :391-420 adds the element to
+// every window that is not late (cleanupTime > wm, isWindowLate :586-589) and EventTimeTrigger.onElement
+// (:37-45) FIREs at once when maxTimestamp <= wm, emitting the window's whole (non-purged) contents.
+// Element order matters (each firing shows the state after that element), so the deferred records are
+// applied in arrival order by one lane; such records are rare (they need a watermark past the window).
+struct LateArgs {
+    IngestArgs in;              // the push's columns + key table / directory / slots
+    const int32_t* order;       // deferred record indices, ascending (arrival order)
+    int64_t n;
+    int32_t kind;               // FWA_TUMBLE or FWA_SLIDE
+    int64_t size, slide, lateness;
+    jm::UDiv64 slide_div;
+    int64_t* o_key;
+    int64_t* o_start;
+    int64_t* o_end;
+    void* o_agg[FWA_MAX_AGGS];
+    unsigned long long* rows;   // row counter
+};
+
+__global__ void __launch_bounds__(64) late_fire_kernel(LateArgs L, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const IngestArgs& a = L.in;
+    unsigned long long nrow = *L.rows;
+    for (int64_t t = 0; t < L.n; ++t) {
+        const int64_t i = L.order[t];
+        const int64_t key = a.keys[i];
+        const int64_t ts = a.ts[i];
+        const int64_t d = jm::wsub(ts, c.off);
+        const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
+        const uint64_t uq = jm::udiv64(ud, c.g_div);
+        const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
+        const DirEntry* e = dir_find(a.dir, a.dir_mask, q);
+        if (e == nullptr || e->slot < 0) { raise_error(a.st, FWA_E_STATE); return; }   // host allocated it
+        const int64_t kid = key_slot(a.key_table, a.key_mask, a.seg_log, a.part_bits, key, a.st);
+        if (kid < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); return; }
+        unsigned long long* base = a.slot_base[e->slot];
+        a.touched[e->slot] = 1;
+        const unsigned long long cadd = a.pcount ? a.pcount[i] : 1ull;
+        base[kid] += cadd;                                           // state.add (slice accumulator)
+        for (int j = 0; j < c.naggs; ++j) {
+            const AggDesc dsc = c.agg[j];
+            if (dsc.acc == 0 || dsc.alias) continue;
+            unsigned long long* col = base + (int64_t)dsc.acc * a.stride + kid;
+            const unsigned long long x = a.pcount ? ((const unsigned long long*)a.cols[j])[i]
+                                                  : acc_input(dsc, a.cols[dsc.col], i);
+            *col = acc_combine(dsc.acc_kind, *col, x);
+        }
+        // windows of the record (TimeWindow.getWindowStartWithOffset + Tumbling/SlidingEventTimeWindows)
+        const int64_t sa = jm::wadd(c.off, (int64_t)((uint64_t)q * (uint64_t)c.g));
+        for (int64_t ws = jm::window_start(sa, c.off, L.slide_div); ws > jm::wsub(sa, L.size); ws = jm::wsub(ws, L.slide)) {
+            const int64_t we = jm::wadd(ws, L.size);
+            const int64_t mt = jm::wsub(we, 1);
+            int64_t cleanup = jm::wadd(mt, L.lateness);
+            if (cleanup < mt) cleanup = LONG_MAX_J;
+            if (cleanup <= a.wm || mt > a.wm) continue;              // late window / timer still pending
+            // FIRE: merge the window's slices for this key (getResult over the window state)
+            uint64_t cnt = 0;
+            unsigned long long acc[FWA_MAX_AGGS];
+            for (int j = 0; j < c.naggs; ++j) acc[j] = ident_of(c.agg[j].acc_kind);
+            for (int64_t s0 = ws; s0 < we; s0 = jm::wadd(s0, c.g)) {
+                const int64_t dd = jm::wsub(s0, c.off);
+                const uint64_t udd = dd < 0 ? (uint64_t)0 - (uint64_t)dd : (uint64_t)dd;
+                const uint64_t uqq = jm::udiv64(udd, c.g_div);
+                const int64_t qq = dd >= 0 ? (int64_t)uqq : ((uqq * c.g_div.d == udd) ? -(int64_t)uqq : -(int64_t)uqq - 1);
+                const DirEntry* ee = dir_find(a.dir, a.dir_mask, qq);
+                if (ee == nullptr || ee->slot < 0) continue;
+                const unsigned long long* b2 = a.slot_base[ee->slot];
+                cnt += b2[kid];
+                for (int j = 0; j < c.naggs; ++j) {
+                    const AggDesc dj = c.agg[j];
+                    if (dj.acc > 0) acc[j] = acc_combine(dj.acc_kind, acc[j], b2[(int64_t)dj.acc * a.stride + kid]);
+                }
+            }
+            L.o_key[nrow] = key;
+            L.o_start[nrow] = ws;
+            L.o_end[nrow] = we;
+            for (int j = 0; j < c.naggs; ++j) write_agg(c.agg[j], cnt, acc[j], L.o_agg[j], (int64_t)nrow);
+            ++nrow;
+        }
+    }
+    *L.rows = nrow;
+}
+
 // two-phase path, the bucket cursors and straggler count: one launch instead of a string of memsets.
 __global__ void push_reset_kernel(DevStatus* st, unsigned long long* want, int32_t nwant, uint32_t* bcnt, int32_t nbcnt,
                                   int32_t* strag_n) {
@@ -1639,6 +1728,11 @@ struct fwa_engine {
     int64_t spill_cap = 0;
     int32_t* d_replay = nullptr;
     int64_t replay_cap = 0;
+    int32_t* d_late = nullptr;        // deferred late-firing record indices (spill_cap entries)
+    // rows fired inside fwa_push (late firings), returned by the next fwa_advance_watermark
+    int64_t late_rows = 0, lr_cap = 0;
+    int64_t* lr_col[3 + FWA_MAX_AGGS] = {};
+    unsigned long long* d_lr_n = nullptr;
     // status
     DevStatus* d_st = nullptr;
     DevStatus* h_st = nullptr;
@@ -2062,6 +2156,9 @@ void fwa_destroy(fwa_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->cfg.device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (int c = 0; c < 3 + FWA_MAX_AGGS; ++c) if (e->lr_col[c]) (void)hipFree(e->lr_col[c]);
+    if (e->d_late) (void)hipFree(e->d_late);
+    if (e->d_lr_n) (void)hipFree(e->d_lr_n);
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n, e->d_reset_list, e->d_upos,
@@ -2279,6 +2376,7 @@ static int launch_ingest(fwa_engine* e, IngestArgs& a, bool replay) {
     a.dir_mask = e->dir_cap - 1;
     a.want = e->d_want;
     a.spill = e->d_spill;
+    a.late = e->d_late;
     a.touched = e->d_touched;
     a.slot_base = e->d_slot_base;
     a.stride = e->stride;
@@ -2573,8 +2671,9 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
 
 // Fire kernel over a list of windows (each a union of slots). raw = 1 emits the accumulators and
 // COUNT(*) instead of the final aggregate values (fwa_drain_partials).
+static int emit_late_rows(fwa_engine* e);
 static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const std::vector<int32_t>& hs, int raw,
-                       int64_t* nrows) {
+                       int64_t* nrows, int64_t row0 = 0) {
     if ((int32_t)hw.size() > e->win_cap) {
         if (e->d_win) HIPCHK(e, hipFree(e->d_win));
         e->d_win = nullptr;
@@ -2593,9 +2692,16 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     if (rc) return rc;
     // rows <= windows x distinct keys; n_keys is current: every push ends with a status sync
     const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
-    rc = ensure_out(e, (int64_t)hw.size() * nkeys);
+    rc = ensure_out(e, (int64_t)hw.size() * nkeys + row0);
     if (rc) return rc;
-    HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
+    if (row0 > 0) {   // late-firing rows of the pushes since the last watermark go first
+        rc = emit_late_rows(e);
+        if (rc) return rc;
+        rc = upload(e, &e->d_st->rows, &row0, 8);
+        if (rc) return rc;
+    } else {
+        HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
+    }
     FireArgs f;
     memset(&f, 0, sizeof(f));
     f.key_table = e->d_keys;
@@ -2628,7 +2734,82 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
     e->fire_ms += ms;
     e->fire_launches++;
-    e->fire_rows += *nrows;
+    e->fire_rows += *nrows - row0;
+    return FWA_OK;
+}
+
+// Late firings of one push (DataStream, allowed lateness > 0): apply the deferred records in arrival order
+// and emit the fired windows' contents into the late-row buffer (late_fire_kernel). The rows are returned
+// by the next fwa_advance_watermark, ahead of the windows that watermark fires.
+static int process_late(fwa_engine* e, const IngestArgs& a0, std::vector<int32_t>& idx) {
+    std::sort(idx.begin(), idx.end());
+    const int64_t n = (int64_t)idx.size();
+    if (n > e->spill_cap) return fail(e, FWA_E_STATE, "late list overflow");
+    HIPCHK(e, hipMemcpyAsync(e->d_late, idx.data(), 4 * (size_t)n, hipMemcpyHostToDevice, e->stream));
+    const int64_t per = e->kind == FWA_SLIDE ? (e->size + e->slide - 1) / e->slide : 1;
+    const int64_t need = e->late_rows + n * per;
+    const int ncol = 3 + e->cfg.num_aggs;
+    if (need > e->lr_cap) {
+        const int64_t cap = std::max<int64_t>(need * 2, 1024);
+        for (int c = 0; c < ncol; ++c) {
+            int64_t* p = nullptr;
+            HIPCHK(e, hipMalloc(&p, 8 * (size_t)cap));
+            if (e->lr_col[c]) {
+                if (e->late_rows) HIPCHK(e, hipMemcpyAsync(p, e->lr_col[c], 8 * (size_t)e->late_rows, hipMemcpyDeviceToDevice, e->stream));
+                HIPCHK(e, hipStreamSynchronize(e->stream));
+                HIPCHK(e, hipFree(e->lr_col[c]));
+            }
+            e->lr_col[c] = p;
+        }
+        e->lr_cap = cap;
+    }
+    if (!e->d_lr_n) HIPCHK(e, hipMalloc(&e->d_lr_n, 8));
+    HIPCHK(e, hipMemcpyAsync(e->d_lr_n, &e->late_rows, 8, hipMemcpyHostToDevice, e->stream));
+    LateArgs L;
+    memset(&L, 0, sizeof(L));
+    L.in = a0;
+    L.in.key_table = e->d_keys;
+    L.in.key_mask = (uint64_t)e->capacity - 1;
+    L.in.seg_log = e->seg_log;
+    L.in.part_bits = e->part_bits;
+    L.in.dir = e->d_dir;
+    L.in.dir_mask = e->dir_cap - 1;
+    L.in.touched = e->d_touched;
+    L.in.slot_base = e->d_slot_base;
+    L.in.stride = e->stride;
+    L.in.st = e->d_st;
+    L.in.wm = e->wm;
+    L.order = e->d_late;
+    L.n = n;
+    L.kind = e->kind;
+    L.size = e->size;
+    L.slide = e->kind == FWA_SLIDE ? e->slide : e->size;
+    L.slide_div = e->kind == FWA_SLIDE ? e->slide_div : e->size_div;
+    L.lateness = e->lateness;
+    L.o_key = e->lr_col[0];
+    L.o_start = e->lr_col[1];
+    L.o_end = e->lr_col[2];
+    for (int j = 0; j < e->cfg.num_aggs; ++j) L.o_agg[j] = e->lr_col[3 + j];
+    L.rows = e->d_lr_n;
+    late_fire_kernel<<<1, 64, 0, e->stream>>>(L, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    unsigned long long rows = 0;
+    HIPCHK(e, hipMemcpyAsync(&rows, e->d_lr_n, 8, hipMemcpyDeviceToHost, e->stream));
+    int rc = sync_status(e);   // also mirrors the touched flags the kernel set
+    if (rc) return rc;
+    if (e->h_st->error) return fail(e, e->h_st->error, "late firing failed");
+    e->late_rows = (int64_t)rows;
+    return FWA_OK;
+}
+
+// Copy the pending late-firing rows to the front of the output columns (rows [0, late_rows)).
+static int emit_late_rows(fwa_engine* e) {
+    for (int c = 0; c < 3 + e->cfg.num_aggs; ++c) {
+        void* dst = c == 0 ? (void*)e->o_key : c == 1 ? (void*)e->o_start : c == 2 ? (void*)e->o_end : e->o_agg[c - 3];
+        const size_t w = c < 3 ? 8 : type_size(e->cfg.aggs[c - 3].kind);
+        HIPCHK(e, hipMemcpyAsync(dst, e->lr_col[c], w * (size_t)e->late_rows, hipMemcpyDeviceToDevice, e->stream));
+    }
+    e->late_rows = 0;
     return FWA_OK;
 }
 
@@ -2678,6 +2859,7 @@ static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, boo
     int64_t dropped = 0;
     int64_t qmin = LONG_MAX_J, qmax = LONG_MIN_J;
     bool republish = false;
+    std::vector<int32_t> late_idx;
     for (int round = 0;; ++round) {
         rc = (round == 0 && status_enqueued) ? wait_status(e) : sync_status(e);
         if (rc) return rc;
@@ -2700,7 +2882,11 @@ static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, boo
                                                   : "device error";
             return fail(e, st.error, m);
         }
-        if (st.late_fire) return fail(e, FWA_E_UNSUPPORTED, "late firing within allowed lateness is not on the GPU path");
+        if (st.late_fire) {   // deferred late-firing records of this round (the next round resets the list)
+            const size_t o = late_idx.size();
+            late_idx.resize(o + st.late_fire);
+            HIPCHK(e, hipMemcpy(late_idx.data() + o, e->d_late, 4 * (size_t)st.late_fire, hipMemcpyDeviceToHost));
+        }
         dropped += (int64_t)st.dropped;
         if (st.max_q) qmax = std::max<int64_t>(qmax, jm::unord_i64(st.max_q));
         if (st.min_q != ~0ull) qmin = std::min<int64_t>(qmin, jm::unord_i64(st.min_q));
@@ -2729,6 +2915,7 @@ static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, boo
         rc = launch_ingest(e, b, true);
         if (rc) return rc;
     }
+    if (!late_idx.empty()) { rc = process_late(e, a, late_idx); if (rc) return rc; }
     if (!e->negative.empty()) { e->negative.clear(); republish = true; }
     // (touched flags were mirrored by the last sync) extend the lookahead so ordered streams rarely miss
     if (qmax != LONG_MIN_J) {
@@ -2783,6 +2970,8 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
         e->spill_cap = std::max<int64_t>(n, 1 << 16);
         HIPCHK(e, hipMalloc(&e->d_spill, sizeof(int32_t) * e->spill_cap));
         HIPCHK(e, hipMalloc(&e->d_replay, sizeof(int32_t) * e->spill_cap));
+        if (e->d_late) HIPCHK(e, hipFree(e->d_late));
+        HIPCHK(e, hipMalloc(&e->d_late, sizeof(int32_t) * e->spill_cap));
     }
     if (e->kind == FWA_SESSION) {
         int64_t dropped = 0;
@@ -2852,6 +3041,8 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
         e->spill_cap = std::max<int64_t>(n, 1 << 16);
         HIPCHK(e, hipMalloc(&e->d_spill, sizeof(int32_t) * e->spill_cap));
         HIPCHK(e, hipMalloc(&e->d_replay, sizeof(int32_t) * e->spill_cap));
+        if (e->d_late) HIPCHK(e, hipFree(e->d_late));
+        HIPCHK(e, hipMalloc(&e->d_late, sizeof(int32_t) * e->spill_cap));
     }
     return push_common(e, a, n, false, (flags & FWA_PUSH_ASYNC) != 0, late_dropped_out);
 }
@@ -3215,7 +3406,7 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
         }
         bool slid = false;
         static const bool noslide = getenv("FWA_NOSLIDE") != nullptr;   // A/B switch (timing experiments)
-        if (e->kind == FWA_SLIDE && wins.size() >= 2 && !noslide) {
+        if (e->kind == FWA_SLIDE && wins.size() >= 2 && !noslide && e->late_rows == 0) {
             int rc = fire_slide(e, wins, &nrows, &slid);
             if (rc) return rc;
         }
@@ -3236,12 +3427,21 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
             if (f.nslots > 0) hw.push_back(f);
         }
         if (!hw.empty()) {
-            int rc = launch_fire(e, hw, hs, 0, &nrows);
+            int rc = launch_fire(e, hw, hs, 0, &nrows, e->late_rows);
             if (rc) return rc;
         }
         int rc = retire_slices(e, wm);
         if (rc) return rc;
         e->wm = wm;
+    }
+    if (e->late_rows > 0) {   // late firings pushed since the last call and no window fired now
+        int rc = ensure_out(e, e->late_rows);
+        if (rc) return rc;
+        nrows = e->late_rows;
+        rc = emit_late_rows(e);
+        if (rc) return rc;
+        rc = stream_sync(e);
+        if (rc) return rc;
     }
     e->rows_out += nrows;
     if (out) {

@@ -265,6 +265,7 @@ typedef struct or_engine {
     hmap wl_head;
     /* output */
     int64_t out_n, out_cap;
+    int out_ret;   /* the rows were returned by the last or_advance_watermark: clear at the next call */
     int64_t *o_key, *o_start, *o_end; aval* o_agg[FWA_MAX_AGGS];
     fwa_stats st;
     char err[256];
@@ -668,6 +669,9 @@ static void tb_fire(or_engine* e, int64_t key, int64_t window_end) {  /* Slicing
 int or_push(or_engine* e, const int64_t* keys, const int64_t* ts, const void* const* cols,
             const int32_t* key_hash, int64_t n, int64_t* late_dropped_out) {
     int64_t dropped = 0;
+    /* rows fired inside processElement (late firings, EventTimeTrigger.onElement :37-45) are kept and
+       returned with the next or_advance_watermark, as the engine does */
+    if (e->out_ret) { e->out_n = 0; e->out_ret = 0; }
     int64_t wsb[4096], web[4096];
     for (int64_t i = 0; i < n; i++) {
         int32_t kg = or_key_group(keys[i], e->c.key_kind, key_hash ? key_hash[i] : 0, e->c.max_parallelism);
@@ -698,7 +702,7 @@ int or_push(or_engine* e, const int64_t* keys, const int64_t* ts, const void* co
 }
 
 int or_advance_watermark(or_engine* e, int64_t wm, fwa_out* out) {
-    e->out_n = 0;
+    if (e->out_ret) { e->out_n = 0; e->out_ret = 0; }
     if (wm > e->wm) {
         e->wm = wm;                                          /* InternalTimerServiceImpl.advanceWatermark :302-314 */
         timer_t_ t;
@@ -714,6 +718,7 @@ int or_advance_watermark(or_engine* e, int64_t wm, fwa_out* out) {
         out->key = e->o_key; out->win_start = e->o_start; out->win_end = e->o_end;
         for (int j = 0; j < e->c.num_aggs; j++) out->agg[j] = e->o_agg[j];
     }
+    e->out_ret = 1;
     return FWA_OK;
 }
 
