@@ -178,7 +178,11 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
              const int32_t* key_hash, int64_t n, int32_t flags, int64_t* late_dropped_out);
 
 /* Advance the event-time watermark; fires every window whose maxTimestamp (end-1) <= wm.
- * Non-advancing watermarks are ignored (SlicingWindowOperator.java:231, StatusWatermarkValve).
+ * Non-advancing watermarks fire nothing (SlicingWindowOperator.java:231, StatusWatermarkValve).
+ * DataStream late firings (allowed lateness > 0: a record for a fired window that is not past cleanup,
+ * EventTimeTrigger.onElement :37-45) are computed during fwa_push, one row per (element, fired window)
+ * in arrival order, and returned at the head of the next fwa_advance_watermark's rows (also when wm
+ * does not advance).
  * Output rows (fired (key, window) results) stay valid until the next call on this handle. */
 int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out);
 
