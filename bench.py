@@ -62,13 +62,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # FWA_DIST_BACKEND=gloo: rehearsal of the N>1 path with several ranks sharing one GPU (the exchange then
+    # runs over gloo on host tensors); the driver's multi-GPU runs use RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("FWA_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     B = args.batch
     S = args.warmup + args.steps
@@ -154,10 +162,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        rdev = dev if backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        rr = torch.tensor([rows_t], dtype=torch.int64, device=dev)
+        rr = torch.tensor([rows_t], dtype=torch.int64, device=rdev)
         dist.all_reduce(rr)
         rows_all = int(rr.item())
     else:
