@@ -208,6 +208,7 @@ template <bool kIdx>
 __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
     const int lane = threadIdx.x & 63;
+    __shared__ unsigned long long s_red[kBlock / 64][1 + FWA_MAX_AGGS];   // hot-key group reduction
     const int64_t stride_grid = (int64_t)gridDim.x * blockDim.x;
     unsigned long long qmax = 0, qmin = ~0ull;
     unsigned long long dropped = 0;
@@ -259,6 +260,66 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         const int32_t slot = e->slot;
         unsigned long long* base = a.slot_base[slot];
         if (a.touched[slot] == 0) a.touched[slot] = 1;
+        // Hot keys (skew: e.g. the bucket-overflow replay of a Zipf head key, where most lanes of a wave
+        // carry the same key): the lanes sharing the wave leader's (kid, slot) combine in LDS first, so
+        // the group costs one set of global atomics instead of one per lane on the same address.
+        {
+            const unsigned long long act = __ballot(1);
+            const int leader = __ffsll((long long)act) - 1;
+            const long long lkid = __shfl((long long)kid, leader);
+            const int lslot = __shfl(slot, leader);
+            const bool grp = kid == lkid && slot == lslot;
+            const unsigned long long gm = __ballot(grp);
+            if (grp && __popcll(gm) > 1) {
+                unsigned long long* r = s_red[threadIdx.x >> 6];
+                if (lane == leader) {
+                    r[0] = cadd;
+                    for (int j = 0; j < c.naggs; ++j) {
+                        const AggDesc dsc = c.agg[j];
+                        if (dsc.acc == 0 || dsc.alias) continue;
+                        r[dsc.acc] = a.pcount ? ((const unsigned long long*)a.cols[j])[i] : acc_input(dsc, a.cols[dsc.col], i);
+                    }
+                }
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+                if (lane != leader) {
+                    atomicAdd(&r[0], cadd);
+                    for (int j = 0; j < c.naggs; ++j) {
+                        const AggDesc dsc = c.agg[j];
+                        if (dsc.acc == 0 || dsc.alias) continue;
+                        const unsigned long long x = a.pcount ? ((const unsigned long long*)a.cols[j])[i]
+                                                              : acc_input(dsc, a.cols[dsc.col], i);
+                        unsigned long long* rp = &r[dsc.acc];
+                        switch (dsc.acc_kind) {
+                            case ACC_ADD_I64: atomicAdd(rp, x); break;
+                            case ACC_ADD_F64: atomicAdd((double*)rp, __longlong_as_double((long long)x)); break;
+                            case ACC_MIN_ORD: atomicMin(rp, x); break;
+                            case ACC_MAX_ORD: atomicMax(rp, x); break;
+                            default: break;
+                        }
+                    }
+                }
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+                if (lane == leader) {
+                    atomicAdd(&base[kid], r[0]);
+                    for (int j = 0; j < c.naggs; ++j) {
+                        const AggDesc dsc = c.agg[j];
+                        if (dsc.acc == 0 || dsc.alias) continue;
+                        unsigned long long* col = base + (int64_t)dsc.acc * a.stride + kid;
+                        const unsigned long long x = r[dsc.acc];
+                        switch (dsc.acc_kind) {
+                            case ACC_ADD_I64: atomicAdd(col, x); break;
+                            case ACC_ADD_F64: atomicAdd((double*)col, __longlong_as_double((long long)x)); break;
+                            case ACC_MIN_ORD: atomicMin(col, x); break;
+                            case ACC_MAX_ORD: atomicMax(col, x); break;
+                            default: break;
+                        }
+                    }
+                }
+                continue;
+            }
+        }
         atomicAdd(&base[kid], cadd);                            // COUNT(*)
 #pragma unroll
         for (int j = 0; j < FWA_MAX_AGGS; ++j) {
@@ -527,6 +588,7 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
     __shared__ uint32_t hist[kMaxPart];
     __shared__ uint32_t toff[kMaxPart];
     __shared__ uint32_t gbase[kMaxPart];
+    __shared__ uint32_t sbase[kMaxPart];   // spill-list base of the tile's overflow records, per partition
     __shared__ unsigned long long x_key[kTile];
     __shared__ unsigned long long x_val[NV > 0 ? NV : 1][NV > 0 ? kTile : 1];
     __shared__ uint16_t x_rel[kTile];
@@ -653,8 +715,19 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
         block_scan_np<THREADS>(hist, toff, wsum, a.np, &s_total);
         __syncthreads();
         QMARK(1);
-        for (int p = tid; p < a.np; p += THREADS)
-            gbase[p] = hist[p] ? atomicAdd(&a.b_cnt[p * kSub + sub], hist[p]) : 0u;
+        for (int p = tid; p < a.np; p += THREADS) {
+            const uint32_t h = hist[p];
+            const uint32_t g = h ? atomicAdd(&a.b_cnt[p * kSub + sub], h) : 0u;
+            gbase[p] = g;
+            // records past the sub-bucket's end (skewed keys) go to the v1 replay: one spill reservation
+            // per (tile, overflowing partition) -- a per-wave reservation on the single spill counter
+            // serialised ~100 K same-address device atomics per push under Zipf(1.1)
+            const uint64_t end = (uint64_t)g + h;
+            if (end > (uint64_t)a.capb) {
+                const uint32_t ov = (uint32_t)(end - std::max<uint64_t>(g, (uint64_t)a.capb));
+                sbase[p] = (uint32_t)atomicAdd(&a.st->spill_n, (int32_t)ov);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             if (r_pos[j] == ~0u) continue;
@@ -671,7 +744,8 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
             const uint32_t x = s_src[sidx];
             const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
             if (dst >= (uint64_t)a.capb) {      // sub-bucket full (skewed keys): the v1 replay takes it
-                a.spill[atomicAdd(&a.st->spill_n, 1)] = (int32_t)(t0 + x);
+                const uint64_t first = std::max<uint64_t>(gbase[p], (uint64_t)a.capb);
+                a.spill[sbase[p] + (uint32_t)(dst - first)] = (int32_t)(t0 + x);
                 continue;
             }
             const uint64_t o = ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
@@ -977,9 +1051,17 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
             if (rel[j] < 0) continue;
             const int32_t local = loc[j];
             if (local < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
-            if (rel[j] < lo) {          // older than the window: applied after the kernel with atomics
+            const bool strag = rel[j] < lo;
+            const unsigned long long msk = __ballot(strag);   // one list reservation per wave (skew)
+            int32_t sbase = 0;
+            if (msk) {
+                const int ld = __ffsll((long long)msk) - 1;
+                if (lane == ld) sbase = atomicAdd(a.strag_n, __popcll(msk));
+                sbase = __shfl(sbase, ld);
+            }
+            if (strag) {                // older than the window: applied after the kernel with atomics
                 if (a.prof) pacc[6] += 1000000;
-                const int32_t si = atomicAdd(a.strag_n, 1);
+                const int32_t si = sbase + __popcll(msk & ((1ull << lane) - 1));
                 const uint64_t so = (uint64_t)(boff + cb + (int64_t)j * LPS + li);
                 const uint32_t sg = (uint32_t)(((int64_t)p << a.seg_log) + local);
                 if (si < a.strag_cap) {
