@@ -263,7 +263,9 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         // Hot keys (skew: e.g. the bucket-overflow replay of a Zipf head key, where most lanes of a wave
         // carry the same key): the lanes sharing the wave leader's (kid, slot) combine in LDS first, so
         // the group costs one set of global atomics instead of one per lane on the same address.
-        {
+        // Replay launches only (kIdx): the plain v1 pass over a large uniform key space (C4) is
+        // latency-bound and lost half its rate to the extra registers.
+        if constexpr (kIdx) {
             const unsigned long long act = __ballot(1);
             const int leader = __ffsll((long long)act) - 1;
             const long long lkid = __shfl((long long)kid, leader);
@@ -1139,6 +1141,7 @@ struct FireArgs {
     void* o_agg[FWA_MAX_AGGS];
     int64_t* o_count;           // partial mode: COUNT(*) per row
     int32_t raw;                // 1: emit accumulators (fwa_drain_partials), not results
+    int64_t out_cap;            // rows past it are counted but not written (the host grows and relaunches)
     DevStatus* st;
 };
 
@@ -1268,6 +1271,7 @@ __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineCo
         if (!((masks[j] >> lane) & 1ull)) continue;
         const int64_t k = k0 + (int64_t)j * kBlock + tid;
         const int64_t row = (int64_t)s_base + woff[j][wid] + __popcll(masks[j] & lt);
+        if (row >= f.out_cap) continue;
         if (PRE) {
             f.o_key[row] = (k < f.capacity) ? (int64_t)kvs[j] : LONG_MIN_J;
             f.o_start[row] = win.start;
@@ -2774,8 +2778,15 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     if (rc) return rc;
     // rows <= windows x distinct keys; n_keys is current: every push ends with a status sync
     const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
-    rc = ensure_out(e, (int64_t)hw.size() * nkeys + row0);
+    // Output sizing: rows <= windows x live keys, which is tens of GB for 1e8 keys (C4) although a
+    // window holds far fewer rows. Start from min(bound, max(current capacity, 4M rows)); the kernel
+    // counts rows past the capacity without writing them, and the host grows once and relaunches.
+    const int64_t bound = (int64_t)hw.size() * nkeys + row0;
+    const char* om = getenv("FWA_OUT_MIN");   // first-sizing floor in rows (tests force the relaunch)
+    const int64_t floor_rows = om ? std::max<int64_t>(1, atoll(om)) : ((int64_t)1 << 22);
+    rc = ensure_out(e, std::min<int64_t>(bound, std::max<int64_t>(e->out_cap, floor_rows + row0)));
     if (rc) return rc;
+  relaunch:
     if (row0 > 0) {   // late-firing rows of the pushes since the last watermark go first
         rc = emit_late_rows(e);
         if (rc) return rc;
@@ -2800,6 +2811,7 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
     f.o_count = raw ? e->o_count : nullptr;
     f.raw = raw;
+    f.out_cap = e->out_cap;
     f.st = e->d_st;
     const int64_t grid = (int64_t)f.blocks_per_win * (int64_t)hw.size();
     HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
@@ -2812,6 +2824,12 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     rc = sync_status(e);
     if (rc) return rc;
     *nrows = (int64_t)e->h_st->rows;
+    if (*nrows > e->out_cap) {   // more rows than the first sizing: grow to the exact count, fire again
+        rc = ensure_out(e, *nrows);
+        if (rc) return rc;
+        goto relaunch;
+    }
+    e->late_rows = 0;            // consumed (emit_late_rows copied them to the head of the output)
     float ms = 0.f;
     HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
     e->fire_ms += ms;
@@ -2891,8 +2909,7 @@ static int emit_late_rows(fwa_engine* e) {
         const size_t w = c < 3 ? 8 : type_size(e->cfg.aggs[c - 3].kind);
         HIPCHK(e, hipMemcpyAsync(dst, e->lr_col[c], w * (size_t)e->late_rows, hipMemcpyDeviceToDevice, e->stream));
     }
-    e->late_rows = 0;
-    return FWA_OK;
+    return FWA_OK;   // the caller clears late_rows once the output is final
 }
 
 // Shared ingest driver: two-phase path when allowed, else the v1 kernel; slice-miss replays;
@@ -3524,6 +3541,7 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
         if (rc) return rc;
         rc = stream_sync(e);
         if (rc) return rc;
+        e->late_rows = 0;
     }
     e->rows_out += nrows;
     if (out) {
