@@ -1711,8 +1711,9 @@ __global__ void reset_slots_kernel(unsigned long long* const* slot_base, const i
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
     for (int col = 0; col < c.nacc; ++col) {
         const unsigned long long v = (col > 0 && c.acc_kind[col] == ACC_MIN_ORD) ? ~0ull : 0ull;
-        unsigned long long* p = base + (int64_t)col * stride;
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < stride; i += step) p[i] = v;
+        ulonglong2* p = (ulonglong2*)(base + (int64_t)col * stride);   // stride % 64 == 0: 16 B stores
+        const ulonglong2 v2 = make_ulonglong2(v, v);
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < stride / 2; i += step) p[i] = v2;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) touched[slot] = 0;
 }
@@ -2090,7 +2091,7 @@ int flush_resets(fwa_engine* e) {
     }
     int rc = upload(e, e->d_reset_list, e->pending_reset.data(), sizeof(int32_t) * n);
     if (rc) return rc;
-    const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 1024 / n), (e->stride + 1023) / 1024);
+    const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 1024 / n), (e->stride / 2 + 1023) / 1024);
     reset_slots_kernel<<<dim3((unsigned)blocks, (unsigned)n), 1024, 0, e->stream>>>(e->d_slot_base, e->d_reset_list,
                                                                                    e->stride, e->d_touched, e->d_ec);
     HIPCHK(e, hipGetLastError());
@@ -2824,8 +2825,8 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     rc = sync_status(e);
     if (rc) return rc;
     *nrows = (int64_t)e->h_st->rows;
-    if (*nrows > e->out_cap) {   // more rows than the first sizing: grow to the exact count, fire again
-        rc = ensure_out(e, *nrows);
+    if (*nrows > e->out_cap) {   // more rows than the first sizing: grow (2x headroom for the following
+        rc = ensure_out(e, std::max<int64_t>(*nrows, std::min<int64_t>(bound, 2 * *nrows)));   // fires), fire again
         if (rc) return rc;
         goto relaunch;
     }
