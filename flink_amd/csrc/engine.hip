@@ -3447,12 +3447,51 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     return FWA_OK;
 }
 
+// Speculative fire (TUMBLE, an FWA_PUSH_ASYNC push still pending): enqueue the fire of every live slice
+// whose window is due right behind the pushed kernels, then settle the push. One host synchronisation
+// instead of two, and the fire starts without the host round trip in between. The result stands only
+// when the push needed no miss replay and had no late firings (then state was final when the fire ran);
+// otherwise *ok = false and the caller fires again after the settle.
+static int speculative_fire(fwa_engine* e, int64_t wm, int64_t* nrows, bool* ok) {
+    *ok = false;
+    std::vector<FireWindow> hw;
+    std::vector<int32_t> hs;
+    for (auto& kv : e->live) {   // touched flags are not settled yet: untouched slots only emit nothing
+        FireWindow f;
+        f.start = slice_start(e, kv.first);
+        f.end = jm::wadd(f.start, e->g);
+        const int64_t mt = jm::wsub(f.end, 1);
+        if (!(mt > e->wm && mt <= wm)) continue;
+        f.slot_off = (int32_t)hs.size();
+        f.nslots = 1;
+        hs.push_back(kv.second);
+        hw.push_back(f);
+    }
+    int rc = FWA_OK;
+    if (!hw.empty()) {
+        rc = launch_fire(e, hw, hs, 0, nrows, 0);   // synchronises: the push's status is in h_st too
+        if (rc) return rc;
+    }
+    const DevStatus st = *e->h_st;
+    rc = settle_pending(e);
+    if (rc) return rc;
+    *ok = hw.empty() ? false : (st.spill_n == 0 && st.late_fire == 0 && st.error == 0 && e->late_rows == 0);
+    return FWA_OK;
+}
+
 int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
     if (!e) return FWA_E_STATE;
     HIPCHK(e, hipSetDevice(e->cfg.device));
+    int64_t nrows = 0;
+    bool spec_done = false;
+    static const bool nospec = getenv("FWA_NOSPEC") != nullptr;   // A/B switch
+    if (e->pend && !nospec && e->kind == FWA_TUMBLE && wm > e->wm && e->late_rows == 0) {
+        int rc = speculative_fire(e, wm, &nrows, &spec_done);
+        if (rc) return rc;
+        if (!spec_done) nrows = 0;
+    }
     if (int rc0 = settle_pending(e)) return rc0;
     if (out) memset(out, 0, sizeof(*out));
-    int64_t nrows = 0;
     if (wm > e->wm && e->kind == FWA_SESSION) {
         int rc = sync_status(e);
         if (rc) return rc;
@@ -3512,7 +3551,7 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
         }
         std::vector<FireWindow> hw;
         std::vector<int32_t> hs;
-        if (!slid) for (auto& w : wins) {
+        if (!slid && !spec_done) for (auto& w : wins) {
             FireWindow f;
             f.end = w.first;
             f.start = w.second;
