@@ -40,9 +40,11 @@ def main():
     ap.add_argument("--keys", type=int, default=1_000_000)
     ap.add_argument("--window-ms", type=int, default=10_000)
     ap.add_argument("--delay-ms", type=int, default=1000)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 26)
+    ap.add_argument("--cpu-sample", type=int, default=6 << 26)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host pinned input) leg")
+    ap.add_argument("--pcie-batches", type=int, default=3)
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "c5s"], default="c2",
                     help="c2: tumbling 10s COUNT+SUM(long), 1M uniform keys (the metric's workload); "
                          "c3: HOP 60s/1s (Table slicing), Zipf(1.1) keys over 1M items; "
@@ -232,7 +234,7 @@ def main():
                          else "raw records (RCCL all_to_all)") if world > 1 else "none",
         },
         "roofline": {
-            "bound": "hbm", "kernel": "ingest_kernel",
+            "bound": "hbm", "kernel": ingest_kernels(args, eng),
             "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": traffic_src, "alg_bytes_per_launch": rec_bytes * B,
@@ -245,12 +247,46 @@ def main():
         "rows_emitted": rows_all,
         "late_dropped": sum(x.stats().late_dropped for x in engines) if args.exchange == "partials" or world == 1 else dropped,
     }
+    out["roofline"]["replay_records"] = st.replay_records
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         out["cpu_baseline"] = cpu_baseline(args, cfg_kw)
+    if rank == 0 and world == 1 and not args.no_pcie and args.config == "c2":
+        out["pcie_inclusive"] = pcie_leg(args, cfg_kw, keys, ts, vals, wms, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def ingest_kernels(args, eng):
+    """Names of the kernels whose device time `roofline.achieved` divides by (HIP events around them)."""
+    if args.config == "c5s":
+        return "sess_key_kernel+radix sort+sess_process_kernel"
+    return "partition2_kernel+combine3_kernel+straggler_kernel" if eng.stats().partition_ms > 0 else "ingest_kernel"
+
+
+def host_cpus():
+    """CPUs this process may run on (affinity, capped by a cgroup v2 quota when one is set) and the model."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, quota, os.cpu_count(), model
 
 
 def cpu_baseline(args, cfg_kw):
@@ -258,7 +294,8 @@ def cpu_baseline(args, cfg_kw):
     one operator instance per thread owning a key-group range), timed on this host's cores."""
     from flink_amd import _abi as A
     from oracle import oracle as O
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    avail, quota, nproc, model = host_cpus()
+    threads = args.cpu_threads or (min(avail, quota) if quota else avail)
     n = args.cpu_sample
     cfg = A.make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=args.window_ms,
                         aggs=[("COUNT", 0), ("SUM_I64", 0)])
@@ -268,8 +305,43 @@ def cpu_baseline(args, cfg_kw):
     log("cpu baseline: %d records, %d threads" % (n, threads))
     secs, rows, _ = O.bench_pipeline(cfg, p, n, min(args.batch, n), threads)
     return {"value": n / secs, "unit": "records/s", "cores": threads, "kind": "port",
-            "sample": "first %d records of the C2 stream (%d s of event time), oracle WindowOperator "
-                      "restatement, %d threads each owning a key-group range; %.2f s" % (n, n // 1_000_000, threads, secs)}
+            "host": {"cpu_model": model, "nproc": nproc, "affinity_cpus": avail, "cgroup_cpu_quota": quota},
+            "sample": "first %d records of the C2 stream (%d batches of %d, %d s of event time), oracle "
+                      "WindowOperator restatement, %d threads each owning a key-group range (keyBy partition "
+                      "untimed); %.2f s" % (n, (n + args.batch - 1) // args.batch, args.batch, n // 1_000_000,
+                                            threads, secs)}
+
+
+def pcie_leg(args, cfg_kw, keys, ts, vals, wms, dev):
+    """Secondary number: the same C2 step with the batch handed over in host pinned
+    memory (fwa_push without FWA_PUSH_DEVICE_PTRS: the engine stages it over PCIe), timed per batch."""
+    import torch
+    from flink_amd import _abi as A
+    from flink_amd import engine as E
+    B = args.batch
+    nb = min(args.pcie_batches, args.warmup + args.steps)
+    hk = torch.empty(nb * B, dtype=torch.int64, pin_memory=True)
+    ht = torch.empty_like(hk, pin_memory=True)
+    hv = torch.empty_like(hk, pin_memory=True)
+    hk.copy_(keys[:nb * B])
+    ht.copy_(ts[:nb * B])
+    hv.copy_(vals[:nb * B])
+    torch.cuda.synchronize()
+    kw = dict(cfg_kw)
+    kw["output_on_device"] = 1
+    eng = E.WindowAggregator(A.make_config(**kw))
+    nk, nt, nv = hk.numpy(), ht.numpy(), hv.numpy()
+    eng.push(nk[:B], nt[:B], [nv[:B]])            # warm-up batch (directory, slots, staging buffer)
+    eng.advance_watermark_raw(wms[0])
+    t0 = time.perf_counter()
+    for b in range(1, nb):
+        sl = slice(b * B, (b + 1) * B)
+        eng.push(nk[sl], nt[sl], [nv[sl]])
+        eng.advance_watermark_raw(wms[b])
+    secs = time.perf_counter() - t0
+    eng.close()
+    return {"value": (nb - 1) * B / secs, "unit": "records/s", "batches_timed": nb - 1,
+            "note": "host pinned input columns, H2D staging inside fwa_push, outputs left in HBM"}
 
 
 if __name__ == "__main__":

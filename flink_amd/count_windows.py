@@ -19,7 +19,7 @@ Reference chain:
 import re
 from collections import defaultdict
 
-_SPLIT = re.compile(r"\W+")   # Java "\\W+" == [^a-zA-Z0-9_]+ for ASCII text
+_SPLIT = re.compile(r"\W+", re.ASCII)   # Java "\\W+" is ASCII-only: [^a-zA-Z0-9_]+ (WordCount.java:171-186)
 
 
 def tokenize(line):

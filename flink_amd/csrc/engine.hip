@@ -113,10 +113,18 @@ struct IngestArgs {
     int32_t* touched;           // per slot
     unsigned long long* const* slot_base;
     int64_t stride;             // elements per accumulator column
+    int64_t spill_cap;          // entries of spill[] and late[] (a store past it raises FWA_E_STATE instead)
     DevStatus* st;
 };
 
 __device__ __forceinline__ void raise_error(DevStatus* st, int code) { atomicCAS(&st->error, 0, code); }
+
+// Bounds-checked scatter of a record index into a spill / late list: an index past the list's capacity
+// would be a logic error upstream; it is reported (FWA_E_STATE) instead of faulting the device.
+__device__ __forceinline__ void put_idx(int32_t* list, int64_t pos, int64_t cap, int32_t v, DevStatus* st) {
+    if (pos >= 0 && pos < cap) list[pos] = v;
+    else raise_error(st, FWA_E_STATE);
+}
 
 // Key table: SEGMENTED open addressing. h = mix64(key); segment p = top part_bits of h (the v2
 // combiner's partition), probe linearly inside the segment from the kBucket-aligned home
@@ -235,7 +243,7 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
             int32_t base = 0;
             if (lane == leader) base = atomicAdd(&a.st->spill_n, __popcll(m));
             base = __shfl(base, leader);
-            a.spill[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)i;
+            put_idx(a.spill, base + __popcll(m & ((1ull << lane) - 1)), a.spill_cap, (int32_t)i, a.st);
             continue;
         }
         const unsigned long long cadd = a.pcount ? a.pcount[i] : 1ull;   // records this row stands for
@@ -243,13 +251,13 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         if (!accepted) { dropped += cadd; continue; }
         if (e->slot < 0) {                                      // known slice without slot: replay
             want_insert(a.want, a.st, q);
-            int32_t si = atomicAdd(&a.st->spill_n, 1);
-            a.spill[si] = (int32_t)i;
+            const int32_t si = atomicAdd(&a.st->spill_n, 1);
+            put_idx(a.spill, si, a.spill_cap, (int32_t)i, a.st);
             continue;
         }
         if (c.lateness_pos && a.wm >= e->first_maxts) {        // some window of the slice fired already:
             const unsigned long long li = atomicAdd(&a.st->late_fire, 1ull);   // EventTimeTrigger.onElement
-            a.late[li] = (int32_t)i;                            // FIRE -> late_fire_kernel, in arrival order
+            put_idx(a.late, (int64_t)li, a.spill_cap, (int32_t)i, a.st);        // FIRE -> late_fire_kernel
             continue;
         }
         const uint64_t oq = jm::ord_i64(q);
@@ -396,6 +404,7 @@ struct PartArgs {
     uint16_t* b_rel;
     uint32_t* b_cnt;                   // [np]
     int64_t capb;
+    int64_t spill_cap;
     int32_t part_bits, np;
     int32_t vcol[2];
     int32_t vsize[2];                  // 4 or 8 bytes
@@ -433,146 +442,6 @@ __device__ __forceinline__ void block_scan_np(const uint32_t* hist, uint32_t* to
     uint32_t excl = wsum[wid] + incl - x;
 #pragma unroll
     for (int q = 0; q < PER; ++q) { if (PER * tid + q < np) toff[PER * tid + q] = excl; excl += v[q]; }
-}
-
-template <int NV, int ITEMS, int THREADS, int MINW = 1>
-__global__ void __launch_bounds__(THREADS, MINW) partition_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
-    constexpr int kThreadsP = THREADS;
-    constexpr int kTile = kThreadsP * ITEMS;
-    const EngineConst& c = *cp;
-    __shared__ uint32_t hist[kMaxPart];
-    __shared__ uint32_t toff[kMaxPart];
-    __shared__ uint32_t gbase[kMaxPart];
-    __shared__ unsigned long long s_key[kTile];
-    __shared__ unsigned long long s_val[NV > 0 ? NV : 1][NV > 0 ? kTile : 1];
-    __shared__ uint16_t s_rel[kTile];
-    __shared__ uint16_t s_part[kTile];
-    __shared__ uint16_t s_src[kTile];   // position of the record inside the tile (bucket-overflow spill)
-    __shared__ uint32_t wsum[kThreadsP / 64];
-    __shared__ uint32_t s_total;
-    __shared__ uint8_t s_code[kRelCap];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    unsigned dropped = 0;
-    uint32_t relmax = 0, relmin = ~0u;   // accepted records' relative slice range (lookahead, touched)
-    const bool kg_all = c.kg_lo == 0 && c.kg_hi == c.max_par - 1;   // whole range owned: no check needed
-    const bool ds = c.sem == FWA_SEM_DATASTREAM;
-    for (int r = tid; r < kRelCap / 4; r += kThreadsP) ((uint32_t*)s_code)[r] = ((const uint32_t*)a.relcode)[r];
-    const int64_t ntiles = (a.n + kTile - 1) / kTile;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        for (int i = tid; i < a.np; i += kThreadsP) hist[i] = 0;
-        __syncthreads();
-        unsigned long long r_key[ITEMS], r_v0[ITEMS], r_v1[ITEMS];
-        uint32_t r_pos[ITEMS];   // (p << 16 | rank) or ~0u when the record does not go to a bucket
-        uint16_t r_rel[ITEMS];
-        const int64_t t0 = tile * kTile;
-        int64_t r_ts[ITEMS];
-        int32_t r_kh[ITEMS];
-        // 1) issue every load of the tile first (no control flow between them)
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const int64_t i = t0 + (int64_t)j * kThreadsP + tid;
-            const bool ok = i < a.n;
-            r_key[j] = ok ? (unsigned long long)a.keys[i] : 0ull;
-            r_ts[j] = ok ? a.ts[i] : 0;
-            r_v0[j] = (NV > 0 && ok) ? load_raw(a.cols[a.vcol[0]], i, a.vsize[0]) : 0ull;
-            r_v1[j] = (NV > 1 && ok) ? load_raw(a.cols[a.vcol[1]], i, a.vsize[1]) : 0ull;
-            r_kh[j] = (a.key_hash && ok) ? a.key_hash[i] : 0;
-        }
-        // 2) compute: straight-line fast path; every rare case goes to the spill list (v1 replay)
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const int64_t i = t0 + (int64_t)j * kThreadsP + tid;
-            const int64_t key = (int64_t)r_key[j];
-            const int64_t ts = r_ts[j];
-            const int64_t d = jm::wsub(ts, c.off);
-            const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
-            const uint64_t uq = jm::udiv64(ud, c.g_div);
-            const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
-            const uint64_t rel = (uint64_t)(q - a.q_base);
-            uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
-            if (!kg_all) {
-                const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, r_kh[j]), c.max_par);
-                if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;     // the replay raises FWA_E_KEYGROUP
-            }
-            if (ds && ts == LONG_MIN_J) code = kCodeSlow;                // the replay raises FWA_E_TS_MIN
-            if ((uint64_t)key == kEmptyKey) code = kCodeSlow;            // side-slot key
-            if (i >= a.n) code = 0xff;
-            dropped += code == kCodeDrop;
-            const bool slow = code == kCodeSlow;
-            const unsigned long long mk = __ballot(slow);
-            if (mk) {                                                    // wave-aggregated spill append
-                const int leader = __ffsll((long long)mk) - 1;
-                int32_t sb = 0;
-                if (lane == leader) sb = atomicAdd(&a.st->spill_n, __popcll(mk));
-                sb = __shfl(sb, leader);
-                if (slow) a.spill[sb + __popcll(mk & ((1ull << lane) - 1))] = (int32_t)i;
-            }
-            r_pos[j] = ~0u;
-            if (code == kCodeAccept) {
-                relmax = max(relmax, (uint32_t)rel);
-                relmin = min(relmin, (uint32_t)rel);
-                const uint64_t h = jm::mix64((uint64_t)key);
-                const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
-                r_rel[j] = (uint16_t)rel;
-                r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
-            }
-        }
-        __syncthreads();
-        block_scan_np<THREADS>(hist, toff, wsum, a.np, &s_total);
-        __syncthreads();
-        const int sub = blockIdx.x % kSub;
-        for (int p = tid; p < a.np; p += kThreadsP)
-            gbase[p] = (a.abl & 1) ? (uint32_t)((tile * 7) & 1023) : (hist[p] ? atomicAdd(&a.b_cnt[p * kSub + sub], hist[p]) : 0u);
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            if (r_pos[j] == ~0u) continue;
-            const uint32_t p = r_pos[j] >> 16;
-            const uint32_t sidx = toff[p] + (r_pos[j] & 0xffffu);
-            s_key[sidx] = r_key[j];
-            s_rel[sidx] = r_rel[j];
-            s_part[sidx] = (uint16_t)p;
-            s_src[sidx] = (uint16_t)(j * kThreadsP + tid);
-            if (NV > 0) s_val[0][sidx] = r_v0[j];
-            if (NV > 1) s_val[NV > 1 ? 1 : 0][sidx] = r_v1[j];
-        }
-        __syncthreads();
-        const uint32_t total = s_total;
-        for (uint32_t sidx = tid; sidx < total; sidx += kThreadsP) {
-            const uint32_t p = s_part[sidx];
-            const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
-            if (dst >= (uint64_t)a.capb) {      // sub-bucket full (skewed keys): the v1 replay takes it
-                a.spill[atomicAdd(&a.st->spill_n, 1)] = (int32_t)(t0 + s_src[sidx]);
-                continue;
-            }
-            if (a.abl & 2) { if (s_key[sidx] == 0x1234567ull) a.b_key[0] = 1; continue; }
-            const uint64_t o = ((uint64_t)p * kSub + (blockIdx.x % kSub)) * (uint64_t)a.capb + dst;
-            a.b_key[o] = s_key[sidx];
-            a.b_rel[o] = s_rel[sidx];
-            if (NV > 0) a.b_val0[o] = s_val[0][sidx];
-            if (NV > 1) a.b_val1[o] = s_val[NV > 1 ? 1 : 0][sidx];
-        }
-        __syncthreads();
-    }
-    for (int sh = 32; sh >= 1; sh >>= 1) {
-        dropped += __shfl_xor(dropped, sh);
-        relmax = max(relmax, (uint32_t)__shfl_xor((int)relmax, sh));
-        relmin = min(relmin, (uint32_t)__shfl_xor((int)relmin, sh));
-    }
-    if (lane == 0) {
-        if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
-        if (relmin != ~0u) {
-            atomicMax(&a.st->max_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmax));
-            atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
-        }
-    }
-    // mark the slots of the accepted slice range touched (over-marking is harmless: a touched slot
-    // without records emits nothing and is merely re-cleared)
-    if (relmin != ~0u)
-        for (uint32_t r = relmin + (uint32_t)lane; r <= relmax; r += 64) {
-            const int32_t slot = a.rel2slot[r];
-            if (slot >= 0 && a.touched[slot] == 0) a.touched[slot] = 1;
-        }
 }
 
 // partition2: Phase P with the next tile's loads in flight while the current tile is scanned,
@@ -695,7 +564,7 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
                 int32_t sb = 0;
                 if (lane == leader) sb = atomicAdd(&a.st->spill_n, __popcll(mk));
                 sb = __shfl(sb, leader);
-                if (slow) a.spill[sb + __popcll(mk & ((1ull << lane) - 1))] = (int32_t)i;
+                if (slow) put_idx(a.spill, sb + __popcll(mk & ((1ull << lane) - 1)), a.spill_cap, (int32_t)i, a.st);
             }
             r_pos[j] = ~0u;
             if (code == kCodeAccept) {
@@ -747,7 +616,7 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
             const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
             if (dst >= (uint64_t)a.capb) {      // sub-bucket full (skewed keys): the v1 replay takes it
                 const uint64_t first = std::max<uint64_t>(gbase[p], (uint64_t)a.capb);
-                a.spill[sbase[p] + (uint32_t)(dst - first)] = (int32_t)(t0 + x);
+                put_idx(a.spill, (int64_t)sbase[p] + (int64_t)(dst - first), a.spill_cap, (int32_t)(t0 + x), a.st);
                 continue;
             }
             const uint64_t o = ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
@@ -1312,6 +1181,7 @@ struct FireSlideArgs {
     int64_t* o_start;
     int64_t* o_end;
     void* o_agg[FWA_MAX_AGGS];
+    int64_t out_cap;                         // rows past it are counted, not written (host grows, relaunches)
     DevStatus* st;
 };
 
@@ -1390,6 +1260,7 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
             if (!((masks[j] >> lane) & 1ull)) continue;
             const int64_t k = k0 + (int64_t)j * kBlock + tid;
             const int64_t row = (int64_t)s_base + woff[j][wid] + __popcll(masks[j] & lt);
+            if (row >= f.out_cap) continue;
             f.o_key[row] = (k < f.capacity) ? (int64_t)kv[j] : LONG_MIN_J;
             f.o_start[row] = ws;
             f.o_end[row] = ws + f.size;
@@ -1864,7 +1735,10 @@ struct fwa_engine {
     // kernel timing (HIP events on this handle's stream)
     hipEvent_t ev[8] = {};
     double partition_ms = 0, combine_ms = 0;
-    int64_t ingest_launches = 0, ingest_records = 0, fire_launches = 0, fire_rows = 0;
+    int64_t ingest_launches = 0, ingest_records = 0, replay_records = 0, fire_launches = 0, fire_rows = 0;
+    // producer stream of device inputs (fwa_set_input_stream): every push waits for it (stream order)
+    hipStream_t in_stream = nullptr;
+    hipEvent_t ev_in = nullptr;
     double ingest_ms = 0, fire_ms = 0;
     // sessions (merging windows)
     int32_t* d_scnt = nullptr;
@@ -2257,6 +2131,7 @@ void fwa_destroy(fwa_engine* e) {
     if (e->h_arena) (void)hipHostFree(e->h_arena);
     if (e->h_touched) (void)hipHostFree(e->h_touched);
     for (hipEvent_t ev : e->ev) if (ev) (void)hipEventDestroy(ev);
+    if (e->ev_in) (void)hipEventDestroy(e->ev_in);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -2397,6 +2272,7 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         if (hipMemsetAsync(e->d_st, 0, sizeof(DevStatus), e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
         bool evok = true;
         for (hipEvent_t& ev : e->ev) evok = evok && hipEventCreate(&ev) == hipSuccess;
+        evok = evok && hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) == hipSuccess;
         if (!evok) { rc = FWA_E_DEVICE; break; }
         if (hipMalloc(&e->d_want, sizeof(unsigned long long) * kWantCap) != hipSuccess) { rc = FWA_E_OOM; break; }
         size_t fr = 0, tot = 0;
@@ -2454,7 +2330,17 @@ static int stage_inputs(fwa_engine* e, const int64_t* keys, const int64_t* ts, c
     return FWA_OK;
 }
 
+// Device inputs are produced on the caller's stream (e.g. torch's current stream): the engine's stream
+// waits for everything enqueued there so far before its kernels read them.
+static int wait_input_stream(fwa_engine* e) {
+    if (!e->in_stream) return FWA_OK;
+    HIPCHK(e, hipEventRecord(e->ev_in, e->in_stream));
+    HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_in, 0));
+    return FWA_OK;
+}
+
 static int launch_ingest(fwa_engine* e, IngestArgs& a, bool replay) {
+    a.spill_cap = e->spill_cap;
     a.key_table = e->d_keys;
     a.key_mask = (uint64_t)e->capacity - 1;
     a.seg_log = e->seg_log;
@@ -2475,7 +2361,8 @@ static int launch_ingest(fwa_engine* e, IngestArgs& a, bool replay) {
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[1], e->stream));
     e->ingest_launches++;
-    e->ingest_records += a.n;
+    if (!replay) e->ingest_records += a.n;   // a replay re-visits records the first launch already counted
+    else e->replay_records += a.n;
     return FWA_OK;
 }
 
@@ -2560,6 +2447,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.b_val1 = e->d_bval[1];
     pa.b_cnt = e->d_bcnt;
     pa.capb = e->capb;
+    pa.spill_cap = e->spill_cap;
     pa.part_bits = e->part_bits;
     pa.np = e->np;
     for (int v = 0; v < 2; ++v) { pa.vcol[v] = e->vcol[v]; pa.vsize[v] = e->vsize[v]; }
@@ -2571,37 +2459,16 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     if (pprof && !d_pprof) HIPCHK(e, hipMalloc(&d_pprof, sizeof(long long) * 8 * 1024));
     pa.prof = pprof ? d_pprof : nullptr;
     HIPCHK(e, hipEventRecord(e->ev[4], e->stream));
-    // tile shape variants (FWA_PVAR): 0 = 512 thr x 12 items, 1 = 1024 x 6, 2 = 512 x 8 (2 WG/CU), 3 = 256 x 12
-    static const int pvar = getenv("FWA_PVAR") ? atoi(getenv("FWA_PVAR")) : 5;
-    int threads = 512, items = 12, per_cu = 1;
-    if (e->nv == 2) items = 8;
-    if (e->nv == 0) items = 16;
-    if (pvar == 1 || pvar == 5) { threads = 1024; items /= 2; }
-    if (pvar == 2) { items = e->nv == 2 ? 4 : (e->nv == 1 ? 6 : 8); per_cu = 2; }
-    if (pvar == 4) { threads = 1024; items = e->nv == 2 ? 2 : (e->nv == 1 ? 3 : 4); per_cu = 2; }
-    if (pvar == 3) { threads = 256; items = e->nv == 2 ? 12 : (e->nv == 1 ? 16 : 24); per_cu = 1; }
+    int threads = 1024;
+    const int items = e->nv == 2 ? 4 : (e->nv == 1 ? 6 : 8);
     const int64_t tile = (int64_t)items * threads;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256 * per_cu));
-#define PLAUNCH(NV, IT, TH, MW) partition_kernel<NV, IT, TH, MW><<<grid, TH, 0, e->stream>>>(pa, e->d_ec)
-    // pvar 2 / 4: two workgroups per CU (LDS <= 80 KB, VGPR <= 128) so one loads while the other computes
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256));
     const int vw = (e->vsize[0] == 8 ? 1 : 0) | (e->vsize[1] == 8 ? 2 : 0);
 #define P2LAUNCH(NV, IT, VW) partition2_kernel<NV, IT, 1024, 1, VW><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec)
-    if (pvar == 5) {   // pipelined (default)
-        if (e->nv == 0) P2LAUNCH(0, 8, 3);
-        else if (e->nv == 1) { if (vw & 1) P2LAUNCH(1, 6, 3); else P2LAUNCH(1, 6, 2); }
-        else if (vw == 3) P2LAUNCH(2, 4, 3); else if (vw == 2) P2LAUNCH(2, 4, 2);
-        else if (vw == 1) P2LAUNCH(2, 4, 1); else P2LAUNCH(2, 4, 0);
-    } else if (e->nv == 0) {
-        if (pvar == 1) PLAUNCH(0, 8, 1024, 1); else if (pvar == 2) PLAUNCH(0, 8, 512, 4); else if (pvar == 3) PLAUNCH(0, 24, 256, 1);
-        else if (pvar == 4) PLAUNCH(0, 4, 1024, 2); else PLAUNCH(0, 16, 512, 1);
-    } else if (e->nv == 1) {
-        if (pvar == 1) PLAUNCH(1, 6, 1024, 1); else if (pvar == 2) PLAUNCH(1, 6, 512, 4); else if (pvar == 3) PLAUNCH(1, 16, 256, 1);
-        else if (pvar == 4) PLAUNCH(1, 3, 1024, 2); else PLAUNCH(1, 12, 512, 1);
-    } else {
-        if (pvar == 1) PLAUNCH(2, 4, 1024, 1); else if (pvar == 2) PLAUNCH(2, 4, 512, 4); else if (pvar == 3) PLAUNCH(2, 12, 256, 1);
-        else if (pvar == 4) PLAUNCH(2, 2, 1024, 2); else PLAUNCH(2, 8, 512, 1);
-    }
-#undef PLAUNCH
+    if (e->nv == 0) P2LAUNCH(0, 8, 3);
+    else if (e->nv == 1) { if (vw & 1) P2LAUNCH(1, 6, 3); else P2LAUNCH(1, 6, 2); }
+    else if (vw == 3) P2LAUNCH(2, 4, 3); else if (vw == 2) P2LAUNCH(2, 4, 2);
+    else if (vw == 1) P2LAUNCH(2, 4, 1); else P2LAUNCH(2, 4, 0);
 #undef P2LAUNCH
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[5], e->stream));
@@ -2830,7 +2697,8 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
         if (rc) return rc;
         goto relaunch;
     }
-    e->late_rows = 0;            // consumed (emit_late_rows copied them to the head of the output)
+    if (row0 > 0) e->late_rows = 0;   // consumed (emit_late_rows copied them to the head of the output);
+                                      // a snapshot / drain fire (row0 == 0) leaves them for the next watermark
     float ms = 0.f;
     HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
     e->fire_ms += ms;
@@ -3051,6 +2919,7 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
     a.n = n;
     a.wm = e->wm;
     if (flags & FWA_PUSH_DEVICE_PTRS) {
+        if (int rc1 = wait_input_stream(e)) return rc1;
         a.keys = keys;
         a.ts = ts;
         a.key_hash = key_hash;
@@ -3116,6 +2985,7 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
     }
     const void* dev[3 + FWA_MAX_AGGS];
     if (flags & FWA_PUSH_DEVICE_PTRS) {
+        if (int rc1 = wait_input_stream(e)) return rc1;
         for (int c = 0; c < nsrc; ++c) dev[c] = src[c];
     } else {                                   // stage host columns (8 bytes each) into the input buffer
         const size_t colb = ((size_t)n * 8 + 255) / 256 * 256;
@@ -3412,6 +3282,7 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
     rc = ensure_out(e, nw * nkeys);
     if (rc) return rc;
+  relaunch:
     HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
     FireSlideArgs f;
     memset(&f, 0, sizeof(f));
@@ -3430,6 +3301,7 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     f.o_start = e->o_start;
     f.o_end = e->o_end;
     for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
+    f.out_cap = e->out_cap;
     f.st = e->d_st;
     const int64_t grid = (e->capacity + 1 + (int64_t)kBlock * kSlideJ - 1) / ((int64_t)kBlock * kSlideJ);
     HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
@@ -3439,6 +3311,11 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     rc = sync_status(e);
     if (rc) return rc;
     *nrows = (int64_t)e->h_st->rows;
+    if (*nrows > e->out_cap) {   // n_keys was stale: grow to the exact count and fire again (idempotent)
+        rc = ensure_out(e, *nrows);
+        if (rc) return rc;
+        goto relaunch;
+    }
     float ms = 0.f;
     HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
     e->fire_ms += ms;
@@ -3636,6 +3513,7 @@ int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
     s->ingest_launches = e->ingest_launches;
     s->ingest_ms = e->ingest_ms;
     s->ingest_records = e->ingest_records;
+    s->replay_records = e->replay_records;
     s->fire_launches = e->fire_launches;
     s->fire_ms = e->fire_ms;
     s->fire_rows = e->fire_rows;
@@ -3647,8 +3525,14 @@ int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
 int fwa_reset_timers(fwa_engine* e) {
     if (!e) return FWA_E_ARG;
     if (int rc0 = settle_pending(e)) return rc0;
-    e->ingest_launches = e->ingest_records = e->fire_launches = e->fire_rows = 0;
+    e->ingest_launches = e->ingest_records = e->replay_records = e->fire_launches = e->fire_rows = 0;
     e->ingest_ms = e->fire_ms = e->partition_ms = e->combine_ms = 0;
+    return FWA_OK;
+}
+
+int fwa_set_input_stream(fwa_engine* e, void* stream) {
+    if (!e) return FWA_E_STATE;
+    e->in_stream = (hipStream_t)stream;
     return FWA_OK;
 }
 

@@ -55,6 +55,8 @@ def lib():
     L.fwa_flush.argtypes = [C.c_void_p]
     L.fwa_flush.restype = C.c_int
     L.fwa_version.restype = C.c_char_p
+    L.fwa_set_input_stream.argtypes = [C.c_void_p, C.c_void_p]
+    L.fwa_set_input_stream.restype = C.c_int
     L.fwa_reset_timers.argtypes = [C.c_void_p]
     L.fwa_reset_timers.restype = C.c_int
     L.fwa_key_groups.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
@@ -103,9 +105,23 @@ class WindowAggregator:
         self.cfg = cfg
         self.names = A.agg_names(cfg)
         self.h = C.c_void_p()
+        self._inflight = None     # inputs of an FWA_PUSH_ASYNC push, kept alive until the next call settles it
+        self._in_stream = None
         rc = lib().fwa_create(C.byref(cfg), C.byref(self.h))
         if rc:
             raise EngineError(rc, "fwa_create")
+
+    def _order_after_producer(self, x):
+        """Device inputs come from torch's current stream: make the engine's stream wait for it."""
+        import torch
+        s = torch.cuda.current_stream(x.device).cuda_stream
+        if s != self._in_stream:
+            _check(lib().fwa_set_input_stream(self.h, C.c_void_p(s)), self.h)
+            self._in_stream = s
+
+    def _settled(self):
+        """Called after every entry point that settles a pending async push."""
+        self._inflight = None
 
     # -- processElement (batched) --
     def push(self, keys, ts, cols=(), key_hash=None, sync=True):
@@ -124,17 +140,23 @@ class WindowAggregator:
         n = int(keys.shape[0])
         arr = (C.c_void_p * max(1, len(cols)))(*[_ptr(c).value for c in cols])
         flags = A.PUSH_DEVICE_PTRS if device else 0
+        if device:
+            self._order_after_producer(keys)
         if not sync and device:
             flags |= A.PUSH_ASYNC
         dropped = C.c_int64(0)
         rc = lib().fwa_push(self.h, _ptr(keys), _ptr(ts), arr, _ptr(key_hash), n, flags, C.byref(dropped))
+        self._settled()
         _check(rc, self.h)
+        if flags & A.PUSH_ASYNC:
+            self._inflight = (keys, ts, list(cols), key_hash)
         return dropped.value
 
     # -- processWatermark --
     def advance_watermark_raw(self, wm):
         out = A.Out()
         rc = lib().fwa_advance_watermark(self.h, int(wm), C.byref(out))
+        self._settled()
         _check(rc, self.h)
         return out
 
@@ -164,7 +186,9 @@ class WindowAggregator:
         complete at wm and forward the watermark. Returns dict key/slice_start/count/acc<j> (numpy, or
         zero-copy torch CUDA views valid until the next call when output_on_device=1)."""
         out = A.Partials()
-        _check(lib().fwa_drain_partials(self.h, int(wm), C.byref(out)), self.h)
+        rc = lib().fwa_drain_partials(self.h, int(wm), C.byref(out))
+        self._settled()
+        _check(rc, self.h)
         n = out.n
         i8 = np.dtype("i8")
         if out.on_device:
@@ -186,9 +210,12 @@ class WindowAggregator:
             count = np.ascontiguousarray(count, np.int64)
             accs = [np.ascontiguousarray(a).view(np.int64) for a in accs]
         arr = (C.c_void_p * A.FWA_MAX_AGGS)(*([_ptr(a).value for a in accs] + [None] * (A.FWA_MAX_AGGS - len(accs))))
+        if device:
+            self._order_after_producer(keys)
         dropped = C.c_int64(0)
         rc = lib().fwa_push_partials(self.h, _ptr(keys), _ptr(slice_ts), _ptr(count), arr, int(keys.shape[0]),
                                      A.PUSH_DEVICE_PTRS if device else 0, C.byref(dropped))
+        self._settled()
         _check(rc, self.h)
         return dropped.value
 
@@ -197,7 +224,9 @@ class WindowAggregator:
         """Return the handle's keyed window state + watermark as bytes (key-group-partitioned blob,
         format in include/flink_amd.h; parse with flink_amd.snapshot.parse)."""
         b = Blob()
-        _check(lib().fwa_snapshot(self.h, C.byref(b)), self.h)
+        rc = lib().fwa_snapshot(self.h, C.byref(b))
+        self._settled()
+        _check(rc, self.h)
         try:
             return C.string_at(b.data, b.size) if b.size else b""
         finally:
@@ -211,23 +240,32 @@ class WindowAggregator:
         bufs = [C.create_string_buffer(bytes(b), len(b)) for b in blobs]
         ptrs = (C.c_void_p * max(1, len(bufs)))(*[C.cast(b, C.c_void_p).value for b in bufs])
         sizes = (C.c_int64 * max(1, len(bufs)))(*[len(b) for b in blobs])
-        _check(lib().fwa_restore(self.h, ptrs, sizes, len(bufs)), self.h)
+        rc = lib().fwa_restore(self.h, ptrs, sizes, len(bufs))
+        self._settled()
+        _check(rc, self.h)
 
     def flush(self):
-        _check(lib().fwa_flush(self.h), self.h)
+        rc = lib().fwa_flush(self.h)
+        self._settled()
+        _check(rc, self.h)
 
     def stats(self):
         st = A.Stats()
-        _check(lib().fwa_get_stats(self.h, C.byref(st)), self.h)
+        rc = lib().fwa_get_stats(self.h, C.byref(st))
+        self._settled()
+        _check(rc, self.h)
         return st
 
     def reset_timers(self):
-        _check(lib().fwa_reset_timers(self.h), self.h)
+        rc = lib().fwa_reset_timers(self.h)
+        self._settled()
+        _check(rc, self.h)
 
     def close(self):
         if self.h:
             lib().fwa_destroy(self.h)
             self.h = C.c_void_p()
+            self._inflight = None
 
     def __del__(self):
         try:

@@ -153,12 +153,13 @@ typedef struct fwa_stats {
     /* device time of the engine's kernels, measured with HIP events on the handle's stream */
     int64_t ingest_launches;
     double ingest_ms;            /* sum over ingest-kernel launches */
-    int64_t ingest_records;      /* records processed by those launches (replays included) */
+    int64_t ingest_records;      /* distinct records pushed through those launches (replays excluded) */
     int64_t fire_launches;
     double fire_ms;
     int64_t fire_rows;
     double partition_ms;         /* two-phase ingest split: phase P (key lookup + partition) */
     double combine_ms;           /* phase A (LDS combine + HBM merge) */
+    int64_t replay_records;      /* records re-visited by slice-miss / bucket-overflow replays (not in ingest_records) */
 } fwa_stats;
 
 
@@ -176,6 +177,13 @@ const char* fwa_version(void);
  * Input buffers are borrowed for the duration of the call only (FWA_PUSH_ASYNC: until the next call). */
 int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
              const int32_t* key_hash, int64_t n, int32_t flags, int64_t* late_dropped_out);
+
+/* Stream ordering of device inputs (FWA_PUSH_DEVICE_PTRS): the caller's HIP stream that produces the
+ * input columns (e.g. the framework's current stream). Every later device-pointer push makes the engine's
+ * own stream wait for the work enqueued on `stream` so far before reading the columns. NULL (default):
+ * the caller guarantees the inputs are complete (e.g. it synchronised). Outputs are complete when the
+ * entry point that returns them returns. */
+int fwa_set_input_stream(fwa_engine* e, void* stream);
 
 /* Advance the event-time watermark; fires every window whose maxTimestamp (end-1) <= wm.
  * Non-advancing watermarks fire nothing (SlicingWindowOperator.java:231, StatusWatermarkValve).

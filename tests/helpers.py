@@ -9,6 +9,18 @@ from flink_amd import _abi as A
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+def java_hash_code(key, key_type):
+    """key.hashCode() per the Java SE spec: Integer -> the value; String -> s[0]*31^(n-1) + ... + s[n-1]
+    over UTF-16 code units, int32 wrap-around (java.lang.String.hashCode)."""
+    if key_type == "Integer":
+        return int(np.int32(key))
+    b = key.encode("utf-16-le")
+    h = 0
+    for i in range(0, len(b), 2):
+        h = (31 * h + int.from_bytes(b[i:i + 2], "little")) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= 1 << 31 else h
+
+
 def load_kats():
     with open(os.path.join(GOLDEN, "reference_kats.json")) as f:
         return json.load(f)

@@ -16,6 +16,8 @@ TEXT = ["The quick brown fox jumps over the lazy dog; the dog sleeps, the fox ru
 def test_tokenizer_matches_java_split():
     assert tokenize("Hello, World!! foo_bar 42x") == [("hello", 1), ("world", 1), ("foo_bar", 1), ("42x", 1)]
     assert tokenize("  --  ") == []
+    # Java's \\W is ASCII-only ([^a-zA-Z0-9_]): non-ASCII letters split tokens (toLowerCase is Unicode)
+    assert tokenize("Café Straße ÆON x") == [("caf", 1), ("stra", 1), ("e", 1), ("on", 1), ("x", 1)]
 
 
 def test_itcase_regexp_and_counts():

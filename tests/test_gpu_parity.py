@@ -402,3 +402,45 @@ def test_c3_shape_zipf_hop_vs_oracle(eng_mod):
         assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), ["COUNT", "SUM_I64"], ctx="wm=%d" % wm)
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("case", KATS["key_groups"], ids=lambda c: c["src"].split("/")[-1].split(" ")[0])
+def test_key_group_literal_kats_on_gpu(eng_mod, case):
+    """fwa_key_groups (PREHASHED: the caller passes key.hashCode()) reproduces the key groups and
+    operator indices the reference's tests assert (RocksIncrementalCheckpointRescalingTest, CEPRescalingTest)."""
+    from helpers import java_hash_code
+    maxp = case["max_parallelism"]
+    keys = np.array([i for i, _ in enumerate(case["cases"])], np.int64)
+    kh = np.array([java_hash_code(k, case["key_type"]) for k, _ in case["cases"]], np.int32)
+    kg, _ = eng_mod.key_groups(keys, maxp, 1, key_kind=A.KEY_PREHASHED, key_hash=kh)
+    assert kg.tolist() == [g for _, g in case["cases"]]
+    for key, par, op in case["operator_index"]:
+        _, o = eng_mod.key_groups(np.array([0], np.int64), maxp, par, key_kind=A.KEY_PREHASHED,
+                                  key_hash=np.array([java_hash_code(key, case["key_type"])], np.int32))
+        assert int(o[0]) == op, (key, par)
+
+
+def test_late_firing_rows_survive_snapshot(eng_mod):
+    """a snapshot (non-destructive raw fire) taken after a push with late firings must not
+    discard the pending late-firing rows; the next watermark returns them, as without the snapshot."""
+    from oracle.oracle import Oracle
+    cfg = A.make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=1000, allowed_lateness_ms=5000,
+                        aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=1024)
+    g, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
+    k = np.array([1, 2, 1, 3], np.int64)
+    t = np.array([100, 200, 1500, 2500], np.int64)
+    v = np.array([1, 2, 3, 4], np.int64)
+    for x in (g, o):
+        x.push(k, t, [v])
+    assert_rows_equal(g.advance_watermark(3000), o.advance_watermark(3000), ["COUNT", "SUM_I64"])
+    k2 = np.array([1, 1, 2], np.int64)           # windows [0,1000) fired at 3000, not past cleanup (5999)
+    t2 = np.array([300, 400, 999], np.int64)
+    v2 = np.array([10, 20, 30], np.int64)
+    for x in (g, o):
+        x.push(k2, t2, [v2])
+    blob = g.snapshot()
+    assert len(blob) > 0
+    rg, ro = g.advance_watermark(3000), o.advance_watermark(3000)   # non-advancing: only the late rows
+    assert len(ro["key"]) == 3
+    assert_rows_equal(rg, ro, ["COUNT", "SUM_I64"])
+    assert_rows_equal(g.advance_watermark(A.LONG_MAX), o.advance_watermark(A.LONG_MAX), ["COUNT", "SUM_I64"])

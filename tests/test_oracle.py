@@ -74,3 +74,17 @@ def test_ts_min_raises():
     with pytest.raises(O.OracleError) as ei:
         o.push(np.array([1]), np.array([A.LONG_MIN]), [np.array([1])])
     assert ei.value.code == -2
+
+
+@pytest.mark.parametrize("case", KATS["key_groups"], ids=lambda c: c["src"].split("/")[-1].split(" ")[0])
+def test_key_group_literal_kats(case):
+    """KeyGroupRangeAssignment integers asserted by the reference's own tests (String / Integer keys:
+    key.hashCode() -> murmurHash -> % maxParallelism; operator index kg * P / maxP)."""
+    from helpers import java_hash_code
+    L = O.lib()
+    maxp = case["max_parallelism"]
+    for key, kg in case["cases"]:
+        assert L.or_key_group(0, A.KEY_PREHASHED, java_hash_code(key, case["key_type"]), maxp) == kg, key
+    for key, par, op in case["operator_index"]:
+        kg = L.or_key_group(0, A.KEY_PREHASHED, java_hash_code(key, case["key_type"]), maxp)
+        assert L.or_operator_index(maxp, par, kg) == op, (key, par)
