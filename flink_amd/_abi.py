@@ -5,7 +5,7 @@ the exact same struct layouts.
 """
 import ctypes as C
 
-FWA_ABI_VERSION = 1
+FWA_ABI_VERSION = 2
 FWA_MAX_AGGS = 8
 
 # enum fwa_window_kind
@@ -39,6 +39,8 @@ AGG_INPUT_DTYPE = {
 STATUS = {0: "OK", -1: "E_ARG", -2: "E_TS_MIN", -3: "E_KEYGROUP", -4: "E_MERGE_LATE", -5: "E_OOM",
           -6: "E_DEVICE", -7: "E_UNSUPPORTED", -8: "E_STATE"}
 
+CFG_DYNAMIC_GAP = 0x1
+
 PUSH_DEVICE_PTRS = 0x1
 PUSH_ASYNC = 0x2
 
@@ -58,6 +60,8 @@ class Config(C.Structure):
         ("max_parallelism", C.c_int32), ("kg_start", C.c_int32), ("kg_end", C.c_int32),
         ("num_aggs", C.c_int32), ("aggs", AggSpec * FWA_MAX_AGGS), ("device", C.c_int32),
         ("output_on_device", C.c_int32), ("key_capacity", C.c_int64), ("max_batch", C.c_int64),
+        ("flags", C.c_int32), ("gap_col", C.c_int32), ("tz_n", C.c_int32), ("reserved", C.c_int32),
+        ("tz", C.c_void_p),
     ]
 
 
@@ -99,8 +103,10 @@ class GenParams(C.Structure):
 def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, slide_ms=0,
                 offset_ms=0, gap_ms=0, allowed_lateness_ms=0, aggs=(("COUNT", 0), ("SUM_I64", 0)),
                 key_kind=KEY_JAVA_LONG, max_parallelism=128, kg_start=0, kg_end=None, device=0,
-                output_on_device=0, key_capacity=0, max_batch=0):
-    """Build a Config struct. aggs: sequence of (agg name, value-column index)."""
+                output_on_device=0, key_capacity=0, max_batch=0, gap_col=None, tz=None):
+    """Build a Config struct. aggs: sequence of (agg name, value-column index). gap_col: value column of
+    per-record session gaps (DynamicEventTimeSessionWindows). tz: [(utc_instant_ms, offset_ms), ...] shift
+    time zone of a TIMESTAMP_LTZ rowtime (the struct keeps a pointer to a buffer held on the struct)."""
     c = Config()
     c.abi_version = FWA_ABI_VERSION
     c.window_kind = WINDOW_KINDS[window_kind] if isinstance(window_kind, str) else int(window_kind)
@@ -121,6 +127,14 @@ def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, sl
     c.output_on_device = output_on_device
     c.key_capacity = key_capacity
     c.max_batch = max_batch
+    if gap_col is not None:
+        c.flags |= CFG_DYNAMIC_GAP
+        c.gap_col = gap_col
+    if tz:
+        buf = (C.c_int64 * (2 * len(tz)))(*[int(x) for pair in tz for x in pair])
+        c._tz_buf = buf                                  # keep the pairs alive as long as the struct
+        c.tz_n = len(tz)
+        c.tz = C.cast(buf, C.c_void_p)
     return c
 
 

@@ -21,6 +21,7 @@
 // empty; a window is emitted for a key iff at least one record contributed to it.
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_radix_sort.hpp>
+#include <hipcub/device/device_scan.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -1277,197 +1278,435 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
 }
 
 // ------------------------------------------------------------------------------------------------
-// sessions (merging windows, DataStream EventTimeSessionWindows with EventTimeTrigger)
+// sessions (merging windows): DataStream EventTimeSessionWindows + EventTimeTrigger (allowed lateness
+// L >= 0) and the Table legacy GROUP BY SESSION (TR/operators/window/WindowOperator.java:331-398 with
+// MergingWindowProcessFunction and EventTimeTriggers.afterEndOfWindow).
 //
-// State per key (kid): up to kMaxSess in-flight sessions {start, end, accumulators} in HBM, SoA by
-// (kid * kMaxSess + s). Semantics restated from MergingWindowSet.addWindow (MergingWindowSet.java:
-// 153-236), TimeWindow.intersects/cover/mergeWindows (TimeWindow.java:116-124, 208-254) and the merging
-// branch of WindowOperator.processElement (WindowOperator.java:288-389):
-//  * a record opens the window [ts, ts + gap) (EventTimeSessionWindows.assignWindows :61-63);
-//  * it merges with every in-flight session that intersects it (touching windows merge); in-flight
-//    sessions never intersect each other, so the merge set is exactly those sessions;
-//  * if nothing merged and the new window is late (maxTimestamp <= wm, allowed lateness 0) the window
-//    is retired and the record dropped (counted iff ts <= wm, isElementLate :597-601);
-//  * a session fires (and is cleared) when wm >= end - 1 (EventTimeTrigger.onEventTime, cleanup timer).
-// Whether a late record survives depends on the sessions in flight when it arrives, so the records
-// of a key are applied in ARRIVAL order: a stable radix sort by kid groups them, one thread walks a
-// key's run sequentially. Keys are independent, so the parallelism is over keys.
+// State: a flat list of in-flight sessions {kid, start, end, acc[nacc]} (column 0 = COUNT), in no
+// particular order; no per-key cap. A push rebuilds it (DESIGN.md §2 "Sessions"):
+//  * Order-free records -- the lone window [ts, ts+gap) ends after the watermark (ts + gap - 1 > wm).
+//    Such a record is never dropped, never fires on arrival, and merging is a union of intersecting
+//    intervals, so the key's session set after the push is the connected components of (its in-flight
+//    sessions + its new windows) regardless of arrival order (MergingWindowSet.addWindow :153-236,
+//    TimeWindow.intersects/cover :116-124 -- touching windows merge). Bulk path: one radix sort by
+//    (kid, start), a segmented max-scan of the ends (a new session starts where start > every earlier
+//    end of the key), a cluster-id scan, and a wave-segmented reduction of the accumulators.
+//  * A key with at least one order-sensitive record in the push (lone window already ends at or before
+//    the watermark: it may be dropped, may fire on arrival with the session contents, or may be saved by
+//    a session an earlier record of the push created) goes through an arrival-order walk instead: its
+//    sessions and records sorted by (kid, arrival), one lane per key applying addWindow / isWindowLate /
+//    EventTimeTrigger.onElement in order (WindowOperator.java:288-389). Late firings are written to the
+//    late-row buffer (returned at the head of the next fwa_advance_watermark).
+//  * Fire at a watermark advance prev -> wm: every session with prev < end - 1 <= wm emits a row
+//    (EventTimeTrigger.onEventTime: sessions whose maxTimestamp <= prev already fired -- at a timer or
+//    on an element); every session with cleanup = end - 1 + L <= wm is cleared (clearAllState).
 
-constexpr int kMaxSess = 16;
+struct SessCtr {                 // per-push device counters (zeroed by the host before a push / fire)
+    unsigned long long ts_min, ts_max;   // ord-encoded, over records and in-flight session starts
+    unsigned long long n_special;        // records whose lone window ends at or before the watermark
+    unsigned long long n_bulk, n_sp;     // elements routed to the bulk / the arrival-order path
+    unsigned long long n_out_sp;         // sessions written by the arrival-order path
+    unsigned long long n_keep;           // fire: sessions kept
+    unsigned long long pad;
+};
 
-struct SessArgs {
+struct SessList {                // one in-flight session list (SoA)
+    uint32_t* kid;
+    int64_t* start;
+    int64_t* end;
+    unsigned long long* acc;     // [nacc][stride]
+    int64_t stride;
+};
+
+struct Sess2Args {
     const int64_t* keys;
     const int64_t* ts;
     const void* cols[FWA_MAX_COLS];
     const int32_t* key_hash;
+    const int64_t* gapc;         // per-record gaps (DynamicEventTimeSessionWindows) or nullptr: fixed `gap`
     int64_t n;
-    int64_t wm;
-    int64_t gap;
+    int64_t wm, gap, lateness;
     unsigned long long* key_table;
     uint64_t key_mask;
     int32_t seg_log, part_bits;
-    uint32_t* kid;              // [n] key-table slot per record, arrival order
-    uint32_t* idx;              // [n] 0..n-1 (sort values)
-    const uint32_t* skid;       // [n] kids, stably sorted
-    const uint32_t* sidx;       // [n] record index of skid[i]
-    int32_t* s_cnt;             // [cap+1] in-flight sessions per kid
-    int64_t* s_start;           // [(cap+1) * kMaxSess]
-    int64_t* s_end;
-    unsigned long long* s_acc;  // [nacc][(cap+1) * kMaxSess]; column 0 = COUNT
-    int64_t sstride;
+    int64_t capacity;            // key-table capacity (side slot at capacity)
+    uint32_t* rkid;              // [n] kid per record (0xffffffff: rejected)
+    uint8_t* kflag;              // [capacity + 1] key has an order-sensitive record in this push
+    SessList in;                 // in-flight sessions before the push
+    int64_t n_in;
+    SessList out;                // after the push
+    // bulk path
+    int64_t base;                // smallest start of the push (records and in-flight sessions)
+    int32_t tb;                  // bits of (start - base) in the sort key (kid << tb | start - base)
+    int32_t all_sp;              // 1: route everything through the arrival-order path
+    unsigned long long* bkey;    // [nb] sort keys (then sorted)
+    uint32_t* bval;              // [nb] payload: record index, or session index | 0x80000000
+    int64_t* bend;               // [nb] window / session end per sorted element
+    int64_t* bmax;               // [nb] inclusive max of bend over the key so far (segmented scan)
+    uint32_t* bcid;              // [nb] head flags, then 1-based cluster ids (inclusive sum)
+    int64_t nb;
+    int32_t col_owner[1 + FWA_MAX_AGGS];   // aggregate that feeds accumulator column c (-1: COUNT)
+    // arrival-order path
+    unsigned long long* skey;    // [ns] (kid << 32) | (0 for a session, 1 + record index)
+    uint32_t* sval;
+    int64_t nsp;
+    int64_t* sc_start;           // [ns] scratch session lists, one region per key run
+    int64_t* sc_end;
+    unsigned long long* sc_acc;  // [nacc][ns]
+    // late-firing rows
+    int64_t* lr_key;
+    int64_t* lr_start;
+    int64_t* lr_end;
+    void* lr_agg[FWA_MAX_AGGS];
+    unsigned long long* lr_n;
+    int64_t lr_cap;
+    SessCtr* ctr;
     DevStatus* st;
 };
 
-__global__ void __launch_bounds__(kBlock) sess_key_kernel(SessArgs a, const EngineConst* __restrict__ cp) {
+__device__ __forceinline__ int64_t sess_cleanup(int64_t max_ts, int64_t lateness) {   // WindowOperator.cleanupTime :647-654
+    const int64_t ct = jm::wadd(max_ts, lateness);
+    return ct >= max_ts ? ct : LONG_MAX_J;
+}
+
+__device__ __forceinline__ void wave_minmax(unsigned long long lo, unsigned long long hi, unsigned long long* dlo,
+                                            unsigned long long* dhi) {
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        const unsigned long long a = __shfl_xor(lo, sh), b = __shfl_xor(hi, sh);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if ((threadIdx.x & 63) == 0 && lo <= hi) { atomicMin(dlo, lo); atomicMax(dhi, hi); }
+}
+
+// Pass 1 over the records: key-group check, kid, order-sensitivity flag per key, start range.
+__global__ void __launch_bounds__(kBlock) sess2_classify_kernel(Sess2Args a, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
+    unsigned long long lo = ~0ull, hi = 0ull, nsp = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t key = a.keys[i];
-        a.idx[i] = (uint32_t)i;
-        a.kid[i] = 0xffffffffu;
+        const int64_t ts = a.ts[i];
+        a.rkid[i] = 0xffffffffu;
         const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0), c.max_par);
         if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }   // StateTable :300-307
-        if (a.ts[i] == LONG_MIN_J) { raise_error(a.st, FWA_E_TS_MIN); continue; }
+        const int64_t gap = a.gapc ? a.gapc[i] : a.gap;
+        if (gap <= 0) { raise_error(a.st, FWA_E_ARG); continue; }   // DynamicEventTimeSessionWindows.java:60-64
         const int64_t kid = key_slot(a.key_table, a.key_mask, a.seg_log, a.part_bits, key, a.st);
         if (kid < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
-        a.kid[i] = (uint32_t)kid;
+        a.rkid[i] = (uint32_t)kid;
+        if (jm::wsub(jm::wadd(ts, gap), 1) <= a.wm) { a.kflag[kid] = 1; ++nsp; }   // lone window maxTs <= wm
+        const unsigned long long o = jm::ord_i64(ts);
+        lo = o < lo ? o : lo;
+        hi = o > hi ? o : hi;
+    }
+    wave_minmax(lo, hi, &a.ctr->ts_min, &a.ctr->ts_max);
+    for (int sh = 32; sh >= 1; sh >>= 1) nsp += __shfl_xor(nsp, sh);
+    if ((threadIdx.x & 63) == 0 && nsp) atomicAdd(&a.ctr->n_special, nsp);
+}
+
+__global__ void __launch_bounds__(kBlock) sess2_range_kernel(Sess2Args a) {
+    unsigned long long lo = ~0ull, hi = 0ull;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.n_in; j += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long o = jm::ord_i64(a.in.start[j]);
+        lo = o < lo ? o : lo;
+        hi = o > hi ? o : hi;
+    }
+    wave_minmax(lo, hi, &a.ctr->ts_min, &a.ctr->ts_max);
+}
+
+// wave-aggregated append: returns this lane's slot (valid only where `take`)
+__device__ __forceinline__ unsigned long long wave_append(bool take, unsigned long long* ctr) {
+    const unsigned long long m = __ballot(take);
+    if (!m) return 0;
+    const int lane = threadIdx.x & 63;
+    const int ld = __ffsll((long long)m) - 1;
+    unsigned long long b = 0;
+    if (lane == ld) b = atomicAdd(ctr, (unsigned long long)__popcll(m));
+    b = __shfl(b, ld);
+    return b + (unsigned long long)__popcll(m & ((1ull << lane) - 1));
+}
+
+// Pass 2: route every record and in-flight session to the bulk sort or the arrival-order sort.
+__global__ void __launch_bounds__(kBlock) sess2_route_kernel(Sess2Args a) {
+    const int64_t total = a.n + a.n_in;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < total; t0 += stride) {   // uniform trip count per wave
+        const int64_t t = t0 + threadIdx.x;
+        bool valid = false, sp = false;
+        unsigned long long bk = 0, sk = 0;
+        uint32_t pay = 0;
+        if (t < a.n) {
+            const uint32_t kid = a.rkid[t];
+            if (kid != 0xffffffffu) {
+                valid = true;
+                sp = a.all_sp || a.kflag[kid];
+                pay = (uint32_t)t;
+                bk = ((unsigned long long)kid << a.tb) | (uint64_t)(a.ts[t] - a.base);
+                sk = ((unsigned long long)kid << 32) | (uint64_t)(t + 1);
+            }
+        } else if (t < total) {
+            const int64_t j = t - a.n;
+            const uint32_t kid = a.in.kid[j];
+            valid = true;
+            sp = a.all_sp || a.kflag[kid];
+            pay = (uint32_t)j | 0x80000000u;
+            bk = ((unsigned long long)kid << a.tb) | (uint64_t)(a.in.start[j] - a.base);
+            sk = (unsigned long long)kid << 32;
+        }
+        const unsigned long long pb = wave_append(valid && !sp, &a.ctr->n_bulk);
+        const unsigned long long ps = wave_append(valid && sp, &a.ctr->n_sp);
+        if (valid && !sp) { a.bkey[pb] = bk; a.bval[pb] = pay; }
+        if (valid && sp) { a.skey[ps] = sk; a.sval[ps] = pay; }
     }
 }
 
-__device__ __forceinline__ void sess_copy(const SessArgs& a, int nacc, int64_t dst, int64_t src) {
-    a.s_start[dst] = a.s_start[src];
-    a.s_end[dst] = a.s_end[src];
-    for (int cc = 0; cc < nacc; ++cc) a.s_acc[cc * a.sstride + dst] = a.s_acc[cc * a.sstride + src];
+// Bulk: end of every sorted element (records: start + gap; sessions: their end).
+__global__ void __launch_bounds__(kBlock) sess2_ends_kernel(Sess2Args a) {
+    const uint64_t smask = a.tb >= 64 ? ~0ull : (((uint64_t)1 << a.tb) - 1);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.nb; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = a.bval[i];
+        const int64_t start = a.base + (int64_t)(a.bkey[i] & smask);
+        a.bend[i] = (p & 0x80000000u) ? a.in.end[p & 0x7fffffffu] : jm::wadd(start, a.gapc ? a.gapc[p] : a.gap);
+    }
 }
 
-__global__ void __launch_bounds__(kBlock) sess_process_kernel(SessArgs a, const EngineConst* __restrict__ cp) {
+// Bulk: head flag = first element of a key, or start after every earlier end of the key.
+__global__ void __launch_bounds__(kBlock) sess2_heads_kernel(Sess2Args a) {
+    const uint64_t smask = (((uint64_t)1 << a.tb) - 1);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.nb; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t h = 1;
+        if (i > 0) {
+            const unsigned long long k = a.bkey[i], kp = a.bkey[i - 1];
+            h = ((k >> a.tb) != (kp >> a.tb) || a.base + (int64_t)(k & smask) > a.bmax[i - 1]) ? 1u : 0u;
+        }
+        a.bcid[i] = h;
+    }
+}
+
+__device__ __forceinline__ unsigned long long sess_acc_of(const Sess2Args& a, const EngineConst& c, int cc, uint32_t p) {
+    if (p & 0x80000000u) return a.in.acc[(int64_t)cc * a.in.stride + (p & 0x7fffffffu)];
+    if (cc == 0) return 1ull;
+    return acc_input(c.agg[a.col_owner[cc]], a.cols[c.agg[a.col_owner[cc]].col], (int64_t)p);
+}
+
+__device__ __forceinline__ void acc_atomic(int acc_kind, unsigned long long* p, unsigned long long v) {
+    switch (acc_kind) {
+        case ACC_NONE: case ACC_ADD_I64: atomicAdd(p, v); break;
+        case ACC_ADD_F64: atomicAdd((double*)p, __longlong_as_double((long long)v)); break;
+        case ACC_MIN_ORD: atomicMin(p, v); break;
+        case ACC_MAX_ORD: atomicMax(p, v); break;
+        default: break;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) sess2_init_kernel(Sess2Args a, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    const int64_t ncl = a.nb > 0 ? (int64_t)a.bcid[a.nb - 1] : 0;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ncl; j += (int64_t)gridDim.x * blockDim.x)
+        for (int cc = 0; cc < c.nacc; ++cc) a.out.acc[(int64_t)cc * a.out.stride + j] = cc == 0 ? 0ull : ident_of(c.acc_kind[cc]);
+}
+
+// Bulk: wave-segmented reduction of each cluster (COUNT + accumulator columns). The cluster's true
+// head writes kid and start, its true tail the end (= the key's running max end there); accumulators
+// of a cluster that lies inside one wave are written with plain stores, a cluster spanning waves is
+// combined into identity-initialised columns with atomics.
+__global__ void __launch_bounds__(kBlock) sess2_reduce_kernel(Sess2Args a, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    const int lane = threadIdx.x & 63;
+    const uint64_t smask = (((uint64_t)1 << a.tb) - 1);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t w0 = (int64_t)blockIdx.x * blockDim.x; w0 < a.nb; w0 += stride) {   // uniform trips per wave
+        const int64_t wb = w0 + (threadIdx.x & ~63);     // this wave's first element
+        const int64_t i = w0 + threadIdx.x;
+        const bool act = i < a.nb;
+        const int64_t cid = act ? (int64_t)a.bcid[i] : -1 - lane;   // inactive lanes: distinct ids
+        const uint32_t p = act ? a.bval[i] : 0u;
+        const int64_t cid0 = __shfl(cid, 0);
+        const bool head0 = wb < a.nb && (wb == 0 || a.bcid[wb] != a.bcid[wb - 1]);
+        const int64_t cn = __shfl_down(cid, 1);
+        const bool last = act && (i + 1 >= a.nb || a.bcid[i + 1] != (uint32_t)cid);   // cluster's true tail
+        const bool tail = act && (lane == 63 || cn != cid);                          // its last lane here
+        const bool whole = (cid != cid0 || head0) && (lane != 63 || last);
+        const int64_t cl = cid - 1;
+        if (act && (i == 0 || a.bcid[i - 1] != (uint32_t)cid)) {
+            a.out.kid[cl] = (uint32_t)(a.bkey[i] >> a.tb);
+            a.out.start[cl] = a.base + (int64_t)(a.bkey[i] & smask);
+        }
+        if (last) a.out.end[cl] = a.bmax[i];
+        for (int cc = 0; cc < c.nacc; ++cc) {
+            const int ak = cc == 0 ? ACC_ADD_I64 : c.acc_kind[cc];
+            unsigned long long v = act ? sess_acc_of(a, c, cc, p) : 0ull;
+            for (int d = 1; d < 64; d <<= 1) {
+                const unsigned long long y = __shfl_up(v, d);
+                const int64_t yc = __shfl_up(cid, d);
+                if (lane >= d && yc == cid) v = acc_combine(ak, v, y);
+            }
+            if (!tail) continue;
+            unsigned long long* dst = &a.out.acc[(int64_t)cc * a.out.stride + cl];
+            if (whole) *dst = v;
+            else acc_atomic(ak, dst, v);
+        }
+    }
+}
+
+__device__ __forceinline__ int64_t sess_key_of(const unsigned long long* key_table, int64_t capacity, uint32_t kid) {
+    return (int64_t)kid < capacity ? (int64_t)key_table[kid] : LONG_MIN_J;   // side slot: the sentinel key
+}
+
+// Arrival-order path: one lane per key run of the (kid, arrival)-sorted list; its in-flight sessions
+// come first (low word 0), then its records in arrival order. The run's scratch region [t, t + len)
+// holds its session list (a run of len elements never has more than len sessions).
+__global__ void __launch_bounds__(kBlock) sess2_ordered_kernel(Sess2Args a, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
     const int nacc = c.nacc;
+    const bool table = c.sem == FWA_SEM_TABLE;
+    const int64_t ncl = a.nb > 0 ? (int64_t)a.bcid[a.nb - 1] : 0;
     unsigned long long dropped = 0;
-    long long live_delta = 0;
-    bool overflow = false;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.n; t += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t k = a.skid[t];
-        if (t > 0 && a.skid[t - 1] == k) continue;          // not the head of this key's run
-        const int64_t base = (int64_t)k * kMaxSess;
-        int ns = a.s_cnt[k];
-        for (int64_t j = t; j < a.n && a.skid[j] == k; ++j) {
-            const int64_t i = a.sidx[j];
-            const int64_t ts = a.ts[i];
-            const int64_t ws = ts, we = jm::wadd(ts, a.gap);
-            int64_t cs = ws, ce = we;
-            int first = -1;
-            for (int s = 0; s < ns; ++s) {
-                const int64_t ss = a.s_start[base + s], se = a.s_end[base + s];
-                if (!(ss <= we && se >= ws)) continue;          // TimeWindow.intersects
-                cs = ss < cs ? ss : cs;                         // TimeWindow.cover
-                ce = se > ce ? se : ce;
-                if (first < 0) { first = s; continue; }
-                for (int cc = 0; cc < nacc; ++cc) {             // mergeNamespaces -> AggregateFunction.merge
-                    unsigned long long* pf = &a.s_acc[cc * a.sstride + base + first];
-                    *pf = acc_combine(c.acc_kind[cc], *pf, a.s_acc[cc * a.sstride + base + s]);
-                }
-                --ns;
-                --live_delta;
-                if (s != ns) sess_copy(a, nacc, base + s, base + ns);
-                --s;                                            // re-examine the session moved into s
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.nsp; t += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t kid = (uint32_t)(a.skey[t] >> 32);
+        if (t > 0 && (uint32_t)(a.skey[t - 1] >> 32) == kid) continue;   // not the head of the key's run
+        int64_t* ss = a.sc_start + t;
+        int64_t* se = a.sc_end + t;
+        auto acc = [&](int cc, int64_t s) -> unsigned long long& { return a.sc_acc[(int64_t)cc * a.nsp + t + s]; };
+        int64_t ns = 0;
+        bool failed = false;
+        for (int64_t j = t; j < a.nsp && (uint32_t)(a.skey[j] >> 32) == kid && !failed; ++j) {
+            const uint32_t p = a.sval[j];
+            if (p & 0x80000000u) {                              // an in-flight session of this key
+                const int64_t q = p & 0x7fffffffu;
+                ss[ns] = a.in.start[q];
+                se[ns] = a.in.end[q];
+                for (int cc = 0; cc < nacc; ++cc) acc(cc, ns) = a.in.acc[(int64_t)cc * a.in.stride + q];
+                ++ns;
+                continue;
             }
-            if (first < 0) {
-                if (jm::wsub(we, 1) <= a.wm) {                  // isWindowLate -> retireWindow; record skipped
-                    if (ts <= a.wm) ++dropped;                  // isElementLate
-                    continue;
-                }
-                if (ns == kMaxSess) { overflow = true; continue; }
-                first = ns++;
-                ++live_delta;
-                a.s_acc[base + first] = 0;
-                for (int cc = 1; cc < nacc; ++cc) a.s_acc[cc * a.sstride + base + first] = ident_of(c.acc_kind[cc]);
+            const int64_t r = p;
+            const int64_t ts = a.ts[r];
+            const int64_t ws = ts, we = jm::wadd(ts, a.gapc ? a.gapc[r] : a.gap);   // EventTimeSessionWindows.assignWindows :61-63
+            // MergingWindowSet.addWindow: the in-flight sessions intersecting the new window
+            int64_t first = -1, nm = 0, cs = ws, ce = we;
+            bool covers = false;
+            for (int64_t s = 0; s < ns; ++s) {
+                if (!(ss[s] <= we && se[s] >= ws)) continue;    // TimeWindow.intersects
+                ++nm;
+                if (first < 0) first = s;
+                cs = ss[s] < cs ? ss[s] : cs;                   // TimeWindow.cover
+                ce = se[s] > ce ? se[s] : ce;
+                covers = covers || (ss[s] <= ws && se[s] >= we);
             }
-            a.s_start[base + first] = cs;
-            a.s_end[base + first] = ce;
-            a.s_acc[base + first] += 1ull;                      // COUNT(*)
-            for (int jj = 0; jj < c.naggs; ++jj) {              // AggregateFunction.add
-                const AggDesc d = c.agg[jj];
-                if (d.acc == 0 || d.alias) continue;
-                unsigned long long* p = &a.s_acc[d.acc * a.sstride + base + first];
-                *p = acc_combine(d.acc_kind, *p, acc_input(d, a.cols[d.col], i));
+            int64_t act = first;
+            if (nm > 1 || (nm == 1 && !covers)) {               // MergeFunction.merge (WindowOperator.java:296-349)
+                if (jm::wadd(jm::wsub(ce, 1), a.lateness) <= a.wm) { raise_error(a.st, FWA_E_MERGE_LATE); failed = true; break; }
+                for (int64_t s = ns - 1; s >= 0; --s) {         // mergeNamespaces into the first, drop the rest
+                    if (s == first || !(ss[s] <= we && se[s] >= ws)) continue;
+                    for (int cc = 0; cc < nacc; ++cc)
+                        acc(cc, first) = acc_combine(cc == 0 ? ACC_ADD_I64 : c.acc_kind[cc], acc(cc, first), acc(cc, s));
+                    --ns;
+                    if (s != ns) {
+                        ss[s] = ss[ns]; se[s] = se[ns];
+                        for (int cc = 0; cc < nacc; ++cc) acc(cc, s) = acc(cc, ns);
+                        if (first == ns) first = s;
+                    }
+                }
+                act = first;
+                ss[act] = cs;
+                se[act] = ce;
+            }
+            const int64_t aw_end = act >= 0 ? se[act] : we;
+            if (sess_cleanup(jm::wsub(aw_end, 1), a.lateness) <= a.wm) {   // isWindowLate -> retireWindow, skip
+                if (act >= 0) {
+                    --ns;
+                    if (act != ns) { ss[act] = ss[ns]; se[act] = se[ns]; for (int cc = 0; cc < nacc; ++cc) acc(cc, act) = acc(cc, ns); }
+                }
+                // Table: every skipped record counts (WindowOperator.java:386-389); DataStream: only if
+                // isElementLate (WindowOperator.java:425-433, :597-601)
+                if (table || jm::wadd(ts, a.lateness) <= a.wm) ++dropped;
+                continue;
+            }
+            if (act < 0) {                                      // new self-contained session
+                act = ns++;
+                ss[act] = ws;
+                se[act] = we;
+                acc(0, act) = 0ull;
+                for (int cc = 1; cc < nacc; ++cc) acc(cc, act) = ident_of(c.acc_kind[cc]);
+            }
+            acc(0, act) += 1ull;                                // windowState.add (AggregateFunction.add)
+            for (int cc = 1; cc < nacc; ++cc)
+                acc(cc, act) = acc_combine(c.acc_kind[cc], acc(cc, act), acc_input(c.agg[a.col_owner[cc]], a.cols[c.agg[a.col_owner[cc]].col], r));
+            if (jm::wsub(se[act], 1) <= a.wm) {                 // EventTimeTrigger.onElement: FIRE at once
+                const unsigned long long row = atomicAdd(a.lr_n, 1ull);
+                if ((int64_t)row >= a.lr_cap) { raise_error(a.st, FWA_E_STATE); continue; }
+                a.lr_key[row] = sess_key_of(a.key_table, a.capacity, kid);
+                a.lr_start[row] = ss[act];
+                a.lr_end[row] = se[act];
+                for (int jj = 0; jj < c.naggs; ++jj) {
+                    const AggDesc d = c.agg[jj];
+                    write_agg(d, acc(0, act), d.acc > 0 ? acc(d.acc, act) : 0ull, a.lr_agg[jj], (int64_t)row);
+                }
             }
         }
-        a.s_cnt[k] = ns;
+        for (int64_t s = 0; s < ns; ++s) {                      // the key's sessions after the push
+            const int64_t o = ncl + (int64_t)atomicAdd(&a.ctr->n_out_sp, 1ull);
+            a.out.kid[o] = kid;
+            a.out.start[o] = ss[s];
+            a.out.end[o] = se[s];
+            for (int cc = 0; cc < nacc; ++cc) a.out.acc[(int64_t)cc * a.out.stride + o] = acc(cc, s);
+        }
     }
-    if (overflow) { a.st->key_full |= 8; raise_error(a.st, FWA_E_OOM); }
-    if (dropped) atomicAdd(&a.st->dropped, dropped);
-    if (live_delta) atomicAdd(&a.st->sess_live, (unsigned long long)live_delta);
+    for (int sh = 32; sh >= 1; sh >>= 1) dropped += __shfl_xor(dropped, sh);
+    if ((threadIdx.x & 63) == 0 && dropped) atomicAdd(&a.st->dropped, dropped);
 }
 
-struct SessFireArgs {
+struct Sess2FireArgs {
+    SessList in, out;
+    int64_t n_in;
+    int64_t prev_wm, wm, lateness;
     const unsigned long long* key_table;
     int64_t capacity;
-    int64_t wm;
-    int32_t* s_cnt;
-    int64_t* s_start;
-    int64_t* s_end;
-    unsigned long long* s_acc;
-    int64_t sstride;
     int64_t* o_key;
     int64_t* o_start;
     int64_t* o_end;
     void* o_agg[FWA_MAX_AGGS];
+    int64_t out_cap;
+    SessCtr* ctr;
     DevStatus* st;
 };
 
-// Fire every in-flight session with end - 1 <= wm (EventTimeTrigger.onEventTime + clearAllState),
-// compacting the survivors; one reservation atomic per wave for the emitted rows.
-__global__ void __launch_bounds__(kBlock) sess_fire_kernel(SessFireArgs f, const EngineConst* __restrict__ cp) {
+// Watermark advance prev -> wm: emit every session with prev < end - 1 <= wm (EventTimeTrigger.onEventTime
+// / AfterEndOfWindow); keep every session whose cleanup time is still after wm (clearAllState otherwise).
+__global__ void __launch_bounds__(kBlock) sess2_fire_kernel(Sess2FireArgs f, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
-    const int lane = threadIdx.x & 63;
-    const int64_t nk = f.capacity + 1;
-    long long fired_total = 0;
-    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < nk; k0 += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t k = k0 + threadIdx.x;
-        const int ns = k < nk ? f.s_cnt[k] : 0;
-        const int64_t base = k * kMaxSess;
-        uint32_t fm = 0;                                        // bit s: session s fires
-        for (int s = 0; s < ns; ++s)
-            if (jm::wsub(f.s_end[base + s], 1) <= f.wm) fm |= 1u << s;
-        const uint32_t nf = __popc(fm);
-        uint32_t incl = nf;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d);
-            if (lane >= d) incl += y;
-        }
-        unsigned long long wbase = 0;
-        if (lane == 63 && incl) wbase = atomicAdd(&f.st->rows, (unsigned long long)incl);
-        wbase = __shfl(wbase, 63);
-        if (!nf) continue;
-        int64_t row = (int64_t)wbase + incl - nf;
-        const int64_t kv = k < f.capacity ? (int64_t)f.key_table[k] : LONG_MIN_J;
-        int keep = 0;
-        for (int s = 0; s < ns; ++s) {
-            const int64_t src = base + s;
-            if (fm & (1u << s)) {
-                f.o_key[row] = kv;
-                f.o_start[row] = f.s_start[src];
-                f.o_end[row] = f.s_end[src];
-                const uint64_t cnt = f.s_acc[src];
-                for (int j = 0; j < c.naggs; ++j) {
-                    const AggDesc d = c.agg[j];
-                    write_agg(d, cnt, d.acc > 0 ? f.s_acc[d.acc * f.sstride + src] : 0ull, f.o_agg[j], row);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < f.n_in; t0 += stride) {
+        const int64_t j = t0 + threadIdx.x;
+        const bool act = j < f.n_in;
+        const int64_t end = act ? f.in.end[j] : 0;
+        const int64_t mt = jm::wsub(end, 1);
+        const bool fire = act && mt > f.prev_wm && mt <= f.wm;
+        const bool keep = act && !(sess_cleanup(mt, f.lateness) <= f.wm);
+        const unsigned long long row = wave_append(fire, &f.st->rows);
+        const unsigned long long k = wave_append(keep, &f.ctr->n_keep);
+        if (fire) {
+            if ((int64_t)row >= f.out_cap) raise_error(f.st, FWA_E_STATE);
+            else {
+                const uint32_t kid = f.in.kid[j];
+                f.o_key[row] = sess_key_of(f.key_table, f.capacity, kid);
+                f.o_start[row] = f.in.start[j];
+                f.o_end[row] = end;
+                const uint64_t cnt = f.in.acc[j];
+                for (int jj = 0; jj < c.naggs; ++jj) {
+                    const AggDesc d = c.agg[jj];
+                    write_agg(d, cnt, d.acc > 0 ? f.in.acc[(int64_t)d.acc * f.in.stride + j] : 0ull, f.o_agg[jj], (int64_t)row);
                 }
-                ++row;
-            } else {
-                if (keep != s) {
-                    f.s_start[base + keep] = f.s_start[src];
-                    f.s_end[base + keep] = f.s_end[src];
-                    for (int cc = 0; cc < c.nacc; ++cc) f.s_acc[cc * f.sstride + base + keep] = f.s_acc[cc * f.sstride + src];
-                }
-                ++keep;
             }
         }
-        f.s_cnt[k] = keep;
-        fired_total += nf;
+        if (keep) {
+            f.out.kid[k] = f.in.kid[j];
+            f.out.start[k] = f.in.start[j];
+            f.out.end[k] = end;
+            for (int cc = 0; cc < c.nacc; ++cc) f.out.acc[(int64_t)cc * f.out.stride + k] = f.in.acc[(int64_t)cc * f.in.stride + j];
+        }
     }
-    for (int d = 32; d >= 1; d >>= 1) fired_total += __shfl_xor(fired_total, d);
-    if (lane == 0 && fired_total) atomicAdd(&f.st->sess_live, (unsigned long long)(-fired_total));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1740,14 +1979,22 @@ struct fwa_engine {
     hipStream_t in_stream = nullptr;
     hipEvent_t ev_in = nullptr;
     double ingest_ms = 0, fire_ms = 0;
-    // sessions (merging windows)
-    int32_t* d_scnt = nullptr;
-    int64_t* d_sstart = nullptr;
-    int64_t* d_send = nullptr;
-    unsigned long long* d_sacc = nullptr;
-    int64_t sstride = 0;
-    uint32_t* d_sess_sort = nullptr;   // kid | idx | skid | sidx, 4 x sess_sort_cap
-    int64_t sess_sort_cap = 0;
+    // sessions (merging windows): in-flight session lists (double-buffered) and per-push scratch
+    SessList ss[2] = {};
+    int32_t ss_cur = 0;
+    int64_t ss_cap = 0, n_ss = 0;
+    uint32_t* d_rkid = nullptr;
+    uint8_t* d_kflag = nullptr;
+    SessCtr* d_sctr = nullptr;
+    SessCtr* h_sctr = nullptr;
+    int64_t sb_cap = 0;                // bulk / ordered sort buffers (elements)
+    unsigned long long* d_skey[4] = {};   // bulk in/out, ordered in/out
+    uint32_t* d_sval[4] = {};
+    int64_t* d_send2 = nullptr;
+    int64_t* d_smax = nullptr;
+    uint32_t* d_scid = nullptr;
+    int64_t sc_cap = 0;                // ordered-path scratch session lists
+    int64_t* d_sc = nullptr;           // start[sc_cap] | end[sc_cap] | acc[nacc][sc_cap]
     void* d_sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
     int32_t kid_bits = 0;
@@ -1827,13 +2074,16 @@ int validate(const fwa_config* c) {
                 return FWA_E_ARG;
             break;
         case FWA_SESSION:                                                    // EventTimeSessionWindows.java:45-50
-            if (c->gap_ms <= 0) return FWA_E_ARG;
-            if (c->semantics != FWA_SEM_DATASTREAM) return FWA_E_UNSUPPORTED;   // legacy Table SESSION: not on this path
-            if (c->allowed_lateness_ms != 0) return FWA_E_UNSUPPORTED;         // late firings of merged windows
+            if (c->gap_ms <= 0 && !(c->flags & FWA_CFG_DYNAMIC_GAP)) return FWA_E_ARG;
             break;
         default:
             return FWA_E_ARG;
     }
+    if (c->flags & ~FWA_CFG_DYNAMIC_GAP) return FWA_E_ARG;
+    if ((c->flags & FWA_CFG_DYNAMIC_GAP) && (c->window_kind != FWA_SESSION || c->gap_col < 0 || c->gap_col >= FWA_MAX_COLS))
+        return FWA_E_ARG;
+    if (c->tz_n < 0 || (c->tz_n > 0 && !c->tz)) return FWA_E_ARG;
+    if (c->tz_n > 0) return FWA_E_UNSUPPORTED;
     if (c->semantics != FWA_SEM_DATASTREAM && c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;
     if (c->semantics == FWA_SEM_TABLE && c->allowed_lateness_ms != 0) return FWA_E_ARG;
     if (c->allowed_lateness_ms < 0) return FWA_E_ARG;
@@ -2123,8 +2373,11 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n, e->d_reset_list, e->d_upos,
-                    e->d_scnt, e->d_sstart, e->d_send, e->d_sacc, e->d_sess_sort, e->d_sort_tmp, e->o_count};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count};
     for (void* p : bufs) if (p) (void)hipFree(p);
+    for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
+    for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
+    if (e->h_sctr) (void)hipHostFree(e->h_sctr);
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
     for (void* p : e->chunks) (void)hipFree(p);
     if (e->h_st) (void)hipHostFree(e->h_st);
@@ -2278,15 +2531,12 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         size_t fr = 0, tot = 0;
         (void)hipMemGetInfo(&fr, &tot);
         e->mem_budget = fr / 2;
-        if (e->kind == FWA_SESSION) {            // per-key in-flight session lists
-            e->sstride = (cap + 1) * kMaxSess;
+        if (e->kind == FWA_SESSION) {            // flat in-flight session lists
             e->kid_bits = 1;
             while (((int64_t)1 << e->kid_bits) < cap + 1) ++e->kid_bits;
-            if (hipMalloc(&e->d_scnt, sizeof(int32_t) * (cap + 1)) != hipSuccess) { rc = FWA_E_OOM; break; }
-            if (hipMalloc(&e->d_sstart, 8 * e->sstride) != hipSuccess) { rc = FWA_E_OOM; break; }
-            if (hipMalloc(&e->d_send, 8 * e->sstride) != hipSuccess) { rc = FWA_E_OOM; break; }
-            if (hipMalloc(&e->d_sacc, 8 * e->sstride * e->nacc) != hipSuccess) { rc = FWA_E_OOM; break; }
-            if (hipMemsetAsync(e->d_scnt, 0, sizeof(int32_t) * (cap + 1), e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+            if (hipMalloc(&e->d_kflag, (size_t)cap + 1) != hipSuccess) { rc = FWA_E_OOM; break; }
+            if (hipMalloc(&e->d_sctr, sizeof(SessCtr)) != hipSuccess) { rc = FWA_E_OOM; break; }
+            if (hipHostMalloc(&e->h_sctr, sizeof(SessCtr)) != hipSuccess) { rc = FWA_E_OOM; break; }
         } else {
             if ((rc = grow_slots(e, 4))) break;
             if ((rc = publish_dir(e))) break;
@@ -2300,7 +2550,7 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
 
 static int stage_inputs(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* cols,
                         const int32_t* kh, int64_t n, IngestArgs& a) {
-    size_t need = (size_t)n * 16 + (kh ? (size_t)n * 4 : 0) + 4096;
+    size_t need = (size_t)n * 24 + (kh ? (size_t)n * 4 : 0) + 4096;   // + a session gap column
     for (int j = 0; j < e->cfg.num_aggs; ++j) need += (size_t)n * 8 + 256;
     if (need > e->d_in_bytes) {
         if (e->d_in) HIPCHK(e, hipFree(e->d_in));
@@ -2325,6 +2575,10 @@ static int stage_inputs(fwa_engine* e, const int64_t* keys, const int64_t* ts, c
         if (s.kind == FWA_COUNT || a.cols[s.col]) continue;
         if (!cols || !cols[s.col]) return fail(e, FWA_E_ARG, "missing value column");
         a.cols[s.col] = put(cols[s.col], (size_t)n * type_size(s.kind));
+    }
+    if ((e->cfg.flags & FWA_CFG_DYNAMIC_GAP) && !a.cols[e->cfg.gap_col]) {
+        if (!cols || !cols[e->cfg.gap_col]) return fail(e, FWA_E_ARG, "missing session gap column");
+        a.cols[e->cfg.gap_col] = put(cols[e->cfg.gap_col], (size_t)n * 8);
     }
     HIPCHK(e, err);
     return FWA_OK;
@@ -2551,75 +2805,276 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     return FWA_OK;
 }
 
-// Sessions: key lookup, stable radix sort of the batch by kid (arrival order kept inside a key),
-// then one sequential MergingWindowSet walk per key (sess_process_kernel).
+// Sessions: classify -> route -> bulk gap-scan (sort by (kid, start), segmented max-scan,
+// cluster ids, wave-segmented reduction) and the arrival-order walk for keys with order-sensitive records.
+struct KidEq {                       // equal kid part of a (kid << tb | start - base) sort key
+    int tb;
+    __host__ __device__ bool operator()(unsigned long long x, unsigned long long y) const { return (x >> tb) == (y >> tb); }
+};
+struct MaxI64 {
+    __host__ __device__ int64_t operator()(int64_t x, int64_t y) const { return x > y ? x : y; }
+};
+
+static int ensure_sort_tmp(fwa_engine* e, size_t bytes) {
+    if (bytes <= e->sort_tmp_bytes) return FWA_OK;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->d_sort_tmp) HIPCHK(e, hipFree(e->d_sort_tmp));
+    e->d_sort_tmp = nullptr;
+    HIPCHK(e, hipMalloc(&e->d_sort_tmp, bytes + bytes / 4));
+    e->sort_tmp_bytes = bytes + bytes / 4;
+    return FWA_OK;
+}
+
+static int ensure_sess_lists(fwa_engine* e, int64_t need) {
+    if (need <= e->ss_cap) return FWA_OK;
+    const int64_t cap = std::max<int64_t>(need + need / 4, 1 << 12);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    for (int q = 0; q < 2; ++q) {
+        SessList nl;
+        nl.stride = cap;
+        HIPCHK(e, hipMalloc(&nl.kid, 4 * (size_t)cap));
+        HIPCHK(e, hipMalloc(&nl.start, 8 * (size_t)cap));
+        HIPCHK(e, hipMalloc(&nl.end, 8 * (size_t)cap));
+        HIPCHK(e, hipMalloc(&nl.acc, 8 * (size_t)cap * e->nacc));
+        SessList& ol = e->ss[q];
+        if (q == e->ss_cur && e->n_ss > 0) {             // keep the live sessions
+            const size_t n = (size_t)e->n_ss;
+            HIPCHK(e, hipMemcpy(nl.kid, ol.kid, 4 * n, hipMemcpyDeviceToDevice));
+            HIPCHK(e, hipMemcpy(nl.start, ol.start, 8 * n, hipMemcpyDeviceToDevice));
+            HIPCHK(e, hipMemcpy(nl.end, ol.end, 8 * n, hipMemcpyDeviceToDevice));
+            for (int cc = 0; cc < e->nacc; ++cc)
+                HIPCHK(e, hipMemcpy(nl.acc + (size_t)cc * cap, ol.acc + (size_t)cc * ol.stride, 8 * n, hipMemcpyDeviceToDevice));
+        }
+        for (void* p : {(void*)ol.kid, (void*)ol.start, (void*)ol.end, (void*)ol.acc}) if (p) HIPCHK(e, hipFree(p));
+        ol = nl;
+    }
+    e->ss_cap = cap;
+    return FWA_OK;
+}
+
+static int ensure_late_rows(fwa_engine* e, int64_t need);
+static int emit_late_rows(fwa_engine* e);
+
+static int read_sess_ctr(fwa_engine* e) {
+    HIPCHK(e, hipMemcpyAsync(e->h_sctr, e->d_sctr, sizeof(SessCtr), hipMemcpyDeviceToHost, e->stream));
+    return sync_status(e);
+}
+
 static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     const int64_t n = a.n;
-    if (n > e->sess_sort_cap) {
-        if (e->d_sess_sort) HIPCHK(e, hipFree(e->d_sess_sort));
-        e->d_sess_sort = nullptr;
-        const int64_t cap = std::max<int64_t>(n, 1 << 16);
-        HIPCHK(e, hipMalloc(&e->d_sess_sort, sizeof(uint32_t) * 4 * cap));
-        e->sess_sort_cap = cap;
-        size_t bytes = 0;
-        HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap, 0,
-                                                     e->kid_bits, e->stream));
-        if (bytes > e->sort_tmp_bytes) {
-            if (e->d_sort_tmp) HIPCHK(e, hipFree(e->d_sort_tmp));
-            e->d_sort_tmp = nullptr;
-            HIPCHK(e, hipMalloc(&e->d_sort_tmp, bytes));
-            e->sort_tmp_bytes = bytes;
+    const int64_t n_in = e->n_ss;
+    int rc = FWA_OK;
+    if (n + n_in > e->sb_cap) {                           // sort / scan buffers for every element of the push
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        const int64_t cap = std::max<int64_t>((n + n_in) + (n + n_in) / 4, 1 << 14);
+        auto re = [&](void** p, size_t elem) -> int {
+            if (*p) HIPCHK(e, hipFree(*p));
+            *p = nullptr;
+            HIPCHK(e, hipMalloc(p, elem * (size_t)cap));
+            return FWA_OK;
+        };
+        for (int q = 0; q < 4; ++q) {
+            if ((rc = re((void**)&e->d_skey[q], 8))) return rc;
+            if ((rc = re((void**)&e->d_sval[q], 4))) return rc;
         }
+        if ((rc = re((void**)&e->d_send2, 8)) || (rc = re((void**)&e->d_smax, 8)) || (rc = re((void**)&e->d_scid, 4)) ||
+            (rc = re((void**)&e->d_rkid, 4)))
+            return rc;
+        e->sb_cap = cap;
     }
-    uint32_t* kid = e->d_sess_sort;
-    uint32_t* idx = kid + e->sess_sort_cap;
-    uint32_t* skid = idx + e->sess_sort_cap;
-    uint32_t* sidx = skid + e->sess_sort_cap;
-    SessArgs s;
+    if ((rc = ensure_sess_lists(e, n_in + n))) return rc;
+    SessCtr z;
+    memset(&z, 0, sizeof(z));
+    z.ts_min = ~0ull;
+    if ((rc = upload(e, e->d_sctr, &z, sizeof(z)))) return rc;
+    HIPCHK(e, hipMemsetAsync(e->d_kflag, 0, (size_t)e->capacity + 1, e->stream));
+    if ((rc = reset_push_status(e))) return rc;
+
+    Sess2Args s;
     memset(&s, 0, sizeof(s));
     s.keys = a.keys;
     s.ts = a.ts;
     for (int c = 0; c < FWA_MAX_COLS; ++c) s.cols[c] = a.cols[c];
     s.key_hash = a.key_hash;
+    s.gapc = (e->cfg.flags & FWA_CFG_DYNAMIC_GAP) ? (const int64_t*)a.cols[e->cfg.gap_col] : nullptr;
     s.n = n;
     s.wm = e->wm;
     s.gap = e->cfg.gap_ms;
+    s.lateness = e->lateness;
     s.key_table = e->d_keys;
     s.key_mask = (uint64_t)e->capacity - 1;
     s.seg_log = e->seg_log;
     s.part_bits = e->part_bits;
-    s.kid = kid;
-    s.idx = idx;
-    s.skid = skid;
-    s.sidx = sidx;
-    s.s_cnt = e->d_scnt;
-    s.s_start = e->d_sstart;
-    s.s_end = e->d_send;
-    s.s_acc = e->d_sacc;
-    s.sstride = e->sstride;
+    s.capacity = e->capacity;
+    s.rkid = e->d_rkid;
+    s.kflag = e->d_kflag;
+    s.in = e->ss[e->ss_cur];
+    s.n_in = n_in;
+    s.out = e->ss[e->ss_cur ^ 1];
+    for (int cc = 0; cc <= FWA_MAX_AGGS; ++cc) s.col_owner[cc] = -1;
+    for (int j = 0; j < e->cfg.num_aggs; ++j)
+        if (e->ec.agg[j].acc > 0 && !e->ec.agg[j].alias) s.col_owner[e->ec.agg[j].acc] = j;
+    s.ctr = e->d_sctr;
     s.st = e->d_st;
-    int rc = reset_push_status(e);
-    if (rc) return rc;
     HIPCHK(e, hipEventRecord(e->ev[0], e->stream));
-    sess_key_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(s, e->d_ec);
+    if (n > 0) sess2_classify_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(s, e->d_ec);
+    if (n_in > 0) sess2_range_kernel<<<grid_for(n_in, 256 * 32), kBlock, 0, e->stream>>>(s);
     HIPCHK(e, hipGetLastError());
-    rc = sync_status(e);
-    if (rc) return rc;
-    if (e->h_st->error) return FWA_OK;               // reported by the caller
-    size_t bytes = e->sort_tmp_bytes;
-    HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(e->d_sort_tmp, bytes, (const uint32_t*)kid, skid, (const uint32_t*)idx,
-                                                 sidx, (int)n, 0, e->kid_bits, e->stream));
-    sess_process_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(s, e->d_ec);
+    if ((rc = read_sess_ctr(e))) return rc;
+    if (e->h_st->error) return FWA_OK;                    // reported by the caller
+    const SessCtr c1 = *e->h_sctr;
+    if (n + n_in == 0 || c1.ts_min > c1.ts_max) {         // nothing to do (empty push, no sessions)
+        *dropped_out = 0;
+        return FWA_OK;
+    }
+    const int64_t lo = jm::unord_i64(c1.ts_min), hi = jm::unord_i64(c1.ts_max);
+    const uint64_t span = (uint64_t)hi - (uint64_t)lo;
+    int tb = 0;
+    while (tb < 64 && (span >> tb) != 0) ++tb;
+    s.base = lo;
+    s.tb = tb;
+    s.all_sp = e->kid_bits + tb > 64 ? 1 : 0;                // start range too wide for one sort key
+    if (s.all_sp) s.tb = 0;
+    s.bkey = e->d_skey[0];
+    s.bval = e->d_sval[0];
+    s.skey = e->d_skey[2];
+    s.sval = e->d_sval[2];
+    sess2_route_kernel<<<grid_for(n + n_in, 256 * 32), kBlock, 0, e->stream>>>(s);
     HIPCHK(e, hipGetLastError());
+    if ((rc = read_sess_ctr(e))) return rc;
+    const int64_t nb = (int64_t)e->h_sctr->n_bulk, nsp = (int64_t)e->h_sctr->n_sp;
+    s.nb = nb;
+    s.nsp = nsp;
+    s.bend = e->d_send2;
+    s.bmax = e->d_smax;
+    s.bcid = e->d_scid;
+    if (nb > 0) {
+        size_t bytes = 0;
+        HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned long long*)e->d_skey[0], e->d_skey[1],
+                                                     (const uint32_t*)e->d_sval[0], e->d_sval[1], (int)nb, 0, e->kid_bits + tb, e->stream));
+        if ((rc = ensure_sort_tmp(e, bytes))) return rc;
+        bytes = e->sort_tmp_bytes;
+        HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(e->d_sort_tmp, bytes, (const unsigned long long*)e->d_skey[0], e->d_skey[1],
+                                                     (const uint32_t*)e->d_sval[0], e->d_sval[1], (int)nb, 0, e->kid_bits + tb, e->stream));
+        s.bkey = e->d_skey[1];
+        s.bval = e->d_sval[1];
+        sess2_ends_kernel<<<grid_for(nb, 256 * 32), kBlock, 0, e->stream>>>(s);
+        HIPCHK(e, hipGetLastError());
+        KidEq eq{tb};
+        bytes = 0;
+        HIPCHK(e, hipcub::DeviceScan::InclusiveScanByKey(nullptr, bytes, (const unsigned long long*)s.bkey, (const int64_t*)s.bend,
+                                                         s.bmax, MaxI64(), (int)nb, eq, e->stream));
+        if ((rc = ensure_sort_tmp(e, bytes))) return rc;
+        bytes = e->sort_tmp_bytes;
+        HIPCHK(e, hipcub::DeviceScan::InclusiveScanByKey(e->d_sort_tmp, bytes, (const unsigned long long*)s.bkey, (const int64_t*)s.bend,
+                                                         s.bmax, MaxI64(), (int)nb, eq, e->stream));
+        Sess2Args h = s;
+        h.bcid = e->d_sval[0];                               // head flags (the unsorted payload is dead)
+        sess2_heads_kernel<<<grid_for(nb, 256 * 32), kBlock, 0, e->stream>>>(h);
+        HIPCHK(e, hipGetLastError());
+        bytes = 0;
+        HIPCHK(e, hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const uint32_t*)h.bcid, s.bcid, (int)nb, e->stream));
+        if ((rc = ensure_sort_tmp(e, bytes))) return rc;
+        bytes = e->sort_tmp_bytes;
+        HIPCHK(e, hipcub::DeviceScan::InclusiveSum(e->d_sort_tmp, bytes, (const uint32_t*)h.bcid, s.bcid, (int)nb, e->stream));
+        sess2_init_kernel<<<grid_for(nb, 256 * 32), kBlock, 0, e->stream>>>(s, e->d_ec);
+        sess2_reduce_kernel<<<grid_for(nb, 256 * 32), kBlock, 0, e->stream>>>(s, e->d_ec);
+        HIPCHK(e, hipGetLastError());
+    }
+    if (nsp > 0) {
+        if (nsp > e->sc_cap) {
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            if (e->d_sc) HIPCHK(e, hipFree(e->d_sc));
+            e->d_sc = nullptr;
+            e->sc_cap = nsp + nsp / 4 + 1024;
+            HIPCHK(e, hipMalloc(&e->d_sc, 8 * (size_t)e->sc_cap * (2 + e->nacc)));
+        }
+        size_t bytes = 0;
+        const int eb = std::min(64, 32 + e->kid_bits);
+        HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned long long*)e->d_skey[2], e->d_skey[3],
+                                                     (const uint32_t*)e->d_sval[2], e->d_sval[3], (int)nsp, 0, eb, e->stream));
+        if ((rc = ensure_sort_tmp(e, bytes))) return rc;
+        bytes = e->sort_tmp_bytes;
+        HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(e->d_sort_tmp, bytes, (const unsigned long long*)e->d_skey[2], e->d_skey[3],
+                                                     (const uint32_t*)e->d_sval[2], e->d_sval[3], (int)nsp, 0, eb, e->stream));
+        s.skey = e->d_skey[3];
+        s.sval = e->d_sval[3];
+        s.sc_start = e->d_sc;
+        s.sc_end = e->d_sc + nsp;
+        s.sc_acc = (unsigned long long*)(e->d_sc + 2 * nsp);
+        if ((rc = ensure_late_rows(e, e->late_rows + nsp))) return rc;
+        if (!e->d_lr_n) HIPCHK(e, hipMalloc(&e->d_lr_n, 8));
+        if ((rc = upload(e, e->d_lr_n, &e->late_rows, 8))) return rc;
+        s.lr_key = e->lr_col[0];
+        s.lr_start = e->lr_col[1];
+        s.lr_end = e->lr_col[2];
+        for (int j = 0; j < e->cfg.num_aggs; ++j) s.lr_agg[j] = e->lr_col[3 + j];
+        s.lr_n = e->d_lr_n;
+        s.lr_cap = e->lr_cap;
+        sess2_ordered_kernel<<<grid_for(nsp, 256 * 32), kBlock, 0, e->stream>>>(s, e->d_ec);
+        HIPCHK(e, hipGetLastError());
+    }
     HIPCHK(e, hipEventRecord(e->ev[1], e->stream));
-    rc = sync_status(e);
-    if (rc) return rc;
-    rc = account_ingest(e);
-    if (rc) return rc;
+    uint32_t ncl = 0;
+    unsigned long long lrn = (unsigned long long)e->late_rows;
+    if (nb > 0) HIPCHK(e, hipMemcpyAsync(&ncl, e->d_scid + nb - 1, 4, hipMemcpyDeviceToHost, e->stream));
+    if (nsp > 0) HIPCHK(e, hipMemcpyAsync(&lrn, e->d_lr_n, 8, hipMemcpyDeviceToHost, e->stream));
+    if ((rc = read_sess_ctr(e))) return rc;
+    if ((rc = account_ingest(e))) return rc;
     e->ingest_launches++;
     e->ingest_records += n;
+    if (e->h_st->error) return FWA_OK;
+    e->late_rows = (int64_t)lrn;
+    e->n_ss = (int64_t)ncl + (int64_t)e->h_sctr->n_out_sp;
+    e->ss_cur ^= 1;
     *dropped_out = (int64_t)e->h_st->dropped;
+    return FWA_OK;
+}
+
+// Watermark advance for sessions: late-firing rows of the pushes since the last call first, then every
+// session with prev < end - 1 <= wm; sessions past cleanup are dropped from the list.
+static int fire_sessions(fwa_engine* e, int64_t wm, int64_t* nrows) {
+    const int64_t n_in = e->n_ss;
+    int rc = ensure_out(e, e->late_rows + n_in);
+    if (rc) return rc;
+    if (e->late_rows > 0 && (rc = emit_late_rows(e))) return rc;
+    if ((rc = upload(e, &e->d_st->rows, &e->late_rows, 8))) return rc;
+    SessCtr z;
+    memset(&z, 0, sizeof(z));
+    if ((rc = upload(e, e->d_sctr, &z, sizeof(z)))) return rc;
+    if ((rc = ensure_sess_lists(e, n_in))) return rc;
+    Sess2FireArgs f;
+    memset(&f, 0, sizeof(f));
+    f.in = e->ss[e->ss_cur];
+    f.out = e->ss[e->ss_cur ^ 1];
+    f.n_in = n_in;
+    f.prev_wm = e->wm;
+    f.wm = wm;
+    f.lateness = e->lateness;
+    f.key_table = e->d_keys;
+    f.capacity = e->capacity;
+    f.o_key = e->o_key;
+    f.o_start = e->o_start;
+    f.o_end = e->o_end;
+    for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
+    f.out_cap = e->out_cap;
+    f.ctr = e->d_sctr;
+    f.st = e->d_st;
+    HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
+    if (n_in > 0) sess2_fire_kernel<<<grid_for(n_in, 256 * 16), kBlock, 0, e->stream>>>(f, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
+    if ((rc = read_sess_ctr(e))) return rc;
+    if (e->h_st->error) return fail(e, e->h_st->error, "session fire failed");
+    *nrows = (int64_t)e->h_st->rows;
+    e->n_ss = (int64_t)e->h_sctr->n_keep;
+    e->ss_cur ^= 1;
+    e->late_rows = 0;
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+    e->fire_ms += ms;
+    e->fire_launches++;
+    e->fire_rows += *nrows;
     return FWA_OK;
 }
 
@@ -2707,6 +3162,24 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     return FWA_OK;
 }
 
+// Capacity of the late-firing row buffer (rows returned by the next fwa_advance_watermark); keeps its rows.
+static int ensure_late_rows(fwa_engine* e, int64_t need) {
+    if (need <= e->lr_cap) return FWA_OK;
+    const int64_t cap = std::max<int64_t>(need * 2, 1024);
+    for (int c = 0; c < 3 + e->cfg.num_aggs; ++c) {
+        int64_t* p = nullptr;
+        HIPCHK(e, hipMalloc(&p, 8 * (size_t)cap));
+        if (e->lr_col[c]) {
+            if (e->late_rows) HIPCHK(e, hipMemcpyAsync(p, e->lr_col[c], 8 * (size_t)e->late_rows, hipMemcpyDeviceToDevice, e->stream));
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            HIPCHK(e, hipFree(e->lr_col[c]));
+        }
+        e->lr_col[c] = p;
+    }
+    e->lr_cap = cap;
+    return FWA_OK;
+}
+
 // Late firings of one push (DataStream, allowed lateness > 0): apply the deferred records in arrival order
 // and emit the fired windows' contents into the late-row buffer (late_fire_kernel). The rows are returned
 // by the next fwa_advance_watermark, ahead of the windows that watermark fires.
@@ -2716,22 +3189,8 @@ static int process_late(fwa_engine* e, const IngestArgs& a0, std::vector<int32_t
     if (n > e->spill_cap) return fail(e, FWA_E_STATE, "late list overflow");
     HIPCHK(e, hipMemcpyAsync(e->d_late, idx.data(), 4 * (size_t)n, hipMemcpyHostToDevice, e->stream));
     const int64_t per = e->kind == FWA_SLIDE ? (e->size + e->slide - 1) / e->slide : 1;
-    const int64_t need = e->late_rows + n * per;
-    const int ncol = 3 + e->cfg.num_aggs;
-    if (need > e->lr_cap) {
-        const int64_t cap = std::max<int64_t>(need * 2, 1024);
-        for (int c = 0; c < ncol; ++c) {
-            int64_t* p = nullptr;
-            HIPCHK(e, hipMalloc(&p, 8 * (size_t)cap));
-            if (e->lr_col[c]) {
-                if (e->late_rows) HIPCHK(e, hipMemcpyAsync(p, e->lr_col[c], 8 * (size_t)e->late_rows, hipMemcpyDeviceToDevice, e->stream));
-                HIPCHK(e, hipStreamSynchronize(e->stream));
-                HIPCHK(e, hipFree(e->lr_col[c]));
-            }
-            e->lr_col[c] = p;
-        }
-        e->lr_cap = cap;
-    }
+    int rc0 = ensure_late_rows(e, e->late_rows + n * per);
+    if (rc0) return rc0;
     if (!e->d_lr_n) HIPCHK(e, hipMalloc(&e->d_lr_n, 8));
     HIPCHK(e, hipMemcpyAsync(e->d_lr_n, &e->late_rows, 8, hipMemcpyHostToDevice, e->stream));
     LateArgs L;
@@ -2929,6 +3388,10 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
             if (!val_cols || !val_cols[s.col]) return fail(e, FWA_E_ARG, "missing value column");
             a.cols[s.col] = val_cols[s.col];
         }
+        if (e->cfg.flags & FWA_CFG_DYNAMIC_GAP) {
+            if (!val_cols || !val_cols[e->cfg.gap_col]) return fail(e, FWA_E_ARG, "missing session gap column");
+            a.cols[e->cfg.gap_col] = val_cols[e->cfg.gap_col];
+        }
     } else {
         int rc = stage_inputs(e, keys, ts, val_cols, key_hash, n, a);
         if (rc) return rc;
@@ -2950,8 +3413,10 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
             const int err = e->h_st->error;
             return fail(e, err, err == FWA_E_KEYGROUP ? "Key group is not in the owned KeyGroupRange (StateTable.getMapForKeyGroup)"
                               : err == FWA_E_TS_MIN ? "Record has Long.MIN_VALUE timestamp (= no timestamp marker)."
-                              : (e->h_st->key_full & 8) ? "more than 16 in-flight sessions for one key"
-                                                         : "key table full: raise fwa_config.key_capacity");
+                              : err == FWA_E_MERGE_LATE ? "The end timestamp of an event-time window cannot become earlier than the current watermark by merging."
+                              : err == FWA_E_STATE ? "session state inconsistency"
+                              : err == FWA_E_ARG ? "Dynamic session time gap must satisfy 0 < gap"
+                                                   : "key table full: raise fwa_config.key_capacity");
         }
         e->records_in += n;
         e->late_dropped += dropped;
@@ -3370,41 +3835,8 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
     if (int rc0 = settle_pending(e)) return rc0;
     if (out) memset(out, 0, sizeof(*out));
     if (wm > e->wm && e->kind == FWA_SESSION) {
-        int rc = sync_status(e);
+        int rc = fire_sessions(e, wm, &nrows);
         if (rc) return rc;
-        const int64_t live = (int64_t)e->h_st->sess_live;
-        if (live > 0) {
-            rc = ensure_out(e, live);
-            if (rc) return rc;
-            HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
-            SessFireArgs f;
-            memset(&f, 0, sizeof(f));
-            f.key_table = e->d_keys;
-            f.capacity = e->capacity;
-            f.wm = wm;
-            f.s_cnt = e->d_scnt;
-            f.s_start = e->d_sstart;
-            f.s_end = e->d_send;
-            f.s_acc = e->d_sacc;
-            f.sstride = e->sstride;
-            f.o_key = e->o_key;
-            f.o_start = e->o_start;
-            f.o_end = e->o_end;
-            for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
-            f.st = e->d_st;
-            HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
-            sess_fire_kernel<<<grid_for(e->capacity + 1, 256 * 16), kBlock, 0, e->stream>>>(f, e->d_ec);
-            HIPCHK(e, hipGetLastError());
-            HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
-            rc = sync_status(e);
-            if (rc) return rc;
-            nrows = (int64_t)e->h_st->rows;
-            float ms = 0.f;
-            HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
-            e->fire_ms += ms;
-            e->fire_launches++;
-            e->fire_rows += nrows;
-        }
         e->wm = wm;
     } else if (wm > e->wm) {
         const int64_t prev = e->wm;
@@ -3508,7 +3940,7 @@ int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
     s->late_dropped = e->late_dropped;
     s->rows_out = e->rows_out;
     s->live_keys = (int64_t)e->h_st->n_keys;
-    s->live_slices = e->kind == FWA_SESSION ? (int64_t)e->h_st->sess_live : (int64_t)e->live.size();
+    s->live_slices = e->kind == FWA_SESSION ? e->n_ss : (int64_t)e->live.size();
     s->current_watermark = e->wm;
     s->ingest_launches = e->ingest_launches;
     s->ingest_ms = e->ingest_ms;

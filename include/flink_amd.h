@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define FWA_ABI_VERSION 1
+#define FWA_ABI_VERSION 2
 #define FWA_MAX_AGGS 8
 #define FWA_MAX_COLS 8
 
@@ -131,7 +131,20 @@ typedef struct fwa_config {
     int32_t output_on_device;    /* 1: fwa_out points into HBM; 0: engine copies rows to host */
     int64_t key_capacity;        /* sizing hint: max distinct live keys (0 = default 1<<20) */
     int64_t max_batch;           /* sizing hint: max records per fwa_push (0 = default 1<<26) */
+    /* ABI 2 */
+    int32_t flags;               /* FWA_CFG_* */
+    int32_t gap_col;             /* FWA_CFG_DYNAMIC_GAP: value column holding each record's session gap (int64 ms) */
+    int32_t tz_n;                /* shift time zone of a Table TIMESTAMP_LTZ rowtime: number of (instant, offset)
+                                    pairs in tz; 0 = UTC (TimeWindowUtil.toUtcTimestampMills :52-60) */
+    int32_t reserved;
+    const int64_t* tz;           /* [2 * tz_n]: from UTC instant tz[2i] (ms, ascending) on, the zone's offset is
+                                    tz[2i+1] ms (java.time ZoneRules transitions); copied by fwa_create */
 } fwa_config;
+
+/* fwa_config.flags */
+#define FWA_CFG_DYNAMIC_GAP 0x1  /* SESSION: per-record gap from value column gap_col -- DynamicEventTimeSessionWindows
+                                  * with a SessionWindowTimeGapExtractor (DynamicEventTimeSessionWindows.java:57-68);
+                                  * a gap <= 0 raises FWA_E_ARG like the assigner's IllegalArgumentException */
 
 typedef struct fwa_out {
     int64_t n_rows;

@@ -380,7 +380,7 @@ int or_create(const fwa_config* c, or_engine** out) {
         if (c->semantics == FWA_SEM_TABLE && c->size_ms % c->slide_ms != 0) return FWA_E_ARG;
     }
     if (c->window_kind == FWA_CUMULATE && (c->semantics != FWA_SEM_TABLE || c->size_ms <= 0 || c->slide_ms <= 0 || c->size_ms % c->slide_ms)) return FWA_E_ARG;
-    if (c->window_kind == FWA_SESSION && (c->gap_ms <= 0 || c->semantics != FWA_SEM_DATASTREAM)) return FWA_E_ARG;
+    if (c->window_kind == FWA_SESSION && c->gap_ms <= 0 && !(c->flags & FWA_CFG_DYNAMIC_GAP)) return FWA_E_ARG;
     if (c->semantics == FWA_SEM_TABLE && c->allowed_lateness_ms != 0) return FWA_E_ARG;
     or_engine* e = (or_engine*)calloc(1, sizeof(or_engine));
     e->c = *c;
@@ -481,7 +481,10 @@ static int tw_cmp(const void* a, const void* b) { const tw* x = (const tw*)a; co
 /* MergingWindowSet.addWindow :153-236 + TimeWindow.mergeWindows :208-254 + the MergeFunction of
  * WindowOperator.processElement :292-349, then the per-window body :352-386. */
 static int ds_process_element_session(or_engine* e, int64_t key, int64_t ts, const void* const* cols, int64_t i, int* skipped) {
-    const int64_t nws = ts, nwe = jladd(ts, e->c.gap_ms);      /* EventTimeSessionWindows.assignWindows */
+    /* EventTimeSessionWindows.assignWindows :61-63; DynamicEventTimeSessionWindows.assignWindows :57-68 */
+    const int64_t gap = (e->c.flags & FWA_CFG_DYNAMIC_GAP) ? ((const int64_t*)cols[e->c.gap_col])[i] : e->c.gap_ms;
+    if (gap <= 0) return set_err(e, FWA_E_ARG, "Dynamic session time gap must satisfy 0 < gap");
+    const int64_t nws = ts, nwe = jladd(ts, gap);
     int64_t cnt = 0;
     for (int64_t j = *wl_headp(e, key); j >= 0; j = e->wl_next[j]) cnt++;
     tw* ws = (tw*)malloc(sizeof(tw) * (cnt + 1));
@@ -680,16 +683,26 @@ int or_push(or_engine* e, const int64_t* keys, const int64_t* ts, const void* co
             return set_err(e, FWA_E_KEYGROUP, m);
         }
         e->st.records_in++;
+        if (e->c.window_kind == FWA_SESSION) {
+            /* DataStream EventTimeSessionWindows (no Long.MIN_VALUE check in its assignWindows :61-63) and the
+             * Table legacy GROUP BY SESSION (TR WindowOperator.processElement :331-378 over
+             * MergingWindowProcessFunction): the same MergingWindowSet walk and trigger */
+            int skipped = 1;
+            int rc = ds_process_element_session(e, keys[i], ts[i], cols, i, &skipped);
+            if (rc) return rc;
+            if (skipped) {
+                if (e->c.semantics == FWA_SEM_TABLE) dropped++;   /* TR WindowOperator.java:386-389: every dropped row */
+                else if (jladd(ts[i], e->c.allowed_lateness_ms) <= e->wm) dropped++;   /* isElementLate :597-601 */
+            }
+            continue;
+        }
         if (e->c.semantics == FWA_SEM_TABLE) {
             dropped += tb_process_element(e, keys[i], ts[i], cols, i);
             continue;
         }
         if (ts[i] == J_LONG_MIN) return set_err(e, FWA_E_TS_MIN, "Record has Long.MIN_VALUE timestamp (= no timestamp marker).");
         int skipped = 1;
-        if (e->c.window_kind == FWA_SESSION) {
-            int rc = ds_process_element_session(e, keys[i], ts[i], cols, i, &skipped);
-            if (rc) return rc;
-        } else {
+        {
             int nw = or_assign_windows(&e->c, ts[i], wsb, web, 4096);
             if (nw < 0) return set_err(e, nw, "window assignment failed");
             ds_process_element_aligned(e, keys[i], ts[i], cols, i, wsb, web, nw, &skipped);
@@ -707,7 +720,7 @@ int or_advance_watermark(or_engine* e, int64_t wm, fwa_out* out) {
         e->wm = wm;                                          /* InternalTimerServiceImpl.advanceWatermark :302-314 */
         timer_t_ t;
         while (th_pop_due(&e->timers, wm, &t)) {
-            if (e->c.semantics == FWA_SEM_TABLE) tb_fire(e, t.key, t.a);
+            if (e->c.semantics == FWA_SEM_TABLE && e->c.window_kind != FWA_SESSION) tb_fire(e, t.key, t.a);
             else ds_on_event_time(e, &t);
         }
         e->st.current_watermark = wm;

@@ -31,7 +31,7 @@ def kat_config(case, **kw):
                          size_ms=case["size_ms"], slide_ms=case["slide_ms"],
                          offset_ms=case["offset_ms"], gap_ms=case["gap_ms"],
                          allowed_lateness_ms=case["allowed_lateness_ms"],
-                         aggs=[tuple(a) for a in case["aggs"]], **kw)
+                         aggs=[tuple(a) for a in case["aggs"]], gap_col=case.get("gap_col"), **kw)
 
 
 def rows_to_tuples(rows, naggs):
@@ -55,12 +55,15 @@ def replay_kat(case, make_engine):
             k = np.array([p[0] for p in pend], np.int64)
             v = np.array([p[1] for p in pend], np.int64)
             t = np.array([p[2] for p in pend], np.int64)
-            dropped += eng.push(k, t, [v])
+            cols = [v]
+            if case.get("gap_col") is not None:          # per-record session gap (5th event field)
+                cols.append(np.array([p[3] for p in pend], np.int64))
+            dropped += eng.push(k, t, cols)
             pend = []
 
     for ev in case["events"]:
         if ev[0] == "e":
-            pend.append((ev[1], ev[2], ev[3]))
+            pend.append((ev[1], ev[2], ev[3], ev[4] if len(ev) > 4 else 0))
         else:
             flush()
             rows = eng.advance_watermark(ev[1])

@@ -51,6 +51,8 @@ CONFIGS = [
     dict(window_kind="CUMULATE", semantics="TABLE", size_ms=3000, slide_ms=1000),
     dict(window_kind="SESSION", semantics="DATASTREAM", gap_ms=700),
     dict(window_kind="SESSION", semantics="DATASTREAM", gap_ms=2500),
+    dict(window_kind="SESSION", semantics="DATASTREAM", gap_ms=700, allowed_lateness_ms=1200),
+    dict(window_kind="SESSION", semantics="TABLE", gap_ms=900),
 ]
 
 
