@@ -1426,37 +1426,64 @@ __device__ __forceinline__ unsigned long long wave_append(bool take, unsigned lo
     return b + (unsigned long long)__popcll(m & ((1ull << lane) - 1));
 }
 
-// Pass 2: route every record and in-flight session to the bulk sort or the arrival-order sort.
+// Pass 2: route every record and in-flight session to the bulk sort or the arrival-order sort. A block
+// owns a contiguous chunk of kRouteItems * blockDim elements and reserves its two output runs with one
+// atomic per list (a per-wave reservation on one counter serialised 1M waves per push: 12.8 ms on C5s).
+constexpr int kRouteItems = 16;
+__device__ __forceinline__ void route_elem(const Sess2Args& a, int64_t t, bool& valid, bool& sp, unsigned long long& bk,
+                                           unsigned long long& sk, uint32_t& pay) {
+    valid = false; sp = false; bk = 0; sk = 0; pay = 0;
+    if (t < a.n) {
+        const uint32_t kid = a.rkid[t];
+        if (kid == 0xffffffffu) return;
+        valid = true;
+        sp = a.all_sp || a.kflag[kid];
+        pay = (uint32_t)t;
+        bk = ((unsigned long long)kid << a.tb) | (uint64_t)(a.ts[t] - a.base);
+        sk = ((unsigned long long)kid << 32) | (uint64_t)(t + 1);
+    } else if (t < a.n + a.n_in) {
+        const int64_t j = t - a.n;
+        const uint32_t kid = a.in.kid[j];
+        valid = true;
+        sp = a.all_sp || a.kflag[kid];
+        pay = (uint32_t)j | 0x80000000u;
+        bk = ((unsigned long long)kid << a.tb) | (uint64_t)(a.in.start[j] - a.base);
+        sk = (unsigned long long)kid << 32;
+    }
+}
+
 __global__ void __launch_bounds__(kBlock) sess2_route_kernel(Sess2Args a) {
-    const int64_t total = a.n + a.n_in;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < total; t0 += stride) {   // uniform trip count per wave
-        const int64_t t = t0 + threadIdx.x;
-        bool valid = false, sp = false;
-        unsigned long long bk = 0, sk = 0;
-        uint32_t pay = 0;
-        if (t < a.n) {
-            const uint32_t kid = a.rkid[t];
-            if (kid != 0xffffffffu) {
-                valid = true;
-                sp = a.all_sp || a.kflag[kid];
-                pay = (uint32_t)t;
-                bk = ((unsigned long long)kid << a.tb) | (uint64_t)(a.ts[t] - a.base);
-                sk = ((unsigned long long)kid << 32) | (uint64_t)(t + 1);
-            }
-        } else if (t < total) {
-            const int64_t j = t - a.n;
-            const uint32_t kid = a.in.kid[j];
-            valid = true;
-            sp = a.all_sp || a.kflag[kid];
-            pay = (uint32_t)j | 0x80000000u;
-            bk = ((unsigned long long)kid << a.tb) | (uint64_t)(a.in.start[j] - a.base);
-            sk = (unsigned long long)kid << 32;
-        }
-        const unsigned long long pb = wave_append(valid && !sp, &a.ctr->n_bulk);
-        const unsigned long long ps = wave_append(valid && sp, &a.ctr->n_sp);
-        if (valid && !sp) { a.bkey[pb] = bk; a.bval[pb] = pay; }
-        if (valid && sp) { a.skey[ps] = sk; a.sval[ps] = pay; }
+    constexpr int kW = kBlock / 64;
+    __shared__ uint32_t s_wb[kW], s_ws[kW];
+    __shared__ unsigned long long s_base[2];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t c0 = (int64_t)blockIdx.x * kBlock * kRouteItems;
+    uint32_t nbk = 0, nsp = 0;
+    for (int j = 0; j < kRouteItems; ++j) {
+        bool valid, sp; unsigned long long bk, sk; uint32_t pay;
+        route_elem(a, c0 + (int64_t)j * kBlock + threadIdx.x, valid, sp, bk, sk, pay);
+        nbk += (uint32_t)__popcll(__ballot(valid && !sp));
+        nsp += (uint32_t)__popcll(__ballot(valid && sp));
+    }
+    if (lane == 0) { s_wb[wv] = nbk; s_ws[wv] = nsp; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tb = 0, ts = 0;
+        for (int w = 0; w < kW; ++w) { const uint32_t x = s_wb[w], y = s_ws[w]; s_wb[w] = tb; s_ws[w] = ts; tb += x; ts += y; }
+        s_base[0] = tb ? atomicAdd(&a.ctr->n_bulk, (unsigned long long)tb) : 0ull;
+        s_base[1] = ts ? atomicAdd(&a.ctr->n_sp, (unsigned long long)ts) : 0ull;
+    }
+    __syncthreads();
+    unsigned long long pb = s_base[0] + s_wb[wv], ps = s_base[1] + s_ws[wv];
+    const unsigned long long lt = (1ull << lane) - 1;
+    for (int j = 0; j < kRouteItems; ++j) {
+        bool valid, sp; unsigned long long bk, sk; uint32_t pay;
+        route_elem(a, c0 + (int64_t)j * kBlock + threadIdx.x, valid, sp, bk, sk, pay);
+        const unsigned long long mb = __ballot(valid && !sp), ms = __ballot(valid && sp);
+        if (valid && !sp) { const unsigned long long o = pb + __popcll(mb & lt); a.bkey[o] = bk; a.bval[o] = pay; }
+        if (valid && sp) { const unsigned long long o = ps + __popcll(ms & lt); a.skey[o] = sk; a.sval[o] = pay; }
+        pb += __popcll(mb);
+        ps += __popcll(ms);
     }
 }
 
@@ -2939,7 +2966,8 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     s.bval = e->d_sval[0];
     s.skey = e->d_skey[2];
     s.sval = e->d_sval[2];
-    sess2_route_kernel<<<grid_for(n + n_in, 256 * 32), kBlock, 0, e->stream>>>(s);
+    sess2_route_kernel<<<(unsigned)((n + n_in + (int64_t)kBlock * kRouteItems - 1) / ((int64_t)kBlock * kRouteItems)), kBlock, 0,
+                         e->stream>>>(s);
     HIPCHK(e, hipGetLastError());
     if ((rc = read_sess_ctr(e))) return rc;
     const int64_t nb = (int64_t)e->h_sctr->n_bulk, nsp = (int64_t)e->h_sctr->n_sp;
