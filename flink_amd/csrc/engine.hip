@@ -3625,15 +3625,135 @@ static void snap_header(const fwa_engine* e, int64_t* h, int64_t n) {
     h[23] = e->cfg.kg_end;
 }
 
+// Sessions: the blob's entries are the in-flight sessions (key, start, count, acc_j..., end) bucketed by
+// key group -- the per-key MergingWindowSet mapping plus the window state of WindowOperator
+// (WindowOperator.java:224-238 mergingSetsState / windowState), with the session end as a last column.
+static int snapshot_sessions(fwa_engine* e, fwa_blob* out) {
+    const int64_t n = e->n_ss;
+    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, ncols = 4 + na;
+    const SessList& L = e->ss[e->ss_cur];
+    std::vector<uint32_t> kid((size_t)n);
+    std::vector<int64_t> st((size_t)n), en((size_t)n), acc((size_t)n * e->nacc);
+    std::vector<unsigned long long> table((size_t)e->capacity + 1);
+    if (n > 0) {
+        HIPCHK(e, hipMemcpy(kid.data(), L.kid, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        HIPCHK(e, hipMemcpy(st.data(), L.start, 8 * (size_t)n, hipMemcpyDeviceToHost));
+        HIPCHK(e, hipMemcpy(en.data(), L.end, 8 * (size_t)n, hipMemcpyDeviceToHost));
+        for (int cc = 0; cc < e->nacc; ++cc)
+            HIPCHK(e, hipMemcpy(acc.data() + (size_t)cc * n, L.acc + (size_t)cc * L.stride, 8 * (size_t)n, hipMemcpyDeviceToHost));
+        HIPCHK(e, hipMemcpy(table.data(), e->d_keys, 8 * (size_t)e->capacity, hipMemcpyDeviceToHost));
+    }
+    std::vector<int32_t> kg((size_t)n);
+    std::vector<int64_t> off((size_t)maxp + 1, 0), key((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        key[i] = (int64_t)kid[i] < e->capacity ? (int64_t)table[kid[i]] : LONG_MIN_J;
+        kg[i] = jm::key_group(jm::key_hash(key[i], e->cfg.key_kind, 0), maxp);
+        off[kg[i] + 1]++;
+    }
+    for (int g = 0; g < maxp; ++g) off[g + 1] += off[g];
+    const size_t words = kSnapHdr + (size_t)maxp + 1 + (size_t)n * ncols;
+    int64_t* b = (int64_t*)malloc(words * 8);
+    if (!b) return fail(e, FWA_E_OOM, "snapshot blob allocation failed");
+    snap_header(e, b, n);
+    memcpy(b + kSnapHdr, off.data(), 8 * ((size_t)maxp + 1));
+    int64_t* body = b + kSnapHdr + maxp + 1;
+    std::vector<int64_t> cur(off.begin(), off.end() - 1);
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t d = cur[kg[i]]++;
+        body[d] = key[i];
+        body[(size_t)n + d] = st[i];
+        body[(size_t)2 * n + d] = acc[i];                                  // COUNT(*)
+        for (int j = 0; j < na; ++j) {
+            const AggDesc& ad = e->ec.agg[j];
+            body[(size_t)(3 + j) * n + d] = ad.acc > 0 ? acc[(size_t)ad.acc * n + i] : acc[i];
+        }
+        body[(size_t)(3 + na) * n + d] = en[i];
+    }
+    out->data = b;
+    out->size = (int64_t)(words * 8);
+    return FWA_OK;
+}
+
+__global__ void __launch_bounds__(kBlock) sess2_restore_kernel(Sess2Args a, const int64_t* keys, const int64_t* start,
+                                                               const int64_t* end, const int64_t* const* accs, int64_t m,
+                                                               int64_t at, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t kid = key_slot(a.key_table, a.key_mask, a.seg_log, a.part_bits, keys[i], a.st);
+        if (kid < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
+        const int64_t o = at + i;
+        a.out.kid[o] = (uint32_t)kid;
+        a.out.start[o] = start[i];
+        a.out.end[o] = end[i];
+        for (int cc = 0; cc < c.nacc; ++cc) a.out.acc[(int64_t)cc * a.out.stride + o] = (unsigned long long)accs[cc][i];
+    }
+}
+
+// Restore sessions: the owned key groups' entries of every blob are appended to the in-flight list
+// (a key lives in one subtask's snapshot, so the lists never overlap); watermark = MIN over the blobs.
+static int restore_sessions(fwa_engine* e, const void* const* blobs, int32_t n_blobs) {
+    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism;
+    int64_t wm = LONG_MAX_J;
+    for (int32_t b = 0; b < n_blobs; ++b) {
+        const int64_t* h = (const int64_t*)blobs[b];
+        const int64_t n = h[21];
+        wm = std::min<int64_t>(wm, h[20]);
+        const int64_t* off = h + kSnapHdr;
+        const int64_t lo = off[e->cfg.kg_start], hi = off[e->cfg.kg_end + 1];
+        if (lo < 0 || hi < lo || hi > n) return fail(e, FWA_E_ARG, "corrupt key-group offsets");
+        const int64_t m = hi - lo;
+        if (m == 0) continue;
+        const int64_t* body = off + maxp + 1;
+        int rc = ensure_sess_lists(e, e->n_ss + m);
+        if (rc) return rc;
+        // device copies: key, start, end, one column per accumulator (COUNT, then each owner aggregate's)
+        const int nc = 3 + e->nacc;
+        int64_t* d = nullptr;
+        HIPCHK(e, hipMalloc(&d, 8 * (size_t)m * nc));
+        std::vector<const int64_t*> src(nc);
+        src[0] = body + lo;
+        src[1] = body + (size_t)n + lo;
+        src[2] = body + (size_t)(3 + na) * n + lo;
+        src[3] = body + (size_t)2 * n + lo;
+        for (int cc = 1; cc < e->nacc; ++cc)
+            for (int j = 0; j < na; ++j)
+                if (e->ec.agg[j].acc == cc && !e->ec.agg[j].alias) src[3 + cc] = body + (size_t)(3 + j) * n + lo;
+        std::vector<const int64_t*> hacc(e->nacc);
+        for (int c = 0; c < nc; ++c) HIPCHK(e, hipMemcpy(d + (size_t)c * m, src[c], 8 * (size_t)m, hipMemcpyHostToDevice));
+        for (int cc = 0; cc < e->nacc; ++cc) hacc[cc] = d + (size_t)(3 + cc) * m;
+        const int64_t** dacc = nullptr;
+        HIPCHK(e, hipMalloc(&dacc, sizeof(int64_t*) * e->nacc));
+        HIPCHK(e, hipMemcpy(dacc, hacc.data(), sizeof(int64_t*) * e->nacc, hipMemcpyHostToDevice));
+        Sess2Args s;
+        memset(&s, 0, sizeof(s));
+        s.key_table = e->d_keys;
+        s.key_mask = (uint64_t)e->capacity - 1;
+        s.seg_log = e->seg_log;
+        s.part_bits = e->part_bits;
+        s.out = e->ss[e->ss_cur];
+        s.st = e->d_st;
+        sess2_restore_kernel<<<grid_for(m), kBlock, 0, e->stream>>>(s, d, d + m, d + 2 * m, dacc, m, e->n_ss, e->d_ec);
+        HIPCHK(e, hipGetLastError());
+        rc = sync_status(e);
+        (void)hipFree(d);
+        (void)hipFree(dacc);
+        if (rc) return rc;
+        if (e->h_st->error) return fail(e, e->h_st->error, "key table full: raise fwa_config.key_capacity");
+        e->n_ss += m;
+    }
+    if (n_blobs > 0) e->wm = wm;
+    return FWA_OK;
+}
+
 // Export every (key, slice) accumulator of every live slice (non-destructive raw fire), then bucket
 // the rows by key group on the host (counting sort) into the blob.
 int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
     if (!e || !out) return FWA_E_ARG;
     memset(out, 0, sizeof(*out));
-    if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "snapshot of session windows is not supported");
     if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "snapshot needs a computable key hash");
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
+    if (e->kind == FWA_SESSION) return snapshot_sessions(e, out);
     std::vector<FireWindow> hw;
     std::vector<int32_t> hs;
     for (auto& kv : e->live) {
@@ -3695,11 +3815,11 @@ void fwa_blob_free(fwa_blob* b) {
 int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, int32_t n_blobs) {
     if (!e) return FWA_E_STATE;
     if (n_blobs < 0 || (n_blobs > 0 && (!blobs || !sizes))) return fail(e, FWA_E_ARG, "null snapshot list");
-    if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "restore of session windows is not supported");
     if (int rc0 = settle_pending(e)) return rc0;
-    if (e->records_in != 0 || e->wm != LONG_MIN_J || !e->live.empty())
+    if (e->records_in != 0 || e->wm != LONG_MIN_J || !e->live.empty() || e->n_ss != 0)
         return fail(e, FWA_E_STATE, "restore needs a fresh handle");
     const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism;
+    const int ncols = (e->kind == FWA_SESSION ? 4 : 3) + na;
     int64_t ref[kSnapHdr];
     snap_header(e, ref, 0);
     // validate every blob before touching state
@@ -3710,9 +3830,10 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
         for (int w = 2; w < 20; ++w)
             if (h[w] != ref[w]) return fail(e, FWA_E_ARG, "snapshot window/aggregate configuration differs");
         const int64_t n = h[21];
-        if (n < 0 || sizes[b] != (int64_t)(8 * (kSnapHdr + maxp + 1 + (size_t)n * (3 + na))))
+        if (n < 0 || sizes[b] != (int64_t)(8 * (kSnapHdr + maxp + 1 + (size_t)n * ncols)))
             return fail(e, FWA_E_ARG, "snapshot size does not match its entry count");
     }
+    if (e->kind == FWA_SESSION) return restore_sessions(e, blobs, n_blobs);
     int64_t wm = LONG_MAX_J;
     bool any = false;
     for (int32_t b = 0; b < n_blobs; ++b) {

@@ -18,12 +18,14 @@ def parse(blob):
     if w.size < HDR_WORDS or int(w[0]) & 0xFFFFFFFFFFFFFFFF != MAGIC or int(w[1]) != 1:
         raise ValueError("not a flink_amd snapshot")
     maxp, naggs, n = int(w[9]), int(w[11]), int(w[21])
-    need = HDR_WORDS + maxp + 1 + n * (3 + naggs)
+    session = int(w[2]) == 3                     # SESSION: a 4th leading column holds the session end (last)
+    ncols = (4 if session else 3) + naggs
+    need = HDR_WORDS + maxp + 1 + n * ncols
     if w.size != need:
         raise ValueError("snapshot size %d words != %d" % (w.size, need))
     off = w[HDR_WORDS:HDR_WORDS + maxp + 1]
-    body = w[HDR_WORDS + maxp + 1:].reshape(3 + naggs, n) if n else np.zeros((3 + naggs, 0), np.int64)
-    return {
+    body = w[HDR_WORDS + maxp + 1:].reshape(ncols, n) if n else np.zeros((ncols, 0), np.int64)
+    out = {
         "window_kind": int(w[2]), "semantics": int(w[3]), "size_ms": int(w[4]), "slide_ms": int(w[5]),
         "offset_ms": int(w[6]), "gap_ms": int(w[7]), "allowed_lateness_ms": int(w[8]),
         "max_parallelism": maxp, "key_kind": int(w[10]), "aggs": [int(x) for x in w[12:12 + naggs]],
@@ -31,6 +33,9 @@ def parse(blob):
         "kg_offsets": off.copy(), "key": body[0].copy(), "slice_start": body[1].copy(),
         "count": body[2].copy(), "acc": [body[3 + j].copy() for j in range(naggs)],
     }
+    if session:
+        out["window_end"] = body[3 + naggs].copy()   # slice_start holds the session start
+    return out
 
 
 def entries_of_key_group(snap, kg):

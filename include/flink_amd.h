@@ -254,8 +254,9 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
  * are [off[g], off[g+1])), then SoA columns key[n], slice_start[n], count[n], acc_j[n] (one per
  * aggregate, same encoding as fwa_partials). Per-key timers are not stored: the engine's timers are
  * derived from the live slices and the watermark, as the reference re-registers them from state.
- * Not available for SESSION windows (FWA_E_UNSUPPORTED). The blob is engine-allocated; free it
- * with fwa_blob_free. */
+ * SESSION windows: the entries are the in-flight sessions (the MergingWindowSet mapping + window state,
+ * WindowOperator.java:224-238) with slice_start = session start and one more column end[n] after the
+ * acc_j columns. The blob is engine-allocated; free it with fwa_blob_free. */
 typedef struct fwa_blob {
     void* data;
     int64_t size;   /* bytes */
