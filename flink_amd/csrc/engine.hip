@@ -405,6 +405,7 @@ struct PartArgs {
     uint16_t* b_rel;
     uint32_t* b_cnt;                   // [np]
     int64_t capb;
+    uint64_t trash;                    // bucket index of a kMaxPart-entry scratch area past the buckets
     int64_t spill_cap;
     int32_t part_bits, np;
     int32_t vcol[2];
@@ -444,6 +445,14 @@ __device__ __forceinline__ void block_scan_np(const uint32_t* hist, uint32_t* to
 #pragma unroll
     for (int q = 0; q < PER; ++q) { if (PER * tid + q < np) toff[PER * tid + q] = excl; excl += v[q]; }
 }
+
+// Make the compiler wait for a loaded register HERE, on every path (see partition3).
+__device__ __forceinline__ void consume(unsigned long long x) {
+    asm volatile("" : : "v"((uint32_t)x), "v"((uint32_t)(x >> 32)));
+}
+__device__ __forceinline__ void consume(int64_t x) { consume((unsigned long long)x); }
+__device__ __forceinline__ void consume(int32_t x) { asm volatile("" : : "v"(x)); }
+__device__ __forceinline__ void consume(uint32_t x) { asm volatile("" : : "v"(x)); }
 
 // partition2: Phase P with the next tile's loads in flight while the current tile is scanned,
 // reserved and stored (r01 ablation: without its bucket stores Phase P still took 0.58 ms per 2^26
@@ -621,6 +630,247 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
                 continue;
             }
             const uint64_t o = ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
+            a.b_key[o] = x_key[x];
+            a.b_rel[o] = x_rel[x];
+            if (NV > 0) a.b_val0[o] = x_val[0][x];
+            if (NV > 1) a.b_val1[o] = x_val[NV > 1 ? 1 : 0][x];
+        }
+        QMARK(3);
+        __syncthreads();
+        QMARK(4);
+    }
+    if (a.prof && tid == 0) for (int q = 0; q < 6; ++q) a.prof[(int64_t)blockIdx.x * 8 + q] = pacc[q];
+#undef QMARK
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        dropped += __shfl_xor(dropped, sh);
+        relmax = max(relmax, (uint32_t)__shfl_xor((int)relmax, sh));
+        relmin = min(relmin, (uint32_t)__shfl_xor((int)relmin, sh));
+    }
+    if (lane == 0) {
+        if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
+        if (relmin != ~0u) {
+            atomicMax(&a.st->max_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmax));
+            atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
+        }
+    }
+    if (relmin != ~0u)
+        for (uint32_t r = relmin + (uint32_t)lane; r <= relmax; r += 64) {
+            const int32_t slot = a.rel2slot[r];
+            if (slot >= 0 && a.touched[slot] == 0) a.touched[slot] = 1;
+        }
+}
+
+// partition3: partition2 with the reservation/prefetch order fixed (below) and the key-group check
+// and key-hash loads compiled in only when needed (KG: 0 whole range owned, 1 hash of the key, 2 supplied
+// key.hashCode()).
+// partition2: Phase P with the next tile's loads in flight while the current tile is scanned,
+// reserved and stored (r01 ablation: without its bucket stores Phase P still took 0.58 ms per 2^26
+// records, twice the streaming time of its 1.6 GB of input -- one tile in flight per CU left every
+// latency in the tile's chain exposed). The tile is staged in LDS in arrival order (x_*), the
+// counting sort only writes a permutation (s_src) and the store loop gathers through it, so the
+// load registers are free as soon as the tile is classified.
+// VW: value-column widths, bit v set = carried value column v is 8 bytes (else 4): a compile-time
+// width keeps the tile's loads branch-free, so none waits for another.
+template <int NV, int ITEMS, int THREADS, int VW, int KG>
+__global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
+    static_assert(THREADS == kMaxPart && ITEMS <= 8, "one partition cursor per thread; trash area of 8 x kMaxPart");
+    constexpr int kTile = THREADS * ITEMS;
+    const EngineConst& c = *cp;
+    __shared__ uint32_t hist[kMaxPart];
+    __shared__ uint32_t toff[kMaxPart];
+    __shared__ uint32_t gbase[kMaxPart];
+    __shared__ uint32_t sbase[kMaxPart];   // spill-list base of the tile's overflow records, per partition
+    __shared__ unsigned long long x_key[kTile];
+    __shared__ unsigned long long x_val[NV > 0 ? NV : 1][NV > 0 ? kTile : 1];
+    __shared__ uint16_t x_rel[kTile];
+    __shared__ uint16_t s_part[kTile];
+    __shared__ uint16_t s_src[kTile];
+    __shared__ uint32_t wsum[THREADS / 64];
+    __shared__ uint32_t s_total;
+    __shared__ uint8_t s_code[kRelCap];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    unsigned dropped = 0;
+    uint32_t relmax = 0, relmin = ~0u;
+    const bool ds = c.sem == FWA_SEM_DATASTREAM;
+    for (int r = tid; r < kRelCap / 4; r += THREADS) ((uint32_t*)s_code)[r] = ((const uint32_t*)a.relcode)[r];
+    const int64_t ntiles = (a.n + kTile - 1) / kTile;
+    const int sub = blockIdx.x % kSub;
+    unsigned long long r_key[ITEMS], r_v0[ITEMS], r_v1[ITEMS];
+    int64_t r_ts[ITEMS];
+    int32_t r_kh[ITEMS];
+    // Column pointers resolved once (uniform, SGPRs): indexing the kernel-argument array per load
+    // made hipcc fetch the pointer with a vector load and wait vmcnt(0) before every value load,
+    // serialising the tile's loads item by item.
+    const int64_t* __restrict__ pkeys = a.keys;
+    const int64_t* __restrict__ pts = a.ts;
+    const void* pc0 = NV > 0 ? a.cols[a.vcol[0]] : nullptr;
+    const void* pc1 = NV > 1 ? a.cols[a.vcol[1]] : nullptr;
+    constexpr bool w0 = (VW & 1) != 0, w1 = (VW & 2) != 0;
+    const int32_t* __restrict__ pkh = a.key_hash;
+    const int64_t n = a.n;
+    // every load of a tile is issued before any is used; uniform branches sit outside the item loops
+    // (a per-item select between a 4- and an 8-byte load made hipcc wait vmcnt(0) at every join)
+    auto load = [&](int64_t t) {
+        int64_t ic[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const int64_t i = t * kTile + (int64_t)j * THREADS + tid;
+            ic[j] = i < n ? i : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) { r_key[j] = (unsigned long long)pkeys[ic[j]]; r_ts[j] = pts[ic[j]]; }
+        if constexpr (NV > 0) {
+            if constexpr (w0) {
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j) r_v0[j] = ((const unsigned long long*)pc0)[ic[j]];
+            } else {
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j) r_v0[j] = ((const uint32_t*)pc0)[ic[j]];
+            }
+        }
+        if constexpr (NV > 1) {
+            if constexpr (w1) {
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j) r_v1[j] = ((const unsigned long long*)pc1)[ic[j]];
+            } else {
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j) r_v1[j] = ((const uint32_t*)pc1)[ic[j]];
+            }
+        }
+        if constexpr (KG == 2) {
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) r_kh[j] = pkh[ic[j]];
+        } else {
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) r_kh[j] = 0;
+        }
+    };
+    long long pt = clock64();
+    long long pacc[6] = {0, 0, 0, 0, 0, 0};
+#define QMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
+    int64_t tile = blockIdx.x;
+    load(tile < ntiles ? tile : 0);
+    // the memory operations of one store phase, to the trash area: hipcc's waitcnt analysis merges the
+    // loop entry with the back-edge, so an entry without the stores made the header wait vmcnt(0) on
+    // every trip (draining the previous tile's stores)
+#pragma unroll
+    for (int jj = 0; jj < ITEMS; ++jj) {
+        const uint64_t o = a.trash + (uint64_t)(jj * THREADS + tid);   // distinct: not merged by the compiler
+        a.b_key[o] = 0ull;
+        a.b_rel[o] = 0;
+        if (NV > 0) a.b_val0[o] = 0ull;
+        if (NV > 1) a.b_val1[o] = 0ull;
+    }
+    for (; tile < ntiles; tile += gridDim.x) {
+        for (int i = tid; i < a.np; i += THREADS) hist[i] = 0;
+        __syncthreads();
+        QMARK(5);
+        const int64_t t0 = tile * kTile;
+        uint32_t r_pos[ITEMS];   // (p << 16 | rank) or ~0u when the record does not go to a bucket
+        // wait for the whole tile HERE, on every path: a loaded register consumed only on some paths (the
+        // value, staged for accepted records only) stays "pending" in hipcc's waitcnt analysis, and the
+        // next reuse of that register then waited vmcnt(0) -- draining the stores and the prefetch
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            consume(r_key[j]);
+            consume(r_ts[j]);
+            if constexpr (NV > 0) consume(r_v0[j]);
+            if constexpr (NV > 1) consume(r_v1[j]);
+            if constexpr (KG == 2) consume(r_kh[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const int64_t i = t0 + (int64_t)j * THREADS + tid;
+            const int64_t key = (int64_t)r_key[j];
+            const int64_t ts = r_ts[j];
+            const int64_t d = jm::wsub(ts, c.off);
+            const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
+            const uint64_t uq = jm::udiv64(ud, c.g_div);
+            const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
+            const uint64_t rel = (uint64_t)(q - a.q_base);
+            uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
+            if constexpr (KG != 0) {
+                const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, r_kh[j]), c.max_par);
+                if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;
+            }
+            if (ds && ts == LONG_MIN_J) code = kCodeSlow;
+            if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
+            if (i >= a.n) code = 0xff;
+            dropped += code == kCodeDrop;
+            const bool slow = code == kCodeSlow;
+            const unsigned long long mk = __ballot(slow);
+            if (mk) {
+                const int leader = __ffsll((long long)mk) - 1;
+                int32_t sb = 0;
+                if (lane == leader) sb = atomicAdd(&a.st->spill_n, __popcll(mk));
+                sb = __shfl(sb, leader);
+                if (slow) put_idx(a.spill, sb + __popcll(mk & ((1ull << lane) - 1)), a.spill_cap, (int32_t)i, a.st);
+            }
+            r_pos[j] = ~0u;
+            if (code == kCodeAccept) {
+                relmax = max(relmax, (uint32_t)rel);
+                relmin = min(relmin, (uint32_t)rel);
+                const uint64_t h = jm::mix64((uint64_t)key);
+                const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
+                const int x = j * THREADS + tid;
+                x_key[x] = r_key[j];
+                x_rel[x] = (uint16_t)rel;
+                if (NV > 0) x_val[0][x] = r_v0[j];
+                if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = r_v1[j];
+                r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
+            }
+        }
+        QMARK(0);
+        __syncthreads();
+        block_scan_np<THREADS>(hist, toff, wsum, a.np, &s_total);
+        __syncthreads();
+        QMARK(1);
+        // the run reservations (returning atomics) are issued BEFORE the next tile's loads: vmcnt retires
+        // in order, so waiting for the reservations no longer drains the prefetch (partition2 waited
+        // vmcnt(0) right after its reservation, leaving no load in flight during scatter and store)
+        const int p = tid;
+        const uint32_t h = p < a.np ? hist[p] : 0u;
+        uint32_t g = 0;
+        if (h) g = atomicAdd(&a.b_cnt[p * kSub + sub], h);
+        load(tile + gridDim.x < ntiles ? tile + gridDim.x : tile);   // next tile in flight from here on (unconditional)
+        if (p < a.np) {
+            gbase[p] = g;
+            // records past the sub-bucket's end (skewed keys) go to the v1 replay: one spill reservation
+            // per (tile, overflowing partition) -- a per-wave reservation on the single spill counter
+            // serialised ~100 K same-address device atomics per push under Zipf(1.1)
+            const uint64_t end = (uint64_t)g + h;
+            if (end > (uint64_t)a.capb) {
+                const uint32_t ov = (uint32_t)(end - std::max<uint64_t>(g, (uint64_t)a.capb));
+                sbase[p] = (uint32_t)atomicAdd(&a.st->spill_n, (int32_t)ov);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            if (r_pos[j] == ~0u) continue;
+            const uint32_t p = r_pos[j] >> 16;
+            const uint32_t sidx = toff[p] + (r_pos[j] & 0xffffu);
+            s_part[sidx] = (uint16_t)p;
+            s_src[sidx] = (uint16_t)(j * THREADS + tid);
+        }
+        __syncthreads();
+        QMARK(2);
+        const uint32_t total = s_total;
+        // fixed trip count, every store issued (lanes without a record write the trash area): the next
+        // classify then waits for its loads with an exact vmcnt instead of draining these stores
+#pragma unroll
+        for (int jj = 0; jj < ITEMS; ++jj) {
+            const uint32_t sidx = (uint32_t)(jj * THREADS + tid);
+            const bool valid = sidx < total;
+            const uint32_t p = valid ? s_part[sidx] : 0u;
+            const uint32_t x = valid ? s_src[sidx] : 0u;
+            const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
+            const bool inb = valid && dst < (uint64_t)a.capb;
+            if (valid && !inb) {                // sub-bucket full (skewed keys): the v1 replay takes it
+                const uint64_t first = std::max<uint64_t>(gbase[p], (uint64_t)a.capb);
+                put_idx(a.spill, (int64_t)sbase[p] + (int64_t)(dst - first), a.spill_cap, (int32_t)(t0 + x), a.st);
+            }
+            const uint64_t o = inb ? ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst : a.trash + (uint64_t)(jj * THREADS + tid);
             a.b_key[o] = x_key[x];
             a.b_rel[o] = x_rel[x];
             if (NV > 0) a.b_val0[o] = x_val[0][x];
@@ -2662,9 +2912,10 @@ static int ensure_v2_buffers(fwa_engine* e, int64_t n) {
         e->d_bkey = nullptr;
         e->d_brel = nullptr;
         e->d_bval[0] = e->d_bval[1] = nullptr;
-        HIPCHK(e, hipMalloc(&e->d_bkey, 8 * capb * e->np * kSub));
-        HIPCHK(e, hipMalloc(&e->d_brel, 2 * capb * e->np * kSub));
-        for (int v = 0; v < e->nv; ++v) HIPCHK(e, hipMalloc(&e->d_bval[v], 8 * capb * e->np * kSub));
+        const int64_t ent = capb * e->np * kSub + 8 * kMaxPart;  // + a trash area (partition3's masked stores)
+        HIPCHK(e, hipMalloc(&e->d_bkey, 8 * ent));
+        HIPCHK(e, hipMalloc(&e->d_brel, 2 * ent));
+        for (int v = 0; v < e->nv; ++v) HIPCHK(e, hipMalloc(&e->d_bval[v], 8 * ent));
         e->capb = capb;
     }
     if (!e->d_bcnt) {
@@ -2728,6 +2979,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.b_val1 = e->d_bval[1];
     pa.b_cnt = e->d_bcnt;
     pa.capb = e->capb;
+    pa.trash = (uint64_t)e->capb * e->np * kSub;
     pa.spill_cap = e->spill_cap;
     pa.part_bits = e->part_bits;
     pa.np = e->np;
@@ -2745,7 +2997,13 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     const int64_t tile = (int64_t)items * threads;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256));
     const int vw = (e->vsize[0] == 8 ? 1 : 0) | (e->vsize[1] == 8 ? 2 : 0);
-#define P2LAUNCH(NV, IT, VW) partition2_kernel<NV, IT, 1024, 1, VW><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec)
+    static const bool p2 = getenv("FWA_P2") != nullptr;   // A/B switch: the r01 Phase P kernel
+    const bool kg_all = e->cfg.kg_start == 0 && e->cfg.kg_end == e->cfg.max_parallelism - 1;
+    const int kgm = kg_all ? 0 : (e->cfg.key_kind == FWA_KEY_PREHASHED ? 2 : 1);
+#define P2LAUNCH(NV, IT, VW) do { if (p2) partition2_kernel<NV, IT, 1024, 1, VW><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
+        else if (kgm == 0) partition3_kernel<NV, IT, 1024, VW, 0><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
+        else if (kgm == 1) partition3_kernel<NV, IT, 1024, VW, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
+        else partition3_kernel<NV, IT, 1024, VW, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
     if (e->nv == 0) P2LAUNCH(0, 8, 3);
     else if (e->nv == 1) { if (vw & 1) P2LAUNCH(1, 6, 3); else P2LAUNCH(1, 6, 2); }
     else if (vw == 3) P2LAUNCH(2, 4, 3); else if (vw == 2) P2LAUNCH(2, 4, 2);
