@@ -92,7 +92,15 @@ struct EngineConst {
     int32_t naggs, nacc;        // nacc = 1 (count) + stateful agg columns
     AggDesc agg[FWA_MAX_AGGS];
     int32_t acc_kind[1 + FWA_MAX_AGGS];
+    const int64_t* tz;          // shift time zone table (device copy of fwa_config.tz), tz_n pairs
+    int32_t tz_n, pad_tz;
 };
+
+// Slice-assignment timestamp: the record's local wall-clock time under a Table shift time zone
+// (AbstractSliceAssigner.assignSliceEnd -> TimeWindowUtil.toUtcTimestampMills), else the timestamp.
+__device__ __forceinline__ int64_t assign_ts(const EngineConst& c, int64_t ts) {
+    return c.tz_n ? jm::tz_to_local(c.tz, c.tz_n, ts) : ts;
+}
 
 struct IngestArgs {
     const int64_t* keys;
@@ -230,7 +238,7 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }
         if (c.sem == FWA_SEM_DATASTREAM && ts == LONG_MIN_J) { raise_error(a.st, FWA_E_TS_MIN); continue; }
         // slice number q = floor((ts - off) / g), Java wrap arithmetic (TimeWindow.java:264-272)
-        const int64_t d = jm::wsub(ts, c.off);
+        const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
         const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
         const uint64_t uq = jm::udiv64(ud, c.g_div);
         int64_t q;
@@ -553,7 +561,7 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
             const int64_t i = t0 + (int64_t)j * THREADS + tid;
             const int64_t key = (int64_t)r_key[j];
             const int64_t ts = r_ts[j];
-            const int64_t d = jm::wsub(ts, c.off);
+            const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
             const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
             const uint64_t uq = jm::udiv64(ud, c.g_div);
             const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
@@ -784,7 +792,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             const int64_t i = t0 + (int64_t)j * THREADS + tid;
             const int64_t key = (int64_t)r_key[j];
             const int64_t ts = r_ts[j];
-            const int64_t d = jm::wsub(ts, c.off);
+            const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
             const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
             const uint64_t uq = jm::udiv64(ud, c.g_div);
             const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
@@ -2018,7 +2026,7 @@ __global__ void __launch_bounds__(64) late_fire_kernel(LateArgs L, const EngineC
         const int64_t i = L.order[t];
         const int64_t key = a.keys[i];
         const int64_t ts = a.ts[i];
-        const int64_t d = jm::wsub(ts, c.off);
+        const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
         const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
         const uint64_t uq = jm::udiv64(ud, c.g_div);
         const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
@@ -2172,6 +2180,8 @@ struct fwa_engine {
     // window geometry (host)
     int32_t kind = 0, sem = 0;
     int64_t g = 0, off = 0, size = 0, slide = 0, lateness = 0;
+    std::vector<int64_t> tz;          // shift time zone (instant, offset) pairs (fwa_config.tz, copied)
+    int64_t* d_tz = nullptr;
     jm::UDiv64 slide_div, size_div;
     // key table
     int64_t capacity = 0;
@@ -2360,7 +2370,11 @@ int validate(const fwa_config* c) {
     if ((c->flags & FWA_CFG_DYNAMIC_GAP) && (c->window_kind != FWA_SESSION || c->gap_col < 0 || c->gap_col >= FWA_MAX_COLS))
         return FWA_E_ARG;
     if (c->tz_n < 0 || (c->tz_n > 0 && !c->tz)) return FWA_E_ARG;
-    if (c->tz_n > 0) return FWA_E_UNSUPPORTED;
+    if (c->tz_n > 0) {                       // TIMESTAMP_LTZ rowtime: Table slicing windows only
+        if (c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;
+        if (c->window_kind == FWA_SESSION) return FWA_E_UNSUPPORTED;
+        for (int32_t i = 1; i < c->tz_n; ++i) if (c->tz[2 * i] <= c->tz[2 * (i - 1)]) return FWA_E_ARG;
+    }
     if (c->semantics != FWA_SEM_DATASTREAM && c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;
     if (c->semantics == FWA_SEM_TABLE && c->allowed_lateness_ms != 0) return FWA_E_ARG;
     if (c->allowed_lateness_ms < 0) return FWA_E_ARG;
@@ -2373,6 +2387,12 @@ int validate(const fwa_config* c) {
 // ---- slice geometry (host) ----
 
 int64_t slice_start(const fwa_engine* e, int64_t q) { return jm::wadd(e->off, (int64_t)((uint64_t)q * (uint64_t)e->g)); }
+
+// Epoch time at which a window whose last local timestamp is `max_ts` fires (TimeWindowUtil.
+// toEpochMillsForTimer / isWindowFired :162-183); identity without a shift time zone.
+int64_t trig(const fwa_engine* e, int64_t max_ts) {
+    return e->tz.empty() ? max_ts : jm::tz_timer(e->tz.data(), (int)(e->tz.size() / 2), max_ts);
+}
 
 int64_t slice_q(const fwa_engine* e, int64_t t) {  // slice number of a timestamp / slice start
     const int64_t d = jm::wsub(t, e->off);
@@ -2417,7 +2437,7 @@ int64_t first_window_end(const fwa_engine* e, int64_t q) {
 // acceptance threshold: accepted iff wm < thr, or always
 void accept_threshold(const fwa_engine* e, int64_t q, int64_t* thr, bool* always) {
     const int64_t last_end = last_window_end(e, q);
-    const int64_t mt = jm::wsub(last_end, 1);
+    const int64_t mt = trig(e, jm::wsub(last_end, 1));
     *always = false;
     if (e->sem == FWA_SEM_TABLE) {                     // !TimeWindowUtil.isWindowFired(lastWindowEnd, wm)
         if (last_end == LONG_MAX_J) *always = true;
@@ -2527,7 +2547,7 @@ int publish_dir(fwa_engine* e) {
         bool always;
         accept_threshold(e, kv.first, &d.thr, &always);
         d.flags = 1 | (always ? 2 : 0);
-        d.first_maxts = jm::wsub(first_window_end(e, kv.first), 1);
+        d.first_maxts = trig(e, jm::wsub(first_window_end(e, kv.first), 1));
     }
     for (int64_t q : e->negative) {
         uint32_t i = (uint32_t)jm::mix64((uint64_t)q) & (e->dir_cap - 1);
@@ -2650,7 +2670,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n, e->d_reset_list, e->d_upos,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -2673,6 +2693,8 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
     if (v) return v;
     fwa_engine* e = new fwa_engine();
     e->cfg = *cfg;
+    if (cfg->tz_n > 0) e->tz.assign(cfg->tz, cfg->tz + 2 * (size_t)cfg->tz_n);
+    e->cfg.tz = nullptr;                         // the caller's table is not kept (copied above)
     e->kind = cfg->window_kind;
     e->sem = cfg->semantics;
     e->size = cfg->size_ms;
@@ -2792,6 +2814,12 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
     e->stride = ((cap + 1 + 63) / 64) * 64;
     int rc = FWA_OK;
     do {
+        if (!e->tz.empty()) {
+            if (hipMalloc(&e->d_tz, 8 * e->tz.size()) != hipSuccess) { rc = FWA_E_OOM; break; }
+            if (hipMemcpy(e->d_tz, e->tz.data(), 8 * e->tz.size(), hipMemcpyHostToDevice) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+            c.tz = e->d_tz;
+            c.tz_n = (int32_t)(e->tz.size() / 2);
+        }
         if (hipMalloc(&e->d_ec, sizeof(EngineConst)) != hipSuccess) { rc = FWA_E_OOM; break; }
         if (hipMemcpy(e->d_ec, &c, sizeof(EngineConst), hipMemcpyHostToDevice) != hipSuccess) { rc = FWA_E_DEVICE; break; }
         if (hipMalloc(&e->d_keys, sizeof(unsigned long long) * (cap + 1)) != hipSuccess) { rc = FWA_E_OOM; break; }
@@ -2953,7 +2981,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         bool always;
         accept_threshold(e, kv.first, &thr, &always);
         if (!always && !(a.wm < thr)) code[rel] = kCodeDrop;
-        else if (e->lateness > 0 && a.wm >= jm::wsub(first_window_end(e, kv.first), 1)) code[rel] = kCodeSlow;
+        else if (e->lateness > 0 && a.wm >= trig(e, jm::wsub(first_window_end(e, kv.first), 1))) code[rel] = kCodeSlow;
         else code[rel] = kCodeAccept;
     }
     rc = upload(e, e->d_rel2slot, r2s.data(), (sizeof(int32_t) + 1) * kRelCap);
@@ -3804,7 +3832,7 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
         FireWindow f;
         f.start = slice_start(e, kv.first);
         f.end = jm::wadd(f.start, e->g);
-        if (wm != LONG_MAX_J && !(jm::wsub(f.end, 1) <= wm)) continue;   // slice not complete at wm
+        if (wm != LONG_MAX_J && !(trig(e, jm::wsub(f.end, 1)) <= wm)) continue;   // slice not complete at wm
         f.slot_off = (int32_t)hs.size();
         f.nslots = 1;
         hs.push_back(kv.second);
@@ -4209,7 +4237,7 @@ static int speculative_fire(fwa_engine* e, int64_t wm, int64_t* nrows, bool* ok)
         FireWindow f;
         f.start = slice_start(e, kv.first);
         f.end = jm::wadd(f.start, e->g);
-        const int64_t mt = jm::wsub(f.end, 1);
+        const int64_t mt = trig(e, jm::wsub(f.end, 1));
         if (!(mt > e->wm && mt <= wm)) continue;
         f.slot_off = (int32_t)hs.size();
         f.nslots = 1;
@@ -4255,7 +4283,7 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
             tmp.clear();
             windows_of_slice(e, kv.first, tmp);
             for (auto& w : tmp) {
-                const int64_t mt = jm::wsub(w.second, 1);
+                const int64_t mt = trig(e, jm::wsub(w.second, 1));
                 if (mt > prev && mt <= wm) wins.insert({w.second, w.first});
             }
         }

@@ -175,4 +175,43 @@ JM_HD uint64_t mix64(uint64_t z) {
 }
 JM_HD uint64_t splitmix64(uint64_t x) { return mix64(x + 0x9e3779b97f4a7c15ull); }
 
+// ---- shift time zone of a TIMESTAMP_LTZ rowtime (Table), TimeWindowUtil.java:52-100 ----
+// tz: n pairs (utc_instant_ms, offset_ms), ascending by instant; pair i's offset applies from its instant
+// until the next pair's (pair 0 also before its instant). n == 0: UTC.
+JM_HD int64_t tz_offset_at(const int64_t* tz, int n, int64_t instant) {   // ZoneRules.getOffset(Instant)
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tz[2 * mid] <= instant) lo = mid; else hi = mid - 1;
+    }
+    return tz[2 * lo + 1];
+}
+// toUtcTimestampMills: the local wall-clock time of an instant, as epoch millis of that time in UTC.
+JM_HD int64_t tz_to_local(const int64_t* tz, int n, int64_t epoch) {
+    if (n == 0 || epoch == INT64_MAX) return epoch;          // Long.MAX_VALUE: the max-watermark flag
+    return wadd(epoch, tz_offset_at(tz, n, epoch));
+}
+// LocalDateTime.atZone(zone).toInstant() (ZonedDateTime.ofLocal, no preferred offset): a unique offset ->
+// local - offset; a gap -> shifted later by the gap (local - offset before); an overlap -> the earlier offset.
+JM_HD int64_t tz_at_zone(const int64_t* tz, int n, int64_t local) {
+    int j = 0;                                                // last segment whose local range starts <= local
+    for (int lo = 1, hi = n - 1; lo <= hi;) {
+        const int mid = (lo + hi) >> 1;
+        if (wadd(tz[2 * mid], tz[2 * mid + 1]) <= local) { j = mid; lo = mid + 1; } else hi = mid - 1;
+    }
+    if (j > 0 && local < wadd(tz[2 * j], tz[2 * (j - 1) + 1])) return wsub(local, tz[2 * (j - 1) + 1]);   // overlap
+    return wsub(local, tz[2 * j + 1]);
+}
+// toEpochMillsForTimer: the instant a local window time triggers at; with daylight saving (more than one
+// offset in the table) the gap / overlap hours follow TimeWindowUtil.java:74-95.
+JM_HD int64_t tz_timer(const int64_t* tz, int n, int64_t local) {
+    if (n == 0 || local == INT64_MAX) return local;
+    if (n == 1) return wsub(local, tz[1]);
+    const int64_t hour = 3600000;
+    const int64_t t1 = tz_at_zone(tz, n, local), t2 = tz_at_zone(tz, n, wadd(local, hour));
+    if (t1 == t2) return t1 - t1 % hour;                      // no epoch maps to this local time
+    if (t2 - t1 > hour) return t1 + hour;                     // two epochs: the later one
+    return t1;
+}
+
 }  // namespace jm

@@ -144,7 +144,51 @@ int or_assign_windows(const fwa_config* c, int64_t ts, int64_t* starts, int64_t*
     return FWA_E_UNSUPPORTED;
 }
 
+/* ---- shift time zone (TimeWindowUtil.java:52-100), tz = tz_n (instant, offset) pairs ---- */
+static int64_t or_tz_offset(const fwa_config* c, int64_t instant) {       /* ZoneRules.getOffset(Instant) */
+    int32_t best = 0;
+    for (int32_t i = 1; i < c->tz_n; i++) if (c->tz[2 * i] <= instant) best = i;
+    return c->tz[2 * best + 1];
+}
+int64_t or_to_local(const fwa_config* c, int64_t epoch) {                /* toUtcTimestampMills :52-60 */
+    if (c->tz_n == 0 || epoch == J_LONG_MAX) return epoch;
+    return jladd(epoch, or_tz_offset(c, epoch));
+}
+static int64_t or_at_zone(const fwa_config* c, int64_t local) {           /* LocalDateTime.atZone(zone) */
+    /* valid offsets o: the instant local - o really has offset o; gap (none): local - offset before the
+       transition; overlap (two): the earlier offset */
+    int64_t found = 0, first = 0;
+    int nf = 0;
+    for (int32_t i = 0; i < c->tz_n; i++) {
+        int64_t o = c->tz[2 * i + 1];
+        int64_t e = jlsub(local, o);
+        int dup = 0;
+        for (int32_t k = 0; k < i; k++) if (c->tz[2 * k + 1] == o) dup = 1;
+        if (dup || or_tz_offset(c, e) != o) continue;
+        if (nf == 0 || e < first) first = e;           /* earlier offset = smaller instant */
+        found = e; nf++;
+    }
+    (void)found;
+    if (nf >= 1) return first;
+    /* gap: the transition T with T + before <= local < T + after */
+    for (int32_t i = 1; i < c->tz_n; i++) {
+        int64_t before = c->tz[2 * (i - 1) + 1], after = c->tz[2 * i + 1], t = c->tz[2 * i];
+        if (jladd(t, before) <= local && local < jladd(t, after)) return jlsub(local, before);
+    }
+    return jlsub(local, c->tz[1]);
+}
+int64_t or_tz_timer(const fwa_config* c, int64_t local) {                 /* toEpochMillsForTimer :67-100 */
+    if (c->tz_n == 0 || local == J_LONG_MAX) return local;
+    if (c->tz_n == 1) return jlsub(local, c->tz[1]);
+    const int64_t hour = 3600000;                      /* useDaylightTime(): more than one offset */
+    int64_t t1 = or_at_zone(c, local), t2 = or_at_zone(c, jladd(local, hour));
+    if (t1 == t2) return t1 - t1 % hour;
+    if (t2 - t1 > hour) return t1 + hour;
+    return t1;
+}
+
 int64_t or_assign_slice_end(const fwa_config* c, int64_t ts) {
+    ts = or_to_local(c, ts);                           /* AbstractSliceAssigner: rowtime -> local millis */
     if (c->window_kind == FWA_TUMBLE) return jladd(or_window_start(ts, c->offset_ms, c->size_ms), c->size_ms);
     if (c->window_kind == FWA_SLIDE) {
         int64_t g = gcd64(c->size_ms, c->slide_ms);
@@ -382,8 +426,14 @@ int or_create(const fwa_config* c, or_engine** out) {
     if (c->window_kind == FWA_CUMULATE && (c->semantics != FWA_SEM_TABLE || c->size_ms <= 0 || c->slide_ms <= 0 || c->size_ms % c->slide_ms)) return FWA_E_ARG;
     if (c->window_kind == FWA_SESSION && c->gap_ms <= 0 && !(c->flags & FWA_CFG_DYNAMIC_GAP)) return FWA_E_ARG;
     if (c->semantics == FWA_SEM_TABLE && c->allowed_lateness_ms != 0) return FWA_E_ARG;
+    if (c->tz_n < 0 || (c->tz_n > 0 && (!c->tz || c->semantics != FWA_SEM_TABLE || c->window_kind == FWA_SESSION))) return FWA_E_ARG;
     or_engine* e = (or_engine*)calloc(1, sizeof(or_engine));
     e->c = *c;
+    if (c->tz_n > 0) {                                 /* own copy of the shift-time-zone table */
+        int64_t* t = (int64_t*)malloc(16 * (size_t)c->tz_n);
+        memcpy(t, c->tz, 16 * (size_t)c->tz_n);
+        e->c.tz = t;
+    }
     if (e->c.max_parallelism <= 0) e->c.max_parallelism = 128;
     e->wm = J_LONG_MIN;
     e->nacc = 1 + c->num_aggs;
@@ -398,6 +448,7 @@ int or_create(const fwa_config* c, or_engine** out) {
 void or_destroy(or_engine* e) {
     if (!e) return;
     hm_free(&e->state); th_free(&e->timers); hm_free(&e->wl_head);
+    if (e->c.tz_n > 0) free((void*)e->c.tz);
     free(e->pool); free(e->free_list);
     free(e->wl_key); free(e->wl_start); free(e->wl_end); free(e->wl_sws); free(e->wl_sw_end); free(e->wl_next);
     free(e->o_key); free(e->o_start); free(e->o_end);
@@ -589,10 +640,11 @@ static int64_t tb_slice_size(const fwa_config* c) {
     if (c->window_kind == FWA_SLIDE) return gcd64(c->size_ms, c->slide_ms);
     return c->slide_ms;
 }
-static int tb_is_fired(int64_t window_end, int64_t progress) {      /* TimeWindowUtil.isWindowFired :175-183 (UTC) */
+static int tb_is_fired_tz(const fwa_config* c, int64_t window_end, int64_t progress) {   /* TimeWindowUtil.isWindowFired :175-183 */
     if (window_end == J_LONG_MAX) return 0;
-    return progress >= jlsub(window_end, 1);
+    return progress >= or_tz_timer(c, jlsub(window_end, 1));
 }
+#define tb_is_fired(we, pr) tb_is_fired_tz(&e->c, (we), (pr))
 static int64_t tb_cum_window_start(const fwa_config* c, int64_t window_end) { return or_window_start(jlsub(window_end, 1), c->offset_ms, c->size_ms); }
 static int64_t tb_last_window_end(const fwa_config* c, int64_t slice_end) {
     if (c->window_kind == FWA_TUMBLE) return slice_end;
@@ -605,7 +657,8 @@ static int64_t tb_merge_target(const fwa_config* c, int64_t slice_end) {
 }
 static aval* tb_state(or_engine* e, int64_t key, int64_t slice, int create) { return ds_state(e, key, slice, 0, create); }
 static void tb_clear(or_engine* e, int64_t key, int64_t slice) { ds_clear_state(e, key, slice, 0); }
-static void tb_register(or_engine* e, int64_t key, int64_t window_end) { th_add(&e->timers, jlsub(window_end, 1), key, window_end, 0); }
+/* WindowTimerServiceImpl.registerEventTimeWindowTimer: the timer fires at toEpochMillsForTimer(windowEnd - 1) */
+static void tb_register(or_engine* e, int64_t key, int64_t window_end) { th_add(&e->timers, or_tz_timer(&e->c, jlsub(window_end, 1)), key, window_end, 0); }
 
 static int tb_process_element(or_engine* e, int64_t key, int64_t ts, const void* const* cols, int64_t i) {
     const fwa_config* c = &e->c;

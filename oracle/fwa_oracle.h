@@ -34,6 +34,9 @@ int32_t or_long_to_int_with_bit_mixing(int64_t in);        /* MathUtils.java:170
 int or_assign_windows(const fwa_config* cfg, int64_t ts, int64_t* starts, int64_t* ends, int cap);
 /* Table slice assigner: sliceEnd for ts (SliceAssigners.java:165-168/232-235/319-322). */
 int64_t or_assign_slice_end(const fwa_config* cfg, int64_t ts);
+/* Shift time zone (cfg->tz): TimeWindowUtil.toUtcTimestampMills / toEpochMillsForTimer. */
+int64_t or_to_local(const fwa_config* cfg, int64_t epoch);
+int64_t or_tz_timer(const fwa_config* cfg, int64_t local);
 
 /* ---- streaming operator restatement ---- */
 typedef struct or_engine or_engine;

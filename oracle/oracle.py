@@ -49,6 +49,9 @@ def lib():
         L.or_assign_windows.restype = C.c_int
         L.or_assign_slice_end.argtypes = [C.POINTER(A.Config), C.c_int64]
         L.or_assign_slice_end.restype = C.c_int64
+        for f in ("or_to_local", "or_tz_timer"):
+            getattr(L, f).argtypes = [C.POINTER(A.Config), C.c_int64]
+            getattr(L, f).restype = C.c_int64
         L.or_splitmix64.argtypes = [C.c_uint64]
         L.or_splitmix64.restype = C.c_uint64
         L.or_generate.argtypes = [C.POINTER(A.GenParams), C.c_int64, C.c_void_p, C.c_void_p,

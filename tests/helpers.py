@@ -26,12 +26,19 @@ def load_kats():
         return json.load(f)
 
 
+def load_tz_kats():
+    """Shift-time-zone KATs (tests/golden/gen_tz_kats.py)."""
+    with open(os.path.join(GOLDEN, "tz_kats.json")) as f:
+        return json.load(f)
+
+
 def kat_config(case, **kw):
     return A.make_config(window_kind=case["window_kind"], semantics=case["semantics"],
                          size_ms=case["size_ms"], slide_ms=case["slide_ms"],
                          offset_ms=case["offset_ms"], gap_ms=case["gap_ms"],
                          allowed_lateness_ms=case["allowed_lateness_ms"],
-                         aggs=[tuple(a) for a in case["aggs"]], gap_col=case.get("gap_col"), **kw)
+                         aggs=[tuple(a) for a in case["aggs"]], gap_col=case.get("gap_col"),
+                         tz=case.get("tz"), **kw)
 
 
 def rows_to_tuples(rows, naggs):

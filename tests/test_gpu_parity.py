@@ -8,11 +8,12 @@ import numpy as np
 import pytest
 
 from flink_amd import _abi as A
-from helpers import assert_rows_equal, load_kats, replay_kat
+from helpers import assert_rows_equal, load_kats, load_tz_kats, replay_kat
 
 pytestmark = pytest.mark.gpu
 
 KATS = load_kats()
+TZ_KATS = load_tz_kats()
 
 # Relative tolerances per aggregate (absolute floor equal to the same number, values are O(1..1e3)).
 #  SUM_F32: reference accumulates in float32 sequentially: |err| <= n * 2^-24 * sum|x|; n <= ~2e3 here.
@@ -34,6 +35,12 @@ def eng_mod():
 
 @pytest.mark.parametrize("case", KATS["operators"], ids=lambda c: c["name"].split(" ")[0])
 def test_reference_kats_on_gpu(eng_mod, case):
+    replay_kat(case, eng_mod.WindowAggregator)
+
+
+@pytest.mark.parametrize("case", TZ_KATS["operators"], ids=lambda c: c["name"].split(" ")[0])
+def test_reference_kats_shift_time_zone_on_gpu(eng_mod, case):
+    """SlicingWindowAggOperatorTest's Asia/Shanghai parameterisation through the engine."""
     replay_kat(case, eng_mod.WindowAggregator)
 
 
@@ -446,3 +453,29 @@ def test_late_firing_rows_survive_snapshot(eng_mod):
     assert len(ro["key"]) == 3
     assert_rows_equal(rg, ro, ["COUNT", "SUM_I64"])
     assert_rows_equal(g.advance_watermark(A.LONG_MAX), o.advance_watermark(A.LONG_MAX), ["COUNT", "SUM_I64"])
+
+
+@pytest.mark.parametrize("zone", ["America/Los_Angeles", "Asia/Shanghai"])
+@pytest.mark.parametrize("kind,size,slide", [("TUMBLE", 3_600_000, 0), ("SLIDE", 4 * 3_600_000, 3_600_000),
+                                             ("CUMULATE", 4 * 3_600_000, 3_600_000)])
+def test_shift_time_zone_streams_vs_oracle(eng_mod, zone, kind, size, slide):
+    """TIMESTAMP_LTZ rowtime: slices in local wall-clock time, windows fire at toEpochMillsForTimer(end - 1);
+    streams span the 2021 America/Los_Angeles DST days (a 23 h and a 25 h day)."""
+    from oracle.oracle import Oracle
+    tzk = {c["zone"]: c["tz"] for c in TZ_KATS["timer"]}
+    cfg = A.make_config(window_kind=kind, semantics="TABLE", size_ms=size, slide_ms=slide, tz=tzk[zone],
+                        aggs=[("COUNT", 0), ("SUM_I64", 0), ("MAX_I64", 0)], key_capacity=2048)
+    names = A.agg_names(cfg)
+    rng = np.random.default_rng(17)
+    batches = []
+    for t0 in (1615593600000, 1636156800000):         # 2021-03-13 and 2021-11-06, 00:00 UTC
+        n = 30_000
+        base = t0 + np.sort(rng.integers(0, 3 * 86_400_000, n)).astype(np.int64)
+        ts = base - rng.integers(0, 600_000, n)
+        keys = rng.integers(0, 300, n).astype(np.int64)
+        vi = rng.integers(-1000, 1000, n).astype(np.int64)
+        for b in range(12):
+            sl = slice(b * n // 12, (b + 1) * n // 12)
+            batches.append((keys[sl], ts[sl], [vi[sl]], int(ts[sl].max()) - 600_001))
+    batches.append((batches[0][0][:0], batches[0][1][:0], [batches[0][2][0][:0]], A.LONG_MAX))
+    run_pair(cfg, batches, eng_mod.WindowAggregator, Oracle, names)

@@ -6,9 +6,10 @@ import pytest
 
 from flink_amd import _abi as A
 from oracle import oracle as O
-from helpers import load_kats, replay_kat
+from helpers import load_kats, load_tz_kats, replay_kat
 
 KATS = load_kats()
+TZ_KATS = load_tz_kats()
 
 
 @pytest.mark.parametrize("case", KATS["assigners"], ids=lambda c: c["src"].split("/")[-1])
@@ -88,3 +89,29 @@ def test_key_group_literal_kats(case):
     for key, par, op in case["operator_index"]:
         kg = L.or_key_group(0, A.KEY_PREHASHED, java_hash_code(key, case["key_type"]), maxp)
         assert L.or_operator_index(maxp, par, kg) == op, (key, par)
+
+
+@pytest.mark.parametrize("case", TZ_KATS["slice_ends"], ids=lambda c: c["src"].split("/")[-1])
+def test_slice_end_kats_shift_time_zone(case):
+    """TIMESTAMP_LTZ rowtimes: slice ends in local wall-clock millis (TimeWindowUtil.toUtcTimestampMills),
+    incl. the America/Los_Angeles DST days of Tumbling/CumulativeSliceAssignerTest.testDstSaving."""
+    cfg = A.make_config(window_kind=case["kind"], semantics="TABLE", size_ms=case["size"],
+                        slide_ms=case["slide"], offset_ms=case["offset"], tz=case["tz"])
+    for ts, exp in case["cases"]:
+        assert O.lib().or_assign_slice_end(C.byref(cfg), ts) == exp, (ts, exp)
+
+
+@pytest.mark.parametrize("case", TZ_KATS["operators"], ids=lambda c: c["name"].split(" ")[0])
+def test_operator_kats_shift_time_zone(case):
+    replay_kat(case, O.Oracle)
+
+
+@pytest.mark.parametrize("case", TZ_KATS["timer"], ids=lambda c: c["zone"])
+def test_time_zone_conversion_kats(case):
+    """TimeWindowUtilTest integers: toEpochMillsForTimer (incl. the DST gap / overlap hours) and
+    toUtcTimestampMills."""
+    cfg = A.make_config(window_kind="TUMBLE", semantics="TABLE", size_ms=1000, tz=case["tz"])
+    for local, exp in case["timer"]:
+        assert O.lib().or_tz_timer(C.byref(cfg), local) == exp, (local, exp)
+    for epoch, exp in case["to_local"]:
+        assert O.lib().or_to_local(C.byref(cfg), epoch) == exp, (epoch, exp)
