@@ -40,6 +40,7 @@ STATUS = {0: "OK", -1: "E_ARG", -2: "E_TS_MIN", -3: "E_KEYGROUP", -4: "E_MERGE_L
           -6: "E_DEVICE", -7: "E_UNSUPPORTED", -8: "E_STATE"}
 
 CFG_DYNAMIC_GAP = 0x1
+CFG_LATE_INDICES = 0x2
 
 PUSH_DEVICE_PTRS = 0x1
 PUSH_ASYNC = 0x2
@@ -103,7 +104,7 @@ class GenParams(C.Structure):
 def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, slide_ms=0,
                 offset_ms=0, gap_ms=0, allowed_lateness_ms=0, aggs=(("COUNT", 0), ("SUM_I64", 0)),
                 key_kind=KEY_JAVA_LONG, max_parallelism=128, kg_start=0, kg_end=None, device=0,
-                output_on_device=0, key_capacity=0, max_batch=0, gap_col=None, tz=None):
+                output_on_device=0, key_capacity=0, max_batch=0, gap_col=None, tz=None, late_indices=False):
     """Build a Config struct. aggs: sequence of (agg name, value-column index). gap_col: value column of
     per-record session gaps (DynamicEventTimeSessionWindows). tz: [(utc_instant_ms, offset_ms), ...] shift
     time zone of a TIMESTAMP_LTZ rowtime (the struct keeps a pointer to a buffer held on the struct)."""
@@ -127,6 +128,8 @@ def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, sl
     c.output_on_device = output_on_device
     c.key_capacity = key_capacity
     c.max_batch = max_batch
+    if late_indices:
+        c.flags |= CFG_LATE_INDICES
     if gap_col is not None:
         c.flags |= CFG_DYNAMIC_GAP
         c.gap_col = gap_col

@@ -70,7 +70,22 @@ struct DevStatus {
     int32_t pad;                // host-side scratch (straggler count copy)
     int32_t pad2;
     unsigned long long sess_live;  // sessions: in-flight sessions (rows a fire can emit at most)
+    unsigned long long drop_n;     // FWA_CFG_LATE_INDICES: entries in the dropped-record index list this push
 };
+
+// FWA_CFG_LATE_INDICES: record index of a late-dropped record (lateDataOutputTag / lateRecordsDroppedRate),
+// appended with one reservation per wave; list capacity = the push's record count.
+__device__ __forceinline__ void note_drop(int32_t* list, DevStatus* st, bool drop, int64_t i) {
+    if (!list) return;
+    const unsigned long long m = __ballot(drop);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    const int ld = __ffsll((long long)m) - 1;
+    unsigned long long b = 0;
+    if (lane == ld) b = atomicAdd(&st->drop_n, (unsigned long long)__popcll(m));
+    b = __shfl(b, ld);
+    if (drop) list[b + __popcll(m & ((1ull << lane) - 1))] = (int32_t)i;
+}
 
 enum AccKind : int32_t { ACC_NONE = 0, ACC_ADD_I64 = 1, ACC_ADD_F64 = 2, ACC_MIN_ORD = 3, ACC_MAX_ORD = 4 };
 
@@ -123,6 +138,7 @@ struct IngestArgs {
     unsigned long long* const* slot_base;
     int64_t stride;             // elements per accumulator column
     int64_t spill_cap;          // entries of spill[] and late[] (a store past it raises FWA_E_STATE instead)
+    int32_t* dropidx;           // FWA_CFG_LATE_INDICES: dropped-record indices (nullptr: not collected)
     DevStatus* st;
 };
 
@@ -257,7 +273,7 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         }
         const unsigned long long cadd = a.pcount ? a.pcount[i] : 1ull;   // records this row stands for
         const bool accepted = (e->flags & 2) || a.wm < e->thr;
-        if (!accepted) { dropped += cadd; continue; }
+        if (!accepted) { dropped += cadd; if (a.dropidx && !a.pcount) a.dropidx[atomicAdd(&a.st->drop_n, 1ull)] = (int32_t)i; continue; }
         if (e->slot < 0) {                                      // known slice without slot: replay
             want_insert(a.want, a.st, q);
             const int32_t si = atomicAdd(&a.st->spill_n, 1);
@@ -419,6 +435,7 @@ struct PartArgs {
     int32_t vcol[2];
     int32_t vsize[2];                  // 4 or 8 bytes
     int32_t abl;                       // ablation bits (timing experiments only; 0 in production)
+    int32_t* dropidx;                  // FWA_CFG_LATE_INDICES list (nullptr: not collected)
     DevStatus* st;
     long long* prof;                   // optional per-block phase cycle counters (FWA_PPROF)
 };
@@ -575,6 +592,7 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
             if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
             if (i >= a.n) code = 0xff;
             dropped += code == kCodeDrop;
+            note_drop(a.dropidx, a.st, code == kCodeDrop, i);
             const bool slow = code == kCodeSlow;
             const unsigned long long mk = __ballot(slow);
             if (mk) {
@@ -806,6 +824,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
             if (i >= a.n) code = 0xff;
             dropped += code == kCodeDrop;
+            note_drop(a.dropidx, a.st, code == kCodeDrop, i);
             const bool slow = code == kCodeSlow;
             const unsigned long long mk = __ballot(slow);
             if (mk) {
@@ -1619,6 +1638,7 @@ struct Sess2Args {
     unsigned long long* lr_n;
     int64_t lr_cap;
     SessCtr* ctr;
+    int32_t* dropidx;            // FWA_CFG_LATE_INDICES list (nullptr: not collected)
     DevStatus* st;
 };
 
@@ -1905,7 +1925,10 @@ __global__ void __launch_bounds__(kBlock) sess2_ordered_kernel(Sess2Args a, cons
                 }
                 // Table: every skipped record counts (WindowOperator.java:386-389); DataStream: only if
                 // isElementLate (WindowOperator.java:425-433, :597-601)
-                if (table || jm::wadd(ts, a.lateness) <= a.wm) ++dropped;
+                if (table || jm::wadd(ts, a.lateness) <= a.wm) {
+                    ++dropped;
+                    if (a.dropidx) a.dropidx[atomicAdd(&a.st->drop_n, 1ull)] = (int32_t)r;
+                }
                 continue;
             }
             if (act < 0) {                                      // new self-contained session
@@ -2213,6 +2236,10 @@ struct fwa_engine {
     int32_t* d_replay = nullptr;
     int64_t replay_cap = 0;
     int32_t* d_late = nullptr;        // deferred late-firing record indices (spill_cap entries)
+    // FWA_CFG_LATE_INDICES: indices of the records the last settled push dropped as late
+    int32_t* d_dropidx = nullptr;
+    int64_t dropidx_cap = 0;
+    std::vector<int32_t> late_idx;
     // rows fired inside fwa_push (late firings), returned by the next fwa_advance_watermark
     int64_t late_rows = 0, lr_cap = 0;
     int64_t* lr_col[3 + FWA_MAX_AGGS] = {};
@@ -2366,7 +2393,7 @@ int validate(const fwa_config* c) {
         default:
             return FWA_E_ARG;
     }
-    if (c->flags & ~FWA_CFG_DYNAMIC_GAP) return FWA_E_ARG;
+    if (c->flags & ~(FWA_CFG_DYNAMIC_GAP | FWA_CFG_LATE_INDICES)) return FWA_E_ARG;
     if ((c->flags & FWA_CFG_DYNAMIC_GAP) && (c->window_kind != FWA_SESSION || c->gap_col < 0 || c->gap_col >= FWA_MAX_COLS))
         return FWA_E_ARG;
     if (c->tz_n < 0 || (c->tz_n > 0 && !c->tz)) return FWA_E_ARG;
@@ -2670,7 +2697,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n, e->d_reset_list, e->d_upos,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -3012,6 +3039,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.part_bits = e->part_bits;
     pa.np = e->np;
     for (int v = 0; v < 2; ++v) { pa.vcol[v] = e->vcol[v]; pa.vsize[v] = e->vsize[v]; }
+    pa.dropidx = a.dropidx;
     pa.st = e->d_st;
     static const int pabl = getenv("FWA_PABL") ? atoi(getenv("FWA_PABL")) : 0;
     pa.abl = pabl;
@@ -3228,6 +3256,7 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     for (int j = 0; j < e->cfg.num_aggs; ++j)
         if (e->ec.agg[j].acc > 0 && !e->ec.agg[j].alias) s.col_owner[e->ec.agg[j].acc] = j;
     s.ctr = e->d_sctr;
+    s.dropidx = a.dropidx;
     s.st = e->d_st;
     HIPCHK(e, hipEventRecord(e->ev[0], e->stream));
     if (n > 0) sess2_classify_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(s, e->d_ec);
@@ -3554,6 +3583,16 @@ static int emit_late_rows(fwa_engine* e) {
     return FWA_OK;   // the caller clears late_rows once the output is final
 }
 
+// FWA_CFG_LATE_INDICES: fetch the dropped-record indices of the push just settled (ascending).
+static int collect_late_indices(fwa_engine* e) {
+    unsigned long long m = 0;
+    HIPCHK(e, hipMemcpy(&m, &e->d_st->drop_n, 8, hipMemcpyDeviceToHost));
+    e->late_idx.resize((size_t)m);
+    if (m) HIPCHK(e, hipMemcpy(e->late_idx.data(), e->d_dropidx, 4 * (size_t)m, hipMemcpyDeviceToHost));
+    std::sort(e->late_idx.begin(), e->late_idx.end());
+    return FWA_OK;
+}
+
 // Shared ingest driver: two-phase path when allowed, else the v1 kernel; slice-miss replays;
 // lookahead slice allocation; stats.
 static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, bool status_enqueued,
@@ -3671,6 +3710,7 @@ static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, boo
             if (!e->live.count(q)) { rc = alloc_slice(e, q); if (rc) return rc; republish = true; }
     }
     if (republish) { rc = publish_dir(e); if (rc) return rc; }
+    if (a.dropidx) { rc = collect_late_indices(e); if (rc) return rc; }
     e->records_in += n;
     e->late_dropped += dropped;
     if (late_dropped_out) *late_dropped_out = dropped;
@@ -3684,12 +3724,23 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
     if (e->cfg.key_kind == FWA_KEY_PREHASHED && n > 0 && !key_hash) return fail(e, FWA_E_ARG, "PREHASHED keys need key_hash");
     if (n > INT32_MAX) return fail(e, FWA_E_ARG, "batch too large (max 2^31-1 records)");
     if (late_dropped_out) *late_dropped_out = 0;
-    if (n == 0) return FWA_OK;
+    if (n == 0) { e->late_idx.clear(); return FWA_OK; }
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
     IngestArgs a;
     memset(&a, 0, sizeof(a));
     a.n = n;
+    e->late_idx.clear();
+    if (e->cfg.flags & FWA_CFG_LATE_INDICES) {        // one index per dropped record at most
+        if (n > e->dropidx_cap) {
+            if (e->d_dropidx) HIPCHK(e, hipFree(e->d_dropidx));
+            e->d_dropidx = nullptr;
+            HIPCHK(e, hipMalloc(&e->d_dropidx, sizeof(int32_t) * (size_t)n));
+            e->dropidx_cap = n;
+        }
+        HIPCHK(e, hipMemsetAsync(&e->d_st->drop_n, 0, 8, e->stream));
+        a.dropidx = e->d_dropidx;
+    }
     a.wm = e->wm;
     if (flags & FWA_PUSH_DEVICE_PTRS) {
         if (int rc1 = wait_input_stream(e)) return rc1;
@@ -3732,6 +3783,7 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
                               : err == FWA_E_ARG ? "Dynamic session time gap must satisfy 0 < gap"
                                                    : "key table full: raise fwa_config.key_capacity");
         }
+        if (a.dropidx) { int rc2 = collect_late_indices(e); if (rc2) return rc2; }
         e->records_in += n;
         e->late_dropped += dropped;
         if (late_dropped_out) *late_dropped_out = dropped;
@@ -3748,12 +3800,23 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
     if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "partials need a computable key hash");
     if (n > INT32_MAX) return fail(e, FWA_E_ARG, "batch too large (max 2^31-1 records)");
     if (late_dropped_out) *late_dropped_out = 0;
-    if (n == 0) return FWA_OK;
+    if (n == 0) { e->late_idx.clear(); return FWA_OK; }
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
     IngestArgs a;
     memset(&a, 0, sizeof(a));
     a.n = n;
+    e->late_idx.clear();
+    if (e->cfg.flags & FWA_CFG_LATE_INDICES) {        // one index per dropped record at most
+        if (n > e->dropidx_cap) {
+            if (e->d_dropidx) HIPCHK(e, hipFree(e->d_dropidx));
+            e->d_dropidx = nullptr;
+            HIPCHK(e, hipMalloc(&e->d_dropidx, sizeof(int32_t) * (size_t)n));
+            e->dropidx_cap = n;
+        }
+        HIPCHK(e, hipMemsetAsync(&e->d_st->drop_n, 0, 8, e->stream));
+        a.dropidx = e->d_dropidx;
+    }
     a.wm = e->wm;
     const void* src[3 + FWA_MAX_AGGS] = {keys, slice_ts, count};
     int nsrc = 3;
@@ -4386,6 +4449,15 @@ int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
     s->fire_rows = e->fire_rows;
     s->partition_ms = e->partition_ms;
     s->combine_ms = e->combine_ms;
+    return FWA_OK;
+}
+
+int fwa_late_records(fwa_engine* e, const int32_t** idx, int64_t* n) {
+    if (!e || !idx || !n) return FWA_E_ARG;
+    if (!(e->cfg.flags & FWA_CFG_LATE_INDICES)) return fail(e, FWA_E_STATE, "configure FWA_CFG_LATE_INDICES");
+    if (int rc0 = settle_pending(e)) return rc0;
+    *idx = e->late_idx.empty() ? nullptr : e->late_idx.data();
+    *n = (int64_t)e->late_idx.size();
     return FWA_OK;
 }
 

@@ -57,6 +57,8 @@ def lib():
     L.fwa_version.restype = C.c_char_p
     L.fwa_set_input_stream.argtypes = [C.c_void_p, C.c_void_p]
     L.fwa_set_input_stream.restype = C.c_int
+    L.fwa_late_records.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+    L.fwa_late_records.restype = C.c_int
     L.fwa_reset_timers.argtypes = [C.c_void_p]
     L.fwa_reset_timers.restype = C.c_int
     L.fwa_key_groups.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
@@ -255,6 +257,16 @@ class WindowAggregator:
         self._settled()
         _check(rc, self.h)
         return st
+
+    def late_records(self):
+        """Indices (into the last push's batch) of the records it dropped as late (FWA_CFG_LATE_INDICES)."""
+        p, n = C.c_void_p(), C.c_int64()
+        rc = lib().fwa_late_records(self.h, C.byref(p), C.byref(n))
+        self._settled()
+        _check(rc, self.h)
+        if n.value == 0:
+            return np.zeros(0, np.int32)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int32)), shape=(n.value,)).copy()
 
     def reset_timers(self):
         rc = lib().fwa_reset_timers(self.h)

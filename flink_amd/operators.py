@@ -49,24 +49,33 @@ def _col_dtypes(aggs, ncols):
 
 
 class _Base:
-    def __init__(self, spec: WindowSpec, aggs, batch_size=1 << 20, engine_factory=None, **cfg_kw):
+    def __init__(self, spec: WindowSpec, aggs, batch_size=1 << 20, engine_factory=None, track_late=False, **cfg_kw):
         if engine_factory is None:
             from .engine import WindowAggregator
             engine_factory = WindowAggregator
         self.aggs = list(aggs)
         self.ncols = max([c + 1 for n, c in self.aggs if A.AGG_INPUT_DTYPE[n]] + [0])
         self.dtypes = _col_dtypes(self.aggs, self.ncols)
-        self.cfg = A.make_config(aggs=self.aggs, **spec.config_kwargs(), **cfg_kw)
+        self.track_late = track_late
+        self.cfg = A.make_config(aggs=self.aggs, late_indices=track_late, **spec.config_kwargs(), **cfg_kw)
         self.engine = engine_factory(self.cfg)
         self.buf = _Batcher(self.ncols, batch_size)
         self.num_late_records_dropped = 0
+        self.late_records = []                 # (key, values, timestamp) of every record dropped as late
         self.current_watermark = A.LONG_MIN
 
     def _push(self):
         if len(self.buf):
             k, t, c = self.buf.arrays(self.dtypes)
-            self.num_late_records_dropped += self.engine.push(k, t, c)
+            n = self.engine.push(k, t, c)
+            if self.track_late:                # the batch's dropped records, by index (fwa_late_records)
+                for i in self.engine.late_records().tolist():
+                    self.late_records.append((self.buf.keys[i], tuple(col[i] for col in self.buf.cols), self.buf.ts[i]))
+            self._count_late(n)
             self.buf.reset()
+
+    def _count_late(self, n):
+        self.num_late_records_dropped += n
 
     def _add(self, key, ts, values):
         self.buf.add(key, ts, values)
@@ -90,8 +99,15 @@ class WindowOperator(_Base):
     restricted to the engine's built-in aggregates). Emits (key, window_start, window_end, aggs)
     with record timestamp window.maxTimestamp() = window_end - 1 (WindowOperator.java:552-557)."""
 
-    def __init__(self, assigner: WindowSpec, aggs, allowed_lateness_ms=0, **kw):
-        super().__init__(assigner, aggs, allowed_lateness_ms=allowed_lateness_ms, **kw)
+    def __init__(self, assigner: WindowSpec, aggs, allowed_lateness_ms=0, late_data_output=False, **kw):
+        """late_data_output: a lateDataOutputTag is set -- late records go to `late_records` (the side output)
+        instead of numLateRecordsDropped (WindowOperator.java:425-433)."""
+        self.late_data_output = late_data_output
+        super().__init__(assigner, aggs, allowed_lateness_ms=allowed_lateness_ms, track_late=late_data_output, **kw)
+
+    def _count_late(self, n):
+        if not self.late_data_output:
+            self.num_late_records_dropped += n
 
     def process_element(self, key, value_columns, timestamp):
         self._add(key, timestamp, value_columns)
@@ -113,8 +129,15 @@ class SlicingWindowProcessor(_Base):
     def initialize_watermark(self, wm):
         self.current_watermark = wm
 
+    def __init__(self, spec, aggs, **kw):
+        kw.setdefault("track_late", True)
+        super().__init__(spec, aggs, **kw)
+
     def process_element(self, key, row_values, rowtime):
-        """Returns False: drops are reported per batch through num_late_records_dropped."""
+        """The reference returns true for a dropped late record and SlicingWindowOperator marks
+        lateRecordsDroppedRate (SlicingWindowOperator.java:222-226). Records are applied in batches, so the
+        GPU processor owns that metric instead: num_late_records_dropped counts them and late_records lists
+        them (per-push indices from fwa_late_records) once the batch is pushed; this returns False."""
         self._add(key, rowtime, row_values)
         return False
 

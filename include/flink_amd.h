@@ -145,6 +145,10 @@ typedef struct fwa_config {
 #define FWA_CFG_DYNAMIC_GAP 0x1  /* SESSION: per-record gap from value column gap_col -- DynamicEventTimeSessionWindows
                                   * with a SessionWindowTimeGapExtractor (DynamicEventTimeSessionWindows.java:57-68);
                                   * a gap <= 0 raises FWA_E_ARG like the assigner's IllegalArgumentException */
+#define FWA_CFG_LATE_INDICES 0x2 /* collect, per push, the indices of the records dropped as late (fwa_late_records):
+                                  * WindowOperator's lateDataOutputTag side output (WindowOperator.java:425-433) and the
+                                  * per-record processElement() == true of SlicingWindowProcessor
+                                  * (SlicingWindowOperator.java:222-226, lateRecordsDroppedRate) */
 
 typedef struct fwa_out {
     int64_t n_rows;
@@ -271,6 +275,13 @@ void fwa_blob_free(fwa_blob* b);
  * MIN of the snapshots' watermarks (SlicingWindowOperator.initializeState :186-202). Windows that
  * fired before the snapshot do not fire again. */
 int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, int32_t n_blobs);
+
+/* FWA_CFG_LATE_INDICES: indices (ascending, into the last push's batch) of the records that push dropped as
+ * late -- the records WindowOperator would send to its lateDataOutputTag side output, and those for which
+ * SlicingWindowProcessor.processElement returns true. Valid until the next call on the handle; for an
+ * FWA_PUSH_ASYNC push, available once it is settled (this call settles it). Replaces
+ * WindowOperator.sideOutput (WindowOperator.java:425-433, :559-567). */
+int fwa_late_records(fwa_engine* e, const int32_t** idx, int64_t* n);
 
 /* Reset the kernel timing counters of fwa_stats (bench warm-up). */
 int fwa_reset_timers(fwa_engine* e);

@@ -312,6 +312,7 @@ typedef struct or_engine {
     int out_ret;   /* the rows were returned by the last or_advance_watermark: clear at the next call */
     int64_t *o_key, *o_start, *o_end; aval* o_agg[FWA_MAX_AGGS];
     fwa_stats st;
+    int32_t* late_idx; int64_t late_n, late_cap;   /* records the last or_push dropped as late */
     char err[256];
 } or_engine;
 
@@ -449,6 +450,7 @@ void or_destroy(or_engine* e) {
     if (!e) return;
     hm_free(&e->state); th_free(&e->timers); hm_free(&e->wl_head);
     if (e->c.tz_n > 0) free((void*)e->c.tz);
+    free(e->late_idx);
     free(e->pool); free(e->free_list);
     free(e->wl_key); free(e->wl_start); free(e->wl_end); free(e->wl_sws); free(e->wl_sw_end); free(e->wl_next);
     free(e->o_key); free(e->o_start); free(e->o_end);
@@ -725,6 +727,8 @@ static void tb_fire(or_engine* e, int64_t key, int64_t window_end) {  /* Slicing
 int or_push(or_engine* e, const int64_t* keys, const int64_t* ts, const void* const* cols,
             const int32_t* key_hash, int64_t n, int64_t* late_dropped_out) {
     int64_t dropped = 0;
+    e->late_n = 0;
+    if (n > e->late_cap) { e->late_cap = n; e->late_idx = (int32_t*)realloc(e->late_idx, 4 * (size_t)n); }
     /* rows fired inside processElement (late firings, EventTimeTrigger.onElement :37-45) are kept and
        returned with the next or_advance_watermark, as the engine does */
     if (e->out_ret) { e->out_n = 0; e->out_ret = 0; }
@@ -743,14 +747,15 @@ int or_push(or_engine* e, const int64_t* keys, const int64_t* ts, const void* co
             int skipped = 1;
             int rc = ds_process_element_session(e, keys[i], ts[i], cols, i, &skipped);
             if (rc) return rc;
-            if (skipped) {
-                if (e->c.semantics == FWA_SEM_TABLE) dropped++;   /* TR WindowOperator.java:386-389: every dropped row */
-                else if (jladd(ts[i], e->c.allowed_lateness_ms) <= e->wm) dropped++;   /* isElementLate :597-601 */
+            if (skipped && (e->c.semantics == FWA_SEM_TABLE ||                /* TR WindowOperator.java:386-389 */
+                            jladd(ts[i], e->c.allowed_lateness_ms) <= e->wm)) {   /* isElementLate :597-601 */
+                dropped++;
+                e->late_idx[e->late_n++] = (int32_t)i;
             }
             continue;
         }
         if (e->c.semantics == FWA_SEM_TABLE) {
-            dropped += tb_process_element(e, keys[i], ts[i], cols, i);
+            if (tb_process_element(e, keys[i], ts[i], cols, i)) { dropped++; e->late_idx[e->late_n++] = (int32_t)i; }
             continue;
         }
         if (ts[i] == J_LONG_MIN) return set_err(e, FWA_E_TS_MIN, "Record has Long.MIN_VALUE timestamp (= no timestamp marker).");
@@ -760,12 +765,18 @@ int or_push(or_engine* e, const int64_t* keys, const int64_t* ts, const void* co
             if (nw < 0) return set_err(e, nw, "window assignment failed");
             ds_process_element_aligned(e, keys[i], ts[i], cols, i, wsb, web, nw, &skipped);
         }
-        if (skipped && jladd(ts[i], e->c.allowed_lateness_ms) <= e->wm) dropped++;   /* isElementLate :597-601 */
+        if (skipped && jladd(ts[i], e->c.allowed_lateness_ms) <= e->wm) {   /* isElementLate :597-601 */
+            dropped++;
+            e->late_idx[e->late_n++] = (int32_t)i;
+        }
     }
     e->st.late_dropped += dropped;
     if (late_dropped_out) *late_dropped_out = dropped;
     return FWA_OK;
 }
+
+/* indices of the records the last or_push dropped as late (sideOutput / processElement() == true) */
+int or_late_records(or_engine* e, const int32_t** idx, int64_t* n) { *idx = e->late_idx; *n = e->late_n; return FWA_OK; }
 
 int or_advance_watermark(or_engine* e, int64_t wm, fwa_out* out) {
     if (e->out_ret) { e->out_n = 0; e->out_ret = 0; }

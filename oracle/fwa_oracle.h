@@ -41,6 +41,7 @@ int64_t or_tz_timer(const fwa_config* cfg, int64_t local);
 /* ---- streaming operator restatement ---- */
 typedef struct or_engine or_engine;
 int or_create(const fwa_config* cfg, or_engine** out);
+int or_late_records(or_engine* e, const int32_t** idx, int64_t* n);
 void or_destroy(or_engine* e);
 /* Same contract as fwa_push / fwa_advance_watermark (host pointers only). */
 int or_push(or_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,

@@ -49,6 +49,8 @@ def lib():
         L.or_assign_windows.restype = C.c_int
         L.or_assign_slice_end.argtypes = [C.POINTER(A.Config), C.c_int64]
         L.or_assign_slice_end.restype = C.c_int64
+        L.or_late_records.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+        L.or_late_records.restype = C.c_int
         for f in ("or_to_local", "or_tz_timer"):
             getattr(L, f).argtypes = [C.POINTER(A.Config), C.c_int64]
             getattr(L, f).restype = C.c_int64
@@ -118,6 +120,14 @@ class Oracle:
         if rc:
             raise OracleError(rc, lib().or_last_error(self.h).decode())
         return dropped.value
+
+    def late_records(self):
+        """Indices of the records the last push dropped as late (ascending)."""
+        p, n = C.c_void_p(), C.c_int64()
+        lib().or_late_records(self.h, C.byref(p), C.byref(n))
+        if n.value == 0:
+            return np.zeros(0, np.int32)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int32)), shape=(n.value,)).copy()
 
     def advance_watermark(self, wm):
         out = A.Out()

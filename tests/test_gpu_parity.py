@@ -479,3 +479,24 @@ def test_shift_time_zone_streams_vs_oracle(eng_mod, zone, kind, size, slide):
             batches.append((keys[sl], ts[sl], [vi[sl]], int(ts[sl].max()) - 600_001))
     batches.append((batches[0][0][:0], batches[0][1][:0], [batches[0][2][0][:0]], A.LONG_MAX))
     run_pair(cfg, batches, eng_mod.WindowAggregator, Oracle, names)
+
+
+@pytest.mark.parametrize("ci", range(len(CONFIGS)))
+def test_late_record_indices_vs_oracle(eng_mod, ci):
+    """FWA_CFG_LATE_INDICES: per push, exactly the records the reference drops as late (the ones WindowOperator
+    sends to lateDataOutputTag, and SlicingWindowProcessor.processElement returns true for)."""
+    from oracle.oracle import Oracle
+    cfg = A.make_config(aggs=I64_AGGS, key_capacity=4096, late_indices=True, **CONFIGS[ci])
+    g, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
+    total = 0
+    for k, t, cols, wm in batches_of(random_stream(900 + ci, 30_000, 500, 50_000, 1500, late_frac=0.05), 10, 1500):
+        dg, do = g.push(k, t, cols), o.push(k, t, cols)
+        lg, lo = g.late_records(), o.late_records()
+        assert dg == do == len(lg) == len(lo)
+        assert np.array_equal(lg, lo)
+        total += dg
+        g.advance_watermark(wm)
+        o.advance_watermark(wm)
+    assert total > 0
+    g.close()
+    o.close()

@@ -55,3 +55,33 @@ def test_slicing_processor_facade_hopping_kat():
     assert proc.num_late_records_dropped == case["late_dropped"]
     proc.prepare_checkpoint()
     proc.close()
+
+
+def test_window_operator_side_output_of_late_records():
+    """lateDataOutputTag set: the late record goes to the side output, not to numLateRecordsDropped
+    (WindowOperatorTest.testSideOutputDueToLatenessTumbling, WindowOperator.java:425-433)."""
+    case = KATS["WindowOperatorTest.testSideOutputDueToLatenessTumbling"]
+    op = WindowOperator(TumblingEventTimeWindows.of(case["size_ms"]), [("SUM_I64", 0)], batch_size=1,
+                        engine_factory=Oracle, late_data_output=True)
+    late = []
+    for ev in case["events"]:
+        if ev[0] == "e":
+            op.process_element(ev[1], [ev[2]], ev[3])
+        else:
+            op.process_watermark(ev[1])
+    assert op.num_late_records_dropped == 0
+    assert len(op.late_records) == case["late_dropped"] > 0
+    op.close()
+
+
+def test_slicing_processor_lists_dropped_records():
+    case = KATS["SlicingWindowAggOperatorTest.testEventTimeHoppingWindows"]
+    proc = SlicingWindowProcessor(SliceAssigners.hopping(3000, 1000), [("SUM_I64", 0), ("COUNT", 0)],
+                                  batch_size=1, engine_factory=Oracle).open()
+    for ev in case["events"]:
+        if ev[0] == "e":
+            proc.process_element(ev[1], [ev[2]], ev[3])
+        else:
+            proc.advance_progress(ev[1])
+    assert [(k, ts) for k, _, ts in proc.late_records] == [(1, 2999)]   # "late for all assigned windows"
+    proc.close()
