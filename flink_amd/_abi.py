@@ -20,20 +20,20 @@ KEY_JAVA_LONG, KEY_BINROW_BIGINT, KEY_PREHASHED = 0, 1, 2
 AGG_KINDS = {
     "COUNT": 0, "SUM_I64": 1, "SUM_F32": 2, "SUM_F64": 3, "MIN_I64": 4, "MAX_I64": 5,
     "MIN_F32": 6, "MAX_F32": 7, "MIN_F64": 8, "MAX_F64": 9, "AVG_I64": 10, "AVG_F32": 11,
-    "AVG_F64": 12,
+    "AVG_F64": 12, "COUNT_COL": 13,
 }
 AGG_NAMES = {v: k for k, v in AGG_KINDS.items()}
 # numpy dtype of each aggregate's RESULT column
 AGG_RESULT_DTYPE = {
     "COUNT": "i8", "SUM_I64": "i8", "SUM_F32": "f4", "SUM_F64": "f8", "MIN_I64": "i8",
     "MAX_I64": "i8", "MIN_F32": "f4", "MAX_F32": "f4", "MIN_F64": "f8", "MAX_F64": "f8",
-    "AVG_I64": "i8", "AVG_F32": "f4", "AVG_F64": "f8",
+    "AVG_I64": "i8", "AVG_F32": "f4", "AVG_F64": "f8", "COUNT_COL": "i8",
 }
 # numpy dtype of each aggregate's INPUT column (None: no input)
 AGG_INPUT_DTYPE = {
     "COUNT": None, "SUM_I64": "i8", "SUM_F32": "f4", "SUM_F64": "f8", "MIN_I64": "i8",
     "MAX_I64": "i8", "MIN_F32": "f4", "MAX_F32": "f4", "MIN_F64": "f8", "MAX_F64": "f8",
-    "AVG_I64": "i8", "AVG_F32": "f4", "AVG_F64": "f8",
+    "AVG_I64": "i8", "AVG_F32": "f4", "AVG_F64": "f8", "COUNT_COL": None,
 }
 
 STATUS = {0: "OK", -1: "E_ARG", -2: "E_TS_MIN", -3: "E_KEYGROUP", -4: "E_MERGE_LATE", -5: "E_OOM",
@@ -61,7 +61,7 @@ class Config(C.Structure):
         ("max_parallelism", C.c_int32), ("kg_start", C.c_int32), ("kg_end", C.c_int32),
         ("num_aggs", C.c_int32), ("aggs", AggSpec * FWA_MAX_AGGS), ("device", C.c_int32),
         ("output_on_device", C.c_int32), ("key_capacity", C.c_int64), ("max_batch", C.c_int64),
-        ("flags", C.c_int32), ("gap_col", C.c_int32), ("tz_n", C.c_int32), ("reserved", C.c_int32),
+        ("flags", C.c_int32), ("gap_col", C.c_int32), ("tz_n", C.c_int32), ("nullable_cols", C.c_int32),
         ("tz", C.c_void_p),
     ]
 
@@ -70,7 +70,7 @@ class Out(C.Structure):
     _fields_ = [
         ("n_rows", C.c_int64), ("on_device", C.c_int32), ("num_aggs", C.c_int32),
         ("key", C.c_void_p), ("win_start", C.c_void_p), ("win_end", C.c_void_p),
-        ("agg", C.c_void_p * FWA_MAX_AGGS),
+        ("agg", C.c_void_p * FWA_MAX_AGGS), ("agg_null", C.c_void_p * FWA_MAX_AGGS),
     ]
 
 
@@ -104,7 +104,8 @@ class GenParams(C.Structure):
 def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, slide_ms=0,
                 offset_ms=0, gap_ms=0, allowed_lateness_ms=0, aggs=(("COUNT", 0), ("SUM_I64", 0)),
                 key_kind=KEY_JAVA_LONG, max_parallelism=128, kg_start=0, kg_end=None, device=0,
-                output_on_device=0, key_capacity=0, max_batch=0, gap_col=None, tz=None, late_indices=False):
+                output_on_device=0, key_capacity=0, max_batch=0, gap_col=None, tz=None, late_indices=False,
+                nullable_cols=()):
     """Build a Config struct. aggs: sequence of (agg name, value-column index). gap_col: value column of
     per-record session gaps (DynamicEventTimeSessionWindows). tz: [(utc_instant_ms, offset_ms), ...] shift
     time zone of a TIMESTAMP_LTZ rowtime (the struct keeps a pointer to a buffer held on the struct)."""
@@ -130,6 +131,8 @@ def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, sl
     c.max_batch = max_batch
     if late_indices:
         c.flags |= CFG_LATE_INDICES
+    for col in nullable_cols:                             # value columns that may hold SQL NULLs
+        c.nullable_cols |= 1 << col
     if gap_col is not None:
         c.flags |= CFG_DYNAMIC_GAP
         c.gap_col = gap_col

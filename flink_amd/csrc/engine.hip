@@ -97,16 +97,19 @@ struct AggDesc {
     int32_t vslot;              // partitioned path: which carried value column feeds this aggregate
     int32_t alias;              // 1: shares the accumulator column of an earlier aggregate (e.g. SUM(d) and
                                 // AVG(d) keep one double sum): read at fire, never updated through it
+    int32_t nn;                 // accumulator column counting the non-NULL inputs of a nullable column (0: none)
 };
+constexpr int kMaxAggsInt = FWA_MAX_AGGS + FWA_MAX_COLS;   // user aggregates + hidden non-NULL counters
 
 struct EngineConst {
     jm::UDiv64 g_div;           // slice size
     int64_t g, off;
     int32_t sem, lateness_pos;  // lateness_pos: DataStream allowed lateness > 0
     int32_t key_kind, max_par, kg_lo, kg_hi;
-    int32_t naggs, nacc;        // nacc = 1 (count) + stateful agg columns
-    AggDesc agg[FWA_MAX_AGGS];
-    int32_t acc_kind[1 + FWA_MAX_AGGS];
+    int32_t naggs, nacc;        // naggs: user + hidden aggregates; nacc = 1 (count) + stateful agg columns
+    int32_t nout, nullable;     // nout: user aggregates (output columns); nullable: fwa_config.nullable_cols
+    AggDesc agg[kMaxAggsInt];
+    int32_t acc_kind[1 + kMaxAggsInt];
     const int64_t* tz;          // shift time zone table (device copy of fwa_config.tz), tz_n pairs
     int32_t tz_n, pad_tz;
 };
@@ -139,6 +142,7 @@ struct IngestArgs {
     int64_t stride;             // elements per accumulator column
     int64_t spill_cap;          // entries of spill[] and late[] (a store past it raises FWA_E_STATE instead)
     int32_t* dropidx;           // FWA_CFG_LATE_INDICES: dropped-record indices (nullptr: not collected)
+    const uint8_t* nulls[FWA_MAX_COLS];   // SQL NULL flags per value column (nullptr: no NULLs)
     DevStatus* st;
 };
 
@@ -224,8 +228,13 @@ __device__ __forceinline__ uint64_t load_ord(const void* col, int64_t i, int kin
     }
 }
 
-// One input value in its accumulator domain (i64 bits, f64 bits, or ordered key).
-__device__ __forceinline__ unsigned long long acc_input(const AggDesc& d, const void* col, int64_t i) {
+// One input value in its accumulator domain (i64 bits, f64 bits, or ordered key). A SQL NULL input (nul[i])
+// contributes the accumulator's identity; a hidden non-NULL counter (COUNT_COL) contributes 1 or 0.
+__device__ __forceinline__ unsigned long long acc_input(const AggDesc& d, const void* col, int64_t i,
+                                                        const uint8_t* nul = nullptr) {
+    const bool isnull = nul && nul[i];
+    if (d.kind == FWA_COUNT_COL) return isnull ? 0ull : 1ull;
+    if (isnull) return d.acc_kind == ACC_MIN_ORD ? ~0ull : 0ull;
     switch (d.acc_kind) {
         case ACC_ADD_I64: return ((const unsigned long long*)col)[i];
         case ACC_ADD_F64: {
@@ -241,7 +250,7 @@ template <bool kIdx>
 __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
     const int lane = threadIdx.x & 63;
-    __shared__ unsigned long long s_red[kBlock / 64][1 + FWA_MAX_AGGS];   // hot-key group reduction
+    __shared__ unsigned long long s_red[kBlock / 64][1 + kMaxAggsInt];   // hot-key group reduction
     const int64_t stride_grid = (int64_t)gridDim.x * blockDim.x;
     unsigned long long qmax = 0, qmin = ~0ull;
     unsigned long long dropped = 0;
@@ -312,7 +321,7 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
                     for (int j = 0; j < c.naggs; ++j) {
                         const AggDesc dsc = c.agg[j];
                         if (dsc.acc == 0 || dsc.alias) continue;
-                        r[dsc.acc] = a.pcount ? ((const unsigned long long*)a.cols[j])[i] : acc_input(dsc, a.cols[dsc.col], i);
+                        r[dsc.acc] = a.pcount ? ((const unsigned long long*)a.cols[j])[i] : acc_input(dsc, a.cols[dsc.col], i, a.nulls[dsc.col]);
                     }
                 }
                 __threadfence_block();
@@ -323,7 +332,7 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
                         const AggDesc dsc = c.agg[j];
                         if (dsc.acc == 0 || dsc.alias) continue;
                         const unsigned long long x = a.pcount ? ((const unsigned long long*)a.cols[j])[i]
-                                                              : acc_input(dsc, a.cols[dsc.col], i);
+                                                              : acc_input(dsc, a.cols[dsc.col], i, a.nulls[dsc.col]);
                         unsigned long long* rp = &r[dsc.acc];
                         switch (dsc.acc_kind) {
                             case ACC_ADD_I64: atomicAdd(rp, x); break;
@@ -357,13 +366,13 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         }
         atomicAdd(&base[kid], cadd);                            // COUNT(*)
 #pragma unroll
-        for (int j = 0; j < FWA_MAX_AGGS; ++j) {
+        for (int j = 0; j < kMaxAggsInt; ++j) {
             if (j >= c.naggs) break;
             const AggDesc dsc = c.agg[j];
             if (dsc.acc == 0 || dsc.alias) continue;
             unsigned long long* col = base + (int64_t)dsc.acc * a.stride + kid;
             const unsigned long long x = a.pcount ? ((const unsigned long long*)a.cols[j])[i]   // accumulator
-                                                  : acc_input(dsc, a.cols[dsc.col], i);
+                                                  : acc_input(dsc, a.cols[dsc.col], i, a.nulls[dsc.col]);
             switch (dsc.acc_kind) {
                 case ACC_ADD_I64: atomicAdd(col, x); break;
                 case ACC_ADD_F64: atomicAdd((double*)col, __longlong_as_double((long long)x)); break;
@@ -436,9 +445,18 @@ struct PartArgs {
     int32_t vsize[2];                  // 4 or 8 bytes
     int32_t abl;                       // ablation bits (timing experiments only; 0 in production)
     int32_t* dropidx;                  // FWA_CFG_LATE_INDICES list (nullptr: not collected)
+    const uint8_t* nulls[FWA_MAX_COLS];   // SQL NULL flags of the push (records with a NULL take the v1 path)
+    int32_t any_null;                  // some nulls[] is set
     DevStatus* st;
     long long* prof;                   // optional per-block phase cycle counters (FWA_PPROF)
 };
+
+__device__ __forceinline__ bool row_has_null(const PartArgs& a, int64_t i) {
+    bool r = false;
+#pragma unroll
+    for (int col = 0; col < FWA_MAX_COLS; ++col) r = r || (a.nulls[col] && a.nulls[col][i]);
+    return r;
+}
 
 __device__ __forceinline__ unsigned long long load_raw(const void* col, int64_t i, int size) {
     return size == 4 ? (unsigned long long)((const uint32_t*)col)[i] : ((const unsigned long long*)col)[i];
@@ -589,6 +607,7 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
                 if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;
             }
             if (ds && ts == LONG_MIN_J) code = kCodeSlow;
+            if (a.any_null && i < a.n && row_has_null(a, i)) code = kCodeSlow;   // SQL NULLs: the v1 path
             if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
             if (i >= a.n) code = 0xff;
             dropped += code == kCodeDrop;
@@ -821,6 +840,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;
             }
             if (ds && ts == LONG_MIN_J) code = kCodeSlow;
+            if (a.any_null && i < a.n && row_has_null(a, i)) code = kCodeSlow;   // SQL NULLs: the v1 path
             if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
             if (i >= a.n) code = 0xff;
             dropped += code == kCodeDrop;
@@ -979,7 +999,7 @@ __device__ __forceinline__ void strag_apply(const CombineArgs& a, const EngineCo
     for (int jj = 0; jj < c.naggs; ++jj) {
         const AggDesc d = c.agg[jj];
         if (d.acc == 0 || d.alias) continue;
-        const unsigned long long raw = d.vslot == 0 ? a.b_val0[o] : a.b_val1[o];
+        const unsigned long long raw = d.kind == FWA_COUNT_COL ? 1ull : d.vslot == 0 ? a.b_val0[o] : a.b_val1[o];
         unsigned long long* gp = base + (int64_t)d.acc * a.stride + g;
         switch (d.acc_kind) {
             case ACC_ADD_I64: atomicAdd(gp, raw); break;
@@ -1022,7 +1042,7 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
     const int seg = 1 << a.seg_log;
     const uint32_t smask = (uint32_t)seg - 1u;
     const int nacc = LAYOUT == 1 ? 2 : (LAYOUT == 2 ? 1 : c.nacc);
-    __shared__ int s_desc[FWA_MAX_AGGS + 1];   // generic layout: per column kind | vslot << 8 | input kind << 16
+    __shared__ int s_desc[kMaxAggsInt + 1];   // generic layout: per column kind | vslot << 8 | input kind << 16
     if (LAYOUT == 0 && tid == 0) {
         for (int j = 0; j < c.naggs; ++j)
             if (c.agg[j].acc > 0 && !c.agg[j].alias) s_desc[c.agg[j].acc] = c.agg[j].acc_kind | (c.agg[j].vslot << 8) | (c.agg[j].kind << 16);
@@ -1230,8 +1250,9 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
                 for (int cc = 1; cc < nacc; ++cc) {
                     const int d = s_desc[cc];
                     unsigned long long* lp = &lacc[(size_t)(cc - 1) * SL * seg + (size_t)w * seg + local];
-                    const unsigned long long raw = (NV > 1 && ((d >> 8) & 0xff) != 0) ? x1[j] : x0[j];
                     const int ik = d >> 16;
+                    const unsigned long long raw = ik == FWA_COUNT_COL ? 1ull   // non-NULL counter (NULL rows take the v1 path)
+                                                 : (NV > 1 && ((d >> 8) & 0xff) != 0) ? x1[j] : x0[j];
                     switch (d & 0xff) {
                         case ACC_ADD_I64: atomicAdd(lp, raw); break;
                         case ACC_ADD_F64: atomicAdd((double*)lp, carried_f64(raw, ik)); break;
@@ -1286,6 +1307,7 @@ struct FireArgs {
     int64_t* o_start;
     int64_t* o_end;
     void* o_agg[FWA_MAX_AGGS];
+    uint8_t* o_null[FWA_MAX_AGGS];   // SQL NULL flags per nullable aggregate (nullptr otherwise)
     int64_t* o_count;           // partial mode: COUNT(*) per row
     int32_t raw;                // 1: emit accumulators (fwa_drain_partials), not results
     int64_t out_cap;            // rows past it are counted but not written (the host grows and relaunches)
@@ -1296,11 +1318,26 @@ constexpr int kFireJ = 16;                        // keys per thread per block: 
 
 // Final value of one aggregate (AggregateFunction.getResult / SQL getValueExpression) from its
 // accumulator column value x (i64 sum bits, f64 sum bits or an ordered MIN/MAX key) and COUNT.
-__device__ __forceinline__ void write_agg(const AggDesc& d, uint64_t cnt, unsigned long long x, void* out, int64_t row) {
+__device__ __forceinline__ int type_size_dev(int kind) {
+    return (kind == FWA_SUM_F32 || kind == FWA_MIN_F32 || kind == FWA_MAX_F32 || kind == FWA_AVG_F32) ? 4 : 8;
+}
+
+// SQL NULLs (nn = the window's non-NULL input count of a nullable aggregate, d.nn > 0): SUM/MIN/MAX/AVG of
+// no non-NULL input is NULL (nul[row] = 1, value 0); AVG divides by the non-NULL count (AvgAggFunction).
+__device__ __forceinline__ void write_agg(const AggDesc& d, uint64_t cnt, unsigned long long x, uint64_t nn, void* out,
+                                          uint8_t* nul, int64_t row) {
+    const bool isnull = d.nn > 0 && d.kind != FWA_COUNT && d.kind != FWA_COUNT_COL && nn == 0;
+    if (nul) nul[row] = isnull ? 1 : 0;
+    if (isnull) {
+        if (type_size_dev(d.kind) == 4) ((uint32_t*)out)[row] = 0u; else ((unsigned long long*)out)[row] = 0ull;
+        return;
+    }
+    if (d.nn > 0 && (d.kind == FWA_AVG_I64 || d.kind == FWA_AVG_F32 || d.kind == FWA_AVG_F64)) cnt = nn;
     const int64_t iv = (int64_t)x;
     const double dv = __longlong_as_double((long long)x);
     switch (d.kind) {
         case FWA_COUNT: ((int64_t*)out)[row] = (int64_t)cnt; break;
+        case FWA_COUNT_COL: ((int64_t*)out)[row] = d.acc > 0 ? (int64_t)x : (int64_t)cnt; break;
         case FWA_SUM_I64: ((int64_t*)out)[row] = iv; break;
         case FWA_SUM_F32: ((float*)out)[row] = (float)dv; break;
         case FWA_SUM_F64: ((double*)out)[row] = dv; break;
@@ -1340,17 +1377,20 @@ __device__ __forceinline__ void emit_row(const FireArgs& f, const EngineConst& c
     f.o_start[row] = win.start;
     f.o_end[row] = win.end;
     if (f.o_count) f.o_count[row] = (int64_t)cnt;
-    for (int j = 0; j < c.naggs; ++j) {
+    for (int j = 0; j < c.nout; ++j) {
         const AggDesc d = c.agg[j];
         unsigned long long x = ident_of(d.acc_kind);
+        uint64_t nn = 0;
         if (d.acc > 0)
             for (int s = 0; s < win.nslots; ++s)
                 x = acc_combine(d.acc_kind, x, f.slot_base[f.win_slots[win.slot_off + s]][(int64_t)d.acc * f.stride + k]);
+        if (d.nn > 0)
+            for (int s = 0; s < win.nslots; ++s) nn += f.slot_base[f.win_slots[win.slot_off + s]][(int64_t)d.nn * f.stride + k];
         if (f.raw) {   // partial accumulators (fwa_drain_partials): the accumulator value itself
             ((unsigned long long*)f.o_agg[j])[row] = d.acc > 0 ? x : cnt;
             continue;
         }
-        write_agg(d, cnt, x, f.o_agg[j], row);
+        write_agg(d, cnt, x, nn, f.o_agg[j], f.o_null[j], row);
     }
 }
 
@@ -1424,11 +1464,11 @@ __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineCo
             f.o_start[row] = win.start;
             f.o_end[row] = win.end;
             if (f.o_count) f.o_count[row] = (int64_t)cnt[j];
-            for (int a = 0; a < c.naggs; ++a) {
+            for (int a = 0; a < c.nout; ++a) {   // one stateful column: a nullable aggregate's counter is that column
                 const AggDesc d = c.agg[a];
                 const unsigned long long x = d.acc > 0 ? xs[PRE ? j : 0] : ident_of(d.acc_kind);
                 if (f.raw) ((unsigned long long*)f.o_agg[a])[row] = d.acc > 0 ? x : cnt[j];
-                else write_agg(d, cnt[j], x, f.o_agg[a], row);
+                else write_agg(d, cnt[j], x, d.nn > 0 ? xs[PRE ? j : 0] : 0ull, f.o_agg[a], f.o_null[a], row);
             }
         } else {
             emit_row(f, c, win, k, kvs[j], cnt[j], row);
@@ -1542,12 +1582,12 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
             f.o_key[row] = (k < f.capacity) ? (int64_t)kv[j] : LONG_MIN_J;
             f.o_start[row] = ws;
             f.o_end[row] = ws + f.size;
-            for (int a = 0; a < c.naggs; ++a) {
+            for (int a = 0; a < c.nout; ++a) {   // (no nullable aggregates on this path: the host checks)
                 const AggDesc d = c.agg[a];
                 unsigned long long x = 0;
 #pragma unroll
                 for (int q = 1; q < kSlideAcc; ++q) if (q == d.acc) x = S[j][q];
-                write_agg(d, S[j][0], x, f.o_agg[a], row);
+                write_agg(d, S[j][0], x, 0, f.o_agg[a], nullptr, row);
             }
         }
         __syncthreads();   // woff / s_base reuse
@@ -1601,6 +1641,7 @@ struct Sess2Args {
     const void* cols[FWA_MAX_COLS];
     const int32_t* key_hash;
     const int64_t* gapc;         // per-record gaps (DynamicEventTimeSessionWindows) or nullptr: fixed `gap`
+    const uint8_t* nulls[FWA_MAX_COLS];   // SQL NULL flags per value column (nullptr: no NULLs)
     int64_t n;
     int64_t wm, gap, lateness;
     unsigned long long* key_table;
@@ -1622,7 +1663,7 @@ struct Sess2Args {
     int64_t* bmax;               // [nb] inclusive max of bend over the key so far (segmented scan)
     uint32_t* bcid;              // [nb] head flags, then 1-based cluster ids (inclusive sum)
     int64_t nb;
-    int32_t col_owner[1 + FWA_MAX_AGGS];   // aggregate that feeds accumulator column c (-1: COUNT)
+    int32_t col_owner[1 + kMaxAggsInt];    // aggregate that feeds accumulator column c (-1: COUNT)
     // arrival-order path
     unsigned long long* skey;    // [ns] (kid << 32) | (0 for a session, 1 + record index)
     uint32_t* sval;
@@ -1791,7 +1832,8 @@ __global__ void __launch_bounds__(kBlock) sess2_heads_kernel(Sess2Args a) {
 __device__ __forceinline__ unsigned long long sess_acc_of(const Sess2Args& a, const EngineConst& c, int cc, uint32_t p) {
     if (p & 0x80000000u) return a.in.acc[(int64_t)cc * a.in.stride + (p & 0x7fffffffu)];
     if (cc == 0) return 1ull;
-    return acc_input(c.agg[a.col_owner[cc]], a.cols[c.agg[a.col_owner[cc]].col], (int64_t)p);
+    const AggDesc& d = c.agg[a.col_owner[cc]];
+    return acc_input(d, a.cols[d.col], (int64_t)p, a.nulls[d.col]);
 }
 
 __device__ __forceinline__ void acc_atomic(int acc_kind, unsigned long long* p, unsigned long long v) {
@@ -1940,16 +1982,19 @@ __global__ void __launch_bounds__(kBlock) sess2_ordered_kernel(Sess2Args a, cons
             }
             acc(0, act) += 1ull;                                // windowState.add (AggregateFunction.add)
             for (int cc = 1; cc < nacc; ++cc)
-                acc(cc, act) = acc_combine(c.acc_kind[cc], acc(cc, act), acc_input(c.agg[a.col_owner[cc]], a.cols[c.agg[a.col_owner[cc]].col], r));
+                acc(cc, act) = acc_combine(c.acc_kind[cc], acc(cc, act),
+                                           acc_input(c.agg[a.col_owner[cc]], a.cols[c.agg[a.col_owner[cc]].col], r,
+                                                     a.nulls[c.agg[a.col_owner[cc]].col]));
             if (jm::wsub(se[act], 1) <= a.wm) {                 // EventTimeTrigger.onElement: FIRE at once
                 const unsigned long long row = atomicAdd(a.lr_n, 1ull);
                 if ((int64_t)row >= a.lr_cap) { raise_error(a.st, FWA_E_STATE); continue; }
                 a.lr_key[row] = sess_key_of(a.key_table, a.capacity, kid);
                 a.lr_start[row] = ss[act];
                 a.lr_end[row] = se[act];
-                for (int jj = 0; jj < c.naggs; ++jj) {
+                for (int jj = 0; jj < c.nout; ++jj) {
                     const AggDesc d = c.agg[jj];
-                    write_agg(d, acc(0, act), d.acc > 0 ? acc(d.acc, act) : 0ull, a.lr_agg[jj], (int64_t)row);
+                    write_agg(d, acc(0, act), d.acc > 0 ? acc(d.acc, act) : 0ull, d.nn > 0 ? acc(d.nn, act) : 0ull,
+                              a.lr_agg[jj], nullptr, (int64_t)row);
                 }
             }
         }
@@ -1975,6 +2020,7 @@ struct Sess2FireArgs {
     int64_t* o_start;
     int64_t* o_end;
     void* o_agg[FWA_MAX_AGGS];
+    uint8_t* o_null[FWA_MAX_AGGS];
     int64_t out_cap;
     SessCtr* ctr;
     DevStatus* st;
@@ -2002,9 +2048,10 @@ __global__ void __launch_bounds__(kBlock) sess2_fire_kernel(Sess2FireArgs f, con
                 f.o_start[row] = f.in.start[j];
                 f.o_end[row] = end;
                 const uint64_t cnt = f.in.acc[j];
-                for (int jj = 0; jj < c.naggs; ++jj) {
+                for (int jj = 0; jj < c.nout; ++jj) {
                     const AggDesc d = c.agg[jj];
-                    write_agg(d, cnt, d.acc > 0 ? f.in.acc[(int64_t)d.acc * f.in.stride + j] : 0ull, f.o_agg[jj], (int64_t)row);
+                    write_agg(d, cnt, d.acc > 0 ? f.in.acc[(int64_t)d.acc * f.in.stride + j] : 0ull,
+                              d.nn > 0 ? f.in.acc[(int64_t)d.nn * f.in.stride + j] : 0ull, f.o_agg[jj], f.o_null[jj], (int64_t)row);
                 }
             }
         }
@@ -2098,7 +2145,7 @@ __global__ void __launch_bounds__(64) late_fire_kernel(LateArgs L, const EngineC
             L.o_key[nrow] = key;
             L.o_start[nrow] = ws;
             L.o_end[nrow] = we;
-            for (int j = 0; j < c.naggs; ++j) write_agg(c.agg[j], cnt, acc[j], L.o_agg[j], (int64_t)nrow);
+            for (int j = 0; j < c.nout; ++j) write_agg(c.agg[j], cnt, acc[j], 0, L.o_agg[j], nullptr, (int64_t)nrow);   // DataStream: no NULLs
             ++nrow;
         }
     }
@@ -2256,6 +2303,7 @@ struct fwa_engine {
     int64_t* o_start = nullptr;
     int64_t* o_end = nullptr;
     void* o_agg[FWA_MAX_AGGS] = {};
+    uint8_t* o_null[FWA_MAX_AGGS] = {};   // SQL NULL flags of the nullable aggregates' output columns
     std::vector<char> h_out;
     FireWindow* d_win = nullptr;
     int32_t win_cap = 0;
@@ -2343,7 +2391,7 @@ int fail(fwa_engine* e, int code, const std::string& msg) {
 
 int acc_kind_of(int kind) {
     switch (kind) {
-        case FWA_COUNT: return ACC_NONE;
+        case FWA_COUNT: case FWA_COUNT_COL: return ACC_NONE;
         case FWA_SUM_I64: case FWA_AVG_I64: return ACC_ADD_I64;
         case FWA_SUM_F32: case FWA_SUM_F64: case FWA_AVG_F32: case FWA_AVG_F64: return ACC_ADD_F64;
         case FWA_MIN_I64: case FWA_MIN_F32: case FWA_MIN_F64: return ACC_MIN_ORD;
@@ -2396,6 +2444,7 @@ int validate(const fwa_config* c) {
     if (c->flags & ~(FWA_CFG_DYNAMIC_GAP | FWA_CFG_LATE_INDICES)) return FWA_E_ARG;
     if ((c->flags & FWA_CFG_DYNAMIC_GAP) && (c->window_kind != FWA_SESSION || c->gap_col < 0 || c->gap_col >= FWA_MAX_COLS))
         return FWA_E_ARG;
+    if (c->nullable_cols && c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;   // SQL NULLs: Table semantics
     if (c->tz_n < 0 || (c->tz_n > 0 && !c->tz)) return FWA_E_ARG;
     if (c->tz_n > 0) {                       // TIMESTAMP_LTZ rowtime: Table slicing windows only
         if (c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;
@@ -2599,6 +2648,9 @@ int ensure_out(fwa_engine* e, int64_t rows) {
     HIPCHK(e, hipMalloc(&e->o_start, 8 * cap));
     HIPCHK(e, hipMalloc(&e->o_end, 8 * cap));
     for (int j = 0; j < e->cfg.num_aggs; ++j) HIPCHK(e, hipMalloc(&e->o_agg[j], 8 * cap));
+    for (int j = 0; j < FWA_MAX_AGGS; ++j) { if (e->o_null[j]) HIPCHK(e, hipFree(e->o_null[j])); e->o_null[j] = nullptr; }
+    for (int j = 0; j < e->cfg.num_aggs; ++j)
+        if (e->ec.agg[j].nn > 0 && e->ec.agg[j].kind != FWA_COUNT_COL) HIPCHK(e, hipMalloc(&e->o_null[j], (size_t)cap));
     if (e->o_count) HIPCHK(e, hipFree(e->o_count));
     HIPCHK(e, hipMalloc(&e->o_count, 8 * cap));
     e->out_cap = cap;
@@ -2703,6 +2755,7 @@ void fwa_destroy(fwa_engine* e) {
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
     if (e->h_sctr) (void)hipHostFree(e->h_sctr);
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
+    for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_null[j]) (void)hipFree(e->o_null[j]);
     for (void* p : e->chunks) (void)hipFree(p);
     if (e->h_st) (void)hipHostFree(e->h_st);
     if (e->h_arena) (void)hipHostFree(e->h_arena);
@@ -2773,6 +2826,29 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         c.acc_kind[c.nacc] = d.acc_kind;
         c.nacc++;
     }
+    // SQL NULLs: one hidden non-NULL counter per nullable input column (an ADD_I64 column fed 1 per
+    // non-NULL value, AvgAggFunction's count / the null flag of Sum/Min/MaxAggFunction's buffer); COUNT(col)
+    // over a nullable column reads it, over a non-nullable one it is COUNT(*)
+    c.nout = cfg->num_aggs;
+    c.nullable = cfg->nullable_cols;
+    int nn_acc[FWA_MAX_COLS] = {};
+    for (int j = 0; j < cfg->num_aggs; ++j) {
+        AggDesc& d = c.agg[j];
+        d.nn = 0;
+        if (d.kind == FWA_COUNT || !((cfg->nullable_cols >> d.col) & 1)) continue;
+        if (!nn_acc[d.col]) {
+            AggDesc& h = c.agg[c.naggs++];
+            memset(&h, 0, sizeof(h));
+            h.kind = FWA_COUNT_COL;
+            h.col = d.col;
+            h.acc_kind = ACC_ADD_I64;
+            h.acc = c.nacc;
+            c.acc_kind[c.nacc] = ACC_ADD_I64;
+            nn_acc[d.col] = c.nacc++;
+        }
+        d.nn = nn_acc[d.col];
+        if (d.kind == FWA_COUNT_COL) { d.acc = d.nn; d.alias = 1; d.acc_kind = ACC_ADD_I64; }
+    }
     e->nacc = c.nacc;
     // key-table segmentation (all paths) and v2 eligibility: <= 2 distinct carried value columns,
     // an LDS window of >= 2 slices next to the SEG-key LDS segment, <= kMaxPart partitions
@@ -2787,9 +2863,10 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         e->part_bits = cap_log - seg_log;
         int cols[2] = {-1, -1}, sizes[2] = {8, 8}, nv = 0;
         bool ok = true;
-        for (int j = 0; j < cfg->num_aggs; ++j) {
+        for (int j = 0; j < c.naggs; ++j) {
             AggDesc& d = c.agg[j];
             if (d.acc == 0) continue;
+            if (d.kind == FWA_COUNT_COL) { d.vslot = 0; continue; }   // counts rows: no value carried
             int slot = -1;
             for (int v = 0; v < nv; ++v) if (cols[v] == d.col) slot = v;
             if (slot < 0) {
@@ -2881,9 +2958,11 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
 }
 
 static int stage_inputs(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* cols,
-                        const int32_t* kh, int64_t n, IngestArgs& a) {
+                        const uint8_t* const* nulls, const int32_t* kh, int64_t n, IngestArgs& a) {
     size_t need = (size_t)n * 24 + (kh ? (size_t)n * 4 : 0) + 4096;   // + a session gap column
     for (int j = 0; j < e->cfg.num_aggs; ++j) need += (size_t)n * 8 + 256;
+    for (int c = 0; c < FWA_MAX_COLS; ++c)
+        if (nulls && ((e->cfg.nullable_cols >> c) & 1) && nulls[c]) need += (size_t)n + 256;
     if (need > e->d_in_bytes) {
         if (e->d_in) HIPCHK(e, hipFree(e->d_in));
         HIPCHK(e, hipMalloc(&e->d_in, need));
@@ -2904,10 +2983,12 @@ static int stage_inputs(fwa_engine* e, const int64_t* keys, const int64_t* ts, c
     for (int c = 0; c < FWA_MAX_COLS; ++c) a.cols[c] = nullptr;
     for (int j = 0; j < e->cfg.num_aggs; ++j) {
         const fwa_agg_spec& s = e->cfg.aggs[j];
-        if (s.kind == FWA_COUNT || a.cols[s.col]) continue;
+        if (s.kind == FWA_COUNT || s.kind == FWA_COUNT_COL || a.cols[s.col]) continue;
         if (!cols || !cols[s.col]) return fail(e, FWA_E_ARG, "missing value column");
         a.cols[s.col] = put(cols[s.col], (size_t)n * type_size(s.kind));
     }
+    for (int c = 0; c < FWA_MAX_COLS; ++c)
+        a.nulls[c] = (nulls && ((e->cfg.nullable_cols >> c) & 1) && nulls[c]) ? (const uint8_t*)put(nulls[c], (size_t)n) : nullptr;
     if ((e->cfg.flags & FWA_CFG_DYNAMIC_GAP) && !a.cols[e->cfg.gap_col]) {
         if (!cols || !cols[e->cfg.gap_col]) return fail(e, FWA_E_ARG, "missing session gap column");
         a.cols[e->cfg.gap_col] = put(cols[e->cfg.gap_col], (size_t)n * 8);
@@ -3040,6 +3121,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.np = e->np;
     for (int v = 0; v < 2; ++v) { pa.vcol[v] = e->vcol[v]; pa.vsize[v] = e->vsize[v]; }
     pa.dropidx = a.dropidx;
+    for (int c = 0; c < FWA_MAX_COLS; ++c) { pa.nulls[c] = a.nulls[c]; pa.any_null |= a.nulls[c] != nullptr; }
     pa.st = e->d_st;
     static const int pabl = getenv("FWA_PABL") ? atoi(getenv("FWA_PABL")) : 0;
     pa.abl = pabl;
@@ -3252,9 +3334,10 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     s.in = e->ss[e->ss_cur];
     s.n_in = n_in;
     s.out = e->ss[e->ss_cur ^ 1];
-    for (int cc = 0; cc <= FWA_MAX_AGGS; ++cc) s.col_owner[cc] = -1;
-    for (int j = 0; j < e->cfg.num_aggs; ++j)
+    for (int cc = 0; cc <= kMaxAggsInt; ++cc) s.col_owner[cc] = -1;
+    for (int j = 0; j < e->ec.naggs; ++j)
         if (e->ec.agg[j].acc > 0 && !e->ec.agg[j].alias) s.col_owner[e->ec.agg[j].acc] = j;
+    for (int col = 0; col < FWA_MAX_COLS; ++col) s.nulls[col] = a.nulls[col];
     s.ctr = e->d_sctr;
     s.dropidx = a.dropidx;
     s.st = e->d_st;
@@ -3399,7 +3482,7 @@ static int fire_sessions(fwa_engine* e, int64_t wm, int64_t* nrows) {
     f.o_key = e->o_key;
     f.o_start = e->o_start;
     f.o_end = e->o_end;
-    for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
+    for (int j = 0; j < e->cfg.num_aggs; ++j) { f.o_agg[j] = e->o_agg[j]; f.o_null[j] = e->o_null[j]; }
     f.out_cap = e->out_cap;
     f.ctr = e->d_sctr;
     f.st = e->d_st;
@@ -3474,7 +3557,7 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     f.o_key = e->o_key;
     f.o_start = e->o_start;
     f.o_end = e->o_end;
-    for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
+    for (int j = 0; j < e->cfg.num_aggs; ++j) { f.o_agg[j] = e->o_agg[j]; f.o_null[j] = e->o_null[j]; }
     f.o_count = raw ? e->o_count : nullptr;
     f.raw = raw;
     f.out_cap = e->out_cap;
@@ -3719,6 +3802,12 @@ static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, boo
 
 int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
              const int32_t* key_hash, int64_t n, int32_t flags, int64_t* late_dropped_out) {
+    return fwa_push_nullable(e, keys, ts, val_cols, nullptr, key_hash, n, flags, late_dropped_out);
+}
+
+int fwa_push_nullable(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
+                      const uint8_t* const* null_cols, const int32_t* key_hash, int64_t n, int32_t flags,
+                      int64_t* late_dropped_out) {
     if (!e) return FWA_E_STATE;
     if (n < 0 || (n > 0 && (!keys || !ts))) return fail(e, FWA_E_ARG, "null input column");
     if (e->cfg.key_kind == FWA_KEY_PREHASHED && n > 0 && !key_hash) return fail(e, FWA_E_ARG, "PREHASHED keys need key_hash");
@@ -3749,7 +3838,7 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
         a.key_hash = key_hash;
         for (int j = 0; j < e->cfg.num_aggs; ++j) {
             const fwa_agg_spec& s = e->cfg.aggs[j];
-            if (s.kind == FWA_COUNT) continue;
+            if (s.kind == FWA_COUNT || s.kind == FWA_COUNT_COL) continue;   // COUNT(col) reads NULL flags only
             if (!val_cols || !val_cols[s.col]) return fail(e, FWA_E_ARG, "missing value column");
             a.cols[s.col] = val_cols[s.col];
         }
@@ -3757,8 +3846,10 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
             if (!val_cols || !val_cols[e->cfg.gap_col]) return fail(e, FWA_E_ARG, "missing session gap column");
             a.cols[e->cfg.gap_col] = val_cols[e->cfg.gap_col];
         }
+        for (int c = 0; c < FWA_MAX_COLS; ++c)       // only entries of declared nullable columns are read
+            a.nulls[c] = (null_cols && ((e->cfg.nullable_cols >> c) & 1)) ? null_cols[c] : nullptr;
     } else {
-        int rc = stage_inputs(e, keys, ts, val_cols, key_hash, n, a);
+        int rc = stage_inputs(e, keys, ts, val_cols, null_cols, key_hash, n, a);
         if (rc) return rc;
     }
     if (n > e->spill_cap) {
@@ -3796,6 +3887,7 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
                       const void* const* acc, int64_t n, int32_t flags, int64_t* late_dropped_out) {
     if (!e) return FWA_E_STATE;
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
+    if (e->cfg.nullable_cols) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of nullable aggregates");
     if (n < 0 || (n > 0 && (!keys || !slice_ts || !count))) return fail(e, FWA_E_ARG, "null input column");
     if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "partials need a computable key hash");
     if (n > INT32_MAX) return fail(e, FWA_E_ARG, "batch too large (max 2^31-1 records)");
@@ -3885,6 +3977,7 @@ static int retire_slices(fwa_engine* e, int64_t wm) {
 int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     if (!e || !out) return FWA_E_ARG;
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
+    if (e->cfg.nullable_cols) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of nullable aggregates");
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
     memset(out, 0, sizeof(*out));
@@ -4100,6 +4193,7 @@ int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
     if (!e || !out) return FWA_E_ARG;
     memset(out, 0, sizeof(*out));
     if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "snapshot needs a computable key hash");
+    if (e->cfg.nullable_cols) return fail(e, FWA_E_UNSUPPORTED, "snapshot of nullable aggregates");
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
     if (e->kind == FWA_SESSION) return snapshot_sessions(e, out);
@@ -4217,7 +4311,7 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
 // leaves the run to the generic fire.
 static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>& wins, int64_t* nrows, bool* done) {
     *done = false;
-    if (e->nacc > kSlideAcc) return FWA_OK;
+    if (e->nacc > kSlideAcc || e->cfg.nullable_cols) return FWA_OK;
     for (int c = 1; c < e->nacc; ++c) if (e->ec.acc_kind[c] != ACC_ADD_I64) return FWA_OK;
     if (e->size % e->g || e->slide % e->g) return FWA_OK;
     const int64_t L = e->size / e->g, r = e->slide / e->g;
@@ -4399,10 +4493,10 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
             out->key = e->o_key;
             out->win_start = e->o_start;
             out->win_end = e->o_end;
-            for (int j = 0; j < e->cfg.num_aggs; ++j) out->agg[j] = e->o_agg[j];
+            for (int j = 0; j < e->cfg.num_aggs; ++j) { out->agg[j] = e->o_agg[j]; out->agg_null[j] = e->o_null[j]; }
         } else {
             out->on_device = 0;
-            e->h_out.resize(std::max<size_t>((size_t)nrows * 8 * (3 + e->cfg.num_aggs), 8));
+            e->h_out.resize(std::max<size_t>((size_t)nrows * 9 * (3 + e->cfg.num_aggs), 8));
             char* p = e->h_out.data();
             hipError_t err = hipSuccess;
             auto get = [&](const void* src, size_t bytes) -> const void* {
@@ -4415,6 +4509,8 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
             out->win_start = (const int64_t*)get(e->o_start, 8 * nrows);
             out->win_end = (const int64_t*)get(e->o_end, 8 * nrows);
             for (int j = 0; j < e->cfg.num_aggs; ++j) out->agg[j] = get(e->o_agg[j], type_size(e->cfg.aggs[j].kind) * nrows);
+            for (int j = 0; j < e->cfg.num_aggs; ++j)
+                if (e->o_null[j]) out->agg_null[j] = (const uint8_t*)get(e->o_null[j], (size_t)nrows);
             HIPCHK(e, err);
         }
     }

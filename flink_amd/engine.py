@@ -41,6 +41,9 @@ def lib():
     L.fwa_push.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                            C.c_int32, C.POINTER(C.c_int64)]
     L.fwa_push.restype = C.c_int
+    L.fwa_push_nullable.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_int64, C.c_int32, C.POINTER(C.c_int64)]
+    L.fwa_push_nullable.restype = C.c_int
     L.fwa_drain_partials.argtypes = [C.c_void_p, C.c_int64, C.POINTER(A.Partials)]
     L.fwa_drain_partials.restype = C.c_int
     L.fwa_push_partials.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
@@ -126,7 +129,7 @@ class WindowAggregator:
         self._inflight = None
 
     # -- processElement (batched) --
-    def push(self, keys, ts, cols=(), key_hash=None, sync=True):
+    def push(self, keys, ts, cols=(), key_hash=None, sync=True, nulls=None):
         """Push a columnar batch; returns the number of late records dropped in it.
 
         sync=False (device inputs only) enqueues the batch and returns 0 at once (FWA_PUSH_ASYNC): the
@@ -147,7 +150,14 @@ class WindowAggregator:
         if not sync and device:
             flags |= A.PUSH_ASYNC
         dropped = C.c_int64(0)
-        rc = lib().fwa_push(self.h, _ptr(keys), _ptr(ts), arr, _ptr(key_hash), n, flags, C.byref(dropped))
+        if nulls is not None:           # SQL NULL flags per value column (None entries: no NULLs)
+            if not device:
+                nulls = [None if x is None else np.ascontiguousarray(x, np.uint8) for x in nulls]
+            narr = (C.c_void_p * max(1, len(nulls)))(*[None if x is None else _ptr(x).value for x in nulls])
+            rc = lib().fwa_push_nullable(self.h, _ptr(keys), _ptr(ts), arr, narr, _ptr(key_hash), n, flags,
+                                         C.byref(dropped))
+        else:
+            rc = lib().fwa_push(self.h, _ptr(keys), _ptr(ts), arr, _ptr(key_hash), n, flags, C.byref(dropped))
         self._settled()
         _check(rc, self.h)
         if flags & A.PUSH_ASYNC:
@@ -170,6 +180,8 @@ class WindowAggregator:
         res = {f: conv(getattr(out, f), n, np.dtype("i8")) for f in ("key", "win_start", "win_end")}
         for j, name in enumerate(self.names):
             res["agg%d" % j] = conv(out.agg[j], n, np.dtype(A.AGG_RESULT_DTYPE[name]))
+            if out.agg_null[j]:
+                res["null%d" % j] = conv(out.agg_null[j], n, np.dtype("u1"))
         return res
 
     def advance_watermark_device(self, wm):

@@ -84,8 +84,16 @@ enum fwa_agg_kind {
     FWA_AVG_I64 = 10,/* AVG(BIGINT): sum/count, truncating division [i64] */
     FWA_AVG_F32 = 11,/* AVG(FLOAT): double sum / count, cast float  [f32] */
     FWA_AVG_F64 = 12,/* AVG(DOUBLE)                                 [f64] */
-    FWA_AGG_KIND_COUNT = 13
+    FWA_COUNT_COL = 13,/* COUNT(col): non-NULL values of col (Count aggregate over a nullable column;
+                          COUNT(*) when col is not nullable)       [i64] */
+    FWA_AGG_KIND_COUNT = 14
 };
+/* SQL NULL semantics (fwa_config.nullable_cols, Table semantics): SUM/MIN/MAX/AVG skip NULL inputs and are
+ * NULL when a window holds no non-NULL input (SumAggFunction.java:54-110, MaxAggFunction.java:63-73,
+ * MinAggFunction.java:63-, AvgAggFunction.java:65-106: AVG = sum / count of non-NULL inputs); COUNT(*) counts
+ * rows, COUNT(col) non-NULL values. SUM(FLOAT) is accumulated in double and rounded to float once at the
+ * fire (the reference keeps a float buffer: the results differ by at most that buffer's own rounding,
+ * n * 2^-24 * sum|x| for n inputs). */
 
 enum fwa_status {
     FWA_OK = 0,
@@ -136,7 +144,7 @@ typedef struct fwa_config {
     int32_t gap_col;             /* FWA_CFG_DYNAMIC_GAP: value column holding each record's session gap (int64 ms) */
     int32_t tz_n;                /* shift time zone of a Table TIMESTAMP_LTZ rowtime: number of (instant, offset)
                                     pairs in tz; 0 = UTC (TimeWindowUtil.toUtcTimestampMills :52-60) */
-    int32_t reserved;
+    int32_t nullable_cols;       /* Table: bit c set = value column c may hold SQL NULLs (fwa_push_nullable) */
     const int64_t* tz;           /* [2 * tz_n]: from UTC instant tz[2i] (ms, ascending) on, the zone's offset is
                                     tz[2i+1] ms (java.time ZoneRules transitions); copied by fwa_create */
 } fwa_config;
@@ -158,6 +166,8 @@ typedef struct fwa_out {
     const int64_t* win_start;
     const int64_t* win_end;      /* DataStream record timestamp = win_end - 1 (TimeWindow.maxTimestamp) */
     const void* agg[FWA_MAX_AGGS];
+    const uint8_t* agg_null[FWA_MAX_AGGS]; /* per aggregate: 1 = the result is SQL NULL; NULL pointer when the
+                                              aggregate can never be NULL (no nullable input) */
 } fwa_out;
 
 typedef struct fwa_stats {
@@ -194,6 +204,15 @@ const char* fwa_version(void);
  * Input buffers are borrowed for the duration of the call only (FWA_PUSH_ASYNC: until the next call). */
 int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
              const int32_t* key_hash, int64_t n, int32_t flags, int64_t* late_dropped_out);
+
+/* fwa_push with SQL NULLs: null_cols[c] (NULL = no NULLs in column c) holds n bytes, nonzero = the value of
+ * value column c is NULL in that record (Flink's columnar isNullAt / heap-vector isNull[]). Columns that
+ * carry NULLs must be declared in fwa_config.nullable_cols; only the entries of declared columns are read
+ * (the array needs at least 1 + the highest declared column entries). Replaces the null handling of the generated
+ * accumulate code (AggsHandleFunction, e.g. SumAggFunction.accumulateExpressions). */
+int fwa_push_nullable(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
+                      const uint8_t* const* null_cols, const int32_t* key_hash, int64_t n, int32_t flags,
+                      int64_t* late_dropped_out);
 
 /* Stream ordering of device inputs (FWA_PUSH_DEVICE_PTRS): the caller's HIP stream that produces the
  * input columns (e.g. the framework's current stream). Every later device-pointer push makes the engine's

@@ -300,7 +300,8 @@ typedef union { int64_t i; double d; float f; } aval;
 typedef struct or_engine {
     fwa_config c;
     int64_t wm;                 /* currentWatermark / currentProgress, init Long.MIN_VALUE */
-    int nacc;                   /* 1 (count) + aggs */
+    int nacc;                   /* 1 (count) + aggs (values) + aggs (non-NULL input counts) */
+    const uint8_t* const* nulls;/* NULL flags of the push being applied (fwa_push_nullable), or NULL */
     aval* pool; int64_t pool_n, pool_cap; int64_t* free_list; int64_t free_n, free_cap;
     hmap state;                 /* (key, nsA, nsB, 0) -> acc id */
     theap timers;
@@ -310,7 +311,7 @@ typedef struct or_engine {
     /* output */
     int64_t out_n, out_cap;
     int out_ret;   /* the rows were returned by the last or_advance_watermark: clear at the next call */
-    int64_t *o_key, *o_start, *o_end; aval* o_agg[FWA_MAX_AGGS];
+    int64_t *o_key, *o_start, *o_end; aval* o_agg[FWA_MAX_AGGS]; uint8_t* o_null[FWA_MAX_AGGS];
     fwa_stats st;
     int32_t* late_idx; int64_t late_n, late_cap;   /* records the last or_push dropped as late */
     char err[256];
@@ -325,6 +326,7 @@ static int64_t acc_new(or_engine* e) {
     }
     aval* a = &e->pool[id * e->nacc];
     a[0].i = 0;
+    for (int j = 0; j < e->c.num_aggs; j++) a[1 + e->c.num_aggs + j].i = 0;
     for (int j = 0; j < e->c.num_aggs; j++) {           /* createAccumulators */
         switch (e->c.aggs[j].kind) {
         case FWA_SUM_F32: a[1 + j].i = 0; a[1 + j].f = 0.0f; break;
@@ -341,13 +343,19 @@ static void acc_free(or_engine* e, int64_t id) {
 
 /* accumulate one record (AggregateFunction.add / ReduceFunction.reduce / SQL accumulate) */
 static void acc_add(or_engine* e, aval* a, const void* const* cols, int64_t i) {
-    int first = (a[0].i == 0);
+    const int na = e->c.num_aggs;
     a[0].i = jladd(a[0].i, 1);
-    for (int j = 0; j < e->c.num_aggs; j++) {
-        const void* col = cols ? cols[e->c.aggs[j].col] : NULL;
+    for (int j = 0; j < na; j++) {
+        const int cj = e->c.aggs[j].col;
+        const void* col = cols ? cols[cj] : NULL;
         aval* x = &a[1 + j];
+        if (e->c.aggs[j].kind == FWA_COUNT) continue;
+        /* SQL NULL input: skipped by SUM/MIN/MAX/AVG/COUNT(col) (their accumulate expressions test isNull) */
+        if ((e->c.nullable_cols >> cj & 1) && e->nulls && e->nulls[cj] && e->nulls[cj][i]) continue;
+        int first = (a[1 + na + j].i == 0);               /* buffer still NULL */
+        a[1 + na + j].i++;
         switch (e->c.aggs[j].kind) {
-        case FWA_COUNT: break;
+        case FWA_COUNT: case FWA_COUNT_COL: break;
         case FWA_SUM_I64: case FWA_AVG_I64: x->i = jladd(x->i, ((const int64_t*)col)[i]); break;
         case FWA_SUM_F32: x->f = x->f + ((const float*)col)[i]; break;            /* float32 buffer (a16) */
         case FWA_SUM_F64: x->d += ((const double*)col)[i]; break;
@@ -366,12 +374,15 @@ static void acc_add(or_engine* e, aval* a, const void* const* cols, int64_t i) {
 /* merge accumulator b into a (AggregateFunction.merge / SQL mergeExpressions) */
 static void acc_merge(or_engine* e, aval* a, const aval* b) {
     if (b[0].i == 0) return;
-    int first = (a[0].i == 0);
+    const int na = e->c.num_aggs;
     a[0].i = jladd(a[0].i, b[0].i);
-    for (int j = 0; j < e->c.num_aggs; j++) {
+    for (int j = 0; j < na; j++) {
         aval* x = &a[1 + j]; const aval* y = &b[1 + j];
+        if (b[1 + na + j].i == 0) continue;               /* merging a NULL buffer changes nothing */
+        int first = (a[1 + na + j].i == 0);
+        a[1 + na + j].i += b[1 + na + j].i;
         switch (e->c.aggs[j].kind) {
-        case FWA_COUNT: break;
+        case FWA_COUNT: case FWA_COUNT_COL: break;
         case FWA_SUM_I64: case FWA_AVG_I64: x->i = jladd(x->i, y->i); break;
         case FWA_SUM_F32: x->f = x->f + y->f; break;
         case FWA_SUM_F64: case FWA_AVG_F32: case FWA_AVG_F64: x->d += y->d; break;
@@ -392,14 +403,23 @@ static void emit(or_engine* e, int64_t key, int64_t ws, int64_t we, const aval* 
         e->o_start = (int64_t*)realloc(e->o_start, 8 * e->out_cap);
         e->o_end = (int64_t*)realloc(e->o_end, 8 * e->out_cap);
         for (int j = 0; j < e->c.num_aggs; j++) e->o_agg[j] = (aval*)realloc(e->o_agg[j], 8 * e->out_cap);
+        for (int j = 0; j < e->c.num_aggs; j++) e->o_null[j] = (uint8_t*)realloc(e->o_null[j], e->out_cap);
     }
     int64_t r = e->out_n++;
     e->o_key[r] = key; e->o_start[r] = ws; e->o_end[r] = we;
     int64_t cnt = a[0].i;
-    for (int j = 0; j < e->c.num_aggs; j++) {     /* getResult / getValueExpression */
+    const int na = e->c.num_aggs;
+    for (int j = 0; j < na; j++) {                /* getResult / getValueExpression */
         const aval* x = &a[1 + j]; aval* o = &e->o_agg[j][r]; o->i = 0;
-        switch (e->c.aggs[j].kind) {
+        const int64_t nn = a[1 + na + j].i;           /* non-NULL inputs */
+        const int kind = e->c.aggs[j].kind;
+        e->o_null[j][r] = (kind != FWA_COUNT && kind != FWA_COUNT_COL && nn == 0);   /* SQL NULL result */
+        if (e->o_null[j][r]) continue;
+        if (kind == FWA_AVG_I64 || kind == FWA_AVG_F32 || kind == FWA_AVG_F64) cnt = nn;   /* AVG: non-NULL count */
+        else cnt = a[0].i;
+        switch (kind) {
         case FWA_COUNT: o->i = cnt; break;
+        case FWA_COUNT_COL: o->i = nn; break;
         case FWA_SUM_I64: case FWA_MIN_I64: case FWA_MAX_I64: o->i = x->i; break;
         case FWA_SUM_F32: case FWA_MIN_F32: case FWA_MAX_F32: o->f = x->f; break;
         case FWA_SUM_F64: case FWA_MIN_F64: case FWA_MAX_F64: o->d = x->d; break;
@@ -418,6 +438,7 @@ static int set_err(or_engine* e, int code, const char* msg) { snprintf(e->err, s
 int or_create(const fwa_config* c, or_engine** out) {
     *out = NULL;
     if (c->num_aggs < 0 || c->num_aggs > FWA_MAX_AGGS) return FWA_E_ARG;
+    if (c->nullable_cols && c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;   /* SQL NULLs: Table only */
     if (c->window_kind == FWA_TUMBLE && (c->size_ms <= 0 || (c->offset_ms < 0 ? -c->offset_ms : c->offset_ms) >= c->size_ms)) return FWA_E_ARG;
     if (c->window_kind == FWA_SLIDE) {
         if (c->size_ms <= 0 || c->slide_ms <= 0) return FWA_E_ARG;
@@ -437,7 +458,7 @@ int or_create(const fwa_config* c, or_engine** out) {
     }
     if (e->c.max_parallelism <= 0) e->c.max_parallelism = 128;
     e->wm = J_LONG_MIN;
-    e->nacc = 1 + c->num_aggs;
+    e->nacc = 1 + 2 * c->num_aggs;
     hm_init(&e->state, 1024);
     th_init(&e->timers);
     hm_init(&e->wl_head, 64);
@@ -454,7 +475,7 @@ void or_destroy(or_engine* e) {
     free(e->pool); free(e->free_list);
     free(e->wl_key); free(e->wl_start); free(e->wl_end); free(e->wl_sws); free(e->wl_sw_end); free(e->wl_next);
     free(e->o_key); free(e->o_start); free(e->o_end);
-    for (int j = 0; j < FWA_MAX_AGGS; j++) free(e->o_agg[j]);
+    for (int j = 0; j < FWA_MAX_AGGS; j++) { free(e->o_agg[j]); free(e->o_null[j]); }
     free(e);
 }
 
@@ -726,7 +747,13 @@ static void tb_fire(or_engine* e, int64_t key, int64_t window_end) {  /* Slicing
 
 int or_push(or_engine* e, const int64_t* keys, const int64_t* ts, const void* const* cols,
             const int32_t* key_hash, int64_t n, int64_t* late_dropped_out) {
+    return or_push_nullable(e, keys, ts, cols, NULL, key_hash, n, late_dropped_out);
+}
+
+int or_push_nullable(or_engine* e, const int64_t* keys, const int64_t* ts, const void* const* cols,
+                     const uint8_t* const* nulls, const int32_t* key_hash, int64_t n, int64_t* late_dropped_out) {
     int64_t dropped = 0;
+    e->nulls = nulls;
     e->late_n = 0;
     if (n > e->late_cap) { e->late_cap = n; e->late_idx = (int32_t*)realloc(e->late_idx, 4 * (size_t)n); }
     /* rows fired inside processElement (late firings, EventTimeTrigger.onElement :37-45) are kept and
@@ -772,6 +799,7 @@ int or_push(or_engine* e, const int64_t* keys, const int64_t* ts, const void* co
     }
     e->st.late_dropped += dropped;
     if (late_dropped_out) *late_dropped_out = dropped;
+    e->nulls = NULL;
     return FWA_OK;
 }
 
@@ -793,7 +821,12 @@ int or_advance_watermark(or_engine* e, int64_t wm, fwa_out* out) {
         memset(out, 0, sizeof(*out));
         out->n_rows = e->out_n; out->on_device = 0; out->num_aggs = e->c.num_aggs;
         out->key = e->o_key; out->win_start = e->o_start; out->win_end = e->o_end;
-        for (int j = 0; j < e->c.num_aggs; j++) out->agg[j] = e->o_agg[j];
+        for (int j = 0; j < e->c.num_aggs; j++) {
+            out->agg[j] = e->o_agg[j];
+            const int kind = e->c.aggs[j].kind;
+            if ((e->c.nullable_cols >> e->c.aggs[j].col & 1) && kind != FWA_COUNT && kind != FWA_COUNT_COL)
+                out->agg_null[j] = e->o_null[j];
+        }
     }
     e->out_ret = 1;
     return FWA_OK;

@@ -42,6 +42,8 @@ int64_t or_tz_timer(const fwa_config* cfg, int64_t local);
 typedef struct or_engine or_engine;
 int or_create(const fwa_config* cfg, or_engine** out);
 int or_late_records(or_engine* e, const int32_t** idx, int64_t* n);
+int or_push_nullable(or_engine* e, const int64_t* keys, const int64_t* ts, const void* const* cols,
+                     const uint8_t* const* nulls, const int32_t* key_hash, int64_t n, int64_t* late_dropped_out);
 void or_destroy(or_engine* e);
 /* Same contract as fwa_push / fwa_advance_watermark (host pointers only). */
 int or_push(or_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,

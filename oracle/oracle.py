@@ -49,6 +49,9 @@ def lib():
         L.or_assign_windows.restype = C.c_int
         L.or_assign_slice_end.argtypes = [C.POINTER(A.Config), C.c_int64]
         L.or_assign_slice_end.restype = C.c_int64
+        L.or_push_nullable.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_int64, C.POINTER(C.c_int64)]
+        L.or_push_nullable.restype = C.c_int
         L.or_late_records.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
         L.or_late_records.restype = C.c_int
         for f in ("or_to_local", "or_tz_timer"):
@@ -95,6 +98,8 @@ def rows_from_out(out, names):
             res["agg%d" % j] = (raw & 0xffffffff).astype(np.uint32).view(dt)
         else:
             res["agg%d" % j] = raw.view(dt)
+        if out.agg_null[j]:
+            res["null%d" % j] = np.ctypeslib.as_array(C.cast(out.agg_null[j], C.POINTER(C.c_uint8)), (n,)).copy()
     return res
 
 
@@ -109,14 +114,18 @@ class Oracle:
         if rc:
             raise OracleError(rc, "or_create")
 
-    def push(self, keys, ts, cols=(), key_hash=None):
+    def push(self, keys, ts, cols=(), key_hash=None, nulls=None):
         keys = np.ascontiguousarray(keys, np.int64)
         ts = np.ascontiguousarray(ts, np.int64)
         cols = [np.ascontiguousarray(c) for c in cols]
         arr = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
         kh = None if key_hash is None else np.ascontiguousarray(key_hash, np.int32)
+        narr = None
+        if nulls is not None:
+            nulls = [None if x is None else np.ascontiguousarray(x, np.uint8) for x in nulls]
+            narr = (C.c_void_p * max(1, len(nulls)))(*[None if x is None else x.ctypes.data for x in nulls])
         dropped = C.c_int64(0)
-        rc = lib().or_push(self.h, _ptr(keys), _ptr(ts), arr, _ptr(kh), len(keys), C.byref(dropped))
+        rc = lib().or_push_nullable(self.h, _ptr(keys), _ptr(ts), arr, narr, _ptr(kh), len(keys), C.byref(dropped))
         if rc:
             raise OracleError(rc, lib().or_last_error(self.h).decode())
         return dropped.value

@@ -82,6 +82,51 @@ def replay_kat(case, make_engine):
     eng.close()
 
 
+def load_sql_kats():
+    """SQL NULL-semantics KATs (tests/golden/gen_sql_kats.py)."""
+    with open(os.path.join(GOLDEN, "sql_kats.json")) as f:
+        return json.load(f)
+
+
+def replay_sql_kat(case, make_engine):
+    """Feed a WindowAggregateITCase event sequence (multi-column, SQL NULLs) through an engine and compare
+    the multiset of ALL emitted rows with the ITCase's expected rows; NULL results compare as None."""
+    cfg = A.make_config(window_kind=case["window_kind"], semantics="TABLE", size_ms=case["size_ms"],
+                        slide_ms=case["slide_ms"], offset_ms=case["offset_ms"],
+                        aggs=[tuple(a) for a in case["aggs"]], nullable_cols=case["nullable_cols"])
+    eng = make_engine(cfg)
+    naggs, types = len(case["aggs"]), case["col_types"]
+    dropped, got, pend = 0, [], []
+
+    def flush():
+        nonlocal dropped, pend
+        if pend:
+            k = np.array([p[0] for p in pend], np.int64)
+            t = np.array([p[2] for p in pend], np.int64)
+            cols = [np.array([0 if p[1][c] is None else p[1][c] for p in pend], types[c]) for c in range(len(types))]
+            nulls = [np.array([p[1][c] is None for p in pend], np.uint8) for c in range(len(types))]
+            dropped += eng.push(k, t, cols, nulls=nulls)
+            pend = []
+
+    for ev in case["events"]:
+        if ev[0] == "e":
+            pend.append((ev[1], ev[2], ev[3]))
+            continue
+        flush()
+        rows = eng.advance_watermark(ev[1])
+        for i in range(len(rows["key"])):
+            r = [rows["key"][i].item(), rows["win_start"][i].item(), rows["win_end"][i].item()]
+            for j in range(naggs):
+                nul = rows.get("null%d" % j)
+                r.append(None if nul is not None and nul[i] else rows["agg%d" % j][i].item())
+            got.append(r)
+    flush()
+    key = lambda r: tuple((x is None, x) for x in r)
+    assert sorted(got, key=key) == sorted(case["expected"], key=key), "%s: got %s" % (case["name"], got)
+    assert dropped == case["late_dropped"], "%s: late dropped %d != %d" % (case["name"], dropped, case["late_dropped"])
+    eng.close()
+
+
 def assert_rows_equal(a, b, names, rtol=None, ctx=""):
     """Multiset equality of two fired-row dicts. Integer columns bit-exact; float columns within rtol
     (relative, with the same absolute floor) when rtol is given, else exact."""
@@ -96,6 +141,13 @@ def assert_rows_equal(a, b, names, rtol=None, ctx=""):
     for j, name in enumerate(names):
         x = a["agg%d" % j][oa]
         y = b["agg%d" % j][ob]
+        na_, nb_ = a.get("null%d" % j), b.get("null%d" % j)
+        if na_ is not None or nb_ is not None:           # SQL NULL results: same rows NULL, values compared elsewhere
+            na_ = np.zeros(n, np.uint8) if na_ is None else na_[oa]
+            nb_ = np.zeros(n, np.uint8) if nb_ is None else nb_[ob]
+            assert np.array_equal(na_ != 0, nb_ != 0), "%s agg %s NULL flags differ" % (ctx, name)
+            keep = nb_ == 0
+            x, y = x[keep], y[keep]
         if x.dtype.kind == "f" and rtol is not None:
             tol = rtol(name) if callable(rtol) else rtol
             assert np.allclose(x, y, rtol=tol, atol=tol), "%s agg %s max rel err %g" % (

@@ -6,7 +6,7 @@ import pytest
 
 from flink_amd import _abi as A
 from oracle import oracle as O
-from helpers import load_kats, load_tz_kats, replay_kat
+from helpers import load_kats, load_sql_kats, load_tz_kats, replay_kat, replay_sql_kat
 
 KATS = load_kats()
 TZ_KATS = load_tz_kats()
@@ -115,3 +115,13 @@ def test_time_zone_conversion_kats(case):
         assert O.lib().or_tz_timer(C.byref(cfg), local) == exp, (local, exp)
     for epoch, exp in case["to_local"]:
         assert O.lib().or_to_local(C.byref(cfg), epoch) == exp, (epoch, exp)
+
+
+SQL_KATS = load_sql_kats()
+
+
+@pytest.mark.parametrize("case", SQL_KATS["operators"], ids=lambda c: c["name"].split(".")[-1])
+def test_sql_null_kats(case):
+    """WindowAggregateITCase TUMBLE/HOP/CUMULATE over TestData.windowDataWithTimestamp: NULL values skipped by
+    SUM/MAX/MIN, a NULL result where a window has no non-NULL value, a NULL grouping key."""
+    replay_sql_kat(case, O.Oracle)
