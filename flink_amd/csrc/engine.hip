@@ -71,6 +71,8 @@ struct DevStatus {
     int32_t pad2;
     unsigned long long sess_live;  // sessions: in-flight sessions (rows a fire can emit at most)
     unsigned long long drop_n;     // FWA_CFG_LATE_INDICES: entries in the dropped-record index list this push
+    int32_t ovf_n;                 // Phase P: bucket entries past their sub-bucket's end this push (skew signal)
+    int32_t strag_n;               // Phase A: entries older than their combiner's LDS window this push
 };
 
 // FWA_CFG_LATE_INDICES: record index of a late-dropped record (lateDataOutputTag / lateRecordsDroppedRate),
@@ -410,7 +412,7 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
 //   loads the segment into LDS, streams its bucket once, finds/inserts keys in LDS (ds_cmpst_b64),
 //   accumulates into an LDS window of `sl` slices with LDS atomics, and merges a slice that leaves
 //   the window into HBM with plain coalesced read-modify-write (exclusive ownership: no atomics).
-//   Records older than the window ("stragglers") are applied afterwards by straggler_kernel.
+//   Records older than the window ("stragglers") are applied in place with global atomics.
 
 constexpr int kMaxPart = 1024;
 constexpr int kRelCap = 4096;                      // slice numbers relative to q_base
@@ -436,6 +438,7 @@ struct PartArgs {
     unsigned long long* b_val0;
     unsigned long long* b_val1;
     uint16_t* b_rel;
+    uint16_t* b_n;                     // PRE: records each bucket entry stands for (tile pre-aggregation)
     uint32_t* b_cnt;                   // [np]
     int64_t capb;
     uint64_t trash;                    // bucket index of a kMaxPart-entry scratch area past the buckets
@@ -447,6 +450,12 @@ struct PartArgs {
     int32_t* dropidx;                  // FWA_CFG_LATE_INDICES list (nullptr: not collected)
     const uint8_t* nulls[FWA_MAX_COLS];   // SQL NULL flags of the push (records with a NULL take the v1 path)
     int32_t any_null;                  // some nulls[] is set
+    // PRE: a pre-aggregated entry past its sub-bucket's end is applied at once with global atomics
+    unsigned long long* key_table;
+    uint64_t key_mask;
+    int32_t seg_log, pad_p;
+    unsigned long long* const* slot_base;
+    int64_t stride;
     DevStatus* st;
     long long* prof;                   // optional per-block phase cycle counters (FWA_PPROF)
 };
@@ -716,10 +725,27 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
 // load registers are free as soon as the tile is classified.
 // VW: value-column widths, bit v set = carried value column v is 8 bytes (else 4): a compile-time
 // width keeps the tile's loads branch-free, so none waits for another.
-template <int NV, int ITEMS, int THREADS, int VW, int KG>
+// PRE (skewed keys, COUNT [+ one BIGINT SUM] layouts): equal (key, slice) records of a tile are first merged
+// in an LDS hash table -- the wavefront/workgroup hot-key reduction of Flink's local pre-aggregation
+// (LocalSlicingWindowAggOperator) -- so a Zipf head key costs one bucket entry per tile instead of one
+// per record: no sub-bucket overflow into the v1 replay, no same-address LDS atomics in the combiner.
+// Entries carry their record count (b_n) and the partial BIGINT sum in the value column.
+__device__ __noinline__ void pre_apply_global(unsigned long long* table, uint64_t mask, int seg_log, int part_bits,
+                                              unsigned long long* base, int64_t stride, int has_sum, int64_t key,
+                                              unsigned long long n, unsigned long long sum, DevStatus* st) {
+    const int64_t kid = key_slot(table, mask, seg_log, part_bits, key, st);
+    if (kid < 0) { st->key_full = 1; raise_error(st, FWA_E_OOM); return; }
+    atomicAdd(&base[kid], n);
+    if (has_sum) atomicAdd(&base[stride + kid], sum);
+}
+
+template <int NV, int ITEMS, int THREADS, int VW, int KG, int PRE = 0>
 __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
     static_assert(THREADS == kMaxPart && ITEMS <= 8, "one partition cursor per thread; trash area of 8 x kMaxPart");
+    static_assert(!PRE || NV <= 1, "pre-aggregation: COUNT [+ one BIGINT sum]");
     constexpr int kTile = THREADS * ITEMS;
+    constexpr int kHt = 2 * kTile;                     // PRE: (key, slice) hash table, load <= 0.5
+    constexpr int kHtLog = __builtin_ctz(kHt);
     const EngineConst& c = *cp;
     __shared__ uint32_t hist[kMaxPart];
     __shared__ uint32_t toff[kMaxPart];
@@ -733,6 +759,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
     __shared__ uint32_t wsum[THREADS / 64];
     __shared__ uint32_t s_total;
     __shared__ uint8_t s_code[kRelCap];
+    __shared__ uint32_t ht[PRE ? kHt : 1];             // PRE: 1 + staging index of the (key, slice)'s representative
+    __shared__ uint32_t x_n[PRE ? kTile : 1];          // PRE: records merged into the representative
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     unsigned dropped = 0;
@@ -804,11 +832,13 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         const uint64_t o = a.trash + (uint64_t)(jj * THREADS + tid);   // distinct: not merged by the compiler
         a.b_key[o] = 0ull;
         a.b_rel[o] = 0;
+        if constexpr (PRE) a.b_n[o] = 0;
         if (NV > 0) a.b_val0[o] = 0ull;
         if (NV > 1) a.b_val1[o] = 0ull;
     }
     for (; tile < ntiles; tile += gridDim.x) {
         for (int i = tid; i < a.np; i += THREADS) hist[i] = 0;
+        if constexpr (PRE) for (int i = tid; i < kHt / 4; i += THREADS) ((uint4*)ht)[i] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
         QMARK(5);
         const int64_t t0 = tile * kTile;
@@ -865,7 +895,35 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 x_rel[x] = (uint16_t)rel;
                 if (NV > 0) x_val[0][x] = r_v0[j];
                 if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = r_v1[j];
-                r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
+                if constexpr (PRE) { x_n[x] = 1u; r_pos[j] = 0x80000000u | p; }   // bucketed after the merge
+                else r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
+            }
+        }
+        if constexpr (PRE) {
+            __syncthreads();                        // the tile's staged (key, rel) visible to every lane
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) {
+                if (r_pos[j] == ~0u) continue;
+                const uint32_t x = (uint32_t)(j * THREADS + tid);
+                const unsigned long long key = r_key[j];
+                const uint32_t rel = x_rel[x];
+                uint32_t hs = ((uint32_t)key * 0x9E3779B1u + (uint32_t)(key >> 32) * 0x85EBCA77u + rel * 0xC2B2AE3Du) >> (32 - kHtLog);
+                for (int probe = 0; probe < kHt; ++probe) {
+                    const uint32_t old = atomicCAS(&ht[hs], 0u, x + 1u);
+                    if (old == 0u) {                // representative of its (key, slice) in this tile
+                        const uint32_t p = r_pos[j] & 0xffffu;
+                        r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
+                        break;
+                    }
+                    const uint32_t o = old - 1u;
+                    if (x_key[o] == key && x_rel[o] == rel) {   // merge into the representative
+                        atomicAdd(&x_n[o], 1u);
+                        if constexpr (NV > 0) atomicAdd(&x_val[0][o], r_v0[j]);
+                        r_pos[j] = ~0u;
+                        break;
+                    }
+                    hs = (hs + 1u) & (kHt - 1);
+                }
             }
         }
         QMARK(0);
@@ -889,7 +947,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             const uint64_t end = (uint64_t)g + h;
             if (end > (uint64_t)a.capb) {
                 const uint32_t ov = (uint32_t)(end - std::max<uint64_t>(g, (uint64_t)a.capb));
-                sbase[p] = (uint32_t)atomicAdd(&a.st->spill_n, (int32_t)ov);
+                atomicAdd(&a.st->ovf_n, (int32_t)ov);
+                if constexpr (!PRE) sbase[p] = (uint32_t)atomicAdd(&a.st->spill_n, (int32_t)ov);
             }
         }
 #pragma unroll
@@ -913,13 +972,21 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             const uint32_t x = valid ? s_src[sidx] : 0u;
             const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
             const bool inb = valid && dst < (uint64_t)a.capb;
-            if (valid && !inb) {                // sub-bucket full (skewed keys): the v1 replay takes it
-                const uint64_t first = std::max<uint64_t>(gbase[p], (uint64_t)a.capb);
-                put_idx(a.spill, (int64_t)sbase[p] + (int64_t)(dst - first), a.spill_cap, (int32_t)(t0 + x), a.st);
+            if (valid && !inb) {                // sub-bucket full (skewed keys)
+                if constexpr (PRE) {            // a merged entry has no record index to replay: apply it now
+                    const int32_t slot = a.rel2slot[x_rel[x]];
+                    if (slot >= 0)
+                        pre_apply_global(a.key_table, a.key_mask, a.seg_log, a.part_bits, a.slot_base[slot], a.stride,
+                                         NV, (int64_t)x_key[x], x_n[x], NV > 0 ? x_val[0][x] : 0ull, a.st);
+                } else {                        // the v1 replay takes it
+                    const uint64_t first = std::max<uint64_t>(gbase[p], (uint64_t)a.capb);
+                    put_idx(a.spill, (int64_t)sbase[p] + (int64_t)(dst - first), a.spill_cap, (int32_t)(t0 + x), a.st);
+                }
             }
             const uint64_t o = inb ? ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst : a.trash + (uint64_t)(jj * THREADS + tid);
             a.b_key[o] = x_key[x];
             a.b_rel[o] = x_rel[x];
+            if constexpr (PRE) a.b_n[o] = (uint16_t)x_n[x];
             if (NV > 0) a.b_val0[o] = x_val[0][x];
             if (NV > 1) a.b_val1[o] = x_val[NV > 1 ? 1 : 0][x];
         }
@@ -948,17 +1015,13 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         }
 }
 
-struct StragEntry {
-    uint64_t o;                        // bucket offset (p * capb + idx)
-    uint32_t g;                        // global kid (key-table slot)
-    uint32_t pad;
-};
 
 struct CombineArgs {
     const unsigned long long* b_key;
     const unsigned long long* b_val0;
     const unsigned long long* b_val1;
     const uint16_t* b_rel;
+    const uint16_t* b_n;               // PRE buckets: records per entry (nullptr: one each)
     const uint32_t* b_cnt;
     int64_t capb;
     int32_t seg_log, np, sl;           // sl: LDS slice window
@@ -966,9 +1029,6 @@ struct CombineArgs {
     unsigned long long* key_table;
     unsigned long long* const* slot_base;
     int64_t stride;
-    StragEntry* strag;
-    int32_t* strag_n;
-    int64_t strag_cap;
     int32_t abl;                       // ablation bits (timing experiments only)
     DevStatus* st;
     long long* prof;                   // optional per-block phase cycle counters (FWA_APROF)
@@ -990,16 +1050,18 @@ __device__ __forceinline__ double carried_f64(unsigned long long raw, int kind) 
                                                          : __longlong_as_double((long long)raw);
 }
 
-// Apply one bucket entry (offset o, global kid g) to its slice's HBM accumulators with global atomics.
-__device__ __forceinline__ void strag_apply(const CombineArgs& a, const EngineConst& c, uint64_t o, uint32_t g) {
-    const int32_t slot = a.rel2slot[a.b_rel[o]];
+// Apply one combiner entry (slice rel, global kid g, n records, carried values) to its slice's HBM
+// accumulators with device atomics (stragglers: their slice was already merged by this block).
+__device__ __forceinline__ void strag_apply(const CombineArgs& a, const EngineConst& c, int rel, uint32_t g, uint32_t n,
+                                            unsigned long long x0, unsigned long long x1) {
+    const int32_t slot = a.rel2slot[rel];
     if (slot < 0) return;
     unsigned long long* base = a.slot_base[slot];
-    atomicAdd(&base[g], 1ull);
+    atomicAdd(&base[g], (unsigned long long)n);
     for (int jj = 0; jj < c.naggs; ++jj) {
         const AggDesc d = c.agg[jj];
         if (d.acc == 0 || d.alias) continue;
-        const unsigned long long raw = d.kind == FWA_COUNT_COL ? 1ull : d.vslot == 0 ? a.b_val0[o] : a.b_val1[o];
+        const unsigned long long raw = d.kind == FWA_COUNT_COL ? (unsigned long long)n : d.vslot == 0 ? x0 : x1;
         unsigned long long* gp = base + (int64_t)d.acc * a.stride + g;
         switch (d.acc_kind) {
             case ACC_ADD_I64: atomicAdd(gp, raw); break;
@@ -1010,6 +1072,14 @@ __device__ __forceinline__ void strag_apply(const CombineArgs& a, const EngineCo
         }
     }
 }
+
+// Stragglers of one combiner block, kept in LDS and applied after the block's last merge.
+constexpr int kStragL = 256;
+struct StragL {
+    uint32_t g, n;
+    int32_t rel, pad;
+    unsigned long long x0, x1;
+};
 
 // ------------------------------------------------------------------------------------------------
 // combine3: the Phase A combiner, restructured for latency tolerance (DESIGN.md §4, r01 clock64
@@ -1029,7 +1099,9 @@ typedef const __attribute__((address_space(1))) unsigned long long* gc_u64_ptr;
 // path has no descriptor switch (a runtime switch over 8 columns cost ~1000 scalar instructions per
 // record from SGPR spills): 1 = COUNT + one ADD_I64 fed by value slot 0 (SUM/AVG over BIGINT);
 // 2 = COUNT only; 0 = generic (descriptor table in LDS, one column per loop trip).
-template <int IT, int SL, int NV, int TH, int LAYOUT>
+// MP: window passes (below) for chunks spanning more slices than the window; chosen per handle once a push
+// saw many stragglers (small HOP/CUMULATE slices), since the passes cost registers the common case needs.
+template <int IT, int SL, int NV, int TH, int LAYOUT, int PRE = 0, int MP = 0>
 __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int kWaves = TH / 64;
@@ -1043,6 +1115,8 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
     const uint32_t smask = (uint32_t)seg - 1u;
     const int nacc = LAYOUT == 1 ? 2 : (LAYOUT == 2 ? 1 : c.nacc);
     __shared__ int s_desc[kMaxAggsInt + 1];   // generic layout: per column kind | vslot << 8 | input kind << 16
+    __shared__ StragL s_strag[kStragL];
+    __shared__ int s_sn;
     if (LAYOUT == 0 && tid == 0) {
         for (int j = 0; j < c.naggs; ++j)
             if (c.agg[j].acc > 0 && !c.agg[j].alias) s_desc[c.agg[j].acc] = c.agg[j].acc_kind | (c.agg[j].vslot << 8) | (c.agg[j].kind << 16);
@@ -1063,7 +1137,7 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
     for (int i = tid; i < SL * seg; i += TH) {
         lcnt[i] = 0;
     }
-    if (tid == 0) *s_new = 0;
+    if (tid == 0) { *s_new = 0; s_sn = 0; }
     __syncthreads();
     for (int cc = 1; cc < nacc; ++cc) {
         const unsigned long long id = LAYOUT == 1 ? 0ull : ident_of(s_desc[cc] & 0xff);
@@ -1077,6 +1151,7 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
     const gc_u64_ptr bv0 = a.b_val0 ? (const gc_u64_ptr)(a.b_val0 + boff) : nullptr;
     const gc_u64_ptr bv1 = a.b_val1 ? (const gc_u64_ptr)(a.b_val1 + boff) : nullptr;
     const __attribute__((address_space(1))) uint16_t* br = (const __attribute__((address_space(1))) uint16_t*)(a.b_rel + boff);
+    const __attribute__((address_space(1))) uint16_t* bn = PRE ? (const __attribute__((address_space(1))) uint16_t*)(a.b_n + boff) : nullptr;
     int lo = 0x7fffffff;
     auto flush = [&](int rel) {   // merge window slice `rel` into HBM; every thread owns seg/TH slots
         constexpr int kPer = 4096 / TH;   // seg <= 4096
@@ -1136,6 +1211,7 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
     // register double buffer: n* = chunk in flight, c* = chunk being combined
     unsigned long long nkey[IT], nx0[IT], nx1[IT];
     int nrel[IT];
+    uint32_t nnn[IT];                   // PRE: records per entry
     auto load_chunk = [&](int64_t cb) {
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
@@ -1145,6 +1221,7 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
             nx0[j] = (NV > 0 && ok) ? bv0[i] : 0ull;
             nx1[j] = (NV > 1 && ok) ? bv1[i] : 0ull;
             nrel[j] = ok ? (int)br[i] : -1;
+            nnn[j] = PRE ? (ok ? (uint32_t)bn[i] : 0u) : 1u;
         }
     };
     constexpr int64_t kChunk = (int64_t)IT * LPS;
@@ -1154,10 +1231,11 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
     for (int64_t cb = 0; cb < cnt; cb += kChunk, ++it) {
         unsigned long long key[IT], x0[IT], x1[IT];
         int rel[IT];
+        uint32_t nr[IT];
         int rmin = 0x7fffffff, rmax = -1;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
-            key[j] = nkey[j]; x0[j] = nx0[j]; x1[j] = nx1[j]; rel[j] = nrel[j];
+            key[j] = nkey[j]; x0[j] = nx0[j]; x1[j] = nx1[j]; rel[j] = nrel[j]; nr[j] = nnn[j];
             if (rel[j] >= 0) { rmin = min(rmin, rel[j]); rmax = max(rmax, rel[j]); }
         }
         PMARK(1);
@@ -1179,11 +1257,20 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         for (int v = 0; v < kWaves; ++v) { cmin = min(cmin, s_min[buf * kWaves + v]); cmax = max(cmax, s_max[buf * kWaves + v]); }
         if (cmax < 0) continue;
         if (lo == 0x7fffffff) lo = cmin;
-        if (cmax >= lo + SL) {
-            while (cmax >= lo + SL) { if (!(a.abl & 4)) flush(lo); ++lo; }
+        if constexpr (MP) {
+            if (cmin >= lo + SL) {          // the whole chunk is past the window: merge it out, jump to cmin
+                for (int r = lo; r < lo + SL; ++r) if (!(a.abl & 4)) flush(r);
+                if (a.prof) pacc[7] += 1000;
+                lo = cmin;
+                __syncthreads();
+            }
+        } else if (cmax >= lo + SL) {       // slide the window up to the chunk's newest slice
+            while (cmax >= lo + SL) { if (!(a.abl & 4)) flush(lo); ++lo; if (a.prof) pacc[7] += 1000; }
             __syncthreads();
         }
+        const int lo_c = lo;                // entries older than this are stragglers
         PMARK(4);
+        if (a.prof) pacc[7] += 1;
         // bucket probing: read the key's 8-slot home bucket (4 x ds_read_b128), compare all 8; only
         // keys displaced past their bucket (a few %) take another round
         int32_t loc[IT];
@@ -1211,79 +1298,78 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
                     continue;                   // lost the slot to another key: re-read this bucket
                 }
                 b = (b + kBucket) & smask;
-                if (a.prof && lane == 0) pacc[7]++;
             }
             loc[j] = found;
         }
+        // window passes (MP): a chunk can span more slices than the LDS window holds (HOP/CUMULATE 1 s slices:
+        // a sub-bucket's 256-entry chunk covers seconds of event time); its entries stay in registers and are
+        // added window by window, merging out between passes only the slices the next pass needs (the window
+        // ends at the chunk's newest slice, so the next chunk's older entries still find it)
+        int from = lo_c;                    // entries below this were added by an earlier pass (or straggle)
+        for (int pass = 0;; ++pass) {
 #pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            if (rel[j] < 0) continue;
-            const int32_t local = loc[j];
-            if (local < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
-            const bool strag = rel[j] < lo;
-            const unsigned long long msk = __ballot(strag);   // one list reservation per wave (skew)
-            int32_t sbase = 0;
-            if (msk) {
-                const int ld = __ffsll((long long)msk) - 1;
-                if (lane == ld) sbase = atomicAdd(a.strag_n, __popcll(msk));
-                sbase = __shfl(sbase, ld);
-            }
-            if (strag) {                // older than the window: applied after the kernel with atomics
-                if (a.prof) pacc[6] += 1000000;
-                const int32_t si = sbase + __popcll(msk & ((1ull << lane) - 1));
-                const uint64_t so = (uint64_t)(boff + cb + (int64_t)j * LPS + li);
-                const uint32_t sg = (uint32_t)(((int64_t)p << a.seg_log) + local);
-                if (si < a.strag_cap) {
-                    a.strag[si].o = so;
-                    a.strag[si].g = sg;
-                } else {   // list full (skewed, out-of-order input): apply it here; this block owns the
-                    strag_apply(a, c, so, sg);   // kid and has already merged that slice, so atomics suffice
+            for (int j = 0; j < IT; ++j) {
+                if (rel[j] < 0 || rel[j] >= lo + SL) continue;
+                const int32_t local = loc[j];
+                if (local < 0) { if (pass == 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); } continue; }
+                if (rel[j] < from) {
+                    if (pass > 0) continue;     // added in an earlier pass
+                    // older than the window (its slice is already merged into HBM): listed in LDS and applied
+                    // with device atomics after the last merge (this block owns the kid; a list shared by all
+                    // blocks serialised them on one counter)
+                    if (a.prof) pacc[6] += 1000000;
+                    const uint32_t g = (uint32_t)(((int64_t)p << a.seg_log) + local);
+                    const int si = atomicAdd(&s_sn, 1);
+                    if (si < kStragL) s_strag[si] = StragL{g, PRE ? nr[j] : 1u, rel[j], 0, x0[j], x1[j]};
+                    else strag_apply(a, c, rel[j], g, PRE ? nr[j] : 1u, x0[j], x1[j]);
+                    continue;
                 }
-                continue;
-            }
-            const int w = rel[j] & (SL - 1);
-            if (a.abl & 2) { if (x0[j] == 0x123456789ull) lcnt[0] = 1; continue; }
-            atomicAdd(&lcnt[w * seg + local], 1u);
-            if constexpr (LAYOUT == 1) {
-                atomicAdd(&lacc[(size_t)w * seg + local], x0[j]);
-            } else if constexpr (LAYOUT == 0) {
-                for (int cc = 1; cc < nacc; ++cc) {
-                    const int d = s_desc[cc];
-                    unsigned long long* lp = &lacc[(size_t)(cc - 1) * SL * seg + (size_t)w * seg + local];
-                    const int ik = d >> 16;
-                    const unsigned long long raw = ik == FWA_COUNT_COL ? 1ull   // non-NULL counter (NULL rows take the v1 path)
-                                                 : (NV > 1 && ((d >> 8) & 0xff) != 0) ? x1[j] : x0[j];
-                    switch (d & 0xff) {
-                        case ACC_ADD_I64: atomicAdd(lp, raw); break;
-                        case ACC_ADD_F64: atomicAdd((double*)lp, carried_f64(raw, ik)); break;
-                        case ACC_MIN_ORD: atomicMin(lp, carried_ord(raw, ik)); break;
-                        case ACC_MAX_ORD: atomicMax(lp, carried_ord(raw, ik)); break;
-                        default: break;
+                const int w = rel[j] & (SL - 1);
+                if (a.abl & 2) { if (x0[j] == 0x123456789ull) lcnt[0] = 1; continue; }
+                atomicAdd(&lcnt[w * seg + local], PRE ? nr[j] : 1u);
+                if constexpr (LAYOUT == 1) {
+                    atomicAdd(&lacc[(size_t)w * seg + local], x0[j]);
+                } else if constexpr (LAYOUT == 0) {
+                    for (int cc = 1; cc < nacc; ++cc) {
+                        const int d = s_desc[cc];
+                        unsigned long long* lp = &lacc[(size_t)(cc - 1) * SL * seg + (size_t)w * seg + local];
+                        const int ik = d >> 16;
+                        const unsigned long long raw = ik == FWA_COUNT_COL ? 1ull   // non-NULL counter (NULL rows take the v1 path)
+                                                     : (NV > 1 && ((d >> 8) & 0xff) != 0) ? x1[j] : x0[j];
+                        switch (d & 0xff) {
+                            case ACC_ADD_I64: atomicAdd(lp, raw); break;
+                            case ACC_ADD_F64: atomicAdd((double*)lp, carried_f64(raw, ik)); break;
+                            case ACC_MIN_ORD: atomicMin(lp, carried_ord(raw, ik)); break;
+                            case ACC_MAX_ORD: atomicMax(lp, carried_ord(raw, ik)); break;
+                            default: break;
+                        }
                     }
                 }
             }
+            if (!MP || cmax < lo + SL) break;
+            __syncthreads();                // the window's adds done before it is merged out
+            from = lo + SL;
+            const int nl = min(lo + SL, cmax - SL + 1);
+            while (lo < nl) { if (!(a.abl & 4)) flush(lo); ++lo; if (a.prof) pacc[7] += 1000; }
+            __syncthreads();                // merged and cleared before the next pass adds
         }
         PMARK(5);
     }
     __syncthreads();
     if (lo != 0x7fffffff)
         for (int r = lo; r < lo + SL; ++r) flush(r);
+    __syncthreads();                    // every merge of this block stored before the stragglers' atomics
+    if (tid == 0 && s_sn) atomicAdd(&a.st->strag_n, s_sn);
+    for (int t = tid; t < min(s_sn, kStragL); t += TH) {
+        const StragL se = s_strag[t];
+        strag_apply(a, c, se.rel, se.g, se.n, se.x0, se.x1);
+    }
     if (*s_new) {                       // publish newly inserted keys (exclusive owner of this segment)
         for (int i = tid; i < seg; i += TH) gkeys[i] = lkey[i];
         if (tid == 0) atomicAdd(&a.st->n_keys, (unsigned long long)*s_new);
     }
     if (a.prof && tid == 0) for (int q = 0; q < 8; ++q) a.prof[(int64_t)p * 8 + q] = pacc[q];
 #undef PMARK
-}
-
-// Stragglers: bucket entries older than their combiner's window, applied with global atomics.
-__global__ void straggler_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
-    const EngineConst& c = *cp;
-    const int32_t n = (int32_t)min((int64_t)*a.strag_n, a.strag_cap);
-    for (int32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-        const StragEntry se = a.strag[t];
-        strag_apply(a, c, se.o, se.g);
-    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2152,15 +2238,13 @@ __global__ void __launch_bounds__(64) late_fire_kernel(LateArgs L, const EngineC
     *L.rows = nrow;
 }
 
-// two-phase path, the bucket cursors and straggler count: one launch instead of a string of memsets.
-__global__ void push_reset_kernel(DevStatus* st, unsigned long long* want, int32_t nwant, uint32_t* bcnt, int32_t nbcnt,
-                                  int32_t* strag_n) {
+// two-phase path, the bucket cursors: one launch instead of a string of memsets.
+__global__ void push_reset_kernel(DevStatus* st, unsigned long long* want, int32_t nwant, uint32_t* bcnt, int32_t nbcnt) {
     const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const int32_t nt = gridDim.x * blockDim.x;
     if (t == 0) {
         st->error = 0; st->spill_n = 0; st->want_n = 0; st->key_full = 0;
-        st->dropped = 0; st->late_fire = 0; st->max_q = 0; st->min_q = ~0ull;
-        if (strag_n) strag_n[0] = 0;
+        st->dropped = 0; st->late_fire = 0; st->max_q = 0; st->min_q = ~0ull; st->ovf_n = 0; st->strag_n = 0;
     }
     for (int32_t i = t; i < nwant; i += nt) want[i] = 0ull;
     for (int32_t i = t; i < nbcnt; i += nt) bcnt[i] = 0u;
@@ -2320,12 +2404,12 @@ struct fwa_engine {
     int64_t capb = 0;
     unsigned long long* d_bkey = nullptr;
     uint16_t* d_brel = nullptr;
+    uint16_t* d_bn = nullptr;         // PRE buckets: records per entry
+    bool pre = false;                 // skew seen (sub-bucket overflow): Phase P pre-aggregates equal (key, slice)
+    bool mp = false;                  // many stragglers seen: the combiner takes window passes (combine3 MP)
     unsigned long long* d_bval[2] = {nullptr, nullptr};
     uint32_t* d_bcnt = nullptr;
     int32_t* d_rel2slot = nullptr;
-    StragEntry* d_strag = nullptr;
-    int64_t strag_cap = 0;
-    int32_t* d_strag_n = nullptr;
     bool v2_timing_pending = false;   // Phase P / A events recorded, read after the next sync
     // FWA_PUSH_ASYNC: the last push is enqueued but not yet settled (status, miss replay, lookahead)
     bool pend = false, pend_v2 = false;
@@ -2720,10 +2804,9 @@ int upload(fwa_engine* e, void* dst, const void* src, size_t bytes) {
 }
 
 int reset_push_status(fwa_engine* e, bool v2bufs = false) {
-    // zero everything but n_keys / rows; min_q starts at ~0; want-set; v2: bucket cursors, stragglers
+    // zero everything but n_keys / rows; min_q starts at ~0; want-set; v2: bucket cursors
     push_reset_kernel<<<64, kBlock, 0, e->stream>>>(e->d_st, e->d_want, e->d_want ? kWantCap : 0,
-                                                    v2bufs ? e->d_bcnt : nullptr, v2bufs ? kMaxPart * kSub : 0,
-                                                    v2bufs ? e->d_strag_n : nullptr);
+                                                    v2bufs ? e->d_bcnt : nullptr, v2bufs ? kMaxPart * kSub : 0);
     HIPCHK(e, hipGetLastError());
     return FWA_OK;
 }
@@ -2747,8 +2830,8 @@ void fwa_destroy(fwa_engine* e) {
     if (e->d_late) (void)hipFree(e->d_late);
     if (e->d_lr_n) (void)hipFree(e->d_lr_n);
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
-                    e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel,
-                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_strag, e->d_strag_n, e->d_reset_list, e->d_upos,
+                    e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel, e->d_bn,
+                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos,
                     e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
@@ -2883,7 +2966,8 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         // while the partition count stays <= kMaxPart
         auto lds_need = [&](int sg) {
             const int64_t sgz = (int64_t)1 << sg;
-            return sgz * 8 + 2 * sgz * 4 + (int64_t)(c.nacc - 1) * 2 * sgz * 8 + 4 * 4 * kSub + 16;
+            return sgz * 8 + 2 * sgz * 4 + (int64_t)(c.nacc - 1) * 2 * sgz * 8 + 4 * 4 * kSub + 16 +
+                   (int64_t)sizeof(StragL) * kStragL + 256;   // + static LDS (straggler list, descriptors)
         };
         while (!getenv("FWA_SEG_LOG") && seg_log > 9 && lds_need(seg_log) > 160 * 1024 &&
                ((int64_t)1 << (cap_log - seg_log + 1)) <= kMaxPart)
@@ -2892,7 +2976,7 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         e->part_bits = cap_log - seg_log;
         const int64_t seg = (int64_t)1 << seg_log;
         const int64_t bps = 4 + 8 * (int64_t)(c.nacc - 1);
-        const int64_t avail = 160 * 1024 - 256 - seg * 8;
+        const int64_t avail = 160 * 1024 - 512 - (int64_t)sizeof(StragL) * kStragL - seg * 8;
         int sl = (int)std::min<int64_t>(8, avail > 0 ? avail / (bps * seg) : 0);
         if (const char* sv = getenv("FWA_SL")) sl = std::min(sl, atoi(sv));
         if (lds_need(seg_log) > 160 * 1024) sl = 0;
@@ -3040,13 +3124,14 @@ static int account_ingest(fwa_engine* e) {  // after the stream was synchronised
     return FWA_OK;
 }
 
-static int ensure_v2_buffers(fwa_engine* e, int64_t n) {
+static int ensure_v2_buffers(fwa_engine* e, int64_t n, bool need_bn) {
     const int64_t per = n / ((int64_t)e->np * kSub);                 // expected records per sub-bucket
     const int64_t capb = per + per / 4 + 2048;
     if (capb > e->capb) {
-        for (void* p : {(void*)e->d_bkey, (void*)e->d_brel, (void*)e->d_bval[0], (void*)e->d_bval[1]}) if (p) HIPCHK(e, hipFree(p));
+        for (void* p : {(void*)e->d_bkey, (void*)e->d_brel, (void*)e->d_bn, (void*)e->d_bval[0], (void*)e->d_bval[1]}) if (p) HIPCHK(e, hipFree(p));
         e->d_bkey = nullptr;
         e->d_brel = nullptr;
+        e->d_bn = nullptr;
         e->d_bval[0] = e->d_bval[1] = nullptr;
         const int64_t ent = capb * e->np * kSub + 8 * kMaxPart;  // + a trash area (partition3's masked stores)
         HIPCHK(e, hipMalloc(&e->d_bkey, 8 * ent));
@@ -3054,16 +3139,10 @@ static int ensure_v2_buffers(fwa_engine* e, int64_t n) {
         for (int v = 0; v < e->nv; ++v) HIPCHK(e, hipMalloc(&e->d_bval[v], 8 * ent));
         e->capb = capb;
     }
+    if (need_bn && !e->d_bn) HIPCHK(e, hipMalloc(&e->d_bn, 2 * (e->capb * e->np * kSub + 8 * kMaxPart)));
     if (!e->d_bcnt) {
         HIPCHK(e, hipMalloc(&e->d_bcnt, sizeof(uint32_t) * kMaxPart * kSub));
         HIPCHK(e, hipMalloc(&e->d_rel2slot, (sizeof(int32_t) + 1) * kRelCap));   // rel2slot | relcode
-        HIPCHK(e, hipMalloc(&e->d_strag_n, 16));
-    }
-    const int64_t scap = std::max<int64_t>(n / 8, 1 << 16);
-    if (scap > e->strag_cap) {
-        if (e->d_strag) HIPCHK(e, hipFree(e->d_strag));
-        HIPCHK(e, hipMalloc(&e->d_strag, sizeof(StragEntry) * scap));
-        e->strag_cap = scap;
     }
     return FWA_OK;
 }
@@ -3072,7 +3151,17 @@ static int ensure_v2_buffers(fwa_engine* e, int64_t n) {
 // batch must take the v1 path instead (bucket overflow on skewed keys).
 static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     *ran = false;
-    int rc = ensure_v2_buffers(e, a.n);
+    // combiner accumulator layout (compile-time in combine3) and the skew mode (PRE, partition3)
+    int layout = 0;
+    if (e->nacc == 1) layout = 2;
+    else if (e->nacc == 2 && e->ec.acc_kind[1] == ACC_ADD_I64) {
+        for (int j = 0; j < e->cfg.num_aggs; ++j)
+            if (e->ec.agg[j].acc == 1 && e->ec.agg[j].vslot == 0) layout = 1;
+    }
+    static const int pre_env = getenv("FWA_PRE") ? atoi(getenv("FWA_PRE")) : -1;   // A/B: 0 never, 1 always
+    const bool pre_ok = (layout == 2 && e->nv == 0) || (layout == 1 && e->nv == 1 && e->vsize[0] == 8);
+    const bool pre = pre_ok && pre_env != 0 && (pre_env == 1 || e->pre) && getenv("FWA_P2") == nullptr;
+    int rc = ensure_v2_buffers(e, a.n, pre);
     if (rc) return rc;
     const int64_t q_base = e->live.empty() ? 0 : e->live.begin()->first;
     // rel2slot (combine) and relcode (partition): the directory restricted to [q_base, q_base + kRelCap)
@@ -3111,6 +3200,12 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.q_base = q_base;
     pa.b_key = e->d_bkey;
     pa.b_rel = e->d_brel;
+    pa.b_n = pre ? e->d_bn : nullptr;
+    pa.key_table = e->d_keys;
+    pa.key_mask = (uint64_t)e->capacity - 1;
+    pa.seg_log = e->seg_log;
+    pa.slot_base = e->d_slot_base;
+    pa.stride = e->stride;
     pa.b_val0 = e->d_bval[0];
     pa.b_val1 = e->d_bval[1];
     pa.b_cnt = e->d_bcnt;
@@ -3142,11 +3237,17 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else if (kgm == 0) partition3_kernel<NV, IT, 1024, VW, 0><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else if (kgm == 1) partition3_kernel<NV, IT, 1024, VW, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else partition3_kernel<NV, IT, 1024, VW, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
-    if (e->nv == 0) P2LAUNCH(0, 8, 3);
+#define PRELAUNCH(NV) do { const int gp = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + 4095) / 4096, 256)); \
+        if (kgm == 0) partition3_kernel<NV, 4, 1024, 3, 0, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); \
+        else if (kgm == 1) partition3_kernel<NV, 4, 1024, 3, 1, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); \
+        else partition3_kernel<NV, 4, 1024, 3, 2, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
+    if (pre) { if (e->nv == 0) PRELAUNCH(0); else PRELAUNCH(1); }
+    else if (e->nv == 0) P2LAUNCH(0, 8, 3);
     else if (e->nv == 1) { if (vw & 1) P2LAUNCH(1, 6, 3); else P2LAUNCH(1, 6, 2); }
     else if (vw == 3) P2LAUNCH(2, 4, 3); else if (vw == 2) P2LAUNCH(2, 4, 2);
     else if (vw == 1) P2LAUNCH(2, 4, 1); else P2LAUNCH(2, 4, 0);
 #undef P2LAUNCH
+#undef PRELAUNCH
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[5], e->stream));
     if (pprof) {
@@ -3161,11 +3262,12 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
                 ms, tot[0], tot[1], tot[2], tot[3], tot[4], tot[5]);
     }
     // no host round trip between the phases: Phase P marks touched slots itself, spills bucket
-    // overflow to the v1 replay list, and the straggler pass reads its count on the device
+    // overflow to the v1 replay list, and the combiner applies stragglers in place
     CombineArgs ca;
     memset(&ca, 0, sizeof(ca));
     ca.b_key = e->d_bkey;
     ca.b_rel = e->d_brel;
+    ca.b_n = pre ? e->d_bn : nullptr;
     ca.key_table = e->d_keys;
     ca.b_val0 = e->d_bval[0];
     ca.b_val1 = e->d_bval[1];
@@ -3177,9 +3279,6 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.rel2slot = e->d_rel2slot;
     ca.slot_base = e->d_slot_base;
     ca.stride = e->stride;
-    ca.strag = e->d_strag;
-    ca.strag_n = e->d_strag_n;
-    ca.strag_cap = e->strag_cap;
     ca.st = e->d_st;
     static const int aabl = getenv("FWA_AABL") ? atoi(getenv("FWA_AABL")) : 0;
     ca.abl = aabl;
@@ -3188,26 +3287,24 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     if (aprof && !d_prof) HIPCHK(e, hipMalloc(&d_prof, sizeof(long long) * 8 * kMaxPart));
     ca.prof = aprof ? d_prof : nullptr;
     HIPCHK(e, hipEventRecord(e->ev[6], e->stream));
-    static const int avar = getenv("FWA_AVAR") ? atoi(getenv("FWA_AVAR")) : 4;
     const size_t seg3 = (size_t)1 << e->seg_log;
     const size_t lds3 = seg3 * 8 + 2 * seg3 * 4 + (size_t)(e->nacc - 1) * 2 * seg3 * 8 + 4 * 4 * kSub + 16;
-    int layout = 0;
-    if (e->nacc == 1) layout = 2;
-    else if (e->nacc == 2 && e->ec.acc_kind[1] == ACC_ADD_I64) {
-        for (int j = 0; j < e->cfg.num_aggs; ++j)
-            if (e->ec.agg[j].acc == 1 && e->ec.agg[j].vslot == 0) layout = 1;
-    }
+    static const int mp_env = getenv("FWA_MP") ? atoi(getenv("FWA_MP")) : -1;      // A/B: 0 never, 1 always
+    const bool mp = mp_env == 1 || (mp_env != 0 && e->mp);
+#define C3M(IT, TH, NV, LY, PR) do { if (mp) combine3_kernel<IT, 2, NV, TH, LY, PR, 1><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); \
+        else combine3_kernel<IT, 2, NV, TH, LY, PR, 0><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); } while (0)
 #define C3L(IT, TH, NV) do { \
-        if (layout == 1) combine3_kernel<IT, 2, NV, TH, 1><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); \
-        else if (layout == 2) combine3_kernel<IT, 2, NV, TH, 2><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); \
-        else combine3_kernel<IT, 2, NV, TH, 0><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); } while (0)
-#define C3LAUNCH(IT, TH) do { if (e->nv == 0) C3L(IT, TH, 0); else if (e->nv == 1) C3L(IT, TH, 1); else C3L(IT, TH, 2); } while (0)
-    if (avar == 1) C3LAUNCH(8, 512);
-    else if (avar == 4) C3LAUNCH(4, 1024);
-    else if (avar == 6) C3LAUNCH(4, 512);
+        if (pre && layout == 1) C3M(IT, TH, 1, 1, 1); \
+        else if (pre) C3M(IT, TH, 0, 2, 1); \
+        else if (layout == 1) C3M(IT, TH, NV, 1, 0); \
+        else if (layout == 2) C3M(IT, TH, NV, 2, 0); \
+        else C3M(IT, TH, NV, 0, 0); } while (0)
+    if (e->nv == 0) C3L(4, 1024, 0);
+    else if (e->nv == 1) C3L(4, 1024, 1);
+    else C3L(4, 1024, 2);
+#undef C3L
+#undef C3M
 
-    HIPCHK(e, hipGetLastError());
-    straggler_kernel<<<256, kBlock, 0, e->stream>>>(ca, e->d_ec);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[7], e->stream));
     e->v2_timing_pending = true;
@@ -3217,10 +3314,18 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         HIPCHK(e, hipEventElapsedTime(&ms, e->ev[6], e->ev[7]));
         std::vector<long long> hp(8 * e->np);
         HIPCHK(e, hipMemcpy(hp.data(), d_prof, sizeof(long long) * 8 * e->np, hipMemcpyDeviceToHost));
-        double tot[8] = {0};
-        for (int b = 0; b < e->np; ++b) for (int k = 0; k < 8; ++k) tot[k] += (double)hp[b * 8 + k] / e->np;
-        fprintf(stderr, "[aprof] kernel %.3f ms; per-block avg cycles: %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n",
-                ms, tot[0], tot[1], tot[2], tot[3], tot[4], tot[5], tot[6], tot[7]);
+        double tot[8] = {0}, mx[8] = {0};
+        int bmax = 0;
+        long long bsum_max = 0;
+        for (int b = 0; b < e->np; ++b) {
+            long long bs = 0;
+            for (int k = 0; k < 8; ++k) { tot[k] += (double)hp[b * 8 + k] / e->np; if (k < 6) bs += hp[b * 8 + k]; }
+            if (bs > bsum_max) { bsum_max = bs; bmax = b; }
+        }
+        for (int k = 0; k < 8; ++k) mx[k] = (double)hp[bmax * 8 + k];
+        fprintf(stderr, "[aprof] kernel %.3f ms; per-block avg cycles: %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f | slowest block %d: %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n",
+                ms, tot[0], tot[1], tot[2], tot[3], tot[4], tot[5], tot[6], tot[7], bmax,
+                mx[0], mx[1], mx[2], mx[3], mx[4], mx[5], mx[6], mx[7]);
     }
     e->ingest_launches++;
     e->ingest_records += a.n;
@@ -3738,6 +3843,8 @@ static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, boo
         }
         if (!ran_v2 || round > 0) { rc = account_ingest(e); if (rc) return rc; }
         const DevStatus st = *e->h_st;
+        if (ran_v2 && round == 0 && (int64_t)st.ovf_n * 64 > n) e->pre = true;   // skewed keys: PRE from the next push
+        if (ran_v2 && round == 0 && (int64_t)st.strag_n * 64 > n) e->mp = true;  // wide chunks: window passes
         if (st.error) {
             const char* m = st.error == FWA_E_KEYGROUP ? "Key group is not in the owned KeyGroupRange (StateTable.getMapForKeyGroup)"
                           : st.error == FWA_E_TS_MIN ? "Record has Long.MIN_VALUE timestamp (= no timestamp marker)."
