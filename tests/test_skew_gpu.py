@@ -96,3 +96,16 @@ def test_pre_entries_past_bucket_end_applied_with_atomics(eng_mod, aggs):
     v = rng.integers(-2**40, 2**40, n).astype(np.int64)
     cfg = A.make_config(window_kind="TUMBLE", semantics="TABLE", size_ms=20_000, aggs=aggs, key_capacity=1 << 20)
     _run(eng_mod, cfg, k, t, v, 4, 500, "one-partition")
+
+
+def test_forced_pre_and_window_passes():
+    """FWA_PRE=1 / FWA_MP=1 (process-wide switches) in a child process: the pre-aggregating Phase P and the
+    combiner's window passes from the first push, over Zipf keys, small HOP/CUMULATE slices and late records."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, FWA_PRE="1", FWA_MP="1")
+    r = subprocess.run([sys.executable, os.path.join(here, "forced_modes_check.py")], env=env, timeout=300,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
