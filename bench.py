@@ -262,7 +262,7 @@ def ingest_kernels(args, eng):
     """Names of the kernels whose device time `roofline.achieved` divides by (HIP events around them)."""
     if args.config == "c5s":
         return "sess2_classify+sess2_route+radix sort+scan-by-key+sess2_reduce (+sess2_ordered)"
-    return "partition2_kernel+combine3_kernel+straggler_kernel" if eng.stats().partition_ms > 0 else "ingest_kernel"
+    return "partition3_kernel+combine3_kernel" if eng.stats().partition_ms > 0 else "ingest_kernel"
 
 
 def host_cpus():
