@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host pinned input) leg")
     ap.add_argument("--pcie-batches", type=int, default=3)
+    ap.add_argument("--no-wire", action="store_true", help="skip the wire-input (network bytes in HBM) leg")
+    ap.add_argument("--wire-batches", type=int, default=4)
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "c5s"], default="c2",
                     help="c2: tumbling 10s COUNT+SUM(long), 1M uniform keys (the metric's workload); "
                          "c3: HOP 60s/1s (Table slicing), Zipf(1.1) keys over 1M items; "
@@ -252,6 +254,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args, cfg_kw)
     if rank == 0 and world == 1 and not args.no_pcie and args.config == "c2":
         out["pcie_inclusive"] = pcie_leg(args, cfg_kw, keys, ts, vals, wms, dev)
+    if rank == 0 and world == 1 and not args.no_wire and args.config == "c2":
+        out["wire_input"] = wire_leg(args, cfg_kw, keys, ts, vals, wms, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -342,6 +346,76 @@ def pcie_leg(args, cfg_kw, keys, ts, vals, wms, dev):
     eng.close()
     return {"value": (nb - 1) * B / secs, "unit": "records/s", "batches_timed": nb - 1,
             "note": "host pinned input columns, H2D staging inside fwa_push, outputs left in HBM"}
+
+
+def encode_c2_wire(k, t, v, wm, dev):
+    """The C2 batch as a network channel would carry it (bench input, built on the device): every record a
+    StreamRecord<Tuple3<Long, Long, Long>>(key, ts, val) with its timestamp -- 4-byte big-endian length 33,
+    tag 0, ts, then the three longs (RecordWriter.serializeRecord + StreamElementSerializer.serialize +
+    TupleSerializer, SURVEY.md a4: 37 B per record) -- followed by the batch's watermark element."""
+    import torch
+
+    def be(x):   # int64 -> 8 big-endian bytes per element
+        return x.contiguous().view(torch.uint8).view(-1, 8).flip(1)
+    n = k.shape[0]
+    rec = torch.empty(n, 37, dtype=torch.uint8, device=dev)
+    rec[:, 0:4] = torch.tensor([0, 0, 0, 33], dtype=torch.uint8, device=dev)
+    rec[:, 4] = 0
+    rec[:, 5:13] = be(t)
+    rec[:, 13:21] = be(k)
+    rec[:, 21:29] = be(t)
+    rec[:, 29:37] = be(v)
+    w = torch.tensor([0, 0, 0, 9, 2], dtype=torch.uint8, device=dev)
+    wv = be(torch.tensor([wm], dtype=torch.int64, device=dev)).reshape(-1)
+    return torch.cat([rec.reshape(-1), w, wv])
+
+
+def wire_leg(args, cfg_kw, keys, ts, vals, wms, dev):
+    """Secondary number: the C2 step fed from network bytes already in HBM --
+    fwa_wire_decode (boundary scan + decode into SoA columns) -> fwa_push of the decoded columns -> the
+    watermark element -> fwa_advance_watermark. Also the decode kernels' own roofline: 37 B of wire bytes
+    read + 24 B of columns written per record (61 B algorithmic), HIP events on the decoder's stream."""
+    import torch
+    from flink_amd import _abi as A
+    from flink_amd import engine as E
+    from flink_amd import wire
+    B = args.batch
+    nb = min(args.wire_batches, args.warmup + args.steps)
+    bufs = [encode_c2_wire(keys[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], vals[b * B:(b + 1) * B], wms[b], dev)
+            for b in range(nb)]
+    torch.cuda.synchronize()
+    eng = E.WindowAggregator(A.make_config(**cfg_kw))
+    dec = wire.WireDecoder(wire.make_schema(["LONG", "LONG", "LONG"], key_field=0, ts_field=-1, cols=[2],
+                                            device=dev.index or 0, max_bytes=bufs[0].numel()))
+
+    def step(b):
+        d = dec.decode(bufs[b])
+        assert d.n_records == B and d.n_events == 1 and d.evt_pos[0] == B
+        eng.push(d.key, d.ts, d.cols)
+        return eng.advance_watermark_raw(int(d.evt_val[0][0])).n_rows
+    step(0)                                        # warm-up batch
+    st0 = dec.stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in range(1, nb):
+        step(b)
+    torch.cuda.synchronize()
+    secs = time.perf_counter() - t0
+    st = dec.stats()
+    calls = st.calls - st0.calls
+    dms = (st.decode_ms - st0.decode_ms) / calls
+    sms = (st.scan_ms - st0.scan_ms) / calls
+    alg = 61 * B
+    eng.close()
+    dec.close()
+    return {"value": (nb - 1) * B / secs, "unit": "records/s", "batches_timed": nb - 1,
+            "wire_bytes_per_batch": int(bufs[0].numel()),
+            "decode": {"kernels": "wire_scan_kernel+wire_compose_kernel+wire_resolve_kernel+wire_decode_kernel",
+                       "ms_per_batch": dms, "scan_ms_per_batch": sms, "records_per_s": B / (dms / 1e3),
+                       "alg_bytes_per_record": 61, "achieved": alg / (dms / 1e3) / 1e9, "peak": HBM_PEAK_GBPS,
+                       "unit": "GB/s", "frac": alg / (dms / 1e3) / 1e9 / HBM_PEAK_GBPS},
+            "note": "Tuple3<Long,Long,Long> StreamRecords with timestamps (37 B each) + one watermark element per "
+                    "batch, in HBM; decode + push + fire timed per batch, outputs left in HBM"}
 
 
 if __name__ == "__main__":

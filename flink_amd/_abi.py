@@ -37,7 +37,7 @@ AGG_INPUT_DTYPE = {
 }
 
 STATUS = {0: "OK", -1: "E_ARG", -2: "E_TS_MIN", -3: "E_KEYGROUP", -4: "E_MERGE_LATE", -5: "E_OOM",
-          -6: "E_DEVICE", -7: "E_UNSUPPORTED", -8: "E_STATE"}
+          -6: "E_DEVICE", -7: "E_UNSUPPORTED", -8: "E_STATE", -9: "E_CORRUPT"}
 
 CFG_DYNAMIC_GAP = 0x1
 CFG_LATE_INDICES = 0x2

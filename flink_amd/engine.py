@@ -315,7 +315,7 @@ def dev_view(p, n, dt):
     """Zero-copy torch view of engine-owned device memory."""
     import torch
     if n == 0 or not p:
-        return torch.zeros(0, dtype=getattr(torch, {"i8": "int64", "f4": "float32", "f8": "float64"}[dt.str[1:]]),
+        return torch.zeros(0, dtype=getattr(torch, {"i8": "int64", "f4": "float32", "f8": "float64", "u1": "uint8"}[dt.str[1:]]),
                            device="cuda")
     return torch.as_tensor(_CudaArray(p, n, dt), device="cuda")
 

@@ -104,7 +104,8 @@ enum fwa_status {
     FWA_E_OOM = -5,         /* device memory exhausted */
     FWA_E_DEVICE = -6,      /* HIP runtime error */
     FWA_E_UNSUPPORTED = -7, /* configuration not supported by this engine build */
-    FWA_E_STATE = -8        /* API misuse (e.g. call on a destroyed handle) */
+    FWA_E_STATE = -8,       /* API misuse (e.g. call on a destroyed handle) */
+    FWA_E_CORRUPT = -9      /* malformed wire bytes (IOException "Corrupt stream", StreamElementSerializer.java:208-210) */
 };
 
 /* Flags for fwa_push */

@@ -182,3 +182,38 @@ def bench_pipeline(cfg, params, n, batch, threads):
     cs = C.c_uint64(0)
     secs = lib().or_bench_pipeline(C.byref(cfg), C.byref(params), n, batch, threads, C.byref(rows), C.byref(cs))
     return secs, rows.value, cs.value
+
+
+def wire_decode(schema, data):
+    """Sequential CPU decode of a channel's bytes (oracle/wire_oracle.c). schema: flink_amd.wire.Schema.
+    Returns (status, dict) with numpy columns, events and `consumed`."""
+    L = lib()
+    if not getattr(L, "_wire_bound", False):
+        P = C.c_void_p
+        L.or_wire_decode.argtypes = [P, P, C.c_int64, P, P, P, P, P, P, P, P, P, P, P, P, P]
+        L.or_wire_decode.restype = C.c_int
+        L._wire_bound = True
+    arr = np.frombuffer(bytes(data), np.uint8)
+    nb = arr.size
+    cap_r, cap_e = nb // 6 + 1, nb // 6 + 1
+    fdt = {0: np.int64, 1: np.float64, 2: np.float32, 3: np.int64}
+    key = np.zeros(cap_r, np.int64)
+    ts = np.zeros(cap_r, np.int64)
+    cols = [np.zeros(cap_r, fdt[schema.field[schema.col_field[j]]]) for j in range(schema.num_cols)]
+    rowdata = schema.format == 1
+    cnull = [np.zeros(cap_r, np.uint8) for _ in range(schema.num_cols)] if rowdata else []
+    knull = np.zeros(cap_r, np.uint8) if rowdata else None
+    epos = np.zeros(cap_e, np.int64)
+    etag = np.zeros(cap_e, np.int32)
+    evals = np.zeros((cap_e, 4), np.int64)
+    colp = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
+    nullp = (C.c_void_p * max(1, len(cnull)))(*[c.ctypes.data for c in cnull]) if rowdata else None
+    nr, ne, cons, etg, eps = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int32(), C.c_int64()
+    rc = L.or_wire_decode(C.byref(schema), _ptr(arr), nb, _ptr(key), _ptr(ts), colp, nullp, _ptr(knull), _ptr(epos),
+                          _ptr(etag), _ptr(evals), C.byref(nr), C.byref(ne), C.byref(cons), C.byref(etg), C.byref(eps))
+    n, m = nr.value, ne.value
+    res = {"n_records": n, "n_events": m, "consumed": cons.value, "key": key[:n], "ts": ts[:n],
+           "cols": [c[:n] for c in cols], "col_null": [c[:n] for c in cnull] if rowdata else None,
+           "key_null": knull[:n] if rowdata else None, "evt_pos": epos[:m], "evt_tag": etag[:m],
+           "evt_val": evals[:m], "err_tag": etg.value, "err_pos": eps.value}
+    return rc, res
