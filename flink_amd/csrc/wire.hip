@@ -38,6 +38,7 @@ constexpr uint32_t kNxtEnd = 0xFE;      // chain ends inside the chunk (stream e
 constexpr uint32_t kNxtCorrupt = 0xFF;  // chain hits a malformed element
 constexpr uint32_t kDead = 0xFF;        // resolve: chunk lies after the stream's END (nothing to decode)
 constexpr int kLdsBudget = 60 * 1024;   // compose / resolve LDS per block
+constexpr int64_t kPersistBlocks = 256 * 24;   // scan / decode: persistent single-wave blocks (24 per CU)
 
 // Per-schema constants (kernel argument, copied by value).
 struct WireConst {
@@ -58,19 +59,32 @@ struct WireStatus {
     int64_t consumed;                  // bytes of whole elements (written by the END chunk)
 };
 
-__device__ __forceinline__ uint32_t be32(const uint8_t* b) {
-    return ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | (uint32_t)b[3];
-}
-__device__ __forceinline__ uint64_t be64(const uint8_t* b) { return ((uint64_t)be32(b) << 32) | be32(b + 4); }
-__device__ __forceinline__ uint32_t le32(const uint8_t* b) {
-    return (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
-}
-__device__ __forceinline__ uint64_t le64(const uint8_t* b) { return (uint64_t)le32(b) | ((uint64_t)le32(b + 4) << 32); }
+// The staged chunk in LDS, read through aligned 32-bit words (two ds_read_b32 + a funnel shift per unaligned
+// 4-byte field instead of four byte reads); the buffer carries 8 bytes of padding past the last staged byte.
+struct Lds {
+    const uint32_t* w;
+    __device__ __forceinline__ uint32_t u32le(int p) const {
+        const int i = p >> 2, sh = (p & 3) * 8;
+        return (uint32_t)((((uint64_t)w[i + 1] << 32) | w[i]) >> sh);
+    }
+    __device__ __forceinline__ uint32_t byte(int p) const { return (w[p >> 2] >> ((p & 3) * 8)) & 0xFF; }
+    __device__ __forceinline__ uint32_t be32(int p) const { return __builtin_bswap32(u32le(p)); }
+    __device__ __forceinline__ uint64_t le64(int p) const {
+        const int i = p >> 2, sh = (p & 3) * 8;
+        const uint32_t a = w[i], b = w[i + 1], c = w[i + 2];
+        const uint32_t lo = (uint32_t)((((uint64_t)b << 32) | a) >> sh);
+        const uint32_t hi = (uint32_t)((((uint64_t)c << 32) | b) >> sh);
+        return ((uint64_t)hi << 32) | lo;
+    }
+    __device__ __forceinline__ uint64_t be64(int p) const { return __builtin_bswap64(le64(p)); }
+};
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kBufWords = (kChunk + kMaxStep + 3 + 8 + 3) / 4;
 
 // Copy bytes [0, lim) of src (a chunk start: 4 KiB-aligned offset into the input) into LDS.
-__device__ __forceinline__ void stage_chunk(uint8_t* buf, const uint8_t* __restrict__ src, int lim, bool aligned) {
+__device__ __forceinline__ void stage_chunk(uint32_t* words, const uint8_t* __restrict__ src, int lim, bool aligned) {
+    uint8_t* buf = reinterpret_cast<uint8_t*>(words);
     int done = 0;
     if (aligned) {
         const int n16 = lim >> 4;
@@ -82,43 +96,104 @@ __device__ __forceinline__ void stage_chunk(uint8_t* buf, const uint8_t* __restr
 }
 
 // The chain step shared by scan and decode: classify the element starting at p (rem = bytes left in the stream
-// from the chunk start). Returns 0: a whole element of length 4 + *len; 1: END; 2: CORRUPT.
-__device__ __forceinline__ int element_at(const uint8_t* buf, int p, int64_t rem, const WireConst& w,
-                                          uint32_t* len, int* tag) {
-    if ((int64_t)p + 5 > rem) return 1;
-    const uint32_t l = be32(buf + p);
-    const int t = buf[p + 4];
+// from the chunk start). Returns 0: a whole element of length 4 + *len; 1: END; 2: CORRUPT. The expected body
+// lengths are selected from uniform values (no per-lane indexed load of the kernel argument).
+__device__ __forceinline__ int element_at(const Lds& b, int p, int rem, const WireConst& w, uint32_t* len,
+                                          int* tag) {
+    if (p + 5 > rem) return 1;
+    const uint32_t l = b.be32(p);
+    const int t = (int)b.byte(p + 4);
     *tag = t;
-    if (t > 5 || l != (uint32_t)w.body[t]) return 2;
-    if ((int64_t)p + 4 + l > rem) return 1;
+    const int32_t want = t == 0 ? w.body[0] : t == 1 ? w.body[1] : t == 2 ? w.body[2] : t == 3 ? w.body[3]
+                       : t == 4 ? w.body[4] : t == 5 ? w.body[5] : -1;
+    if (l != (uint32_t)want) return 2;
+    if (p + 4 + (int)l > rem) return 1;
     *len = l;
     return 0;
 }
 
-// ---- scan: one 64-lane block per chunk; lane e walks candidate entry offsets e, e+64, ... < S ----
-__global__ __launch_bounds__(64) void wire_scan_kernel(const uint8_t* __restrict__ in, int64_t nbytes,
-                                                        int64_t nchunks, WireConst w, bool aligned,
-                                                        uint32_t* __restrict__ map0) {
-    __shared__ uint8_t buf[kChunk + kMaxStep + 3];
-    const int64_t c = blockIdx.x;
+// Wave-cooperative walk of the element chain from p through the chunk. Element boundaries are a sequential
+// chain, but almost every element has the length of the one before it (a channel carries one record type), so
+// the wave SPECULATES: lane i checks the header at p + i * R (R = the last element's size); the longest prefix of
+// lanes whose header is a whole element of size R is exactly the next stretch of the chain (each check confirms
+// the previous lane's boundary), one ballot per 64 elements. The first lane that fails is resolved by one scalar
+// step (another element kind / END / CORRUPT), which also sets the new R. visit(pos, tag, rec_before, evt_rank)
+// runs on the lane owning each element. Returns 0 (left the chunk: *stop >= kChunk), 1 END, 2 CORRUPT.
+template <class F>
+__device__ __forceinline__ int wave_walk(const Lds& b, int p, int remi, const WireConst& w, uint32_t* nrec,
+                                         uint32_t* nevt, int* stop, int* badtag, F&& visit) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t nr = 0, ne = 0;
+    int R = 0;
+    for (;;) {
+        if (p >= kChunk) { *nrec = nr; *nevt = ne; *stop = p; return 0; }
+        if (R > 0) {
+            const int pos = p + lane * R;
+            uint32_t len = 0;
+            int tag = 0;
+            const bool ok = pos < kChunk && element_at(b, pos, remi, w, &len, &tag) == 0 && (int)len + 4 == R;
+            const uint64_t m = __ballot(ok);
+            const int k = ~m == 0 ? 64 : __builtin_ctzll(~m);
+            const bool mine = lane < k;
+            const uint64_t rm = __ballot(mine && tag <= 1), em = __ballot(mine && tag > 1);
+            if (mine) visit(pos, tag, nr + (uint32_t)__popcll(rm & below), ne + (uint32_t)__popcll(em & below));
+            nr += (uint32_t)__popcll(rm);
+            ne += (uint32_t)__popcll(em);
+            p += k * R;
+            if (k == 64 || p >= kChunk) continue;
+        }
+        uint32_t len = 0;                                          // scalar step at p (uniform)
+        int tag = 0;
+        const int st = element_at(b, p, remi, w, &len, &tag);
+        if (st) { *nrec = nr; *nevt = ne; *stop = p; *badtag = tag; return st; }
+        if (lane == 0) visit(p, tag, nr, ne);
+        if (tag <= 1) ++nr; else ++ne;
+        R = 4 + (int)len;
+        p += R;
+    }
+}
+
+// Stage chunk c (bytes [cs, cs + min(rem, C + S))) into the block's LDS buffer.
+__device__ __forceinline__ int stage(uint32_t* buf, const uint8_t* __restrict__ in, int64_t nbytes, int64_t c,
+                                     const WireConst& w, bool aligned) {
     const int64_t cs = c * kChunk;
     const int64_t rem = nbytes - cs;
     const int lim = (int)std::min<int64_t>(rem, kChunk + w.step);
+    __syncthreads();                                              // previous chunk fully read
     if (lim > 0) stage_chunk(buf, in + cs, lim, aligned);
     __syncthreads();
-    for (int e = threadIdx.x; e < w.step; e += 64) {
-        int p = e;
-        uint32_t nrec = 0, nevt = 0, nx;
-        for (;;) {
-            if (p >= kChunk) { nx = (uint32_t)(p - kChunk); break; }
+    return (int)std::min<int64_t>(rem, 1 << 30);                  // bytes left, clamped (chains stop within C + S)
+}
+
+// ---- scan: persistent 64-lane blocks, one chunk at a time. Candidates whose first header is already invalid
+// (nearly all of them on real data) are settled in one lane-parallel check; each surviving candidate is walked
+// by the whole wave. ----
+__global__ __launch_bounds__(64) void wire_scan_kernel(const uint8_t* __restrict__ in, int64_t nbytes,
+                                                        int64_t nchunks, WireConst w, bool aligned,
+                                                        uint32_t* __restrict__ map0) {
+    __shared__ uint32_t buf[kBufWords];
+    const Lds b{buf};
+    const int lane = threadIdx.x;
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const int remi = stage(buf, in, nbytes, c, w, aligned);
+        for (int e0 = 0; e0 < w.step; e0 += 64) {
+            const int e = e0 + lane;
             uint32_t len = 0;
             int tag = 0;
-            const int k = element_at(buf, p, rem, w, &len, &tag);
-            if (k) { nx = k == 1 ? kNxtEnd : kNxtCorrupt; break; }
-            if (tag <= 1) ++nrec; else ++nevt;
-            p += 4 + (int)len;
+            const int first = e < w.step ? element_at(b, e, remi, w, &len, &tag) : 3;
+            if (first == 1 || first == 2) map0[c * w.step + e] = first == 1 ? kNxtEnd : kNxtCorrupt;
+            uint64_t alive = __ballot(first == 0);
+            while (alive) {
+                const int j = __builtin_ctzll(alive);
+                alive &= alive - 1;
+                uint32_t nrec = 0, nevt = 0;
+                int stop = 0, bt = 0;
+                const int r = wave_walk(b, e0 + j, remi, w, &nrec, &nevt, &stop, &bt, [](int, int, uint32_t, uint32_t) {});
+                const uint32_t nx = r == 0 ? (uint32_t)(stop - kChunk) : r == 1 ? kNxtEnd : kNxtCorrupt;
+                if (lane == 0) map0[c * w.step + e0 + j] = nx | (nrec << 8) | (nevt << 20);   // <= 683 elements per chunk
+            }
         }
-        map0[c * w.step + e] = nx | (nrec << 8) | (nevt << 20);   // <= 683 elements per 4 KiB chunk
     }
 }
 
@@ -227,107 +302,85 @@ __device__ void raise_err(WireStatus* st, int code, int tag, int64_t pos) {
 
 // Field f of a record whose value starts at q (TUPLE) / whose row starts at q (ROWDATA), as 64 bits
 // (INT sign-extended, FLOAT as its 32 bits in the low word, DOUBLE bits).
-__device__ __forceinline__ uint64_t read_field(const uint8_t* buf, int q, int f, const WireConst& w) {
+__device__ __forceinline__ uint64_t read_field(const Lds& b, int q, int f, const WireConst& w) {
     const int t = w.ftype[f];
-    const uint8_t* b = buf + q + w.foff[f];
+    const int at = q + w.foff[f];
     if (w.format == FWA_WIRE_TUPLE) {
-        if (t == FWA_FIELD_LONG || t == FWA_FIELD_DOUBLE) return be64(b);
-        const uint32_t v = be32(b);
+        if (t == FWA_FIELD_LONG || t == FWA_FIELD_DOUBLE) return b.be64(at);
+        const uint32_t v = b.be32(at);
         return t == FWA_FIELD_INT ? (uint64_t)(int64_t)(int32_t)v : (uint64_t)v;
     }
-    if (t == FWA_FIELD_LONG || t == FWA_FIELD_DOUBLE) return le64(b);
-    const uint32_t v = le32(b);
+    if (t == FWA_FIELD_LONG || t == FWA_FIELD_DOUBLE) return b.le64(at);
+    const uint32_t v = b.u32le(at);
     return t == FWA_FIELD_INT ? (uint64_t)(int64_t)(int32_t)v : (uint64_t)v;
 }
 
-__device__ __forceinline__ bool field_null(const uint8_t* buf, int row, int f) {   // BinarySegmentUtils.bitGet
-    const int bit = f + 8;                                                         // (BinaryRowData header: 8 bits)
-    return (buf[row + (bit >> 3)] >> (bit & 7)) & 1;
+__device__ __forceinline__ bool field_null(const Lds& b, int row, int f) {   // BinarySegmentUtils.bitGet
+    const int bit = f + 8;                                                  // (BinaryRowData header: 8 bits)
+    return (b.byte(row + (bit >> 3)) >> (bit & 7)) & 1;
 }
 
-// ---- decode: one 64-lane block per chunk ----
-__global__ __launch_bounds__(64) void wire_decode_kernel(const uint8_t* __restrict__ in, int64_t nbytes, WireConst w,
-                                                          bool aligned, const uint8_t* __restrict__ c_ent,
+// ---- decode: persistent 64-lane blocks; the chunk's true chain is walked from its resolved entry and every
+// element is decoded by the lane that confirmed it ----
+__global__ __launch_bounds__(64) void wire_decode_kernel(const uint8_t* __restrict__ in, int64_t nbytes, int64_t nchunks,
+                                                          WireConst w, bool aligned, const uint8_t* __restrict__ c_ent,
                                                           const uint64_t* __restrict__ c_rec,
                                                           const uint64_t* __restrict__ c_evt, DecodeOut o) {
-    __shared__ uint8_t buf[kChunk + kMaxStep + 3];
-    __shared__ uint16_t s_off[kChunk / 6 + 1];
-    __shared__ uint16_t s_rank[kChunk / 6 + 1];   // record rank (records) / event rank (events)
-    __shared__ uint16_t s_before[kChunk / 6 + 1]; // events: records of the chunk before it
-    __shared__ int s_ne;
-    const int64_t c = blockIdx.x;
-    const uint32_t ent = c_ent[c];
-    if (ent == kDead) return;
-    const int64_t cs = c * kChunk;
-    const int64_t rem = nbytes - cs;
-    const int lim = (int)std::min<int64_t>(rem, kChunk + w.step);
-    if (lim > 0) stage_chunk(buf, in + cs, lim, aligned);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int p = (int)ent, ne = 0, nr = 0, nv = 0;
-        for (;;) {
-            if (p >= kChunk) break;
-            uint32_t len = 0;
-            int tag = 0;
-            const int k = element_at(buf, p, rem, w, &len, &tag);
-            if (k == 1) { o.st->consumed = cs + p; break; }
-            if (k == 2) { raise_err(o.st, FWA_E_CORRUPT, tag, cs + p); break; }
-            s_off[ne] = (uint16_t)p;
+    __shared__ uint32_t buf[kBufWords];
+    const Lds b{buf};
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const uint32_t ent = c_ent[c];
+        if (ent == kDead) continue;
+        const int64_t cs = c * kChunk;
+        const int remi = stage(buf, in, nbytes, c, w, aligned);
+        const uint64_t rb = c_rec[c], eb = c_evt[c];
+        auto visit = [&](int p, int tag, uint32_t rbefore, uint32_t erank) {
+            int q = p + 5;
             if (tag <= 1) {
-                s_rank[ne] = (uint16_t)nr++;
+                const int64_t g = (int64_t)(rb + rbefore);
+                int64_t ts = (int64_t)0x8000000000000000LL;          // StreamRecord without timestamp
+                if (tag == FWA_TAG_REC_WITH_TIMESTAMP) { ts = (int64_t)b.be64(q); q += 8; }
+                bool knull = false;
+                if (w.format == FWA_WIRE_ROWDATA) {
+                    if ((int32_t)b.be32(q) != w.row_size) { raise_err(o.st, FWA_E_UNSUPPORTED, tag, cs + p); return; }
+                    q += 4;                                          // row bytes start; byte 0 = RowKind
+                    if (b.byte(q) != 0) { raise_err(o.st, FWA_E_UNSUPPORTED, 256 + (int)b.byte(q), cs + p); return; }
+                    knull = field_null(b, q, w.key_field);
+                    if (w.ts_field >= 0 && field_null(b, q, w.ts_field)) { raise_err(o.st, FWA_E_ARG, tag, cs + p); return; }
+                    for (int j = 0; j < w.num_cols; ++j) o.col_null[j][g] = field_null(b, q, w.col_field[j]);
+                    o.key_null[g] = knull;
+                }
+                o.key[g] = knull ? 0 : (int64_t)read_field(b, q, w.key_field, w);
+                o.ts[g] = w.ts_field >= 0 ? (int64_t)read_field(b, q, w.ts_field, w) : ts;
+                for (int j = 0; j < w.num_cols; ++j) {
+                    const int f = w.col_field[j];
+                    const uint64_t v = read_field(b, q, f, w);
+                    if (w.ftype[f] == FWA_FIELD_FLOAT) reinterpret_cast<uint32_t*>(o.col[j])[g] = (uint32_t)v;
+                    else reinterpret_cast<uint64_t*>(o.col[j])[g] = v;
+                }
             } else {
-                s_rank[ne] = (uint16_t)nv++;
-                s_before[ne] = (uint16_t)nr;
+                const int64_t g = (int64_t)(eb + erank);
+                if (g >= o.evt_cap) return;                          // host grows the list and decodes again
+                int64_t v[4] = {0, 0, 0, 0};
+                if (tag == FWA_TAG_WATERMARK) v[0] = (int64_t)b.be64(q);
+                else if (tag == FWA_TAG_STREAM_STATUS) v[0] = (int32_t)b.be32(q);
+                else if (tag == FWA_TAG_LATENCY_MARKER) {
+                    v[0] = (int64_t)b.be64(q);
+                    v[1] = (int64_t)b.be64(q + 8);
+                    v[2] = (int64_t)b.be64(q + 16);
+                    v[3] = (int32_t)b.be32(q + 24);
+                } else v[0] = b.byte(q) != 0;                        // RECORD_ATTRIBUTES: readBoolean
+                o.evt_pos[g] = (int64_t)(rb + rbefore);
+                o.evt_tag[g] = tag;
+                for (int k = 0; k < 4; ++k) o.evt_val[4 * g + k] = v[k];
             }
-            ++ne;
-            p += 4 + (int)len;
-        }
-        s_ne = ne;
-    }
-    __syncthreads();
-    const int ne = s_ne;
-    const uint64_t rb = c_rec[c], eb = c_evt[c];
-    for (int i = threadIdx.x; i < ne; i += 64) {
-        const int p = s_off[i];
-        const int tag = buf[p + 4];
-        int q = p + 5;
-        if (tag <= 1) {
-            const int64_t g = (int64_t)(rb + s_rank[i]);
-            int64_t ts = (int64_t)0x8000000000000000LL;         // StreamRecord without timestamp
-            if (tag == FWA_TAG_REC_WITH_TIMESTAMP) { ts = (int64_t)be64(buf + q); q += 8; }
-            bool knull = false;
-            if (w.format == FWA_WIRE_ROWDATA) {
-                if ((int32_t)be32(buf + q) != w.row_size) { raise_err(o.st, FWA_E_UNSUPPORTED, tag, cs + p); continue; }
-                q += 4;                                            // row bytes start; byte 0 = RowKind
-                if (buf[q] != 0) { raise_err(o.st, FWA_E_UNSUPPORTED, 256 + buf[q], cs + p); continue; }
-                knull = field_null(buf, q, w.key_field);
-                if (w.ts_field >= 0 && field_null(buf, q, w.ts_field)) { raise_err(o.st, FWA_E_ARG, tag, cs + p); continue; }
-                for (int j = 0; j < w.num_cols; ++j) o.col_null[j][g] = field_null(buf, q, w.col_field[j]);
-                o.key_null[g] = knull;
-            }
-            o.key[g] = knull ? 0 : (int64_t)read_field(buf, q, w.key_field, w);
-            o.ts[g] = w.ts_field >= 0 ? (int64_t)read_field(buf, q, w.ts_field, w) : ts;
-            for (int j = 0; j < w.num_cols; ++j) {
-                const int f = w.col_field[j];
-                const uint64_t v = read_field(buf, q, f, w);
-                if (w.ftype[f] == FWA_FIELD_FLOAT) reinterpret_cast<uint32_t*>(o.col[j])[g] = (uint32_t)v;
-                else reinterpret_cast<uint64_t*>(o.col[j])[g] = v;
-            }
-        } else {
-            const int64_t g = (int64_t)(eb + s_rank[i]);
-            if (g >= o.evt_cap) continue;                          // host grows the list and decodes again
-            int64_t v[4] = {0, 0, 0, 0};
-            if (tag == FWA_TAG_WATERMARK) v[0] = (int64_t)be64(buf + q);
-            else if (tag == FWA_TAG_STREAM_STATUS) v[0] = (int32_t)be32(buf + q);
-            else if (tag == FWA_TAG_LATENCY_MARKER) {
-                v[0] = (int64_t)be64(buf + q);
-                v[1] = (int64_t)be64(buf + q + 8);
-                v[2] = (int64_t)be64(buf + q + 16);
-                v[3] = (int32_t)be32(buf + q + 24);
-            } else v[0] = buf[q] != 0;                             // RECORD_ATTRIBUTES: readBoolean
-            o.evt_pos[g] = (int64_t)(rb + s_before[i]);
-            o.evt_tag[g] = tag;
-            for (int k = 0; k < 4; ++k) o.evt_val[4 * g + k] = v[k];
+        };
+        uint32_t nrec = 0, nevt = 0;
+        int stop = 0, bt = 0;
+        const int r = wave_walk(b, (int)ent, remi, w, &nrec, &nevt, &stop, &bt, visit);
+        if (threadIdx.x == 0) {
+            if (r == 1) o.st->consumed = cs + stop;
+            else if (r == 2) raise_err(o.st, FWA_E_CORRUPT, bt, cs + stop);
         }
     }
 }
@@ -594,7 +647,8 @@ int fwa_wire_decode(fwa_wire_decoder* d, const uint8_t* bytes, int64_t nbytes, i
     hipStream_t st = d->stream;
     WCK(hipMemsetAsync(d->d_st, 0, sizeof(WireStatus), st));
     WCK(hipEventRecord(d->ev[0], st));
-    hipLaunchKernelGGL(wire_scan_kernel, dim3((unsigned)nchunks), dim3(64), 0, st, in, nbytes, nchunks, w, aligned, d->map0);
+    const unsigned grid = (unsigned)std::min<int64_t>(nchunks, kPersistBlocks);
+    hipLaunchKernelGGL(wire_scan_kernel, dim3(grid), dim3(64), 0, st, in, nbytes, nchunks, w, aligned, d->map0);
     WCK(hipGetLastError());
     WCK(hipEventRecord(d->ev[1], st));
     auto level_map = [&](int l) {
@@ -640,7 +694,7 @@ int fwa_wire_decode(fwa_wire_decoder* d, const uint8_t* bytes, int64_t nbytes, i
         o.evt_tag = d->d_evt_tag;
         o.evt_val = d->d_evt_val;
         o.evt_cap = d->evt_cap;
-        hipLaunchKernelGGL(wire_decode_kernel, dim3((unsigned)nchunks), dim3(64), 0, st, in, nbytes, w, aligned,
+        hipLaunchKernelGGL(wire_decode_kernel, dim3(grid), dim3(64), 0, st, in, nbytes, nchunks, w, aligned,
                            d->ent, d->rec, d->evt, o);
         WCK(hipGetLastError());
         WCK(hipEventRecord(d->ev[2], st));
