@@ -189,12 +189,13 @@ def main():
     # HBM traffic per ingest launch (Phase P + Phase A) from the committed rocprofv3 PMC passes of this
     # same workload (counters need their own runs: tools/gpu_pmc.sh); null for other shapes
     traffic, traffic_src = None, None
-    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_c2_final.json")
-    if args.config == "c2" and os.path.exists(pmc_path):
+    pmc_path = os.path.join(ROOT, "profiles", "r02_pmc_%s.json" % args.config)
+    if world == 1 and os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
         if pmc["config"]["batch"] == B:
             traffic = pmc["ingest_bytes_per_launch"]
-            traffic_src = "profiles/r01_pmc_c2_final.json (FETCH_SIZE x2 + WRITE_SIZE, partition2 + combine3)"
+            traffic_src = ("profiles/r02_pmc_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the ingest kernels per "
+                           "timed step, tools/gpu_pmc_all.sh)" % args.config)
     if args.config == "c3":
         metric = "records/sec aggregated (C3: HOP 60s/1s, Zipf(1.1) keys over %d items)" % args.keys
         workload = ("C3: Table HOP 60s/1s (1s slices) COUNT+SUM(long), Zipf(1.1) over %d keys, %d records/GPU "

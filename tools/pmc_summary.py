@@ -1,0 +1,83 @@
+"""Summarise tools/gpu_pmc_all.sh output into profiles/<tag>_pmc_<cfg>.json.
+
+Per kernel: FETCH_SIZE (x2, the gfx950 correction of MI355X_MICROARCH.md: FETCH_SIZE reports half the bytes of a
+wide coalesced read) and WRITE_SIZE per dispatch. Per timed step: the bytes of the ingest kernels (everything but
+the fire, generator, torch and runtime-copy kernels) over the last `steps` steps' share of the dispatches,
+against the algorithmic bytes of the step (24 B per record, 28 B for the C5 float columns).
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+EXCLUDE = re.compile(r"fire|generate_kernel|reduce_kernel|elementwise|rocclr|reset|fill_u64|push_reset|wire_")
+
+
+def short(name):
+    m = re.search(r"(?:::)?([A-Za-z_][A-Za-z0-9_]*)(?:<|\()", name)
+    base = m.group(1) if m else name[:40]
+    if "DeviceRadixSort" in name or "radix" in name.lower():
+        base = "hipcub_radix_sort"
+    elif "DeviceScan" in name or "scan" in name.lower() and "hipcub" in name.lower():
+        base = "hipcub_scan"
+    return base
+
+
+def read(path):
+    f = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)
+    if not f:
+        return {}
+    per = {}
+    with open(f[0]) as fh:
+        for r in csv.DictReader(fh):
+            k = short(r["Kernel_Name"])
+            per.setdefault(k, []).append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    for k in per:
+        per[k].sort()
+    return per
+
+
+def main(root, tag, steps=3):
+    out_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
+    for cfg in ("c2", "c3", "c4", "c5", "c5s"):
+        fe = read(os.path.join(root, "%s_FETCH_SIZE" % cfg))
+        wr = read(os.path.join(root, "%s_WRITE_SIZE" % cfg))
+        if not fe or not wr:
+            continue
+        warm = 2 if cfg == "c3" else 1
+        total_steps = steps + warm
+        # timed steps = the dispatches after the last warm-up step's fire (one fire kernel per step)
+        fires = sorted(d for k, v in fe.items() if "fire" in k for d, _ in v)
+        bound = fires[len(fires) - steps - 1] if len(fires) > steps else -1
+        res, step_bytes = {}, 0.0
+        for k in sorted(set(fe) | set(wr)):
+            f = [(d, v * 1024 * 2) for d, v in fe.get(k, [])]   # KB -> bytes, x2 gfx950 correction
+            w = [(d, v * 1024) for d, v in wr.get(k, [])]
+            res[k] = {"dispatches": max(len(f), len(w)), "fetch_bytes_x2_per_dispatch": [v for _, v in f],
+                      "write_bytes_per_dispatch": [v for _, v in w]}
+            if not EXCLUDE.search(k):
+                tf = [v for d, v in f if d > bound]
+                tw = [v for d, v in w if d > bound]
+                sb = (sum(tf) + sum(tw)) / steps
+                res[k]["bytes_per_timed_step"] = sb
+                res[k]["timed_dispatches"] = len(tf)
+                step_bytes += sb
+        batch = 1 << 26
+        rec = 28 if cfg in ("c5", "c5s") else 24
+        doc = {"note": "rocprofv3 --pmc FETCH_SIZE; WRITE_SIZE in separate runs (tools/gpu_pmc_all.sh), bench.py "
+                       "--config %s --steps %d --warmup %d; FETCH_SIZE x2 (gfx950), WRITE_SIZE as reported; "
+                       "ingest = every kernel except fire / generator / torch / runtime copies, dispatched after the warm-up's last fire (%d timed steps)"
+                       % (cfg, steps, warm, steps),
+               "config": {"workload": cfg, "batch": batch}, "per_kernel": res,
+               "ingest_bytes_per_launch": step_bytes, "alg_bytes_per_launch": rec * batch,
+               "traffic_over_alg": step_bytes / (rec * batch)}
+        with open(os.path.join(out_dir, "%s_pmc_%s.json" % (tag, cfg)), "w") as fh:
+            json.dump(doc, fh, indent=1)
+        print(cfg, "ingest bytes/step %.3g" % step_bytes, "x alg %.2f" % (step_bytes / (rec * batch)),
+              {k: round(v.get("bytes_per_timed_step", 0) / 1e6) for k, v in res.items() if "bytes_per_timed_step" in v})
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmca", sys.argv[2] if len(sys.argv) > 2 else "r02")
