@@ -2822,6 +2822,14 @@ const char* fwa_version(void) { return "flink_amd 0.1 (gfx950)"; }
 
 const char* fwa_last_error(const fwa_engine* e) { return e ? e->err.c_str() : "null engine"; }
 
+// internal accessors for the host-only layers compiled into the same library (heap_snapshot.cpp)
+int fwa_get_config(const fwa_engine* e, fwa_config* out) {
+    if (!e || !out) return FWA_E_ARG;
+    *out = e->cfg;
+    return FWA_OK;
+}
+int fwa_set_error(fwa_engine* e, int code, const char* msg) { return fail(e, code, msg); }
+
 void fwa_destroy(fwa_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->cfg.device);

@@ -55,6 +55,11 @@ def lib():
     L.fwa_blob_free.restype = None
     L.fwa_restore.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.c_int32]
     L.fwa_restore.restype = C.c_int
+    L.fwa_snapshot_heap.argtypes = [C.c_void_p, C.POINTER(Blob), C.c_void_p, C.POINTER(C.c_int64)]
+    L.fwa_snapshot_heap.restype = C.c_int
+    L.fwa_restore_heap.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                   C.c_int32]
+    L.fwa_restore_heap.restype = C.c_int
     L.fwa_flush.argtypes = [C.c_void_p]
     L.fwa_flush.restype = C.c_int
     L.fwa_version.restype = C.c_char_p
@@ -255,6 +260,30 @@ class WindowAggregator:
         ptrs = (C.c_void_p * max(1, len(bufs)))(*[C.cast(b, C.c_void_p).value for b in bufs])
         sizes = (C.c_int64 * max(1, len(bufs)))(*[len(b) for b in blobs])
         rc = lib().fwa_restore(self.h, ptrs, sizes, len(bufs))
+        self._settled()
+        _check(rc, self.h)
+
+    def snapshot_heap(self):
+        """Keyed window state in Flink's heap-backend key-group byte layout (fwa_snapshot_heap): returns
+        (body bytes, per-key-group section offsets, watermark)."""
+        b = Blob()
+        nkg = self.cfg.kg_end - self.cfg.kg_start + 1
+        offs = np.zeros(nkg, np.int64)
+        wm = C.c_int64(0)
+        rc = lib().fwa_snapshot_heap(self.h, C.byref(b), offs.ctypes.data_as(C.c_void_p), C.byref(wm))
+        self._settled()
+        _check(rc, self.h)
+        try:
+            return (C.string_at(b.data, b.size) if b.size else b""), offs, wm.value
+        finally:
+            lib().fwa_blob_free(C.byref(b))
+
+    def restore_heap(self, bodies, watermarks):
+        bufs = [C.create_string_buffer(bytes(b), max(1, len(b))) for b in bodies]
+        ptrs = (C.c_void_p * len(bufs))(*[C.cast(b, C.c_void_p).value for b in bufs])
+        sizes = (C.c_int64 * len(bufs))(*[len(b) for b in bodies])
+        wms = (C.c_int64 * len(bufs))(*[int(w) for w in watermarks])
+        rc = lib().fwa_restore_heap(self.h, ptrs, sizes, wms, len(bufs))
         self._settled()
         _check(rc, self.h)
 

@@ -31,6 +31,8 @@
  *   fwa_snapshot           HeapSnapshotStrategy (keyed window state by key group) + the watermark union
  *                            state of SlicingWindowOperator.snapshotState (:204-209)
  *   fwa_restore            HeapRestoreOperation / SlicingWindowOperator.initializeState (:186-202)
+ *   fwa_snapshot_heap      HeapSnapshotStrategy key-group sections (HeapSnapshotStrategy.java:154-175) in Flink's bytes
+ *   fwa_restore_heap       HeapRestoreOperation over those sections
  *   fwa_destroy            WindowOperator.close / SlicingWindowProcessor.close
  *
  * Status codes mirror the Java exceptions the reference throws.
@@ -295,6 +297,28 @@ void fwa_blob_free(fwa_blob* b);
  * MIN of the snapshots' watermarks (SlicingWindowOperator.initializeState :186-202). Windows that
  * fired before the snapshot do not fire again. */
 int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, int32_t n_blobs);
+
+/* The same keyed state in the byte layout of Flink's heap keyed-state backend (HeapSnapshotStrategy.java:154-175):
+ * for each owned key group g = kg_start..kg_end, in order: int g; short 0 (window state), int n, n x (namespace,
+ * key, accumulator) (CopyOnWriteStateMapSnapshot.writeState :138-148); short 1 (event-time timers), int m, m x
+ * (long flipSignBit(ts), key, namespace) (TimerSerializer.serialize :147-152). Big-endian java.io.DataOutput.
+ *   DATASTREAM TUMBLE (WindowOperator): namespace TimeWindow (long start, long end), key Long, accumulator a Tuple of
+ *     Long COUNT(*) then one field per aggregate (Long for COUNT / BIGINT SUM / AVG / MIN / MAX, Double for floating
+ *     SUM / AVG / MIN / MAX), timers at window.maxTimestamp() and, with allowed lateness, at the cleanup time.
+ *   TABLE TUMBLE (SlicingWindowOperator): namespace Long slice end, key BinaryRowData(BIGINT), accumulator a
+ *     BinaryRowData of the same fields (BinaryRowDataSerializer), timer at slice end - 1.
+ * kg_offsets[g - kg_start] receives the byte offset of key group g's section (KeyGroupRangeOffsets; the Java shim
+ * writes its KeyedBackendSerializationProxy header in front and shifts them), *watermark the operator watermark
+ * (union list state, SlicingWindowOperator.java:204-209). Other window kinds, a shift time zone, nullable columns or
+ * PREHASHED keys: FWA_E_UNSUPPORTED (fwa_snapshot covers them). The blob is freed with fwa_blob_free. */
+int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark);
+
+/* Restore a fresh handle from heap-layout bodies (as written by fwa_snapshot_heap on handles with the same window
+ * and aggregate configuration, any key-group ranges): the key groups of [kg_start, kg_end] are read, timers are
+ * re-derived from the window state, the watermark is the MIN of watermarks[] (HeapRestoreOperation /
+ * SlicingWindowOperator.initializeState :186-202). */
+int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* sizes, const int64_t* watermarks,
+                     int32_t n_bodies);
 
 /* FWA_CFG_LATE_INDICES: indices (ascending, into the last push's batch) of the records that push dropped as
  * late -- the records WindowOperator would send to its lateDataOutputTag side output, and those for which
