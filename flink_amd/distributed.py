@@ -52,6 +52,7 @@ class KeyedWindowPipeline:
             engine_factory = WindowAggregator
         self.engine = engine_factory(self.cfg)
         self.route = router or _gpu_router(maxp, world, self.cfg.key_kind)
+        self.route_on_gpu = router is None          # a custom router (tests) keeps the torch grouping
         self.names = A.agg_names(self.cfg)
         self.exchanged = 0
 
@@ -94,18 +95,25 @@ def unpack_col(cell, dtype):
 
 
 def exchange_rows(pipe, keys, cols):
-    """keyBy exchange of a row set: route by key group, pack the columns into one int64 [n, m] tensor,
-    one all_to_all of the counts and one all_to_all_single of the rows (RCCL over xGMI). Returns the
-    received rows (int64 [n_recv, m]; 4-byte columns travel zero-extended in their 8-byte cell)."""
-    dest = pipe.route(keys)
+    """keyBy exchange of a row set: route by key group, pack the columns into one int64 [n, m] tensor grouped by
+    destination, one all_to_all of the counts and one all_to_all_single of the rows (RCCL over xGMI). Returns the
+    received rows (int64 [n_recv, m]; 4-byte columns travel zero-extended in their 8-byte cell).
+    Device batches are routed and packed by the HIP counting sort (fwa_route_rows); host tensors (the gloo tests)
+    by the same stable grouping in torch."""
     n = int(keys.shape[0])
-    packed = torch.empty((n, len(cols)), dtype=torch.int64, device=keys.device)
-    for j, x in enumerate(cols):
-        packed[:, j] = x.view(torch.int64) if x.dtype.itemsize == 8 else x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
-    if pipe.world > 1:
-        order = torch.argsort(dest, stable=True)
-        packed = packed[order]
-    counts = torch.bincount(dest, minlength=pipe.world)
+    if keys.is_cuda and pipe.route_on_gpu:
+        from . import engine
+        packed, counts = engine.route_rows(keys, [c.contiguous() for c in cols], pipe.cfg.max_parallelism, pipe.world,
+                                           key_kind=pipe.cfg.key_kind)
+    else:
+        dest = pipe.route(keys)
+        packed = torch.empty((n, len(cols)), dtype=torch.int64, device=keys.device)
+        for j, x in enumerate(cols):
+            packed[:, j] = x.view(torch.int64) if x.dtype.itemsize == 8 else x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        if pipe.world > 1:
+            order = torch.argsort(dest, stable=True)
+            packed = packed[order]
+        counts = torch.bincount(dest, minlength=pipe.world)
     recv_counts = torch.empty_like(counts)
     dist.all_to_all_single(recv_counts, counts, group=pipe.group)
     send = counts.tolist()

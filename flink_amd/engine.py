@@ -72,6 +72,9 @@ def lib():
     L.fwa_key_groups.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                  C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
     L.fwa_key_groups.restype = C.c_int
+    L.fwa_route_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                 C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+    L.fwa_route_rows.restype = C.c_int
     L.fwa_generate.argtypes = [C.POINTER(A.GenParams), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                                C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     L.fwa_generate.restype = C.c_int
@@ -374,6 +377,24 @@ def key_groups(keys, max_parallelism=128, parallelism=1, key_kind=A.KEY_JAVA_LON
                               _ptr(kg), _ptr(op), A.PUSH_DEVICE_PTRS if dev else 0, device)
     _check(rc, None, "fwa_key_groups")
     return kg, op
+
+
+def route_rows(keys, cols, max_parallelism, parallelism, key_kind=A.KEY_JAVA_LONG, key_hash=None):
+    """keyBy send side on the GPU (fwa_route_rows): torch CUDA columns -> (int64 [n, len(cols)] rows grouped by
+    destination subtask, in arrival order within one; int64 [parallelism] row counts). Runs on torch's current
+    stream."""
+    import torch
+    n = int(keys.shape[0])
+    dev = keys.device
+    out = torch.empty((n, len(cols)), dtype=torch.int64, device=dev)
+    counts = torch.empty(parallelism, dtype=torch.int64, device=dev)
+    ptrs = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
+    nbytes = (C.c_int32 * len(cols))(*[c.element_size() for c in cols])
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    rc = lib().fwa_route_rows(_ptr(keys), _ptr(key_hash), n, key_kind, max_parallelism, parallelism, ptrs, nbytes,
+                              len(cols), _ptr(out), _ptr(counts), dev.index or 0, C.c_void_p(stream))
+    _check(rc, None, "fwa_route_rows")
+    return out, counts
 
 
 def generate(params, n, keys=None, ts=None, v_i64=None, v_f32=None, v_f64=None, device=0, stream=None):

@@ -25,6 +25,7 @@
  *   fwa_drain_partials     LocalSlicingWindowAggOperator -> RecordsWindowBuffer.flush (local half of two-phase)
  *                            LocalSlicingWindowAggOperator.java:111-137
  *   fwa_push_partials      GlobalAggCombiner.combine (global half)  GlobalAggCombiner.java:77-110
+ *   fwa_route_rows         KeyGroupStreamPartitioner.selectChannel + per-channel packing (the keyBy send side)
  *   fwa_key_groups         KeyGroupRangeAssignment.assignToKeyGroup + computeOperatorIndexForKeyGroup
  *                            flink-runtime/.../state/KeyGroupRangeAssignment.java:63-127
  *                          (the keyBy partitioner KeyGroupStreamPartitioner.selectChannel :55-65)
@@ -336,6 +337,16 @@ int fwa_reset_timers(fwa_engine* e);
 int fwa_key_groups(const int64_t* keys, const int32_t* key_hash, int64_t n, int32_t key_kind,
                    int32_t max_parallelism, int32_t parallelism, int32_t* kg_out, int32_t* op_out,
                    int32_t flags, int32_t device);
+
+/* keyBy send side of a columnar batch (KeyGroupStreamPartitioner.selectChannel :55-65 + the RecordWriter's
+ * per-channel serialisation, RecordWriter.java:104-157), on the device: dest(i) = computeOperatorIndexForKeyGroup(
+ * max_parallelism, parallelism, assignToKeyGroup(key_i)); the ncols columns (cols[c]: col_bytes[c] = 4 or 8 bytes
+ * per row, 4-byte columns zero-extended) are packed into out[n][ncols] int64 rows grouped by destination, in arrival
+ * order within a destination, and counts[d] receives the rows for destination d (parallelism <= 64, ncols <= 16).
+ * All pointers are device pointers; work is enqueued on `stream` (NULL: the default stream) and complete on return. */
+int fwa_route_rows(const int64_t* keys, const int32_t* key_hash, int64_t n, int32_t key_kind, int32_t max_parallelism,
+                   int32_t parallelism, const void* const* cols, const int32_t* col_bytes, int32_t ncols, int64_t* out,
+                   int64_t* counts, int32_t device, void* stream);
 
 /* ---- bench / test support (synthetic streams of SURVEY.md §8(d), generated in HBM) ---- */
 typedef struct fwa_gen_params {
