@@ -434,6 +434,10 @@ struct PartArgs {
     int32_t* touched;                  // per slot
     int32_t* spill;
     int64_t q_base;
+    int64_t base_ts;                   // off + q_base * g: first timestamp of slice q_base (fast path)
+    uint64_t fast_lim;                 // kRelCap * g (< 2^32) or 0
+    uint64_t fast_m;                   // ceil(2^fast_sh / g): exact floor(dd / g) for dd < fast_lim; 0 = no fast path
+    int32_t fast_sh, pad_fast;
     unsigned long long* b_key;         // [np][capb]
     unsigned long long* b_val0;
     unsigned long long* b_val1;
@@ -487,10 +491,16 @@ __device__ __forceinline__ void block_scan_np(const uint32_t* hist, uint32_t* to
     }
     if (lane == 63) wsum[wid] = incl;
     __syncthreads();
-    if (tid == 0) {
-        uint32_t run = 0;
-        for (int w = 0; w < THREADS / 64; ++w) { const uint32_t t = wsum[w]; wsum[w] = run; run += t; }
-        *total = run;
+    if (wid == 0) {                     // the per-wave sums, scanned by one wave (not a serial loop)
+        constexpr int NW = THREADS / 64;
+        const uint32_t v = lane < NW ? wsum[lane] : 0u;
+        uint32_t r = v;
+        for (int d = 1; d < NW; d <<= 1) {
+            const uint32_t y = __shfl_up(r, d);
+            if (lane >= d) r += y;
+        }
+        if (lane < NW) wsum[lane] = r - v;
+        if (lane == NW - 1) *total = r;
     }
     __syncthreads();
     uint32_t excl = wsum[wid] + incl - x;
@@ -739,10 +749,13 @@ __device__ __noinline__ void pre_apply_global(unsigned long long* table, uint64_
     if (has_sum) atomicAdd(&base[stride + kid], sum);
 }
 
-template <int NV, int ITEMS, int THREADS, int VW, int KG, int PRE = 0>
+// W16: the tile's columns are read with 16-byte loads (two records per lane per column; 8-byte loads reach
+// roughly 0.6x the 16-byte rate, MI355X_MICROARCH.md): item j of a lane is record 2 * ((j / 2) * THREADS + tid) + j % 2.
+template <int NV, int ITEMS, int THREADS, int VW, int KG, int PRE = 0, int W16 = 0>
 __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
     static_assert(THREADS == kMaxPart && ITEMS <= 8, "one partition cursor per thread; trash area of 8 x kMaxPart");
     static_assert(!PRE || NV <= 1, "pre-aggregation: COUNT [+ one BIGINT sum]");
+    static_assert(!W16 || (ITEMS % 2 == 0 && KG != 2 && NV <= 1), "paired loads: even ITEMS, no key-hash column");
     constexpr int kTile = THREADS * ITEMS;
     constexpr int kHt = 2 * kTile;                     // PRE: (key, slice) hash table, load <= 0.5
     constexpr int kHtLog = __builtin_ctz(kHt);
@@ -784,7 +797,32 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
     const int64_t n = a.n;
     // every load of a tile is issued before any is used; uniform branches sit outside the item loops
     // (a per-item select between a 4- and an 8-byte load made hipcc wait vmcnt(0) at every join)
+    auto xof = [&](int j) -> int { return W16 ? 2 * ((j >> 1) * THREADS + tid) + (j & 1) : j * THREADS + tid; };
     auto load = [&](int64_t t) {
+        if constexpr (W16) {
+            // pair p = records 2p, 2p+1 of the tile; a pair reaching past n is not loaded (its record n-1, if any,
+            // goes to the slow path below)
+#pragma unroll
+            for (int jj = 0; jj < ITEMS / 2; ++jj) {
+                const int64_t pi = t * (kTile / 2) + (int64_t)jj * THREADS + tid;
+                const int64_t ip = 2 * pi + 1 < n ? pi : 0;
+                const ulonglong2 kk = reinterpret_cast<const ulonglong2*>(pkeys)[ip];
+                const longlong2 tt = reinterpret_cast<const longlong2*>(pts)[ip];
+                r_key[2 * jj] = kk.x; r_key[2 * jj + 1] = kk.y;
+                r_ts[2 * jj] = tt.x; r_ts[2 * jj + 1] = tt.y;
+                if constexpr (NV > 0) {
+                    if constexpr (w0) {
+                        const ulonglong2 vv = reinterpret_cast<const ulonglong2*>(pc0)[ip];
+                        r_v0[2 * jj] = vv.x; r_v0[2 * jj + 1] = vv.y;
+                    } else {
+                        const uint2 vv = reinterpret_cast<const uint2*>(pc0)[ip];
+                        r_v0[2 * jj] = vv.x; r_v0[2 * jj + 1] = vv.y;
+                    }
+                }
+                r_kh[2 * jj] = 0; r_kh[2 * jj + 1] = 0;
+            }
+            return;
+        }
         int64_t ic[ITEMS];
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
@@ -856,14 +894,22 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         }
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-            const int64_t i = t0 + (int64_t)j * THREADS + tid;
+            const int64_t i = t0 + xof(j);
             const int64_t key = (int64_t)r_key[j];
             const int64_t ts = r_ts[j];
-            const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
-            const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
-            const uint64_t uq = jm::udiv64(ud, c.g_div);
-            const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
-            const uint64_t rel = (uint64_t)(q - a.q_base);
+            // slice relative to q_base: a timestamp within kRelCap slices of the base takes a 32-bit division
+            // (one 32 x 33-bit multiply); anything else (and shift time zones) the exact 64-bit floor division
+            uint64_t rel;
+            const uint64_t dd = (uint64_t)ts - (uint64_t)a.base_ts;
+            if (a.fast_m && dd < a.fast_lim) {
+                rel = (dd * a.fast_m) >> a.fast_sh;
+            } else {
+                const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
+                const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
+                const uint64_t uq = jm::udiv64(ud, c.g_div);
+                const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
+                rel = (uint64_t)(q - a.q_base);
+            }
             uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
             if constexpr (KG != 0) {
                 const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, r_kh[j]), c.max_par);
@@ -872,6 +918,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             if (ds && ts == LONG_MIN_J) code = kCodeSlow;
             if (a.any_null && i < a.n && row_has_null(a, i)) code = kCodeSlow;   // SQL NULLs: the v1 path
             if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
+            if (W16 && i == a.n - 1 && (a.n & 1)) code = kCodeSlow;     // unpaired last record: the v1 replay
             if (i >= a.n) code = 0xff;
             dropped += code == kCodeDrop;
             note_drop(a.dropidx, a.st, code == kCodeDrop, i);
@@ -890,7 +937,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 relmin = min(relmin, (uint32_t)rel);
                 const uint64_t h = jm::mix64((uint64_t)key);
                 const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
-                const int x = j * THREADS + tid;
+                const int x = xof(j);
                 x_key[x] = r_key[j];
                 x_rel[x] = (uint16_t)rel;
                 if (NV > 0) x_val[0][x] = r_v0[j];
@@ -904,7 +951,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j) {
                 if (r_pos[j] == ~0u) continue;
-                const uint32_t x = (uint32_t)(j * THREADS + tid);
+                const uint32_t x = (uint32_t)xof(j);
                 const unsigned long long key = r_key[j];
                 const uint32_t rel = x_rel[x];
                 uint32_t hs = ((uint32_t)key * 0x9E3779B1u + (uint32_t)(key >> 32) * 0x85EBCA77u + rel * 0xC2B2AE3Du) >> (32 - kHtLog);
@@ -939,6 +986,14 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         uint32_t g = 0;
         if (h) g = atomicAdd(&a.b_cnt[p * kSub + sub], h);
         load(tile + gridDim.x < ntiles ? tile + gridDim.x : tile);   // next tile in flight from here on (unconditional)
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {               // the LDS scatter does not need the reservation: the
+            if (r_pos[j] == ~0u) continue;              // reservation's latency overlaps this loop
+            const uint32_t p = r_pos[j] >> 16;
+            const uint32_t sidx = toff[p] + (r_pos[j] & 0xffffu);
+            s_part[sidx] = (uint16_t)p;
+            s_src[sidx] = (uint16_t)xof(j);
+        }
         if (p < a.np) {
             gbase[p] = g;
             // records past the sub-bucket's end (skewed keys) go to the v1 replay: one spill reservation
@@ -950,14 +1005,6 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 atomicAdd(&a.st->ovf_n, (int32_t)ov);
                 if constexpr (!PRE) sbase[p] = (uint32_t)atomicAdd(&a.st->spill_n, (int32_t)ov);
             }
-        }
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            if (r_pos[j] == ~0u) continue;
-            const uint32_t p = r_pos[j] >> 16;
-            const uint32_t sidx = toff[p] + (r_pos[j] & 0xffffu);
-            s_part[sidx] = (uint16_t)p;
-            s_src[sidx] = (uint16_t)(j * THREADS + tid);
         }
         __syncthreads();
         QMARK(2);
@@ -3206,6 +3253,23 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.touched = e->d_touched;
     pa.spill = e->d_spill;
     pa.q_base = q_base;
+    pa.fast_m = 0;
+    pa.fast_lim = 0;
+    pa.base_ts = 0;
+    pa.fast_sh = 0;
+    if (!e->cfg.tz_n && e->g > 0 && (uint64_t)e->g * kRelCap < (1ull << 32) && q_base > -(1ll << 40) && q_base < (1ll << 40)) {
+        // floor(n / g) = (n * ceil(2^(32+L) / g)) >> (32+L) for every n < 2^32, L = ceil(log2 g) (round-up method;
+        // the magic has at most 33 bits, so n * m fits 64 bits)
+        int L = 0;
+        while ((1ull << L) < (uint64_t)e->g) ++L;
+        const __int128 b = (__int128)e->off + (__int128)q_base * e->g;
+        if (b > (__int128)INT64_MIN / 2 && b < (__int128)INT64_MAX / 2) {
+            pa.fast_sh = 32 + L;
+            pa.fast_m = ((1ull << (32 + L)) + (uint64_t)e->g - 1) / (uint64_t)e->g;
+            pa.fast_lim = (uint64_t)e->g * kRelCap;
+            pa.base_ts = (int64_t)b;
+        }
+    }
     pa.b_key = e->d_bkey;
     pa.b_rel = e->d_brel;
     pa.b_n = pre ? e->d_bn : nullptr;
@@ -3241,6 +3305,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     static const bool p2 = getenv("FWA_P2") != nullptr;   // A/B switch: the r01 Phase P kernel
     const bool kg_all = e->cfg.kg_start == 0 && e->cfg.kg_end == e->cfg.max_parallelism - 1;
     const int kgm = kg_all ? 0 : (e->cfg.key_kind == FWA_KEY_PREHASHED ? 2 : 1);
+    static const bool now16 = getenv("FWA_NOW16") != nullptr;  // A/B switch: 8-byte Phase P loads
+    auto al16 = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; };
+    const bool w16 = !now16 && !p2 && kgm == 0 && al16(pa.keys) && al16(pa.ts) &&
+                     (e->nv == 0 || ((uintptr_t)pa.cols[pa.vcol[0]] & ((e->vsize[0] == 8) ? 15 : 7)) == 0);
 #define P2LAUNCH(NV, IT, VW) do { if (p2) partition2_kernel<NV, IT, 1024, 1, VW><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else if (kgm == 0) partition3_kernel<NV, IT, 1024, VW, 0><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else if (kgm == 1) partition3_kernel<NV, IT, 1024, VW, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
@@ -3251,6 +3319,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else partition3_kernel<NV, 4, 1024, 3, 2, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
     if (pre) { if (e->nv == 0) PRELAUNCH(0); else PRELAUNCH(1); }
     else if (e->nv == 0) P2LAUNCH(0, 8, 3);
+    else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
+    else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1) { if (vw & 1) P2LAUNCH(1, 6, 3); else P2LAUNCH(1, 6, 2); }
     else if (vw == 3) P2LAUNCH(2, 4, 3); else if (vw == 2) P2LAUNCH(2, 4, 2);
     else if (vw == 1) P2LAUNCH(2, 4, 1); else P2LAUNCH(2, 4, 0);

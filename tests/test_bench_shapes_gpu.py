@@ -150,3 +150,29 @@ def test_c2_full_size_conservation(eng_mod):
 def test_c4_full_size_conservation(eng_mod):
     """C4 at N=1: 1e8-key table (2^28 slots), 1e9 records."""
     _full_size_conservation(eng_mod, 100_000_000, 100_000_000)
+
+
+@pytest.mark.parametrize("dtype", ["i64", "f32"])
+def test_phase_p_paired_loads_odd_sizes_and_offsets(eng_mod, dtype):
+    """Phase P reads two records per lane per column when the columns are 16-byte aligned (W16): pushes of odd
+    length (the unpaired last record goes to the replay) and pushes starting at odd offsets (8-byte-aligned
+    columns: the per-record load path) must both equal the oracle."""
+    import torch
+    from oracle.oracle import Oracle
+    rng = np.random.default_rng(5)
+    n = 200_001
+    keys = rng.integers(0, 20_000, n).astype(np.int64)
+    ts = (np.arange(n) * 5 + rng.integers(0, 3000, n)).astype(np.int64)
+    vals = rng.integers(-2**40, 2**40, n).astype(np.int64) if dtype == "i64" else rng.random(n).astype(np.float32)
+    aggs = [("COUNT", 0), ("SUM_I64", 0)] if dtype == "i64" else [("COUNT", 0), ("MAX_F32", 0), ("SUM_F32", 0)]
+    cfg = A.make_config(window_kind="TUMBLE", size_ms=10_000, aggs=aggs, key_capacity=1 << 15)
+    g, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
+    names = A.agg_names(cfg)
+    tk, tt, tv = (torch.from_numpy(x).cuda() for x in (keys, ts, vals))
+    cuts = [0, 33_333, 33_334, 100_001, 150_000, n]              # odd / even lengths, odd / even starts
+    for a_, b_ in zip(cuts[:-1], cuts[1:]):
+        g.push(tk[a_:b_], tt[a_:b_], [tv[a_:b_]])
+        o.push(keys[a_:b_], ts[a_:b_], [vals[a_:b_]])
+        wm = int(ts[:b_].max()) - 3001 if b_ < n else A.LONG_MAX
+        assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), names, rtol=1e-5, ctx="cut %d" % b_)
+    g.close()
