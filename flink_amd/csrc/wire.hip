@@ -154,15 +154,49 @@ __device__ __forceinline__ int wave_walk(const Lds& b, int p, int remi, const Wi
     }
 }
 
-// Stage chunk c (bytes [cs, cs + min(rem, C + S))) into the block's LDS buffer.
-__device__ __forceinline__ int stage(uint32_t* buf, const uint8_t* __restrict__ in, int64_t nbytes, int64_t c,
-                                     const WireConst& w, bool aligned) {
+// Next-chunk prefetch in registers: while the wave walks chunk c, the 16-byte loads of its next chunk are in
+// flight (they land in LDS after the walk). Chunks reaching the stream end and unaligned inputs are staged byte-wise.
+struct Prefetch {
+    static constexpr int kVec = 5;                     // 16-byte loads per lane: 320 x 16 B >= kChunk + kMaxStep + 3
+    u32x4 r[kVec];
+    bool ok = false;
+    __device__ __forceinline__ void issue(const uint8_t* __restrict__ in, int64_t nbytes, int64_t c, int nvec,
+                                          bool aligned) {
+        const int64_t cs = c * kChunk;
+        ok = aligned && cs + (int64_t)nvec * 16 <= nbytes;
+        if (!ok) return;
+        const u32x4* src = reinterpret_cast<const u32x4*>(in + cs);
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int i = threadIdx.x + 64 * k;
+            if (i < nvec) r[k] = __builtin_nontemporal_load(src + i);
+        }
+    }
+    __device__ __forceinline__ void land(uint32_t* buf, int nvec) const {
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int i = threadIdx.x + 64 * k;
+            if (i < nvec) reinterpret_cast<u32x4*>(buf)[i] = r[k];
+        }
+    }
+};
+static_assert(Prefetch::kVec * 64 * 16 >= kChunk + kMaxStep + 3, "prefetch covers a chunk and its halo");
+
+// Stage chunk c from the prefetch (or byte-wise), then put chunk `next` in flight. Returns the bytes left.
+__device__ __forceinline__ int stage_pf(uint32_t* buf, const uint8_t* __restrict__ in, int64_t nbytes, int64_t nchunks,
+                                        int64_t c, int64_t next, const WireConst& w, bool aligned, Prefetch& pf) {
+    const int nvec = (kChunk + w.step + 15) / 16;
     const int64_t cs = c * kChunk;
     const int64_t rem = nbytes - cs;
-    const int lim = (int)std::min<int64_t>(rem, kChunk + w.step);
     __syncthreads();                                              // previous chunk fully read
-    if (lim > 0) stage_chunk(buf, in + cs, lim, aligned);
+    if (pf.ok) pf.land(buf, nvec);
+    else {
+        const int lim = (int)std::min<int64_t>(rem, kChunk + w.step);
+        if (lim > 0) stage_chunk(buf, in + cs, lim, aligned);
+    }
     __syncthreads();
+    if (next < nchunks) pf.issue(in, nbytes, next, nvec, aligned);
+    else pf.ok = false;
     return (int)std::min<int64_t>(rem, 1 << 30);                  // bytes left, clamped (chains stop within C + S)
 }
 
@@ -175,8 +209,10 @@ __global__ __launch_bounds__(64) void wire_scan_kernel(const uint8_t* __restrict
     __shared__ uint32_t buf[kBufWords];
     const Lds b{buf};
     const int lane = threadIdx.x;
+    Prefetch pf;
+    if ((int64_t)blockIdx.x < nchunks) pf.issue(in, nbytes, blockIdx.x, (kChunk + w.step + 15) / 16, aligned);
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-        const int remi = stage(buf, in, nbytes, c, w, aligned);
+        const int remi = stage_pf(buf, in, nbytes, nchunks, c, c + gridDim.x, w, aligned, pf);
         for (int e0 = 0; e0 < w.step; e0 += 64) {
             const int e = e0 + lane;
             uint32_t len = 0;
@@ -328,11 +364,13 @@ __global__ __launch_bounds__(64) void wire_decode_kernel(const uint8_t* __restri
                                                           const uint64_t* __restrict__ c_evt, DecodeOut o) {
     __shared__ uint32_t buf[kBufWords];
     const Lds b{buf};
+    Prefetch pf;
+    if ((int64_t)blockIdx.x < nchunks) pf.issue(in, nbytes, blockIdx.x, (kChunk + w.step + 15) / 16, aligned);
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
         const uint32_t ent = c_ent[c];
-        if (ent == kDead) continue;
         const int64_t cs = c * kChunk;
-        const int remi = stage(buf, in, nbytes, c, w, aligned);
+        const int remi = stage_pf(buf, in, nbytes, nchunks, c, c + gridDim.x, w, aligned, pf);
+        if (ent == kDead) continue;
         const uint64_t rb = c_rec[c], eb = c_evt[c];
         auto visit = [&](int p, int tag, uint32_t rbefore, uint32_t erank) {
             int q = p + 5;
