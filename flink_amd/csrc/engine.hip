@@ -454,6 +454,8 @@ struct PartArgs {
     int32_t* dropidx;                  // FWA_CFG_LATE_INDICES list (nullptr: not collected)
     const uint8_t* nulls[FWA_MAX_COLS];   // SQL NULL flags of the push (records with a NULL take the v1 path)
     int32_t any_null;                  // some nulls[] is set
+    const unsigned long long* pcount;  // fwa_push_partials (PRE only): records each row stands for (bucket n);
+                                       // rows are not merged in the tile, counts > 65535 take the v1 path
     // PRE: a pre-aggregated entry past its sub-bucket's end is applied at once with global atomics
     unsigned long long* key_table;
     uint64_t key_mask;
@@ -919,8 +921,16 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             if (a.any_null && i < a.n && row_has_null(a, i)) code = kCodeSlow;   // SQL NULLs: the v1 path
             if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
             if (W16 && i == a.n - 1 && (a.n & 1)) code = kCodeSlow;     // unpaired last record: the v1 replay
+            uint32_t rn = 1;                                          // records this row stands for
+            if constexpr (PRE) {
+                if (a.pcount && i < a.n) {
+                    const unsigned long long pc = a.pcount[i];
+                    rn = (uint32_t)pc;
+                    if (pc == 0 || pc > 0xFFFFull) code = kCodeSlow;  // does not fit a bucket's u16 count
+                }
+            }
             if (i >= a.n) code = 0xff;
-            dropped += code == kCodeDrop;
+            dropped += code == kCodeDrop ? rn : 0u;
             note_drop(a.dropidx, a.st, code == kCodeDrop, i);
             const bool slow = code == kCodeSlow;
             const unsigned long long mk = __ballot(slow);
@@ -942,7 +952,11 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 x_rel[x] = (uint16_t)rel;
                 if (NV > 0) x_val[0][x] = r_v0[j];
                 if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = r_v1[j];
-                if constexpr (PRE) { x_n[x] = 1u; r_pos[j] = 0x80000000u | p; }   // bucketed after the merge
+                if constexpr (PRE) {
+                    x_n[x] = rn;
+                    r_pos[j] = a.pcount ? ((p << 16) | atomicAdd(&hist[p], 1u))   // partial rows: no merge
+                                        : (0x80000000u | p);                        // bucketed after the merge
+                }
                 else r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
             }
         }
@@ -950,7 +964,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             __syncthreads();                        // the tile's staged (key, rel) visible to every lane
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j) {
-                if (r_pos[j] == ~0u) continue;
+                if (r_pos[j] == ~0u || !(r_pos[j] & 0x80000000u)) continue;
                 const uint32_t x = (uint32_t)xof(j);
                 const unsigned long long key = r_key[j];
                 const uint32_t rel = x_rel[x];
@@ -3215,7 +3229,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     }
     static const int pre_env = getenv("FWA_PRE") ? atoi(getenv("FWA_PRE")) : -1;   // A/B: 0 never, 1 always
     const bool pre_ok = (layout == 2 && e->nv == 0) || (layout == 1 && e->nv == 1 && e->vsize[0] == 8);
-    const bool pre = pre_ok && pre_env != 0 && (pre_env == 1 || e->pre) && getenv("FWA_P2") == nullptr;
+    // partial accumulators (fwa_push_partials): the PRE buckets carry each row's record count, the value
+    // column is the partial BIGINT sum; other aggregate lists keep the v1 path
+    if (a.pcount && (!pre_ok || getenv("FWA_P2") != nullptr || getenv("FWA_PARTIALS_V1") != nullptr)) return FWA_OK;
+    const bool pre = a.pcount || (pre_ok && pre_env != 0 && (pre_env == 1 || e->pre) && getenv("FWA_P2") == nullptr);
     int rc = ensure_v2_buffers(e, a.n, pre);
     if (rc) return rc;
     const int64_t q_base = e->live.empty() ? 0 : e->live.begin()->first;
@@ -3245,6 +3262,11 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.keys = a.keys;
     pa.ts = a.ts;
     for (int c = 0; c < FWA_MAX_COLS; ++c) pa.cols[c] = a.cols[c];
+    if (a.pcount) {                   // partial rows: cols[] is indexed by aggregate; the carried value is the
+        pa.pcount = a.pcount;         // accumulator column of the BIGINT sum (layout 1)
+        for (int j = 0; j < e->cfg.num_aggs; ++j)
+            if (e->ec.agg[j].acc == 1 && layout == 1) pa.cols[e->vcol[0]] = a.cols[j];
+    }
     pa.key_hash = a.key_hash;
     pa.n = a.n;
     pa.wm = a.wm;
@@ -3287,7 +3309,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.part_bits = e->part_bits;
     pa.np = e->np;
     for (int v = 0; v < 2; ++v) { pa.vcol[v] = e->vcol[v]; pa.vsize[v] = e->vsize[v]; }
-    pa.dropidx = a.dropidx;
+    pa.dropidx = a.pcount ? nullptr : a.dropidx;   // partial rows: no record indices (as in v1)
     for (int c = 0; c < FWA_MAX_COLS; ++c) { pa.nulls[c] = a.nulls[c]; pa.any_null |= a.nulls[c] != nullptr; }
     pa.st = e->d_st;
     static const int pabl = getenv("FWA_PABL") ? atoi(getenv("FWA_PABL")) : 0;
@@ -4133,7 +4155,7 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
         if (e->d_late) HIPCHK(e, hipFree(e->d_late));
         HIPCHK(e, hipMalloc(&e->d_late, sizeof(int32_t) * e->spill_cap));
     }
-    return push_common(e, a, n, false, (flags & FWA_PUSH_ASYNC) != 0, late_dropped_out);
+    return push_common(e, a, n, true, (flags & FWA_PUSH_ASYNC) != 0, late_dropped_out);
 }
 
 // Export every (key, slice) accumulator that received records since the last drain and reset those

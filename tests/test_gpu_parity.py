@@ -301,8 +301,11 @@ def test_session_hot_key_many_records(eng_mod):
         assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), A.agg_names(cfg), ctx="b=%d" % b)
 
 
+C2_AGGS = [("COUNT", 0), ("SUM_I64", 0)]
+
+
 @pytest.mark.parametrize("ci", [i for i, c in enumerate(CONFIGS) if c["window_kind"] != "SESSION"])
-@pytest.mark.parametrize("aggs", [I64_AGGS, F64_AGGS], ids=["i64", "f64"])
+@pytest.mark.parametrize("aggs", [I64_AGGS, F64_AGGS, C2_AGGS, [("COUNT", 0)]], ids=["i64", "f64", "c2", "count"])
 def test_two_phase_partials_vs_oracle(eng_mod, ci, aggs):
     """Flink's two-phase plan (TwoStageOptimizedWindowAggregateRule.java:88-103): two local
     pre-aggregators (LocalSlicingWindowAggOperator) drain (key, slice) partials at every watermark, the
@@ -500,3 +503,40 @@ def test_late_record_indices_vs_oracle(eng_mod, ci):
     assert total > 0
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("ci", [0, 3])
+def test_partials_large_counts_and_late(eng_mod, ci):
+    """Partial rows through the owner's two-phase path (COUNT + SUM(BIGINT): PRE buckets carry each row's record
+    count) against the per-row v1 path (FWA_PARTIALS_V1) on the same rows: counts above a bucket's u16 take the v1
+    path, late partials add their counts to the drops, rows are identical."""
+    import os
+    cfg = A.make_config(aggs=C2_AGGS, key_capacity=4096, **CONFIGS[ci])
+    names = A.agg_names(cfg)
+    rng = np.random.default_rng(17)
+    n = 40_000
+    keys = rng.integers(0, 3000, n).astype(np.int64)
+    sts = np.sort(rng.integers(0, 60_000, n)).astype(np.int64)
+    sts[rng.random(n) < 0.05] -= 25_000                             # late once the first watermark fired
+    cnt = rng.integers(1, 50, n).astype(np.int64)
+    big = rng.random(n) < 0.01
+    cnt[big] = rng.integers(65_536, 1 << 40, int(big.sum()))
+    acc = rng.integers(-2**40, 2**40, n).astype(np.int64)
+    handles = {}
+    for mode in ("v2", "v1"):
+        if mode == "v1":
+            os.environ["FWA_PARTIALS_V1"] = "1"
+        try:
+            g = eng_mod.WindowAggregator(cfg)
+            out, drops = [], 0
+            for sl, wm in ((slice(0, n // 2), 30_000), (slice(n // 2, n), A.LONG_MAX)):
+                drops += g.push_partials(keys[sl], sts[sl], cnt[sl], [cnt[sl], acc[sl]])
+                out.append(g.advance_watermark(wm))
+            handles[mode] = (out, drops, g.stats().ingest_launches)
+            g.close()
+        finally:
+            os.environ.pop("FWA_PARTIALS_V1", None)
+    (o2, d2, _), (o1, d1, _) = handles["v2"], handles["v1"]
+    assert d2 == d1 and d1 > 0
+    for a_, b_ in zip(o2, o1):
+        assert_rows_equal(a_, b_, names, ctx="partials v2 vs v1")
