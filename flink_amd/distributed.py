@@ -149,15 +149,23 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
     def advance_watermark(self, local_wm, device_output=False):
         wm = self.global_watermark(local_wm)
         p = self.local.drain_partials(wm)
-        na = len(self.names)
-        cols = [p["key"], p["slice_start"], p["count"]] + [p["acc%d" % j] for j in range(na)]
+        # a COUNT(*) aggregate's accumulator repeats the row count: it is not shipped (rebuilt on arrival)
+        ship = [j for j, name in enumerate(self.names) if name != "COUNT"]
+        cols = [p["key"], p["slice_start"], p["count"]] + [p["acc%d" % j] for j in ship]
         cols = [c if isinstance(c, torch.Tensor) else torch.from_numpy(c) for c in cols]
         recv = exchange_rows(self, cols[0], cols)
         self.partials_sent += int(cols[0].shape[0])
         col = [recv[:, j].contiguous() for j in range(recv.shape[1])]
         if not recv.is_cuda:
             col = [c.numpy() for c in col]
-        self.engine.push_partials(col[0], col[1], col[2], col[3:])
+        accs, k = [], 3
+        for name in self.names:
+            if name == "COUNT":
+                accs.append(col[2])
+            else:
+                accs.append(col[k])
+                k += 1
+        self.engine.push_partials(col[0], col[1], col[2], accs)
         if device_output:
             return self.engine.advance_watermark_device(wm)
         return self.engine.advance_watermark(wm)
