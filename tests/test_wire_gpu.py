@@ -217,3 +217,85 @@ def test_network_input_feeds_window_engine():
     assert inp.records_in == n and inp.carry == b""
     inp.close()
     eng.close()
+
+
+def test_network_input_table_rows_with_nulls():
+    """Table path from the wire: BinaryRowData rows (key BIGINT, rowtime TIMESTAMP(3), f FLOAT, d DOUBLE) with NULL
+    values, without StreamRecord timestamps, cut into 32 KiB buffers -> NetworkInput -> a TABLE engine with nullable
+    columns (SQL NULL semantics: SUM/MAX skip NULLs, COUNT(col) counts non-NULL); the oracle gets the same rows and
+    NULL flags in order."""
+    from flink_amd.engine import WindowAggregator
+    from helpers import assert_rows_equal
+    from oracle.oracle import Oracle
+    rng = np.random.default_rng(33)
+    n = 120_000
+    keys = rng.integers(0, 4000, n).astype(np.int64)
+    ts = (np.arange(n) * 2 + rng.integers(0, 1500, n)).astype(np.int64)
+    f = (rng.random(n) * 10).astype(np.float32)
+    d = rng.random(n) * 100 - 50
+    nf = rng.random(n) < 0.1
+    nd = rng.random(n) < 0.2
+    events = [(p, 2, (int(ts[:p].max()) - 1501,)) for p in range(15_000, n, 15_000)]
+    data = W.encode_stream(C5, [keys, ts, f, d], None, "ROWDATA", events, [None, None, nf, nd])
+    aggs = [("COUNT", 0), ("MAX_F32", 0), ("SUM_F64", 1), ("COUNT_COL", 1), ("AVG_F64", 1)]
+    cfg = A.make_config(window_kind="TUMBLE", semantics="TABLE", size_ms=5000, aggs=aggs, key_capacity=1 << 13,
+                        nullable_cols=(0, 1))
+    names = A.agg_names(cfg)
+    eng = WindowAggregator(cfg)
+    inp = wire.NetworkInput(wire.make_schema(C5, key_field=0, ts_field=1, cols=[2, 3], fmt="ROWDATA"), eng)
+    got = []
+    for buf in W.split_buffers(data):
+        got += inp.feed(buf)
+    got.append(eng.advance_watermark(A.LONG_MAX))
+    o = Oracle(cfg)
+    exp, at = [], 0
+    for pos, _, v in events + [(n, None, (A.LONG_MAX,))]:
+        o.push(keys[at:pos], ts[at:pos], [f[at:pos], d[at:pos]], nulls=[nf[at:pos], nd[at:pos]])
+        at = pos
+        exp.append(o.advance_watermark(v[0]))
+    cat = lambda rs: {k: np.concatenate([r[k] for r in rs]) for k in rs[0]}   # noqa: E731
+    assert_rows_equal(cat(got), cat(exp), names, rtol=1e-9)
+    assert inp.records_in == n
+    inp.close()
+    eng.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_schemas_and_element_mixes(seed):
+    """Random schemas (Tuple of LONG / INT / FLOAT / DOUBLE fields or BinaryRowData, 1-6 fields, with or without
+    StreamRecord timestamps), random element mixes (event-heavy to record-only) and random cut points: the GPU
+    decode equals the sequential oracle bit for bit."""
+    rng = np.random.default_rng(100 + seed)
+    fmt = "TUPLE" if seed % 2 == 0 else "ROWDATA"
+    arity = int(rng.integers(2, 7))
+    fields = ["LONG", "LONG"] + [str(x) for x in rng.choice(["LONG", "INT", "FLOAT", "DOUBLE"], arity - 2)]
+    if fmt == "TUPLE" and rng.random() < 0.5:
+        fields[0] = "INT"                                          # Integer key (sign-extended)
+    ts_field = -1 if rng.random() < 0.5 else 1
+    cols = [int(c) for c in rng.choice(np.arange(2, arity), min(3, arity - 2), replace=False)] if arity > 2 else []
+    s = wire.make_schema(fields, key_field=0, ts_field=ts_field, cols=cols, fmt=fmt)
+    dec = wire.WireDecoder(s)
+    n = int(rng.integers(1, 150_000))
+    vals = []
+    for fl in fields:
+        if fl in ("LONG", "INT"):
+            v = rng.integers(-(1 << 31), 1 << 31, n)
+            vals.append(v.astype(np.int64 if fl == "LONG" else np.int32))
+        else:
+            vals.append(rng.standard_normal(n).astype(np.float64 if fl == "DOUBLE" else np.float32))
+    with_ts = ts_field == -1 or rng.random() < 0.5
+    ts = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64) if with_ts else None
+    n_ev = int(rng.choice([0, 3, n // 50, n // 2]))
+    pos = np.sort(rng.integers(0, n + 1, n_ev))
+    events = []
+    for p, t in zip(pos.tolist(), rng.choice([2, 3, 4, 5], n_ev).tolist()):
+        v = (int(rng.integers(-(1 << 62), 1 << 62)), -1, -1, int(rng.integers(0, 100)))
+        events.append((p, t, (v[0] & 1,) if t == 5 else ((-1,) if t == 4 else v)))
+    nulls = None
+    if fmt == "ROWDATA":
+        nulls = [None, None] + [rng.random(n) < 0.05 for _ in fields[2:]]
+    data = W.encode_stream(fields, vals, ts, fmt, events, nulls)
+    _check(dec, s, data)
+    for cut in rng.integers(1, len(data), 5).tolist():           # the head of an element continues later
+        _check(dec, s, data[:cut])
+    dec.close()
