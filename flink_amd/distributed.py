@@ -94,34 +94,43 @@ def unpack_col(cell, dtype):
     return cell.to(torch.int32).view(dtype).contiguous()
 
 
-def exchange_rows(pipe, keys, cols):
-    """keyBy exchange of a row set: route by key group, pack the columns into one int64 [n, m] tensor grouped by
-    destination, one all_to_all of the counts and one all_to_all_single of the rows (RCCL over xGMI). Returns the
-    received rows (int64 [n_recv, m]; 4-byte columns travel zero-extended in their 8-byte cell).
-    Device batches are routed and packed by the HIP counting sort (fwa_route_rows); host tensors (the gloo tests)
-    by the same stable grouping in torch."""
+def route_rows(pipe, keys, cols):
+    """The send side of the keyBy exchange: rows packed by destination (int64 [n, m]) and per-destination counts.
+    Device batches use the HIP counting sort (fwa_route_rows); host tensors (the gloo tests) the same stable
+    grouping in torch."""
     n = int(keys.shape[0])
     if keys.is_cuda and pipe.route_on_gpu:
         from . import engine
-        packed, counts = engine.route_rows(keys, [c.contiguous() for c in cols], pipe.cfg.max_parallelism, pipe.world,
-                                           key_kind=pipe.cfg.key_kind)
-    else:
-        dest = pipe.route(keys)
-        packed = torch.empty((n, len(cols)), dtype=torch.int64, device=keys.device)
-        for j, x in enumerate(cols):
-            packed[:, j] = x.view(torch.int64) if x.dtype.itemsize == 8 else x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
-        if pipe.world > 1:
-            order = torch.argsort(dest, stable=True)
-            packed = packed[order]
-        counts = torch.bincount(dest, minlength=pipe.world)
+        return engine.route_rows(keys, [c.contiguous() for c in cols], pipe.cfg.max_parallelism, pipe.world,
+                                 key_kind=pipe.cfg.key_kind)
+    dest = pipe.route(keys)
+    packed = torch.empty((n, len(cols)), dtype=torch.int64, device=keys.device)
+    for j, x in enumerate(cols):
+        packed[:, j] = x.view(torch.int64) if x.dtype.itemsize == 8 else x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    if pipe.world > 1:
+        order = torch.argsort(dest, stable=True)
+        packed = packed[order]
+    return packed, torch.bincount(dest, minlength=pipe.world)
+
+
+def send_rows(pipe, packed, counts):
+    """One all_to_all of the counts and one all_to_all_single of the packed rows (RCCL over xGMI)."""
     recv_counts = torch.empty_like(counts)
     dist.all_to_all_single(recv_counts, counts, group=pipe.group)
     send = counts.tolist()
     recv = recv_counts.tolist()
-    out = torch.empty((sum(recv), len(cols)), dtype=torch.int64, device=keys.device)
+    out = torch.empty((sum(recv), packed.shape[1]), dtype=torch.int64, device=packed.device)
     dist.all_to_all_single(out, packed, recv, send, group=pipe.group)
     pipe.exchanged += int(sum(send)) - int(send[pipe.rank])
     return out
+
+
+def exchange_rows(pipe, keys, cols):
+    """keyBy exchange of a row set: route by key group, pack the columns into one int64 [n, m] tensor grouped by
+    destination, exchange (RCCL over xGMI). Returns the received rows (int64 [n_recv, m]; 4-byte columns travel
+    zero-extended in their 8-byte cell)."""
+    packed, counts = route_rows(pipe, keys, cols)
+    return send_rows(pipe, packed, counts)
 
 
 class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
@@ -146,14 +155,21 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
             return self.local.push(keys, ts, list(cols), sync=False)
         return self.local.push(keys.numpy(), ts.numpy(), [x.numpy() for x in cols])
 
-    def advance_watermark(self, local_wm, device_output=False):
+    def advance_watermark(self, local_wm, device_output=False, then_push=None):
+        """then_push: (keys, ts, cols) of this rank's next batch, pushed into the local pre-aggregator as soon as the
+        drained partials are routed -- its ingest then runs while the exchange, the owner's merge and the fire of
+        this watermark proceed (software pipelining across steps; each engine still sees its own calls in stream
+        order: drain(wm), push(next) on the local one, merge(wm), fire(wm) on the owner)."""
         wm = self.global_watermark(local_wm)
         p = self.local.drain_partials(wm)
         # a COUNT(*) aggregate's accumulator repeats the row count: it is not shipped (rebuilt on arrival)
         ship = [j for j, name in enumerate(self.names) if name != "COUNT"]
         cols = [p["key"], p["slice_start"], p["count"]] + [p["acc%d" % j] for j in ship]
         cols = [c if isinstance(c, torch.Tensor) else torch.from_numpy(c) for c in cols]
-        recv = exchange_rows(self, cols[0], cols)
+        packed, counts = route_rows(self, cols[0], cols)    # done with the drained buffers from here on
+        if then_push is not None:
+            self.push(*then_push)
+        recv = send_rows(self, packed, counts)
         self.partials_sent += int(cols[0].shape[0])
         col = [recv[:, j].contiguous() for j in range(recv.shape[1])]
         if not recv.is_cuda:

@@ -89,7 +89,7 @@ class _OracleFromPartials:
         self.o.close()
 
 
-def _worker(rank, world, port, outdir, two_phase=False):
+def _worker(rank, world, port, outdir, two_phase=False, pipelined=False):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -113,24 +113,32 @@ def _worker(rank, world, port, outdir, two_phase=False):
     keys, ts, vals = _stream(42 + rank, 6000)   # each rank is one source subtask
     rows = []
     nb = 4
+    batch = lambda b: (torch.from_numpy(keys[b * 1500:(b + 1) * 1500]), torch.from_numpy(ts[b * 1500:(b + 1) * 1500]),  # noqa: E731
+                       [torch.from_numpy(vals[b * 1500:(b + 1) * 1500])])
+    if pipelined:
+        pipe.push(*batch(0))
     for b in range(nb + 1):
         if b < nb:
-            sl = slice(b * 1500, (b + 1) * 1500)
-            pipe.push(torch.from_numpy(keys[sl]), torch.from_numpy(ts[sl]), [torch.from_numpy(vals[sl])])
+            if not pipelined:
+                pipe.push(*batch(b))
             local_wm = int(ts[: (b + 1) * 1500].max()) - 2001
         else:
             local_wm = A.LONG_MAX
-        r = pipe.advance_watermark(local_wm)
+        if pipelined:       # the next batch enters the local pre-aggregator during this watermark's exchange
+            r = pipe.advance_watermark(local_wm, then_push=batch(b + 1) if b + 1 < nb else None)
+        else:
+            r = pipe.advance_watermark(local_wm)
         rows.append(np.stack([r["key"], r["win_start"], r["win_end"], r["agg0"], r["agg1"]], axis=1))
     np.save(os.path.join(outdir, "rank%d.npy" % rank), np.concatenate(rows))
     pipe.close()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("two_phase", [False, True], ids=["raw_records", "two_phase_partials"])
-def test_two_rank_keyby_pipeline_matches_single_operator(tmp_path, two_phase):
+@pytest.mark.parametrize("two_phase,pipelined", [(False, False), (True, False), (True, True)],
+                         ids=["raw_records", "two_phase_partials", "two_phase_pipelined"])
+def test_two_rank_keyby_pipeline_matches_single_operator(tmp_path, two_phase, pipelined):
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), two_phase), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), two_phase, pipelined), nprocs=world, join=True)
     got = np.concatenate([np.load(tmp_path / ("rank%d.npy" % r)) for r in range(world)])
     # reference: one operator over the union of both sources, watermark = min over sources per step
     from oracle.oracle import Oracle

@@ -71,12 +71,16 @@ def test_two_phase_exchange_uses_gpu_router_single_rank():
         ts = np.sort(rng.integers(0, 50_000, n)).astype(np.int64)
         vals = rng.integers(0, 1 << 30, n).astype(np.int64)
         got, exp = [], []
+        batch = lambda b: (torch.from_numpy(keys[b * n // 4:(b + 1) * n // 4]).cuda(),  # noqa: E731
+                           torch.from_numpy(ts[b * n // 4:(b + 1) * n // 4]).cuda(),
+                           [torch.from_numpy(vals[b * n // 4:(b + 1) * n // 4]).cuda()])
+        pipe.push(*batch(0))
         for b in range(4):
             sl = slice(b * n // 4, (b + 1) * n // 4)
-            pipe.push(*(torch.from_numpy(x[sl]).cuda() for x in (keys, ts)), [torch.from_numpy(vals[sl]).cuda()])
             o.push(keys[sl], ts[sl], [vals[sl]])
             wm = int(ts[sl].max()) - 1 if b < 3 else A.LONG_MAX
-            got.append(pipe.advance_watermark(wm))
+            # pipelined: the next batch enters the local engine during this watermark's exchange + merge
+            got.append(pipe.advance_watermark(wm, then_push=batch(b + 1) if b < 3 else None))
             exp.append(o.advance_watermark(wm))
         from helpers import assert_rows_equal
         assert_rows_equal(merge_rows(got, pipe.names), merge_rows(exp, pipe.names), pipe.names)
