@@ -25,6 +25,10 @@ constexpr int kMaxDest = 64;
 constexpr int kRouteBlocks = 2048;
 constexpr int kMaxRouteCols = 16;
 
+struct UnpackCols {
+    int64_t* col[kMaxRouteCols];
+};
+
 struct RouteArgs {
     const int64_t* keys;
     const int32_t* key_hash;
@@ -119,7 +123,34 @@ __global__ void __launch_bounds__(kRouteBlock) route_scatter_kernel(RouteArgs a)
     }
 }
 
+// The receive side: packed rows -> one contiguous column per cell (one kernel instead of a strided copy per column)
+__global__ void __launch_bounds__(kRouteBlock) unpack_rows_kernel(const int64_t* __restrict__ rows, int64_t n,
+                                                                  int32_t ncols, UnpackCols out) {
+    for (int64_t i = (int64_t)blockIdx.x * kRouteBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kRouteBlock) {
+        const int64_t* r = rows + i * ncols;
+        for (int c = 0; c < ncols; ++c) out.col[c][i] = r[c];
+    }
+}
+
 }  // namespace
+
+extern "C" int fwa_unpack_rows(const int64_t* rows, int64_t n, int32_t ncols, int64_t* const* cols, int32_t device,
+                               void* stream) {
+    if (n < 0 || ncols < 1 || ncols > kMaxRouteCols || (n > 0 && (!rows || !cols))) return FWA_E_ARG;
+    if (n == 0) return FWA_OK;
+    UnpackCols o{};
+    for (int c = 0; c < ncols; ++c) {
+        if (!cols[c]) return FWA_E_ARG;
+        o.col[c] = cols[c];
+    }
+    if (hipSetDevice(device) != hipSuccess) return FWA_E_DEVICE;
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = (int)std::min<int64_t>(4096, (n + kRouteBlock - 1) / kRouteBlock);
+    hipLaunchKernelGGL(unpack_rows_kernel, dim3(nb), dim3(kRouteBlock), 0, st, rows, n, ncols, o);
+    const hipError_t e1 = hipGetLastError();
+    const hipError_t e2 = hipStreamSynchronize(st);
+    return (e1 == hipSuccess && e2 == hipSuccess) ? FWA_OK : FWA_E_DEVICE;
+}
 
 extern "C" int fwa_route_rows(const int64_t* keys, const int32_t* key_hash, int64_t n, int32_t key_kind,
                               int32_t max_parallelism, int32_t parallelism, const void* const* cols,

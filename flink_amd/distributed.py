@@ -171,7 +171,11 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
             self.push(*then_push)
         recv = send_rows(self, packed, counts)
         self.partials_sent += int(cols[0].shape[0])
-        col = [recv[:, j].contiguous() for j in range(recv.shape[1])]
+        if recv.is_cuda:
+            from . import engine
+            col = engine.unpack_rows(recv)
+        else:
+            col = [recv[:, j].contiguous() for j in range(recv.shape[1])]
         if not recv.is_cuda:
             col = [c.numpy() for c in col]
         accs, k = [], 3

@@ -75,6 +75,8 @@ def lib():
     L.fwa_route_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                  C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     L.fwa_route_rows.restype = C.c_int
+    L.fwa_unpack_rows.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]
+    L.fwa_unpack_rows.restype = C.c_int
     L.fwa_generate.argtypes = [C.POINTER(A.GenParams), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                                C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     L.fwa_generate.restype = C.c_int
@@ -395,6 +397,18 @@ def route_rows(keys, cols, max_parallelism, parallelism, key_kind=A.KEY_JAVA_LON
                               len(cols), _ptr(out), _ptr(counts), dev.index or 0, C.c_void_p(stream))
     _check(rc, None, "fwa_route_rows")
     return out, counts
+
+
+def unpack_rows(rows):
+    """Packed int64 rows [n, m] (torch CUDA) -> m contiguous int64 columns (fwa_unpack_rows, one kernel)."""
+    import torch
+    n, m = int(rows.shape[0]), int(rows.shape[1])
+    cols = [torch.empty(n, dtype=torch.int64, device=rows.device) for _ in range(m)]
+    ptrs = (C.c_void_p * m)(*[c.data_ptr() for c in cols])
+    stream = torch.cuda.current_stream(rows.device).cuda_stream
+    rc = lib().fwa_unpack_rows(_ptr(rows.contiguous()), n, m, ptrs, rows.device.index or 0, C.c_void_p(stream))
+    _check(rc, None, "fwa_unpack_rows")
+    return cols
 
 
 def generate(params, n, keys=None, ts=None, v_i64=None, v_f32=None, v_f64=None, device=0, stream=None):

@@ -348,6 +348,9 @@ int fwa_route_rows(const int64_t* keys, const int32_t* key_hash, int64_t n, int3
                    int32_t parallelism, const void* const* cols, const int32_t* col_bytes, int32_t ncols, int64_t* out,
                    int64_t* counts, int32_t device, void* stream);
 
+/* The receive side of that exchange: rows[n][ncols] (int64 cells) -> cols[c][n], device pointers, on `stream`. */
+int fwa_unpack_rows(const int64_t* rows, int64_t n, int32_t ncols, int64_t* const* cols, int32_t device, void* stream);
+
 /* ---- bench / test support (synthetic streams of SURVEY.md §8(d), generated in HBM) ---- */
 typedef struct fwa_gen_params {
     uint64_t seed_k, seed_t, seed_v;

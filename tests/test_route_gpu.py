@@ -87,3 +87,16 @@ def test_two_phase_exchange_uses_gpu_router_single_rank():
         pipe.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_unpack_rows_inverts_packing():
+    """fwa_unpack_rows: packed int64 rows -> contiguous columns (the receive side of the exchange)."""
+    import torch
+    from flink_amd import engine
+    rng = np.random.default_rng(8)
+    for n, m in ((0, 3), (1, 1), (12345, 5), (1 << 20, 7)):
+        rows = torch.from_numpy(rng.integers(-2**62, 2**62, (n, m)).astype(np.int64)).cuda()
+        cols = engine.unpack_rows(rows)
+        assert len(cols) == m
+        for j in range(m):
+            assert torch.equal(cols[j], rows[:, j])

@@ -43,7 +43,7 @@ for b in range(S):
     packed, counts = E.route_rows(cols[0], cols, 128, 8)
     torch.cuda.synchronize()
     t3 = time.perf_counter()
-    c = [packed[:, j].contiguous() for j in range(packed.shape[1])]
+    c = E.unpack_rows(packed)
     torch.cuda.synchronize()
     t4 = time.perf_counter()
     owner.push_partials(c[0], c[1], c[2], c[3:])
