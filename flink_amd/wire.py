@@ -117,6 +117,8 @@ class WireDecoder:
         """data: bytes / numpy uint8 (host, staged by the decoder) or a torch CUDA uint8 tensor (HBM)."""
         b = Batch()
         if _is_torch_cuda(data):
+            import torch
+            torch.cuda.current_stream(data.device).synchronize()   # the bytes' producer ran on torch's stream
             ptr, n, flags = C.c_void_p(data.data_ptr()), data.numel(), WIRE_DEVICE_BYTES
             keep = data
         else:
