@@ -109,9 +109,10 @@ void fwa_wire_destroy(fwa_wire_decoder* d);
 const char* fwa_wire_last_error(const fwa_wire_decoder* d);
 
 /* Decode the elements of bytes[0, nbytes) (concatenated buffer payloads of one channel, starting at an
- * element boundary). Device bytes (FWA_WIRE_DEVICE_BYTES) must be complete when the call is made: the decoder runs
- * on its own stream (the caller synchronises the producer's stream first); everything is complete on return. A malformed element (unknown tag, or a length that does not match its tag and the
- * schema) returns FWA_E_CORRUPT ("Corrupt stream, found tag", StreamElementSerializer.java:208-210).
+ * element boundary). Device bytes (FWA_WIRE_DEVICE_BYTES) must be complete when the call is made: the decoder
+ * runs on its own stream (the caller synchronises the producer's stream first); everything is complete on
+ * return. A malformed element (unknown tag, or a length that does not match its tag and the schema) returns
+ * FWA_E_CORRUPT ("Corrupt stream, found tag", StreamElementSerializer.java:208-210).
  * Device timing of the decode kernels accumulates in fwa_wire_stats. */
 int fwa_wire_decode(fwa_wire_decoder* d, const uint8_t* bytes, int64_t nbytes, int32_t flags,
                     fwa_wire_batch* out);
