@@ -10,19 +10,28 @@
 // KeyGroupRangeOffsets holds each key group's section start. The KeyedBackendSerializationProxy header in front of
 // the sections (state names, serializer snapshots) is JVM metadata the Java shim writes itself.
 //
-// State 0 is the window contents, state 1 the event-time timers:
-//   DATASTREAM TUMBLE  WindowOperator: namespace TimeWindow (TimeWindow.Serializer: long start, long end), key Long,
-//                      timers at window.maxTimestamp() (EventTimeTrigger.onElement) and at the cleanup time
-//                      maxTimestamp + allowedLateness (WindowOperator.registerCleanupTimer :608-620), deduplicated
-//                      like HeapPriorityQueueSet.
-//   TABLE TUMBLE       SlicingWindowOperator: namespace Long slice end, key BinaryRowData(BIGINT) (BinaryRowDataSerializer:
-//                      int size + row), timer at sliceEnd - 1 (WindowTimerServiceImpl / TimeWindowUtil, UTC).
+// The states per key group (registration order):
+//   DATASTREAM TUMBLE  WindowOperator: 0 window contents -- namespace TimeWindow (TimeWindow.Serializer: long start,
+//                      long end), key Long; 1 timers at window.maxTimestamp() (EventTimeTrigger.onElement) and at the
+//                      cleanup time maxTimestamp + allowedLateness (WindowOperator.registerCleanupTimer :608-620),
+//                      deduplicated like HeapPriorityQueueSet.
+//   DATASTREAM SESSION 0 window contents under each session's state window; 1 merging-window-set (ListState of
+//                      Tuple2<actual, state> TimeWindows under VoidNamespace, MergingWindowSet.persist :100-105);
+//                      2 timers as for TUMBLE, per session.
+//   TABLE TUMBLE / HOP / CUMULATE  SlicingWindowOperator: 0 namespace Long slice end, key BinaryRowData(BIGINT)
+//                      (BinaryRowDataSerializer: int size + row); 1 timers at the first unfired window end - 1 of each
+//                      live slice (WindowTimerServiceImpl / TimeWindowUtil, UTC). CUMULATE folds fired slices into the
+//                      window's first slice.
 // The accumulator is the engine's built-in aggregate state: a Tuple (DataStream, TupleSerializer: big-endian fields)
 // or a BinaryRowData (Table) of COUNT(*) followed by one field per aggregate -- BIGINT for COUNT / integer SUM, AVG,
 // MIN, MAX, DOUBLE for floating SUM / AVG / MIN / MAX (the AggregateFunction's ACC type in the shim).
-// Other window kinds, shift time zones, nullable columns: FWA_E_UNSUPPORTED (FWASNAP1 covers them).
+// DataStream SLIDE / CUMULATE, Table SESSION, shift time zones, nullable columns: FWA_E_UNSUPPORTED (FWASNAP1 covers
+// them).
 #include <algorithm>
 #include <cstdint>
+#include <map>
+#include <set>
+#include <tuple>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -108,9 +117,57 @@ struct In {
     }
 };
 
+// Layouts this file writes: DataStream TUMBLE and SESSION (WindowOperator), Table TUMBLE / HOP / CUMULATE
+// (SlicingWindowOperator: per-slice state, so the engine's slices map 1:1).
 bool supported(const fwa_config& c) {
-    return c.window_kind == FWA_TUMBLE && c.tz_n == 0 && c.nullable_cols == 0 && c.key_kind != FWA_KEY_PREHASHED;
+    if (c.tz_n != 0 || c.nullable_cols != 0 || c.key_kind == FWA_KEY_PREHASHED) return false;
+    if (c.semantics == FWA_SEM_DATASTREAM) return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SESSION;
+    return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SLIDE || c.window_kind == FWA_CUMULATE;
 }
+const char* kUnsupported = "heap layout: DataStream TUMBLE / SESSION and Table TUMBLE / HOP / CUMULATE in UTC without NULLs";
+
+int64_t gcd64(int64_t a, int64_t b) { while (b) { const int64_t t = a % b; a = b; b = t; } return a; }
+
+// Table slice width (SliceAssigners: tumble = size, hop = gcd(size, slide), cumulate = step)
+int64_t slice_width(const fwa_config& c) {
+    if (c.window_kind == FWA_SLIDE) return gcd64(c.size_ms, c.slide_ms);
+    if (c.window_kind == FWA_CUMULATE) return c.slide_ms;
+    return c.size_ms;
+}
+
+int64_t floor_div(int64_t a, int64_t b) { int64_t q = a / b; if ((a % b != 0) && ((a < 0) != (b < 0))) --q; return q; }
+
+// End of the first window containing the slice that ends at se (SliceAssigner.nextTriggerWindow chain start):
+// hop windows end at offset + k * slide, cumulative and tumbling windows at every slice end.
+int64_t first_window_end(const fwa_config& c, int64_t se) {
+    if (c.window_kind != FWA_SLIDE) return se;
+    const int64_t k = -floor_div(-(se - c.offset_ms), c.slide_ms);   // ceil((se - off) / slide)
+    return c.offset_ms + k * c.slide_ms;
+}
+
+// AggregateFunction.merge on one engine accumulator word (engine.hip acc_combine: counts and BIGINT sums add,
+// floating sums add as double, MIN / MAX compare the order-preserving words)
+uint64_t merge_word(int64_t kind, uint64_t x, uint64_t y) {
+    switch (kind) {
+        case FWA_SUM_F32: case FWA_SUM_F64: case FWA_AVG_F32: case FWA_AVG_F64: {
+            double a, b;
+            memcpy(&a, &x, 8); memcpy(&b, &y, 8);
+            a += b;
+            memcpy(&x, &a, 8);
+            return x;
+        }
+        case FWA_MIN_I64: case FWA_MIN_F32: case FWA_MIN_F64: return y < x ? y : x;
+        case FWA_MAX_I64: case FWA_MAX_F32: case FWA_MAX_F64: return y > x ? y : x;
+        default: return x + y;
+    }
+}
+
+// number of registered states per key group section and their ids
+//   DataStream TUMBLE: 0 window-contents, 1 event-time timers
+//   DataStream SESSION: 0 window-contents, 1 merging-window-set (ListState<Tuple2<TimeWindow, TimeWindow>> under the
+//                       VoidNamespace, WindowOperator.java:256-263), 2 event-time timers
+//   Table: 0 window state (per slice), 1 event-time timers
+int nstates(const fwa_config& c) { return (c.semantics == FWA_SEM_DATASTREAM && c.window_kind == FWA_SESSION) ? 3 : 2; }
 
 }  // namespace
 
@@ -125,26 +182,63 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
     fwa_config c;
     int rc = fwa_get_config(e, &c);
     if (rc) return rc;
-    if (!supported(c)) return fwa_set_error(e, FWA_E_UNSUPPORTED, "heap layout: TUMBLE windows in UTC without NULLs only");
+    if (!supported(c)) return fwa_set_error(e, FWA_E_UNSUPPORTED, kUnsupported);
     fwa_blob snap{nullptr, 0};
     if ((rc = fwa_snapshot(e, &snap))) return rc;
     Snap s;
     if (!parse(snap.data, snap.size, &s)) { fwa_blob_free(&snap); return fwa_set_error(e, FWA_E_STATE, "bad FWASNAP1 blob"); }
     const bool ds = c.semantics == FWA_SEM_DATASTREAM;
+    const bool sess = c.window_kind == FWA_SESSION;
     const int na = (int)s.naggs, arity = 1 + na;
-    const int64_t n = s.n;
+    const int64_t n = s.n, g = ds ? s.size : slice_width(c);
+    auto end_of = [&](int64_t i) { return sess ? s.col[(3 + na) * n + i] : s.col[n + i] + g; };
     Out o;
     std::vector<uint64_t> f((size_t)arity);
-    for (int64_t g = c.kg_start; g <= c.kg_end; ++g) {
-        kg_offsets[g - c.kg_start] = (int64_t)o.b.size();
-        o.i32(g);
-        const int64_t lo = s.koff[g], hi = s.koff[g + 1];
-        o.i16(0);                                                      // window contents
-        o.i32(hi - lo);
+    struct Row { int64_t key, start, end; uint64_t w[1 + FWA_MAX_AGGS]; };
+    std::vector<Row> rows;
+    for (int64_t kg = c.kg_start; kg <= c.kg_end; ++kg) {
+        kg_offsets[kg - c.kg_start] = (int64_t)o.b.size();
+        o.i32(kg);
+        const int64_t lo = s.koff[kg], hi = s.koff[kg + 1];
+        // the state entries: the engine keeps every slice until its last window fires; a CUMULATE window's fired
+        // slices are folded into its first slice in ascending order, the shared state SliceSharedWindowAggProcessor
+        // merges them into (CumulativeSliceAssigner.mergeSlices / expiredSlices, SliceAssigners.java:335-371)
+        rows.clear();
         for (int64_t i = lo; i < hi; ++i) {
-            const int64_t key = s.col[i], start = s.col[n + i], end = start + s.size;
-            f[0] = (uint64_t)s.col[2 * n + i];
-            for (int j = 0; j < na; ++j) f[1 + j] = acc_to_field(s.agg[j], (uint64_t)s.col[(3 + j) * n + i]);
+            Row r{s.col[i], s.col[n + i], end_of(i), {}};
+            r.w[0] = (uint64_t)s.col[2 * n + i];
+            for (int j = 0; j < na; ++j) r.w[1 + j] = (uint64_t)s.col[(3 + j) * n + i];
+            rows.push_back(r);
+        }
+        if (!ds && c.window_kind == FWA_CUMULATE && s.wm != INT64_MIN) {
+            std::map<std::pair<int64_t, int64_t>, Row> first;          // (key, window start) -> folded first slice
+            std::vector<Row> keep;
+            std::sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) {
+                return a.key != b.key ? a.key < b.key : a.start < b.start; });
+            for (const Row& r : rows) {
+                if (r.end - 1 > s.wm) { keep.push_back(r); continue; }
+                const int64_t ws = c.offset_ms + floor_div(r.end - 1 - c.offset_ms, c.size_ms) * c.size_ms;
+                auto it = first.find({r.key, ws});
+                if (it == first.end()) {
+                    Row m = r;
+                    m.start = ws;
+                    m.end = ws + g;
+                    first.emplace(std::make_pair(r.key, ws), m);
+                } else {
+                    it->second.w[0] += r.w[0];
+                    for (int j = 0; j < na; ++j) it->second.w[1 + j] = merge_word(s.agg[j], it->second.w[1 + j], r.w[1 + j]);
+                }
+            }
+            rows.clear();
+            for (auto& kv : first) rows.push_back(kv.second);
+            rows.insert(rows.end(), keep.begin(), keep.end());
+        }
+        o.i16(0);                                                      // window contents
+        o.i32((int64_t)rows.size());
+        for (const Row& r : rows) {
+            const int64_t key = r.key, start = r.start, end = r.end;
+            f[0] = r.w[0];
+            for (int j = 0; j < na; ++j) f[1 + j] = acc_to_field(s.agg[j], r.w[1 + j]);
             if (ds) {
                 o.i64((uint64_t)start); o.i64((uint64_t)end);          // TimeWindow.Serializer
                 o.i64((uint64_t)key);                                  // LongSerializer
@@ -156,17 +250,42 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
                 o.row(f.data(), arity);                                // accumulator row
             }
         }
-        o.i16(1);                                                      // event-time timers
-        o.i32((hi - lo) * ((ds && s.late > 0) ? 2 : 1));
-        for (int64_t i = lo; i < hi; ++i) {
-            const int64_t key = s.col[i], start = s.col[n + i], end = start + s.size;
-            const int64_t ts[2] = {end - 1, (end - 1 > INT64_MAX - s.late) ? INT64_MAX : end - 1 + s.late};
-            const int nts = (ds && s.late > 0) ? 2 : 1;
-            for (int t = 0; t < nts; ++t) {
-                o.i64((uint64_t)ts[t] ^ 0x8000000000000000ull);        // MathUtils.flipSignBit
-                if (ds) { o.i64((uint64_t)key); o.i64((uint64_t)start); o.i64((uint64_t)end); }
-                else { const uint64_t kf = (uint64_t)key; o.row(&kf, 1); o.i64((uint64_t)end); }
+        if (ds && sess) {                                              // merging-window-set: each in-flight session
+            std::map<int64_t, std::vector<int64_t>> by_key;            // maps to itself as its state window
+            for (int64_t i = lo; i < hi; ++i) by_key[s.col[i]].push_back(i);
+            o.i16(1);
+            o.i32((int64_t)by_key.size());
+            for (auto& kv : by_key) {
+                o.u8(0);                                               // VoidNamespaceSerializer: one byte
+                o.i64((uint64_t)kv.first);
+                o.i32((int64_t)kv.second.size());                      // ListSerializer: size, then the elements
+                for (int64_t i : kv.second) {
+                    const int64_t st = s.col[n + i], en = end_of(i);
+                    o.i64((uint64_t)st); o.i64((uint64_t)en); o.i64((uint64_t)st); o.i64((uint64_t)en);
+                }
             }
+        }
+        // event-time timers: DataStream at window.maxTimestamp() (+ the cleanup time with lateness); Table at the
+        // end - 1 of the first unfired window containing each slice, one per (key, window)
+        std::set<std::tuple<int64_t, int64_t, int64_t, int64_t>> timers;   // (ts, key, ns start, ns end)
+        for (int64_t i = lo; i < hi; ++i) {
+            const int64_t key = s.col[i], start = s.col[n + i], end = end_of(i);
+            if (ds) {
+                timers.insert({end - 1, key, start, end});
+                if (s.late > 0) timers.insert({(end - 1 > INT64_MAX - s.late) ? INT64_MAX : end - 1 + s.late, key, start, end});
+            } else {
+                int64_t we = first_window_end(c, end);
+                while (we - 1 <= s.wm && s.wm != INT64_MIN) we += (c.window_kind == FWA_SLIDE ? c.slide_ms : g);
+                timers.insert({we - 1, key, 0, we});
+            }
+        }
+        o.i16(ds && sess ? 2 : 1);
+        o.i32((int64_t)timers.size());
+        for (const auto& t : timers) {
+            o.i64((uint64_t)std::get<0>(t) ^ 0x8000000000000000ull);   // MathUtils.flipSignBit
+            const int64_t key = std::get<1>(t);
+            if (ds) { o.i64((uint64_t)key); o.i64((uint64_t)std::get<2>(t)); o.i64((uint64_t)std::get<3>(t)); }
+            else { const uint64_t kf = (uint64_t)key; o.row(&kf, 1); o.i64((uint64_t)std::get<3>(t)); }
         }
     }
     *watermark = s.wm;
@@ -184,42 +303,60 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
     fwa_config c;
     int rc = fwa_get_config(e, &c);
     if (rc) return rc;
-    if (!supported(c)) return fwa_set_error(e, FWA_E_UNSUPPORTED, "heap layout: TUMBLE windows in UTC without NULLs only");
+    if (!supported(c)) return fwa_set_error(e, FWA_E_UNSUPPORTED, kUnsupported);
     const bool ds = c.semantics == FWA_SEM_DATASTREAM;
-    const int na = c.num_aggs, arity = 1 + na, maxp = c.max_parallelism;
+    const bool sess = c.window_kind == FWA_SESSION;
+    const int na = c.num_aggs, arity = 1 + na, maxp = c.max_parallelism, ns = nstates(c);
+    const int64_t g = ds ? c.size_ms : slice_width(c);
+    const int64_t ncols = (sess ? 4 : 3) + na;
     std::vector<std::vector<int64_t>> blobs((size_t)n_bodies);
     std::vector<const void*> ptrs;
     std::vector<int64_t> bsz;
     for (int b = 0; b < n_bodies; ++b) {
-        // entries per key group, in section order
-        std::vector<std::vector<int64_t>> per((size_t)maxp);   // flattened (key, start, count, acc_j...) records
+        std::vector<std::vector<int64_t>> per((size_t)maxp);   // flattened (key, start, count, acc_j... [, end]) rows
         In in{(const uint8_t*)bodies[b], sizes[b]};
         int64_t lo = maxp, hi = -1, total = 0;
         std::vector<uint64_t> f((size_t)arity);
+        struct Pending { int64_t kg, key, start, end; std::vector<uint64_t> f; };
+        std::vector<Pending> pend;
+        std::map<std::tuple<int64_t, int64_t, int64_t>, std::pair<int64_t, int64_t>> actual;
         while (in.ok && in.at < in.n) {
-            const int64_t g = in.i32();
-            if (!in.ok || g < 0 || g >= maxp) return fwa_set_error(e, FWA_E_ARG, "heap body: bad key group id");
-            lo = std::min(lo, g); hi = std::max(hi, g);
-            for (int st = 0; st < 2; ++st) {
+            const int64_t kg = in.i32();
+            if (!in.ok || kg < 0 || kg >= maxp) return fwa_set_error(e, FWA_E_ARG, "heap body: bad key group id");
+            lo = std::min(lo, kg); hi = std::max(hi, kg);
+            for (int st = 0; st < ns; ++st) {
                 const int64_t id = (int16_t)in.get(2), cnt = in.i32();
-                if (!in.ok || id < 0 || id > 1 || cnt < 0) return fwa_set_error(e, FWA_E_ARG, "heap body: bad state section");
+                if (!in.ok || id < 0 || id >= ns || cnt < 0) return fwa_set_error(e, FWA_E_ARG, "heap body: bad state section");
                 for (int64_t i = 0; i < cnt && in.ok; ++i) {
-                    if (id == 1) {                                     // timers: re-derived from the window state
+                    if (id == ns - 1) {                                // timers: re-derived from the window state
                         in.i64();
                         if (ds) { in.i64(); in.i64(); in.i64(); } else { uint64_t k; in.row(&k, 1); in.i64(); }
                         continue;
                     }
-                    int64_t key, start;
-                    if (ds) { start = in.i64(); in.i64(); key = in.i64(); for (int k = 0; k < arity; ++k) f[k] = (uint64_t)in.i64(); }
+                    if (id == 1) {                                     // merging-window-set: (actual, state) pairs
+                        in.get(1);                                     // MergingWindowSet(...) :83-87
+                        const int64_t key = in.i64(), m = in.i32();
+                        for (int64_t q = 0; q < m && in.ok; ++q) {
+                            const int64_t as = in.i64(), ae = in.i64(), ss = in.i64(), se = in.i64();
+                            actual[std::make_tuple(key, ss, se)] = std::make_pair(as, ae);
+                        }
+                        continue;
+                    }
+                    int64_t key, start, end;
+                    if (ds) { start = in.i64(); end = in.i64(); key = in.i64(); for (int k = 0; k < arity; ++k) f[k] = (uint64_t)in.i64(); }
                     else {
-                        const int64_t end = in.i64();
+                        end = in.i64();
                         uint64_t kf;
                         in.row(&kf, 1);
                         key = (int64_t)kf;
                         in.row(f.data(), arity);
-                        start = end - c.size_ms;
+                        start = end - g;
                     }
-                    std::vector<int64_t>& v = per[(size_t)g];
+                    if (sess) {                                        // resolved against the mapping below
+                        pend.push_back({kg, key, start, end, std::vector<uint64_t>(f)});
+                        continue;
+                    }
+                    std::vector<int64_t>& v = per[(size_t)kg];
                     v.push_back(key);
                     v.push_back(start);
                     v.push_back((int64_t)f[0]);
@@ -227,10 +364,25 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
                     ++total;
                 }
             }
+            // a session's window contents live under its state window; the session itself is the actual window
+            // that maps to it (Flink names an older window as the state namespace after merges)
+            for (const Pending& p : pend) {
+                auto it = actual.find(std::make_tuple(p.key, p.start, p.end));
+                const int64_t st = it == actual.end() ? p.start : it->second.first;
+                const int64_t en = it == actual.end() ? p.end : it->second.second;
+                std::vector<int64_t>& v = per[(size_t)p.kg];
+                v.push_back(p.key);
+                v.push_back(st);
+                v.push_back((int64_t)p.f[0]);
+                for (int j = 0; j < na; ++j) v.push_back((int64_t)field_to_acc(c.aggs[j].kind, p.f[1 + j]));
+                v.push_back(en);
+                ++total;
+            }
+            pend.clear();
+            actual.clear();
         }
         if (!in.ok) return fwa_set_error(e, FWA_E_ARG, "heap body: truncated");
         // the equivalent FWASNAP1 blob (engine.hip snap_header layout)
-        const int64_t ncols = 3 + na;
         std::vector<int64_t>& w = blobs[(size_t)b];
         w.assign((size_t)(kHdr + maxp + 1 + total * ncols), 0);
         w[0] = (int64_t)kMagic; w[1] = 1; w[2] = c.window_kind; w[3] = c.semantics; w[4] = c.size_ms;
@@ -241,9 +393,9 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
         int64_t* koff = w.data() + kHdr;
         int64_t* body = koff + maxp + 1;
         int64_t d = 0;
-        for (int g = 0; g < maxp; ++g) {
-            koff[g] = d;
-            const std::vector<int64_t>& v = per[(size_t)g];
+        for (int kg = 0; kg < maxp; ++kg) {
+            koff[kg] = d;
+            const std::vector<int64_t>& v = per[(size_t)kg];
             for (size_t r = 0; r < v.size(); r += (size_t)ncols, ++d)
                 for (int64_t k = 0; k < ncols; ++k) body[k * total + d] = v[r + (size_t)k];
         }

@@ -301,22 +301,29 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
 
 /* The same keyed state in the byte layout of Flink's heap keyed-state backend (HeapSnapshotStrategy.java:154-175):
  * for each owned key group g = kg_start..kg_end, in order: int g; short 0 (window state), int n, n x (namespace,
- * key, accumulator) (CopyOnWriteStateMapSnapshot.writeState :138-148); short 1 (event-time timers), int m, m x
- * (long flipSignBit(ts), key, namespace) (TimerSerializer.serialize :147-152). Big-endian java.io.DataOutput.
- *   DATASTREAM TUMBLE (WindowOperator): namespace TimeWindow (long start, long end), key Long, accumulator a Tuple of
- *     Long COUNT(*) then one field per aggregate (Long for COUNT / BIGINT SUM / AVG / MIN / MAX, Double for floating
- *     SUM / AVG / MIN / MAX), timers at window.maxTimestamp() and, with allowed lateness, at the cleanup time.
- *   TABLE TUMBLE (SlicingWindowOperator): namespace Long slice end, key BinaryRowData(BIGINT), accumulator a
- *     BinaryRowData of the same fields (BinaryRowDataSerializer), timer at slice end - 1.
+ * key, accumulator) (CopyOnWriteStateMapSnapshot.writeState :138-148); [sessions: short 1 (merging-window-set),
+ * int k, k x (byte 0 VoidNamespace, key, int size, size x (TimeWindow actual, TimeWindow state)) (ListSerializer)];
+ * then the event-time timers: short id, int m, m x (long flipSignBit(ts), key, namespace) (TimerSerializer.serialize
+ * :147-152). Big-endian java.io.DataOutput.
+ *   DATASTREAM TUMBLE / SESSION (WindowOperator): namespace TimeWindow (long start, long end), key Long, accumulator a
+ *     Tuple of Long COUNT(*) then one field per aggregate (Long for COUNT / BIGINT SUM / AVG / MIN / MAX, Double for
+ *     floating SUM / AVG / MIN / MAX), timers at window.maxTimestamp() and, with allowed lateness, at the cleanup
+ *     time. Each in-flight session is written as its own state window (an equivalent MergingWindowSet mapping).
+ *   TABLE TUMBLE / HOP / CUMULATE (SlicingWindowOperator): namespace Long slice end, key BinaryRowData(BIGINT),
+ *     accumulator a BinaryRowData of the same fields (BinaryRowDataSerializer); a CUMULATE window's fired slices are
+ *     folded into its first slice (the shared state SliceSharedWindowAggProcessor keeps); one timer per (key, first
+ *     unfired window end of each live slice) at window end - 1.
  * kg_offsets[g - kg_start] receives the byte offset of key group g's section (KeyGroupRangeOffsets; the Java shim
  * writes its KeyedBackendSerializationProxy header in front and shifts them), *watermark the operator watermark
- * (union list state, SlicingWindowOperator.java:204-209). Other window kinds, a shift time zone, nullable columns or
- * PREHASHED keys: FWA_E_UNSUPPORTED (fwa_snapshot covers them). The blob is freed with fwa_blob_free. */
+ * (union list state, SlicingWindowOperator.java:204-209). DataStream SLIDE / CUMULATE, Table SESSION, a shift time
+ * zone, nullable columns or PREHASHED keys: FWA_E_UNSUPPORTED (fwa_snapshot covers them). The blob is freed with
+ * fwa_blob_free. */
 int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark);
 
 /* Restore a fresh handle from heap-layout bodies (as written by fwa_snapshot_heap on handles with the same window
  * and aggregate configuration, any key-group ranges): the key groups of [kg_start, kg_end] are read, timers are
- * re-derived from the window state, the watermark is the MIN of watermarks[] (HeapRestoreOperation /
+ * re-derived from the window state, session contents are re-keyed from their state window to the actual window
+ * the merging-window-set maps to it, the watermark is the MIN of watermarks[] (HeapRestoreOperation /
  * SlicingWindowOperator.initializeState :186-202). */
 int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* sizes, const int64_t* watermarks,
                      int32_t n_bodies);
