@@ -282,6 +282,8 @@ def ingest_kernels(args, eng):
     """Names of the kernels whose device time `roofline.achieved` divides by (HIP events around them)."""
     if args.config == "c5s":
         return "sess2_classify+sess2_route+radix sort+scan-by-key+sess2_reduce (+sess2_ordered)"
+    if eng.record_lists:
+        return "sp_range_kernel+sp_hist_kernel+sp_scan_kernel+sp_scatter_kernel (record lists)"
     return "partition3_kernel+combine3_kernel" if eng.stats().partition_ms > 0 else "ingest_kernel"
 
 

@@ -41,6 +41,7 @@ STATUS = {0: "OK", -1: "E_ARG", -2: "E_TS_MIN", -3: "E_KEYGROUP", -4: "E_MERGE_L
 
 CFG_DYNAMIC_GAP = 0x1
 CFG_LATE_INDICES = 0x2
+CFG_RECORD_LISTS = 0x4
 
 PUSH_DEVICE_PTRS = 0x1
 PUSH_ASYNC = 0x2
@@ -105,7 +106,7 @@ def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, sl
                 offset_ms=0, gap_ms=0, allowed_lateness_ms=0, aggs=(("COUNT", 0), ("SUM_I64", 0)),
                 key_kind=KEY_JAVA_LONG, max_parallelism=128, kg_start=0, kg_end=None, device=0,
                 output_on_device=0, key_capacity=0, max_batch=0, gap_col=None, tz=None, late_indices=False,
-                nullable_cols=()):
+                nullable_cols=(), record_lists=False):
     """Build a Config struct. aggs: sequence of (agg name, value-column index). gap_col: value column of
     per-record session gaps (DynamicEventTimeSessionWindows). tz: [(utc_instant_ms, offset_ms), ...] shift
     time zone of a TIMESTAMP_LTZ rowtime (the struct keeps a pointer to a buffer held on the struct)."""
@@ -131,6 +132,8 @@ def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, sl
     c.max_batch = max_batch
     if late_indices:
         c.flags |= CFG_LATE_INDICES
+    if record_lists:                                      # TUMBLE state as record lists (huge key spaces)
+        c.flags |= CFG_RECORD_LISTS
     for col in nullable_cols:                             # value columns that may hold SQL NULLs
         c.nullable_cols |= 1 << col
     if gap_col is not None:

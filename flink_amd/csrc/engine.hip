@@ -2386,6 +2386,8 @@ int64_t gcd64(int64_t a, int64_t b) {
 // ==================================================================================================
 // host engine
 
+struct SpState;                       // record-list window state (sparse.inc)
+
 struct fwa_engine {
     fwa_config cfg;
     EngineConst ec;
@@ -2513,6 +2515,9 @@ struct fwa_engine {
     size_t arena_cap = 0, arena_used = 0;
     int32_t* h_touched = nullptr;     // pinned landing buffer of the touched-flag mirror
     int32_t h_touched_cap = 0;
+    // FWA_CFG_RECORD_LISTS: TUMBLE window state as hash-partitioned record lists, aggregated at fire (sparse.inc)
+    bool sparse = false;
+    SpState* sp = nullptr;
 };
 
 namespace {
@@ -2586,7 +2591,10 @@ int validate(const fwa_config* c) {
         default:
             return FWA_E_ARG;
     }
-    if (c->flags & ~(FWA_CFG_DYNAMIC_GAP | FWA_CFG_LATE_INDICES)) return FWA_E_ARG;
+    if (c->flags & ~(FWA_CFG_DYNAMIC_GAP | FWA_CFG_LATE_INDICES | FWA_CFG_RECORD_LISTS)) return FWA_E_ARG;
+    if ((c->flags & FWA_CFG_RECORD_LISTS) && !(c->window_kind == FWA_TUMBLE && c->nullable_cols == 0 && c->tz_n == 0 &&
+                                              (c->semantics == FWA_SEM_TABLE || c->allowed_lateness_ms == 0)))
+        return FWA_E_UNSUPPORTED;
     if ((c->flags & FWA_CFG_DYNAMIC_GAP) && (c->window_kind != FWA_SESSION || c->gap_col < 0 || c->gap_col >= FWA_MAX_COLS))
         return FWA_E_ARG;
     if (c->nullable_cols && c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;   // SQL NULLs: Table semantics
@@ -2874,6 +2882,8 @@ int reset_push_status(fwa_engine* e, bool v2bufs = false) {
 
 }  // namespace
 
+#include "sparse.inc"
+
 // ==================================================================================================
 // C-ABI
 
@@ -2887,6 +2897,7 @@ const char* fwa_last_error(const fwa_engine* e) { return e ? e->err.c_str() : "n
 int fwa_get_config(const fwa_engine* e, fwa_config* out) {
     if (!e || !out) return FWA_E_ARG;
     *out = e->cfg;
+    if (e->sparse) out->flags |= FWA_CFG_RECORD_LISTS;   // reports the auto-selected mode too
     return FWA_OK;
 }
 int fwa_set_error(fwa_engine* e, int code, const char* msg) { return fail(e, code, msg); }
@@ -2895,6 +2906,7 @@ void fwa_destroy(fwa_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->cfg.device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    sp_destroy(e);
     for (int c = 0; c < 3 + FWA_MAX_AGGS; ++c) if (e->lr_col[c]) (void)hipFree(e->lr_col[c]);
     if (e->d_late) (void)hipFree(e->d_late);
     if (e->d_lr_n) (void)hipFree(e->d_lr_n);
@@ -3051,7 +3063,11 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         if (lds_need(seg_log) > 160 * 1024) sl = 0;
         const int64_t np = (int64_t)1 << e->part_bits;
         const char* force = getenv("FWA_INGEST");
-        ok = ok && np <= kMaxPart && sl >= 2 && !(force && !strcmp(force, "v1")) && e->kind != FWA_SESSION;
+        // record lists (sparse.inc): asked for, or a key space of >= 2^25 keys (FWA_SPARSE=0 / 1 overrides)
+        bool want_sp = (cfg->flags & FWA_CFG_RECORD_LISTS) || kc0 >= ((int64_t)1 << 25);
+        if (const char* fs = getenv("FWA_SPARSE")) want_sp = atoi(fs) != 0;
+        e->sparse = want_sp && sp_eligible(cfg);
+        ok = ok && np <= kMaxPart && sl >= 2 && !(force && !strcmp(force, "v1")) && e->kind != FWA_SESSION && !e->sparse;
         e->v2 = ok;
         if (ok) {
             e->np = (int32_t)np;
@@ -3064,7 +3080,7 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
     }
     if (hipSetDevice(cfg->device) != hipSuccess) { delete e; return FWA_E_DEVICE; }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return FWA_E_DEVICE; }
-    const int64_t kc = cfg->key_capacity > 0 ? cfg->key_capacity : (1 << 20);
+    const int64_t kc = e->sparse ? 512 : (cfg->key_capacity > 0 ? cfg->key_capacity : (1 << 20));   // no key table
     int64_t cap = 1024;
     while (cap < 2 * kc) cap <<= 1;
     e->capacity = cap;
@@ -3099,6 +3115,8 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
             if (hipMalloc(&e->d_kflag, (size_t)cap + 1) != hipSuccess) { rc = FWA_E_OOM; break; }
             if (hipMalloc(&e->d_sctr, sizeof(SessCtr)) != hipSuccess) { rc = FWA_E_OOM; break; }
             if (hipHostMalloc(&e->h_sctr, sizeof(SessCtr)) != hipSuccess) { rc = FWA_E_OOM; break; }
+        } else if (e->sparse) {
+            if ((rc = sp_init(e))) break;
         } else {
             if ((rc = grow_slots(e, 4))) break;
             if ((rc = publish_dir(e))) break;
@@ -3895,6 +3913,7 @@ static int settle_pending(fwa_engine* e) {
 }
 
 static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, bool async, int64_t* late_dropped_out) {
+    if (e->sparse) return sp_push(e, a, n, late_dropped_out);
     int rc = FWA_OK;
     bool ran_v2 = false;
     if (e->v2 && allow_v2) {
@@ -4190,7 +4209,13 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     memset(out, 0, sizeof(*out));
     std::vector<FireWindow> hw;
     std::vector<int32_t> hs;
-    for (auto& kv : e->live) {
+    int64_t nrows = 0;
+    if (e->sparse) {
+        int rc = sp_fire(e, sp_due(e, wm), 1, true, &nrows);
+        if (rc) return rc;
+        if (wm > e->wm) e->wm = wm;
+    }
+    if (!e->sparse) for (auto& kv : e->live) {
         if (!e->touched[kv.second]) continue;
         FireWindow f;
         f.start = slice_start(e, kv.first);
@@ -4201,7 +4226,6 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
         hs.push_back(kv.second);
         hw.push_back(f);
     }
-    int64_t nrows = 0;
     if (!hw.empty()) {
         int rc = launch_fire(e, hw, hs, 1, &nrows);
         if (rc) return rc;
@@ -4212,7 +4236,7 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
         rc = flush_resets(e);
         if (rc) return rc;
     }
-    if (wm > e->wm) {   // forward the watermark: lateness from now on, release slices past cleanup
+    if (wm > e->wm && !e->sparse) {   // forward the watermark: lateness from now on, release slices past cleanup
         int rc = retire_slices(e, wm);
         if (rc) return rc;
         e->wm = wm;
@@ -4406,7 +4430,19 @@ int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
     if (e->kind == FWA_SESSION) return snapshot_sessions(e, out);
     std::vector<FireWindow> hw;
     std::vector<int32_t> hs;
-    for (auto& kv : e->live) {
+    int64_t n = 0;
+    if (e->sparse) {   // every live window's (key, window) accumulators, lists kept
+        std::vector<int64_t> all;
+        for (auto& kv : e->sp->wins) all.push_back(kv.first);
+        const int64_t rows0 = e->fire_rows, launches0 = e->fire_launches;
+        const double ms0 = e->fire_ms;
+        int rc = sp_fire(e, all, 1, false, &n);
+        if (rc) return rc;
+        e->fire_rows = rows0;
+        e->fire_launches = launches0;
+        e->fire_ms = ms0;
+    }
+    if (!e->sparse) for (auto& kv : e->live) {
         if (!e->touched[kv.second]) continue;
         FireWindow f;
         f.start = slice_start(e, kv.first);
@@ -4416,7 +4452,6 @@ int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
         hs.push_back(kv.second);
         hw.push_back(f);
     }
-    int64_t n = 0;
     if (!hw.empty()) {
         const int64_t rows0 = e->fire_rows, launches0 = e->fire_launches;
         const double ms0 = e->fire_ms;
@@ -4466,7 +4501,7 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
     if (!e) return FWA_E_STATE;
     if (n_blobs < 0 || (n_blobs > 0 && (!blobs || !sizes))) return fail(e, FWA_E_ARG, "null snapshot list");
     if (int rc0 = settle_pending(e)) return rc0;
-    if (e->records_in != 0 || e->wm != LONG_MIN_J || !e->live.empty() || e->n_ss != 0)
+    if (e->records_in != 0 || e->wm != LONG_MIN_J || !e->live.empty() || e->n_ss != 0 || sp_live_windows(e) != 0)
         return fail(e, FWA_E_STATE, "restore needs a fresh handle");
     const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism;
     const int ncols = (e->kind == FWA_SESSION ? 4 : 3) + na;
@@ -4507,8 +4542,8 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
     e->records_in = 0;   // metrics are not part of the snapshot
     e->late_dropped = 0;
     if (any && wm > e->wm) {   // windows with maxTs <= wm fired before the snapshot: no re-fire
-        int rc = retire_slices(e, wm);
-        if (rc) return rc;
+        if (e->sparse) sp_retire(e, wm);
+        else if (int rc = retire_slices(e, wm)) return rc;
         e->wm = wm;
     }
     return FWA_OK;
@@ -4637,6 +4672,10 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
         int rc = fire_sessions(e, wm, &nrows);
         if (rc) return rc;
         e->wm = wm;
+    } else if (wm > e->wm && e->sparse) {   // windows with prev < maxTimestamp <= wm (every live one is > prev)
+        int rc = sp_fire(e, sp_due(e, wm), 0, true, &nrows);
+        if (rc) return rc;
+        e->wm = wm;
     } else if (wm > e->wm) {
         const int64_t prev = e->wm;
         // windows of touched slices that fire now: prev < end-1 <= wm  (EventTimeTrigger / isWindowFired)
@@ -4741,7 +4780,7 @@ int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
     s->late_dropped = e->late_dropped;
     s->rows_out = e->rows_out;
     s->live_keys = (int64_t)e->h_st->n_keys;
-    s->live_slices = e->kind == FWA_SESSION ? e->n_ss : (int64_t)e->live.size();
+    s->live_slices = e->kind == FWA_SESSION ? e->n_ss : e->sparse ? sp_live_windows(e) : (int64_t)e->live.size();
     s->current_watermark = e->wm;
     s->ingest_launches = e->ingest_launches;
     s->ingest_ms = e->ingest_ms;

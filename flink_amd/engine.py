@@ -61,6 +61,8 @@ def lib():
                                    C.c_int32]
     L.fwa_restore_heap.restype = C.c_int
     L.fwa_flush.argtypes = [C.c_void_p]
+    L.fwa_get_config.argtypes = [C.c_void_p, C.POINTER(A.Config)]
+    L.fwa_get_config.restype = C.c_int
     L.fwa_flush.restype = C.c_int
     L.fwa_version.restype = C.c_char_p
     L.fwa_set_input_stream.argtypes = [C.c_void_p, C.c_void_p]
@@ -296,6 +298,13 @@ class WindowAggregator:
         rc = lib().fwa_flush(self.h)
         self._settled()
         _check(rc, self.h)
+
+    @property
+    def record_lists(self):
+        """True when the handle keeps TUMBLE window state as record lists (FWA_CFG_RECORD_LISTS, chosen or auto)."""
+        c = A.Config()
+        _check(lib().fwa_get_config(self.h, C.byref(c)), self.h)
+        return bool(c.flags & A.CFG_RECORD_LISTS)
 
     def stats(self):
         st = A.Stats()

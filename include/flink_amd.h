@@ -161,6 +161,12 @@ typedef struct fwa_config {
                                   * WindowOperator's lateDataOutputTag side output (WindowOperator.java:425-433) and the
                                   * per-record processElement() == true of SlicingWindowProcessor
                                   * (SlicingWindowOperator.java:222-226, lateRecordsDroppedRate) */
+#define FWA_CFG_RECORD_LISTS 0x4 /* TUMBLE, lateness 0, no NULLs, UTC: keep each window's state as its accepted records
+                                  * (key + accumulator words) bucketed by hash partition, aggregated once when the window
+                                  * fires -- for key spaces where keys barely repeat within a window (C4: 1e8 keys).
+                                  * Selected automatically when key_capacity >= 2^25; fwa_get_config reports it.
+                                  * Same results, snapshots and partials as the dense layout. Other configurations:
+                                  * FWA_E_UNSUPPORTED. */
 
 typedef struct fwa_out {
     int64_t n_rows;
