@@ -12,7 +12,8 @@ import os
 import re
 import sys
 
-EXCLUDE = re.compile(r"fire|generate_kernel|reduce_kernel|elementwise|rocclr|reset|fill_u64|push_reset|wire_")
+EXCLUDE = re.compile(r"fire|sp_refine|sp_agg|generate_kernel|reduce_kernel|elementwise|rocclr|reset|fill_u64|push_reset|wire_")
+FIRE = re.compile(r"fire|sp_agg")   # one per step: marks the timed region
 
 
 def short(name):
@@ -49,7 +50,7 @@ def main(root, tag, steps=3):
         warm = 2 if cfg == "c3" else 1
         total_steps = steps + warm
         # timed steps = the dispatches after the last warm-up step's fire (one fire kernel per step)
-        fires = sorted(d for k, v in fe.items() if "fire" in k for d, _ in v)
+        fires = sorted(d for k, v in fe.items() if FIRE.search(k) for d, _ in v)
         bound = fires[len(fires) - steps - 1] if len(fires) > steps else -1
         res, step_bytes = {}, 0.0
         for k in sorted(set(fe) | set(wr)):
@@ -68,7 +69,7 @@ def main(root, tag, steps=3):
         rec = 28 if cfg in ("c5", "c5s") else 24
         doc = {"note": "rocprofv3 --pmc FETCH_SIZE; WRITE_SIZE in separate runs (tools/gpu_pmc_all.sh), bench.py "
                        "--config %s --steps %d --warmup %d; FETCH_SIZE x2 (gfx950), WRITE_SIZE as reported; "
-                       "ingest = every kernel except fire / generator / torch / runtime copies, dispatched after the warm-up's last fire (%d timed steps)"
+                       "ingest = every kernel except fire (incl. the record-list refine / aggregate) / generator / torch / runtime copies, dispatched after the warm-up's last fire (%d timed steps)"
                        % (cfg, steps, warm, steps),
                "config": {"workload": cfg, "batch": batch}, "per_kernel": res,
                "ingest_bytes_per_launch": step_bytes, "alg_bytes_per_launch": rec * batch,
