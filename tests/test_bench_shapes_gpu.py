@@ -88,10 +88,12 @@ def test_c5_bench_aggregates_vs_oracle(eng_mod, offset):
     o.close()
 
 
+@pytest.mark.parametrize("rl", [False, True], ids=["dense", "record_lists"])
 @pytest.mark.parametrize("kg_range", [(0, 127), (0, 63), (96, 127)], ids=["all", "p2r0", "p4r3"])
-def test_c4_large_key_table_vs_oracle(eng_mod, kg_range):
-    """bench.py --config c4 engine shape: key capacity above 2^22 slots (single-pass primary ingest),
-    keys drawn from 1e8, maxParallelism 128; partial ranges get only their own key groups (the keyBy)."""
+def test_c4_large_key_table_vs_oracle(eng_mod, kg_range, rl):
+    """bench.py --config c4 engine shape: keys drawn from 1e8, maxParallelism 128, partial ranges get only their own
+    key groups (the keyBy); dense: key capacity above 2^22 slots (single-pass primary ingest); record lists: the
+    layout bench.py's 1e8-key capacity selects (FWA_CFG_RECORD_LISTS)."""
     from oracle import oracle as O
     n = 1 << 22
     k, t, cols = _gen(eng_mod, n, 100_000_000, 0xc4, 0, span_ms=n // 1000)
@@ -101,8 +103,9 @@ def test_c4_large_key_table_vs_oracle(eng_mod, kg_range):
         sel = (kg >= lo) & (kg <= hi)
         k, t, cols = k[sel].contiguous(), t[sel].contiguous(), [c[sel].contiguous() for c in cols]
     cfg = A.make_config(window_kind="TUMBLE", size_ms=10_000, aggs=[("COUNT", 0), ("SUM_I64", 0)],
-                        key_capacity=8_000_000, max_parallelism=128, kg_start=lo, kg_end=hi)
+                        key_capacity=8_000_000, max_parallelism=128, kg_start=lo, kg_end=hi, record_lists=rl)
     g, o = eng_mod.WindowAggregator(cfg), O.Oracle(cfg)
+    assert g.record_lists == rl
     _run_batches(g, o, k, t, cols, 3, 1000, A.agg_names(cfg))
     g.close()
     o.close()
@@ -148,7 +151,7 @@ def test_c2_full_size_conservation(eng_mod):
 
 
 def test_c4_full_size_conservation(eng_mod):
-    """C4 at N=1: 1e8-key table (2^28 slots), 1e9 records."""
+    """C4 at N=1: 1e8 keys (record lists, auto-selected), 1e9 records."""
     _full_size_conservation(eng_mod, 100_000_000, 100_000_000)
 
 
