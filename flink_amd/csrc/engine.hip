@@ -3913,7 +3913,7 @@ static int settle_pending(fwa_engine* e) {
 }
 
 static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, bool async, int64_t* late_dropped_out) {
-    if (e->sparse) return sp_push(e, a, n, late_dropped_out);
+    if (e->sparse) return sp_push(e, a, n, async ? nullptr : late_dropped_out);   // settled at once; async: count via stats
     int rc = FWA_OK;
     bool ran_v2 = false;
     if (e->v2 && allow_v2) {
