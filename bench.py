@@ -259,6 +259,24 @@ def main():
             "alg_bytes_per_record": rec_bytes, "launches": st.ingest_launches,
             "avg_launch_ms": st.ingest_ms / max(1, st.ingest_launches),
         },
+        # the fire kernels' own roofline (per step: emitted rows x row bytes over the fire device time, HIP
+        # events on the engine stream); for C4 (record lists) the fire is the larger device cost of a step
+        "roofline_fire": {
+            "bound": "hbm", "kernel": fire_kernels(args, eng),
+            "achieved": (row_bytes * st.fire_rows / (st.fire_ms / 1e3) / 1e9) if st.fire_ms > 0 else 0.0,
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": (row_bytes * st.fire_rows / (st.fire_ms / 1e3) / 1e9 / HBM_PEAK_GBPS) if st.fire_ms > 0 else 0.0,
+            "alg_bytes_per_launch": row_bytes * st.fire_rows / max(1, args.steps), "alg_bytes_per_row": row_bytes,
+            "ms_per_step": st.fire_ms / max(1, args.steps),
+        },
+        # push + fire device time of a step against the step's algorithmic bytes (input + emitted rows)
+        "roofline_step": {
+            "achieved": ((alg_bytes_ingest + row_bytes * st.fire_rows) / ((st.ingest_ms + st.fire_ms) / 1e3) / 1e9)
+            if st.ingest_ms + st.fire_ms > 0 else 0.0,
+            "frac": ((alg_bytes_ingest + row_bytes * st.fire_rows) / ((st.ingest_ms + st.fire_ms) / 1e3) / 1e9
+                     / HBM_PEAK_GBPS) if st.ingest_ms + st.fire_ms > 0 else 0.0,
+            "device_ms_per_step": (st.ingest_ms + st.fire_ms) / max(1, args.steps),
+        },
         "end_to_end_hbm_frac": e2e_bytes / elapsed / 1e9 / HBM_PEAK_GBPS / world,
         "fire": {"launches": st.fire_launches, "ms": st.fire_ms, "rows": st.fire_rows},
         "ingest_split_ms": {"partition": st.partition_ms, "combine": st.combine_ms, "total": st.ingest_ms},
@@ -285,6 +303,15 @@ def ingest_kernels(args, eng):
     if eng.record_lists:
         return "sp_range_kernel+sp_hist_kernel+sp_scan_kernel+sp_scatter_kernel (record lists)"
     return "partition3_kernel+combine3_kernel" if eng.stats().partition_ms > 0 else "ingest_kernel"
+
+
+def fire_kernels(args, eng):
+    """Names of the kernels whose device time `roofline_fire` divides by."""
+    if args.config == "c5s":
+        return "sess2_fire_kernel"
+    if eng.record_lists:
+        return "sp_refine_kernel+sp_agg_kernel (record lists)"
+    return "fire_slide_kernel" if args.config == "c3" else "fire_kernel"
 
 
 def host_cpus():

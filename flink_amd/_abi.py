@@ -5,8 +5,9 @@ the exact same struct layouts.
 """
 import ctypes as C
 
-FWA_ABI_VERSION = 2
+FWA_ABI_VERSION = 3
 FWA_MAX_AGGS = 8
+FWA_MAX_COLS = 8
 
 # enum fwa_window_kind
 TUMBLE, SLIDE, CUMULATE, SESSION = 0, 1, 2, 3
@@ -79,7 +80,8 @@ class Partials(C.Structure):
     _fields_ = [
         ("n", C.c_int64), ("on_device", C.c_int32), ("num_aggs", C.c_int32),
         ("key", C.c_void_p), ("slice_start", C.c_void_p), ("count", C.c_void_p),
-        ("acc", C.c_void_p * FWA_MAX_AGGS),
+        ("acc", C.c_void_p * FWA_MAX_AGGS), ("num_hidden", C.c_int32), ("pad", C.c_int32),
+        ("hidden", C.c_void_p * FWA_MAX_COLS),
     ]
 
 

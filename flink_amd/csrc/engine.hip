@@ -125,7 +125,8 @@ __device__ __forceinline__ int64_t assign_ts(const EngineConst& c, int64_t ts) {
 struct IngestArgs {
     const int64_t* keys;
     const int64_t* ts;
-    const void* cols[FWA_MAX_COLS];
+    const void* cols[FWA_MAX_AGGS + FWA_MAX_COLS];   // value columns; partials: aggregate j's accumulator column
+                                                     // (hidden non-NULL counters after the user aggregates)
     const int32_t* key_hash;
     const int32_t* idx;         // optional index list (miss replay)
     const unsigned long long* pcount;  // partial accumulators (fwa_push_partials): COUNT per row; cols[j] = acc of agg j
@@ -265,7 +266,7 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }
         if (c.sem == FWA_SEM_DATASTREAM && ts == LONG_MIN_J) { raise_error(a.st, FWA_E_TS_MIN); continue; }
         // slice number q = floor((ts - off) / g), Java wrap arithmetic (TimeWindow.java:264-272)
-        const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
+        const int64_t d = jm::wsub(a.pcount ? ts : assign_ts(c, ts), c.off);   // partial rows: slice start, already local
         const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
         const uint64_t uq = jm::udiv64(ud, c.g_div);
         int64_t q;
@@ -906,7 +907,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             if (a.fast_m && dd < a.fast_lim) {
                 rel = (dd * a.fast_m) >> a.fast_sh;
             } else {
-                const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
+                const int64_t d = jm::wsub(PRE && a.pcount ? ts : assign_ts(c, ts), c.off);
                 const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
                 const uint64_t uq = jm::udiv64(ud, c.g_div);
                 const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
@@ -1456,6 +1457,7 @@ struct FireArgs {
     void* o_agg[FWA_MAX_AGGS];
     uint8_t* o_null[FWA_MAX_AGGS];   // SQL NULL flags per nullable aggregate (nullptr otherwise)
     int64_t* o_count;           // partial mode: COUNT(*) per row
+    int64_t* o_hid[FWA_MAX_COLS];   // partial mode of a nullable handle: hidden non-NULL counter h per row
     int32_t raw;                // 1: emit accumulators (fwa_drain_partials), not results
     int64_t out_cap;            // rows past it are counted but not written (the host grows and relaunches)
     DevStatus* st;
@@ -1539,6 +1541,13 @@ __device__ __forceinline__ void emit_row(const FireArgs& f, const EngineConst& c
         }
         write_agg(d, cnt, x, nn, f.o_agg[j], f.o_null[j], row);
     }
+    if (f.raw)   // SQL NULLs: the hidden non-NULL counters travel with the partial accumulators
+        for (int h = c.nout; h < c.naggs; ++h) {
+            const AggDesc d = c.agg[h];
+            uint64_t nn = 0;
+            for (int s = 0; s < win.nslots; ++s) nn += f.slot_base[f.win_slots[win.slot_off + s]][(int64_t)d.acc * f.stride + k];
+            f.o_hid[h - c.nout][row] = (int64_t)nn;
+        }
 }
 
 // One block = one window x one chunk of kBlock*kFireJ consecutive kids. Pass 1 sums COUNT over the
@@ -2451,6 +2460,7 @@ struct fwa_engine {
     int64_t* o_end = nullptr;
     void* o_agg[FWA_MAX_AGGS] = {};
     uint8_t* o_null[FWA_MAX_AGGS] = {};   // SQL NULL flags of the nullable aggregates' output columns
+    int64_t* o_hid[FWA_MAX_COLS] = {};    // raw exports of a nullable handle: hidden non-NULL counters
     std::vector<char> h_out;
     FireWindow* d_win = nullptr;
     int32_t win_cap = 0;
@@ -2806,6 +2816,8 @@ int ensure_out(fwa_engine* e, int64_t rows) {
         if (e->ec.agg[j].nn > 0 && e->ec.agg[j].kind != FWA_COUNT_COL) HIPCHK(e, hipMalloc(&e->o_null[j], (size_t)cap));
     if (e->o_count) HIPCHK(e, hipFree(e->o_count));
     HIPCHK(e, hipMalloc(&e->o_count, 8 * cap));
+    for (int h = 0; h < FWA_MAX_COLS; ++h) { if (e->o_hid[h]) HIPCHK(e, hipFree(e->o_hid[h])); e->o_hid[h] = nullptr; }
+    for (int h = 0; h < e->ec.naggs - e->ec.nout; ++h) HIPCHK(e, hipMalloc(&e->o_hid[h], 8 * cap));
     e->out_cap = cap;
     return FWA_OK;
 }
@@ -2898,6 +2910,7 @@ int fwa_get_config(const fwa_engine* e, fwa_config* out) {
     if (!e || !out) return FWA_E_ARG;
     *out = e->cfg;
     if (e->sparse) out->flags |= FWA_CFG_RECORD_LISTS;   // reports the auto-selected mode too
+    out->tz = e->tz.empty() ? nullptr : e->tz.data();    // the handle's own copy (valid while it lives)
     return FWA_OK;
 }
 int fwa_set_error(fwa_engine* e, int code, const char* msg) { return fail(e, code, msg); }
@@ -2920,6 +2933,7 @@ void fwa_destroy(fwa_engine* e) {
     if (e->h_sctr) (void)hipHostFree(e->h_sctr);
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_null[j]) (void)hipFree(e->o_null[j]);
+    for (int h = 0; h < FWA_MAX_COLS; ++h) if (e->o_hid[h]) (void)hipFree(e->o_hid[h]);
     for (void* p : e->chunks) (void)hipFree(p);
     if (e->h_st) (void)hipHostFree(e->h_st);
     if (e->h_arena) (void)hipHostFree(e->h_arena);
@@ -3249,7 +3263,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     const bool pre_ok = (layout == 2 && e->nv == 0) || (layout == 1 && e->nv == 1 && e->vsize[0] == 8);
     // partial accumulators (fwa_push_partials): the PRE buckets carry each row's record count, the value
     // column is the partial BIGINT sum; other aggregate lists keep the v1 path
-    if (a.pcount && (!pre_ok || getenv("FWA_P2") != nullptr || getenv("FWA_PARTIALS_V1") != nullptr)) return FWA_OK;
+    if (a.pcount && (!pre_ok || e->cfg.nullable_cols || getenv("FWA_P2") != nullptr || getenv("FWA_PARTIALS_V1") != nullptr))
+        return FWA_OK;
     const bool pre = a.pcount || (pre_ok && pre_env != 0 && (pre_env == 1 || e->pre) && getenv("FWA_P2") == nullptr);
     int rc = ensure_v2_buffers(e, a.n, pre);
     if (rc) return rc;
@@ -3782,12 +3797,15 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     f.o_end = e->o_end;
     for (int j = 0; j < e->cfg.num_aggs; ++j) { f.o_agg[j] = e->o_agg[j]; f.o_null[j] = e->o_null[j]; }
     f.o_count = raw ? e->o_count : nullptr;
+    for (int h = 0; h < e->ec.naggs - e->ec.nout; ++h) f.o_hid[h] = e->o_hid[h];
     f.raw = raw;
     f.out_cap = e->out_cap;
     f.st = e->d_st;
     const int64_t grid = (int64_t)f.blocks_per_win * (int64_t)hw.size();
     HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
-    bool single = e->nacc == 2;   // one stateful accumulator column, every window one slot
+    // one stateful accumulator column, every window one slot (a raw export of a nullable handle also
+    // writes the hidden counters: the generic path)
+    bool single = e->nacc == 2 && !(raw && e->ec.naggs > e->ec.nout);
     for (const FireWindow& w : hw) single = single && w.nslots == 1;
     if (single) fire_kernel<1><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
     else fire_kernel<0><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
@@ -4113,7 +4131,6 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
                       const void* const* acc, int64_t n, int32_t flags, int64_t* late_dropped_out) {
     if (!e) return FWA_E_STATE;
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
-    if (e->cfg.nullable_cols) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of nullable aggregates");
     if (n < 0 || (n > 0 && (!keys || !slice_ts || !count))) return fail(e, FWA_E_ARG, "null input column");
     if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "partials need a computable key hash");
     if (n > INT32_MAX) return fail(e, FWA_E_ARG, "batch too large (max 2^31-1 records)");
@@ -4136,14 +4153,15 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
         a.dropidx = e->d_dropidx;
     }
     a.wm = e->wm;
-    const void* src[3 + FWA_MAX_AGGS] = {keys, slice_ts, count};
+    const void* src[3 + FWA_MAX_AGGS + FWA_MAX_COLS] = {keys, slice_ts, count};
     int nsrc = 3;
-    for (int j = 0; j < e->cfg.num_aggs; ++j) {
+    for (int j = 0; j < e->ec.naggs; ++j) {   // user aggregates, then the hidden non-NULL counters
         if (e->ec.agg[j].acc == 0) continue;
-        if (!acc || !acc[j]) return fail(e, FWA_E_ARG, "missing accumulator column");
+        if (!acc || !acc[j]) return fail(e, FWA_E_ARG, j < e->ec.nout ? "missing accumulator column"
+                                                                       : "missing hidden non-NULL counter column");
         src[nsrc++] = acc[j];
     }
-    const void* dev[3 + FWA_MAX_AGGS];
+    const void* dev[3 + FWA_MAX_AGGS + FWA_MAX_COLS];
     if (flags & FWA_PUSH_DEVICE_PTRS) {
         if (int rc1 = wait_input_stream(e)) return rc1;
         for (int c = 0; c < nsrc; ++c) dev[c] = src[c];
@@ -4163,7 +4181,7 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
     a.keys = (const int64_t*)dev[0];
     a.ts = (const int64_t*)dev[1];
     a.pcount = (const unsigned long long*)dev[2];
-    for (int j = 0, c = 3; j < e->cfg.num_aggs; ++j)
+    for (int j = 0, c = 3; j < e->ec.naggs; ++j)
         if (e->ec.agg[j].acc > 0) a.cols[j] = dev[c++];
     if (n > e->spill_cap) {
         if (e->d_spill) HIPCHK(e, hipFree(e->d_spill));
@@ -4203,7 +4221,6 @@ static int retire_slices(fwa_engine* e, int64_t wm) {
 int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     if (!e || !out) return FWA_E_ARG;
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
-    if (e->cfg.nullable_cols) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of nullable aggregates");
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
     memset(out, 0, sizeof(*out));
@@ -4243,6 +4260,7 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     }
     out->n = nrows;
     out->num_aggs = e->cfg.num_aggs;
+    out->num_hidden = e->ec.naggs - e->ec.nout;
     out->on_device = e->cfg.output_on_device ? 1 : 0;
     const int64_t* cols[3] = {e->o_key, e->o_start, e->o_count};
     const void* accs[FWA_MAX_AGGS] = {};
@@ -4252,9 +4270,10 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
         out->slice_start = cols[1];
         out->count = cols[2];
         for (int j = 0; j < e->cfg.num_aggs; ++j) out->acc[j] = accs[j];
+        for (int h = 0; h < out->num_hidden; ++h) out->hidden[h] = e->o_hid[h];
         return FWA_OK;
     }
-    e->h_out.resize(std::max<size_t>((size_t)nrows * 8 * (3 + e->cfg.num_aggs), 8));
+    e->h_out.resize(std::max<size_t>((size_t)nrows * 8 * (3 + e->cfg.num_aggs + out->num_hidden), 8));
     char* p = e->h_out.data();
     auto get = [&](const void* d) -> const void* {
         if (nrows) { hipError_t r = hipMemcpy(p, d, 8 * nrows, hipMemcpyDeviceToHost); if (r != hipSuccess) return nullptr; }
@@ -4266,6 +4285,7 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     out->slice_start = (const int64_t*)get(cols[1]);
     out->count = (const int64_t*)get(cols[2]);
     for (int j = 0; j < e->cfg.num_aggs; ++j) out->acc[j] = get(accs[j]);
+    for (int h = 0; h < out->num_hidden; ++h) out->hidden[h] = (const int64_t*)get(e->o_hid[h]);
     if (!out->key || !out->slice_start || !out->count) return fail(e, FWA_E_DEVICE, "partials copy failed");
     return FWA_OK;
 }
@@ -4275,7 +4295,8 @@ static const uint64_t kSnapMagic = 0x3150414E53415746ull;   // "FWASNAP1"
 enum { kSnapHdr = 32 };                                       // header words
 // header word layout: 0 magic, 1 version, 2 window kind, 3 semantics, 4 size, 5 slide, 6 offset, 7 gap,
 // 8 allowed lateness, 9 max parallelism, 10 key kind, 11 num aggs, 12..19 agg kinds, 20 watermark,
-// 21 entries, 22 kg_start, 23 kg_end of the snapshotting handle, 24..31 reserved (0)
+// 21 entries, 22 kg_start, 23 kg_end of the snapshotting handle, 24 nullable_cols, 25 hidden non-NULL
+// counters (columns after the acc_j columns), 26 aggregate input columns (4 bits each), 27..31 reserved (0)
 
 static void snap_header(const fwa_engine* e, int64_t* h, int64_t n) {
     memset(h, 0, sizeof(int64_t) * kSnapHdr);
@@ -4296,6 +4317,9 @@ static void snap_header(const fwa_engine* e, int64_t* h, int64_t n) {
     h[21] = n;
     h[22] = e->cfg.kg_start;
     h[23] = e->cfg.kg_end;
+    h[24] = e->cfg.nullable_cols;
+    h[25] = e->ec.naggs - e->ec.nout;
+    for (int j = 0; j < e->cfg.num_aggs; ++j) h[26] |= (int64_t)(e->cfg.aggs[j].col & 15) << (4 * j);
 }
 
 // Sessions: the blob's entries are the in-flight sessions (key, start, count, acc_j..., end) bucketed by
@@ -4303,7 +4327,7 @@ static void snap_header(const fwa_engine* e, int64_t* h, int64_t n) {
 // (WindowOperator.java:224-238 mergingSetsState / windowState), with the session end as a last column.
 static int snapshot_sessions(fwa_engine* e, fwa_blob* out) {
     const int64_t n = e->n_ss;
-    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, ncols = 4 + na;
+    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, nh = e->ec.naggs - e->ec.nout, ncols = 4 + na + nh;
     const SessList& L = e->ss[e->ss_cur];
     std::vector<uint32_t> kid((size_t)n);
     std::vector<int64_t> st((size_t)n), en((size_t)n), acc((size_t)n * e->nacc);
@@ -4340,7 +4364,8 @@ static int snapshot_sessions(fwa_engine* e, fwa_blob* out) {
             const AggDesc& ad = e->ec.agg[j];
             body[(size_t)(3 + j) * n + d] = ad.acc > 0 ? acc[(size_t)ad.acc * n + i] : acc[i];
         }
-        body[(size_t)(3 + na) * n + d] = en[i];
+        for (int h = 0; h < nh; ++h) body[(size_t)(3 + na + h) * n + d] = acc[(size_t)e->ec.agg[e->ec.nout + h].acc * n + i];
+        body[(size_t)(3 + na + nh) * n + d] = en[i];
     }
     out->data = b;
     out->size = (int64_t)(words * 8);
@@ -4365,7 +4390,7 @@ __global__ void __launch_bounds__(kBlock) sess2_restore_kernel(Sess2Args a, cons
 // Restore sessions: the owned key groups' entries of every blob are appended to the in-flight list
 // (a key lives in one subtask's snapshot, so the lists never overlap); watermark = MIN over the blobs.
 static int restore_sessions(fwa_engine* e, const void* const* blobs, int32_t n_blobs) {
-    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism;
+    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, nh = e->ec.naggs - e->ec.nout;
     int64_t wm = LONG_MAX_J;
     for (int32_t b = 0; b < n_blobs; ++b) {
         const int64_t* h = (const int64_t*)blobs[b];
@@ -4386,11 +4411,14 @@ static int restore_sessions(fwa_engine* e, const void* const* blobs, int32_t n_b
         std::vector<const int64_t*> src(nc);
         src[0] = body + lo;
         src[1] = body + (size_t)n + lo;
-        src[2] = body + (size_t)(3 + na) * n + lo;
+        src[2] = body + (size_t)(3 + na + nh) * n + lo;
         src[3] = body + (size_t)2 * n + lo;
-        for (int cc = 1; cc < e->nacc; ++cc)
+        for (int cc = 1; cc < e->nacc; ++cc) {
             for (int j = 0; j < na; ++j)
                 if (e->ec.agg[j].acc == cc && !e->ec.agg[j].alias) src[3 + cc] = body + (size_t)(3 + j) * n + lo;
+            for (int h = 0; h < nh; ++h)   // hidden non-NULL counters
+                if (e->ec.agg[e->ec.nout + h].acc == cc) src[3 + cc] = body + (size_t)(3 + na + h) * n + lo;
+        }
         std::vector<const int64_t*> hacc(e->nacc);
         for (int c = 0; c < nc; ++c) HIPCHK(e, hipMemcpy(d + (size_t)c * m, src[c], 8 * (size_t)m, hipMemcpyHostToDevice));
         for (int cc = 0; cc < e->nacc; ++cc) hacc[cc] = d + (size_t)(3 + cc) * m;
@@ -4424,7 +4452,6 @@ int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
     if (!e || !out) return FWA_E_ARG;
     memset(out, 0, sizeof(*out));
     if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "snapshot needs a computable key hash");
-    if (e->cfg.nullable_cols) return fail(e, FWA_E_UNSUPPORTED, "snapshot of nullable aggregates");
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
     if (e->kind == FWA_SESSION) return snapshot_sessions(e, out);
@@ -4461,10 +4488,11 @@ int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
         e->fire_launches = launches0;
         e->fire_ms = ms0;
     }
-    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, ncols = 3 + na;
+    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, nh = e->ec.naggs - e->ec.nout, ncols = 3 + na + nh;
     std::vector<int64_t> cols((size_t)n * ncols);
-    const void* src[3 + FWA_MAX_AGGS] = {e->o_key, e->o_start, e->o_count};
+    const void* src[3 + FWA_MAX_AGGS + FWA_MAX_COLS] = {e->o_key, e->o_start, e->o_count};
     for (int j = 0; j < na; ++j) src[3 + j] = e->o_agg[j];
+    for (int h = 0; h < nh; ++h) src[3 + na + h] = e->o_hid[h];
     for (int c = 0; c < ncols && n > 0; ++c)
         HIPCHK(e, hipMemcpy(cols.data() + (size_t)c * n, src[c], 8 * (size_t)n, hipMemcpyDeviceToHost));
     std::vector<int32_t> kg((size_t)n);
@@ -4503,8 +4531,8 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
     if (int rc0 = settle_pending(e)) return rc0;
     if (e->records_in != 0 || e->wm != LONG_MIN_J || !e->live.empty() || e->n_ss != 0 || sp_live_windows(e) != 0)
         return fail(e, FWA_E_STATE, "restore needs a fresh handle");
-    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism;
-    const int ncols = (e->kind == FWA_SESSION ? 4 : 3) + na;
+    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, nh = e->ec.naggs - e->ec.nout;
+    const int ncols = (e->kind == FWA_SESSION ? 4 : 3) + na + nh;
     int64_t ref[kSnapHdr];
     snap_header(e, ref, 0);
     // validate every blob before touching state
@@ -4514,6 +4542,8 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
             return fail(e, FWA_E_ARG, "not a flink_amd snapshot (bad magic/version/size)");
         for (int w = 2; w < 20; ++w)
             if (h[w] != ref[w]) return fail(e, FWA_E_ARG, "snapshot window/aggregate configuration differs");
+        for (int w = 24; w < 27; ++w)
+            if (h[w] != ref[w]) return fail(e, FWA_E_ARG, "snapshot nullable-column configuration differs");
         const int64_t n = h[21];
         if (n < 0 || sizes[b] != (int64_t)(8 * (kSnapHdr + maxp + 1 + (size_t)n * ncols)))
             return fail(e, FWA_E_ARG, "snapshot size does not match its entry count");
@@ -4531,8 +4561,9 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
         if (lo < 0 || hi < lo || hi > n) return fail(e, FWA_E_ARG, "corrupt key-group offsets");
         if (hi == lo) continue;
         const int64_t* body = off + maxp + 1;
-        const void* acc[FWA_MAX_AGGS] = {};
+        const void* acc[FWA_MAX_AGGS + FWA_MAX_COLS] = {};
         for (int j = 0; j < na; ++j) acc[j] = body + (size_t)(3 + j) * n + lo;
+        for (int h = 0; h < nh; ++h) acc[na + h] = body + (size_t)(3 + na + h) * n + lo;
         int64_t late = 0;
         int rc = fwa_push_partials(e, body + lo, body + (size_t)n + lo, body + (size_t)2 * n + lo, acc, hi - lo, 0, &late);
         if (rc) return rc;

@@ -25,8 +25,9 @@
 // The accumulator is the engine's built-in aggregate state: a Tuple (DataStream, TupleSerializer: big-endian fields)
 // or a BinaryRowData (Table) of COUNT(*) followed by one field per aggregate -- BIGINT for COUNT / integer SUM, AVG,
 // MIN, MAX, DOUBLE for floating SUM / AVG / MIN / MAX (the AggregateFunction's ACC type in the shim).
-// DataStream SLIDE / CUMULATE, Table SESSION, shift time zones, nullable columns: FWA_E_UNSUPPORTED (FWASNAP1 covers
-// them).
+// Table rows carry SQL NULLs as BinaryRowData null bits (an aggregate whose column held only NULLs) and one more
+// BIGINT field per hidden non-NULL counter; Table timers under a shift time zone are toEpochMillsForTimer(end - 1).
+// DataStream SLIDE / CUMULATE, Table SESSION and PREHASHED keys: FWA_E_UNSUPPORTED (FWASNAP1 covers them).
 #include <algorithm>
 #include <cstdint>
 #include <map>
@@ -38,6 +39,7 @@
 #include <vector>
 
 #include "../../include/flink_amd.h"
+#include "java_math.h"
 
 namespace {
 
@@ -45,7 +47,7 @@ constexpr uint64_t kMagic = 0x3150414E53415746ull;   // "FWASNAP1" (engine.hip s
 constexpr int kHdr = 32;
 
 struct Snap {                                        // parsed FWASNAP1 blob
-    int64_t kind, sem, size, slide, off, gap, late, maxp, key_kind, naggs, wm, n, kg_lo, kg_hi;
+    int64_t kind, sem, size, slide, off, gap, late, maxp, key_kind, naggs, wm, n, kg_lo, kg_hi, nh;
     int64_t agg[FWA_MAX_AGGS];
     const int64_t* koff;                             // [maxp + 1]
     const int64_t* col;                              // SoA [3 + naggs][n]
@@ -56,9 +58,10 @@ bool parse(const void* p, int64_t bytes, Snap* s) {
     if (bytes < kHdr * 8 || (uint64_t)w[0] != kMagic || w[1] != 1) return false;
     s->kind = w[2]; s->sem = w[3]; s->size = w[4]; s->slide = w[5]; s->off = w[6]; s->gap = w[7]; s->late = w[8];
     s->maxp = w[9]; s->key_kind = w[10]; s->naggs = w[11]; s->wm = w[20]; s->n = w[21]; s->kg_lo = w[22]; s->kg_hi = w[23];
-    if (s->naggs < 0 || s->naggs > FWA_MAX_AGGS || s->maxp <= 0) return false;
+    s->nh = w[25];
+    if (s->naggs < 0 || s->naggs > FWA_MAX_AGGS || s->maxp <= 0 || s->nh < 0 || s->nh > FWA_MAX_COLS) return false;
     for (int j = 0; j < s->naggs; ++j) s->agg[j] = w[12 + j];
-    const int64_t ncols = (s->kind == FWA_SESSION ? 4 : 3) + s->naggs;
+    const int64_t ncols = (s->kind == FWA_SESSION ? 4 : 3) + s->naggs + s->nh;
     if (bytes != (kHdr + s->maxp + 1 + s->n * ncols) * 8) return false;
     s->koff = w + kHdr;
     s->col = w + kHdr + s->maxp + 1;
@@ -86,12 +89,15 @@ struct Out {
     void i32(int64_t v) { for (int s = 24; s >= 0; s -= 8) u8((uint8_t)((uint64_t)v >> s)); }
     void i64(uint64_t v) { for (int s = 56; s >= 0; s -= 8) u8((uint8_t)(v >> s)); }
     void le64(uint64_t v) { for (int s = 0; s < 64; s += 8) u8((uint8_t)(v >> s)); }
-    // BinaryRowData with `arity` 8-byte fixed-length fields, RowKind INSERT, no NULLs (BinaryRowDataSerializer)
-    void row(const uint64_t* f, int arity) {
+    // BinaryRowData with `arity` 8-byte fixed-length fields, RowKind INSERT (BinaryRowDataSerializer; BinaryRowData
+    // layout: header byte then one null bit per field from bit 8 on, 8-byte aligned, BinaryRowData.java:68-123)
+    void row(const uint64_t* f, int arity, const bool* isnull = nullptr) {
         const int nb = ((arity + 63 + 8) / 64) * 8;
         i32(nb + 8 * arity);
-        for (int i = 0; i < nb; ++i) u8(0);
-        for (int i = 0; i < arity; ++i) le64(f[i]);
+        std::vector<uint8_t> hdr((size_t)nb, 0);
+        for (int i = 0; i < arity; ++i) if (isnull && isnull[i]) hdr[(size_t)(i + 8) / 8] |= (uint8_t)(1u << ((i + 8) % 8));
+        for (int i = 0; i < nb; ++i) u8(hdr[(size_t)i]);
+        for (int i = 0; i < arity; ++i) le64(isnull && isnull[i] ? 0 : f[i]);
     }
 };
 
@@ -108,23 +114,29 @@ struct In {
     }
     int64_t i32() { return (int32_t)get(4); }
     int64_t i64() { return (int64_t)get(8); }
-    void row(uint64_t* f, int arity) {
+    void row(uint64_t* f, int arity, bool* isnull = nullptr) {
         const int nb = ((arity + 63 + 8) / 64) * 8;
         if (i32() != nb + 8 * arity) { ok = false; return; }
-        if (get(1) != 0) ok = false;                                  // RowKind INSERT
-        for (int i = 1; i < nb; ++i) if (get(1) != 0) ok = false;     // no NULL fields
+        std::vector<uint8_t> hdr((size_t)nb);
+        for (int i = 0; i < nb; ++i) hdr[(size_t)i] = (uint8_t)get(1);
+        if (hdr[0] != 0) ok = false;                                  // RowKind INSERT
+        for (int i = 0; i < arity; ++i) {
+            const bool nl = (hdr[(size_t)(i + 8) / 8] >> ((i + 8) % 8)) & 1;
+            if (isnull) isnull[i] = nl;
+            else if (nl) ok = false;                                  // a NULL where the layout has none
+        }
         for (int i = 0; i < arity; ++i) f[i] = get(8, true);
     }
 };
 
 // Layouts this file writes: DataStream TUMBLE and SESSION (WindowOperator), Table TUMBLE / HOP / CUMULATE
-// (SlicingWindowOperator: per-slice state, so the engine's slices map 1:1).
+// (SlicingWindowOperator: per-slice state, so the engine's slices map 1:1), Table shift time zones and SQL NULLs.
 bool supported(const fwa_config& c) {
-    if (c.tz_n != 0 || c.nullable_cols != 0 || c.key_kind == FWA_KEY_PREHASHED) return false;
+    if (c.key_kind == FWA_KEY_PREHASHED) return false;
     if (c.semantics == FWA_SEM_DATASTREAM) return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SESSION;
     return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SLIDE || c.window_kind == FWA_CUMULATE;
 }
-const char* kUnsupported = "heap layout: DataStream TUMBLE / SESSION and Table TUMBLE / HOP / CUMULATE in UTC without NULLs";
+const char* kUnsupported = "heap layout: DataStream TUMBLE / SESSION and Table TUMBLE / HOP / CUMULATE with a computable key hash";
 
 int64_t gcd64(int64_t a, int64_t b) { while (b) { const int64_t t = a % b; a = b; b = t; } return a; }
 
@@ -162,12 +174,39 @@ uint64_t merge_word(int64_t kind, uint64_t x, uint64_t y) {
     }
 }
 
-// number of registered states per key group section and their ids
-//   DataStream TUMBLE: 0 window-contents, 1 event-time timers
-//   DataStream SESSION: 0 window-contents, 1 merging-window-set (ListState<Tuple2<TimeWindow, TimeWindow>> under the
-//                       VoidNamespace, WindowOperator.java:256-263), 2 event-time timers
-//   Table: 0 window state (per slice), 1 event-time timers
-int nstates(const fwa_config& c) { return (c.semantics == FWA_SEM_DATASTREAM && c.window_kind == FWA_SESSION) ? 3 : 2; }
+// the accumulator word of an aggregate that saw no (non-NULL) input (engine.hip ident_of)
+uint64_t identity_word(int64_t kind) { return (kind == FWA_MIN_I64 || kind == FWA_MIN_F32 || kind == FWA_MIN_F64) ? ~0ull : 0ull; }
+
+// SQL NULLs: the engine keeps one hidden non-NULL counter per nullable input column an aggregate reads, in first-use
+// order (engine.hip fwa_create); hid[j] = that counter's index for aggregate j, -1 for none. Returns their number.
+int hidden_map(const fwa_config& c, int* hid) {
+    int of_col[FWA_MAX_COLS], nh = 0;
+    for (int k = 0; k < FWA_MAX_COLS; ++k) of_col[k] = -1;
+    for (int j = 0; j < c.num_aggs; ++j) {
+        hid[j] = -1;
+        const int col = c.aggs[j].col;
+        if (c.aggs[j].kind == FWA_COUNT || col < 0 || col >= FWA_MAX_COLS || !((c.nullable_cols >> col) & 1)) continue;
+        if (of_col[col] < 0) of_col[col] = nh++;
+        hid[j] = of_col[col];
+    }
+    return nh;
+}
+
+// Event-time timer of a window end under the shift time zone (TimeWindowUtil.toEpochMillsForTimer :67-100; UTC:
+// the end - 1 itself)
+int64_t timer_of(const fwa_config& c, int64_t max_ts) { return c.tz_n ? jm::tz_timer(c.tz, c.tz_n, max_ts) : max_ts; }
+
+// State ids of the registered states, as a heap backend numbers them (HeapSnapshotResources.java:100-139: key/value
+// states first, then the timer queues, each group in java.util.HashMap order of the state names -- pinned by the
+// reference's own snapshots in tests/test_heap_reference_cpu.py):
+//   DataStream TUMBLE  (WindowOperator):        0 window-contents, 1 processing timers, 2 event timers
+//   DataStream SESSION (WindowOperator):        0 window-contents, 1 merging-window-set, 2 processing, 3 event timers
+//   Table (SlicingWindowOperator, window-aggs): 0 window-aggs, 1 processing timers, 2 event timers
+struct Ids { int contents, mset, proc, event, n; };
+Ids ids_of(const fwa_config& c) {
+    if (c.semantics == FWA_SEM_DATASTREAM && c.window_kind == FWA_SESSION) return Ids{0, 1, 2, 3, 4};
+    return Ids{0, -1, 1, 2, 3};
+}
 
 }  // namespace
 
@@ -178,7 +217,8 @@ int fwa_get_config(const fwa_engine* e, fwa_config* out);
 int fwa_set_error(fwa_engine* e, int code, const char* msg);
 
 int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark) {
-    if (!e || !out || !kg_offsets) return FWA_E_ARG;
+    if (!e) return FWA_E_ARG;
+    if (!out || !kg_offsets || !watermark) return fwa_set_error(e, FWA_E_ARG, "fwa_snapshot_heap: null output pointer");
     fwa_config c;
     int rc = fwa_get_config(e, &c);
     if (rc) return rc;
@@ -189,12 +229,17 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
     if (!parse(snap.data, snap.size, &s)) { fwa_blob_free(&snap); return fwa_set_error(e, FWA_E_STATE, "bad FWASNAP1 blob"); }
     const bool ds = c.semantics == FWA_SEM_DATASTREAM;
     const bool sess = c.window_kind == FWA_SESSION;
-    const int na = (int)s.naggs, arity = 1 + na;
+    const Ids id = ids_of(c);
+    int hid[FWA_MAX_AGGS];
+    const int nh = hidden_map(c, hid);
+    const int na = (int)s.naggs, arity = 1 + na + nh;
     const int64_t n = s.n, g = ds ? s.size : slice_width(c);
-    auto end_of = [&](int64_t i) { return sess ? s.col[(3 + na) * n + i] : s.col[n + i] + g; };
+    auto end_of = [&](int64_t i) { return sess ? s.col[(3 + na + nh) * n + i] : s.col[n + i] + g; };
+    const bool fired_any = s.wm != INT64_MIN;
     Out o;
     std::vector<uint64_t> f((size_t)arity);
-    struct Row { int64_t key, start, end; uint64_t w[1 + FWA_MAX_AGGS]; };
+    std::vector<uint8_t> fnull((size_t)arity);
+    struct Row { int64_t key, start, end; uint64_t w[1 + FWA_MAX_AGGS + FWA_MAX_COLS]; };
     std::vector<Row> rows;
     for (int64_t kg = c.kg_start; kg <= c.kg_end; ++kg) {
         kg_offsets[kg - c.kg_start] = (int64_t)o.b.size();
@@ -207,16 +252,16 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
         for (int64_t i = lo; i < hi; ++i) {
             Row r{s.col[i], s.col[n + i], end_of(i), {}};
             r.w[0] = (uint64_t)s.col[2 * n + i];
-            for (int j = 0; j < na; ++j) r.w[1 + j] = (uint64_t)s.col[(3 + j) * n + i];
+            for (int j = 0; j < na + nh; ++j) r.w[1 + j] = (uint64_t)s.col[(3 + j) * n + i];
             rows.push_back(r);
         }
-        if (!ds && c.window_kind == FWA_CUMULATE && s.wm != INT64_MIN) {
+        if (!ds && c.window_kind == FWA_CUMULATE && fired_any) {
             std::map<std::pair<int64_t, int64_t>, Row> first;          // (key, window start) -> folded first slice
             std::vector<Row> keep;
             std::sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) {
                 return a.key != b.key ? a.key < b.key : a.start < b.start; });
             for (const Row& r : rows) {
-                if (r.end - 1 > s.wm) { keep.push_back(r); continue; }
+                if (timer_of(c, r.end - 1) > s.wm) { keep.push_back(r); continue; }
                 const int64_t ws = c.offset_ms + floor_div(r.end - 1 - c.offset_ms, c.size_ms) * c.size_ms;
                 auto it = first.find({r.key, ws});
                 if (it == first.end()) {
@@ -227,18 +272,26 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
                 } else {
                     it->second.w[0] += r.w[0];
                     for (int j = 0; j < na; ++j) it->second.w[1 + j] = merge_word(s.agg[j], it->second.w[1 + j], r.w[1 + j]);
+                    for (int h = 0; h < nh; ++h) it->second.w[1 + na + h] += r.w[1 + na + h];
                 }
             }
             rows.clear();
             for (auto& kv : first) rows.push_back(kv.second);
             rows.insert(rows.end(), keep.begin(), keep.end());
         }
-        o.i16(0);                                                      // window contents
+        o.i16(id.contents);                                            // window contents / window-aggs
         o.i32((int64_t)rows.size());
         for (const Row& r : rows) {
             const int64_t key = r.key, start = r.start, end = r.end;
             f[0] = r.w[0];
-            for (int j = 0; j < na; ++j) f[1 + j] = acc_to_field(s.agg[j], r.w[1 + j]);
+            fnull[0] = 0;
+            for (int j = 0; j < na; ++j) {
+                f[1 + j] = acc_to_field(s.agg[j], r.w[1 + j]);
+                // SQL: an aggregate whose input column held only NULLs has a NULL buffer (Sum/Min/MaxAggFunction);
+                // COUNT(col) is the counter itself
+                fnull[1 + j] = hid[j] >= 0 && s.agg[j] != FWA_COUNT_COL && r.w[1 + na + hid[j]] == 0;
+            }
+            for (int h = 0; h < nh; ++h) { f[1 + na + h] = r.w[1 + na + h]; fnull[1 + na + h] = 0; }
             if (ds) {
                 o.i64((uint64_t)start); o.i64((uint64_t)end);          // TimeWindow.Serializer
                 o.i64((uint64_t)key);                                  // LongSerializer
@@ -247,13 +300,15 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
                 o.i64((uint64_t)end);                                  // slice end (LongSerializer)
                 const uint64_t kf = (uint64_t)key;
                 o.row(&kf, 1);                                         // key row
-                o.row(f.data(), arity);                                // accumulator row
+                bool nl[1 + FWA_MAX_AGGS + FWA_MAX_COLS];
+                for (int k = 0; k < arity; ++k) nl[k] = fnull[k] != 0;
+                o.row(f.data(), arity, nl);                            // accumulator row
             }
         }
         if (ds && sess) {                                              // merging-window-set: each in-flight session
             std::map<int64_t, std::vector<int64_t>> by_key;            // maps to itself as its state window
             for (int64_t i = lo; i < hi; ++i) by_key[s.col[i]].push_back(i);
-            o.i16(1);
+            o.i16(id.mset);
             o.i32((int64_t)by_key.size());
             for (auto& kv : by_key) {
                 o.u8(0);                                               // VoidNamespaceSerializer: one byte
@@ -265,21 +320,27 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
                 }
             }
         }
-        // event-time timers: DataStream at window.maxTimestamp() (+ the cleanup time with lateness); Table at the
-        // end - 1 of the first unfired window containing each slice, one per (key, window)
+        o.i16(id.proc);                                                // processing-time timers: none on this path
+        o.i32(0);
+        // event-time timers. DataStream: window.maxTimestamp() while the window has not fired
+        // (EventTimeTrigger.onElement / onEventTime: a fired window keeps no trigger timer, a late element within
+        // allowed lateness FIREs at once) and always the cleanup timer maxTimestamp + allowedLateness
+        // (WindowOperator.registerCleanupTimer :608-620, cleanupTime :647-654; the same timer when the lateness is 0).
+        // Table: toEpochMillsForTimer(end - 1) of the first unfired window containing each slice, one per
+        // (key, window) (AbstractWindowAggProcessor.processElement :160-164, SliceSharedWindowAggProcessor.fireWindow :76-84).
         std::set<std::tuple<int64_t, int64_t, int64_t, int64_t>> timers;   // (ts, key, ns start, ns end)
         for (int64_t i = lo; i < hi; ++i) {
             const int64_t key = s.col[i], start = s.col[n + i], end = end_of(i);
             if (ds) {
-                timers.insert({end - 1, key, start, end});
-                if (s.late > 0) timers.insert({(end - 1 > INT64_MAX - s.late) ? INT64_MAX : end - 1 + s.late, key, start, end});
+                if (!fired_any || end - 1 > s.wm) timers.insert({end - 1, key, start, end});
+                timers.insert({(end - 1 > INT64_MAX - s.late) ? INT64_MAX : end - 1 + s.late, key, start, end});
             } else {
                 int64_t we = first_window_end(c, end);
-                while (we - 1 <= s.wm && s.wm != INT64_MIN) we += (c.window_kind == FWA_SLIDE ? c.slide_ms : g);
-                timers.insert({we - 1, key, 0, we});
+                while (fired_any && timer_of(c, we - 1) <= s.wm) we += (c.window_kind == FWA_SLIDE ? c.slide_ms : g);
+                timers.insert({timer_of(c, we - 1), key, 0, we});
             }
         }
-        o.i16(ds && sess ? 2 : 1);
+        o.i16(id.event);
         o.i32((int64_t)timers.size());
         for (const auto& t : timers) {
             o.i64((uint64_t)std::get<0>(t) ^ 0x8000000000000000ull);   // MathUtils.flipSignBit
@@ -306,34 +367,45 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
     if (!supported(c)) return fwa_set_error(e, FWA_E_UNSUPPORTED, kUnsupported);
     const bool ds = c.semantics == FWA_SEM_DATASTREAM;
     const bool sess = c.window_kind == FWA_SESSION;
-    const int na = c.num_aggs, arity = 1 + na, maxp = c.max_parallelism, ns = nstates(c);
+    const Ids id = ids_of(c);
+    int hid[FWA_MAX_AGGS];
+    const int nh = hidden_map(c, hid);
+    const int na = c.num_aggs, arity = 1 + na + nh, maxp = c.max_parallelism;
     const int64_t g = ds ? c.size_ms : slice_width(c);
-    const int64_t ncols = (sess ? 4 : 3) + na;
+    const int64_t ncols = (sess ? 4 : 3) + na + nh;
     std::vector<std::vector<int64_t>> blobs((size_t)n_bodies);
     std::vector<const void*> ptrs;
     std::vector<int64_t> bsz;
     for (int b = 0; b < n_bodies; ++b) {
-        std::vector<std::vector<int64_t>> per((size_t)maxp);   // flattened (key, start, count, acc_j... [, end]) rows
+        std::vector<std::vector<int64_t>> per((size_t)maxp);   // flattened (key, start, count, acc_j..., hid_h... [, end]) rows
         In in{(const uint8_t*)bodies[b], sizes[b]};
         int64_t lo = maxp, hi = -1, total = 0;
         std::vector<uint64_t> f((size_t)arity);
-        struct Pending { int64_t kg, key, start, end; std::vector<uint64_t> f; };
+        bool fnull[1 + FWA_MAX_AGGS + FWA_MAX_COLS];
+        struct Pending { int64_t kg, key, start, end; std::vector<int64_t> w; };
         std::vector<Pending> pend;
         std::map<std::tuple<int64_t, int64_t, int64_t>, std::pair<int64_t, int64_t>> actual;
+        // the engine's words of one accumulator tuple / row: COUNT(*), each aggregate (NULL: its identity), counters
+        auto words = [&](std::vector<int64_t>& v) {
+            v.push_back((int64_t)f[0]);
+            for (int j = 0; j < na; ++j)
+                v.push_back((int64_t)(fnull[1 + j] ? identity_word(c.aggs[j].kind) : field_to_acc(c.aggs[j].kind, f[1 + j])));
+            for (int h = 0; h < nh; ++h) v.push_back((int64_t)f[1 + na + h]);
+        };
         while (in.ok && in.at < in.n) {
             const int64_t kg = in.i32();
             if (!in.ok || kg < 0 || kg >= maxp) return fwa_set_error(e, FWA_E_ARG, "heap body: bad key group id");
             lo = std::min(lo, kg); hi = std::max(hi, kg);
-            for (int st = 0; st < ns; ++st) {
-                const int64_t id = (int16_t)in.get(2), cnt = in.i32();
-                if (!in.ok || id < 0 || id >= ns || cnt < 0) return fwa_set_error(e, FWA_E_ARG, "heap body: bad state section");
+            for (int st = 0; st < id.n; ++st) {
+                const int64_t sid = (int16_t)in.get(2), cnt = in.i32();
+                if (!in.ok || sid < 0 || sid >= id.n || cnt < 0) return fwa_set_error(e, FWA_E_ARG, "heap body: bad state section");
                 for (int64_t i = 0; i < cnt && in.ok; ++i) {
-                    if (id == ns - 1) {                                // timers: re-derived from the window state
+                    if (sid == id.proc || sid == id.event) {           // timers: re-derived from the window state
                         in.i64();
                         if (ds) { in.i64(); in.i64(); in.i64(); } else { uint64_t k; in.row(&k, 1); in.i64(); }
                         continue;
                     }
-                    if (id == 1) {                                     // merging-window-set: (actual, state) pairs
+                    if (sid == id.mset) {                              // merging-window-set: (actual, state) pairs
                         in.get(1);                                     // MergingWindowSet(...) :83-87
                         const int64_t key = in.i64(), m = in.i32();
                         for (int64_t q = 0; q < m && in.ok; ++q) {
@@ -343,24 +415,27 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
                         continue;
                     }
                     int64_t key, start, end;
+                    for (int k = 0; k < arity; ++k) fnull[k] = false;
                     if (ds) { start = in.i64(); end = in.i64(); key = in.i64(); for (int k = 0; k < arity; ++k) f[k] = (uint64_t)in.i64(); }
                     else {
                         end = in.i64();
                         uint64_t kf;
                         in.row(&kf, 1);
                         key = (int64_t)kf;
-                        in.row(f.data(), arity);
+                        in.row(f.data(), arity, fnull);
+                        if (fnull[0]) in.ok = false;                   // COUNT(*) is never NULL
                         start = end - g;
                     }
                     if (sess) {                                        // resolved against the mapping below
-                        pend.push_back({kg, key, start, end, std::vector<uint64_t>(f)});
+                        Pending p{kg, key, start, end, {}};
+                        words(p.w);
+                        pend.push_back(std::move(p));
                         continue;
                     }
                     std::vector<int64_t>& v = per[(size_t)kg];
                     v.push_back(key);
                     v.push_back(start);
-                    v.push_back((int64_t)f[0]);
-                    for (int j = 0; j < na; ++j) v.push_back((int64_t)field_to_acc(c.aggs[j].kind, f[1 + j]));
+                    words(v);
                     ++total;
                 }
             }
@@ -373,15 +448,14 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
                 std::vector<int64_t>& v = per[(size_t)p.kg];
                 v.push_back(p.key);
                 v.push_back(st);
-                v.push_back((int64_t)p.f[0]);
-                for (int j = 0; j < na; ++j) v.push_back((int64_t)field_to_acc(c.aggs[j].kind, p.f[1 + j]));
+                v.insert(v.end(), p.w.begin(), p.w.end());
                 v.push_back(en);
                 ++total;
             }
             pend.clear();
             actual.clear();
         }
-        if (!in.ok) return fwa_set_error(e, FWA_E_ARG, "heap body: truncated");
+        if (!in.ok) return fwa_set_error(e, FWA_E_ARG, "heap body: truncated or malformed");
         // the equivalent FWASNAP1 blob (engine.hip snap_header layout)
         std::vector<int64_t>& w = blobs[(size_t)b];
         w.assign((size_t)(kHdr + maxp + 1 + total * ncols), 0);
@@ -390,6 +464,8 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
         w[10] = c.key_kind; w[11] = na;
         for (int j = 0; j < na; ++j) w[12 + j] = c.aggs[j].kind;
         w[20] = watermarks[b]; w[21] = total; w[22] = hi >= 0 ? lo : 0; w[23] = hi >= 0 ? hi : maxp - 1;
+        w[24] = c.nullable_cols; w[25] = nh;
+        for (int j = 0; j < na; ++j) w[26] |= (int64_t)(c.aggs[j].col & 15) << (4 * j);
         int64_t* koff = w.data() + kHdr;
         int64_t* body = koff + maxp + 1;
         int64_t d = 0;

@@ -164,7 +164,9 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
         p = self.local.drain_partials(wm)
         # a COUNT(*) aggregate's accumulator repeats the row count: it is not shipped (rebuilt on arrival)
         ship = [j for j, name in enumerate(self.names) if name != "COUNT"]
-        cols = [p["key"], p["slice_start"], p["count"]] + [p["acc%d" % j] for j in ship]
+        nh = sum(1 for f in p if f.startswith("hidden"))  # SQL NULLs: the hidden non-NULL counters travel too
+        cols = [p["key"], p["slice_start"], p["count"]] + [p["acc%d" % j] for j in ship] + \
+            [p["hidden%d" % h] for h in range(nh)]
         cols = [c if isinstance(c, torch.Tensor) else torch.from_numpy(c) for c in cols]
         packed, counts = route_rows(self, cols[0], cols)    # done with the drained buffers from here on
         if then_push is not None:
@@ -185,7 +187,7 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
             else:
                 accs.append(col[k])
                 k += 1
-        self.engine.push_partials(col[0], col[1], col[2], accs)
+        self.engine.push_partials(col[0], col[1], col[2], accs, hidden=col[k:k + nh])
         if device_output:
             return self.engine.advance_watermark_device(wm)
         return self.engine.advance_watermark(wm)

@@ -224,18 +224,24 @@ class WindowAggregator:
         res = {"key": conv(out.key, n, i8), "slice_start": conv(out.slice_start, n, i8), "count": conv(out.count, n, i8)}
         for j in range(out.num_aggs):
             res["acc%d" % j] = conv(out.acc[j], n, i8)
+        for h in range(out.num_hidden):                # nullable handles: hidden non-NULL counters
+            res["hidden%d" % h] = conv(out.hidden[h], n, i8)
         return res
 
-    def push_partials(self, keys, slice_ts, count, accs):
+    def push_partials(self, keys, slice_ts, count, accs, hidden=()):
         """Merge partial accumulators (from drain_partials on a handle with the same window / aggregate
-        configuration) into this handle's state; returns the number of late records dropped."""
+        configuration) into this handle's state; returns the number of late records dropped. `hidden`: the
+        hidden non-NULL counter columns of a nullable handle (drain_partials' hidden<h>)."""
         device = _is_torch_cuda(keys)
         if not device:
             keys = np.ascontiguousarray(keys, np.int64)
             slice_ts = np.ascontiguousarray(slice_ts, np.int64)
             count = np.ascontiguousarray(count, np.int64)
             accs = [np.ascontiguousarray(a).view(np.int64) for a in accs]
-        arr = (C.c_void_p * A.FWA_MAX_AGGS)(*([_ptr(a).value for a in accs] + [None] * (A.FWA_MAX_AGGS - len(accs))))
+            hidden = [np.ascontiguousarray(a, np.int64) for a in hidden]
+        nslot = A.FWA_MAX_AGGS + A.FWA_MAX_COLS
+        ptrs = [_ptr(a).value for a in accs] + [None] * (self.cfg.num_aggs - len(accs)) + [_ptr(a).value for a in hidden]
+        arr = (C.c_void_p * nslot)(*(ptrs + [None] * (nslot - len(ptrs))))
         if device:
             self._order_after_producer(keys)
         dropped = C.c_int64(0)

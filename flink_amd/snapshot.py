@@ -17,9 +17,9 @@ def parse(blob):
     w = np.frombuffer(bytes(blob), dtype="<i8")
     if w.size < HDR_WORDS or int(w[0]) & 0xFFFFFFFFFFFFFFFF != MAGIC or int(w[1]) != 1:
         raise ValueError("not a flink_amd snapshot")
-    maxp, naggs, n = int(w[9]), int(w[11]), int(w[21])
+    maxp, naggs, n, nh = int(w[9]), int(w[11]), int(w[21]), int(w[25])
     session = int(w[2]) == 3                     # SESSION: a 4th leading column holds the session end (last)
-    ncols = (4 if session else 3) + naggs
+    ncols = (4 if session else 3) + naggs + nh   # nullable handles: nh hidden non-NULL counters after the acc_j
     need = HDR_WORDS + maxp + 1 + n * ncols
     if w.size != need:
         raise ValueError("snapshot size %d words != %d" % (w.size, need))
@@ -32,9 +32,10 @@ def parse(blob):
         "watermark": int(w[20]), "n": n, "kg_range": (int(w[22]), int(w[23])),
         "kg_offsets": off.copy(), "key": body[0].copy(), "slice_start": body[1].copy(),
         "count": body[2].copy(), "acc": [body[3 + j].copy() for j in range(naggs)],
+        "nullable_cols": int(w[24]), "hidden": [body[3 + naggs + h].copy() for h in range(nh)],
     }
     if session:
-        out["window_end"] = body[3 + naggs].copy()   # slice_start holds the session start
+        out["window_end"] = body[3 + naggs + nh].copy()   # slice_start holds the session start
     return out
 
 

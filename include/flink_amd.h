@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FWA_ABI_VERSION 2
+#define FWA_ABI_VERSION 3
 #define FWA_MAX_AGGS 8
 #define FWA_MAX_COLS 8
 
@@ -260,7 +260,13 @@ typedef struct fwa_partials {
     const int64_t* slice_start;  /* start timestamp of the (key, slice) accumulator */
     const int64_t* count;        /* COUNT(*) of the records it holds */
     const void* acc[FWA_MAX_AGGS]; /* 8-byte accumulator of agg j: i64 sum, f64 sum bits, or the engine's
-                                      order-preserving MIN/MAX key; COUNT aggregates repeat count */
+                                      order-preserving MIN/MAX key (the accumulator's identity when the
+                                      aggregate saw no non-NULL input); COUNT aggregates repeat count */
+    int32_t num_hidden;          /* handles with nullable_cols: hidden non-NULL counters (one per nullable
+                                    input column an aggregate reads, in first-use order), else 0 */
+    int32_t pad;
+    const int64_t* hidden[FWA_MAX_COLS]; /* the non-NULL input count of each hidden counter (AvgAggFunction's
+                                            count, the null flag of Sum/Min/MaxAggFunction's buffer) */
 } fwa_partials;
 
 /* Local pre-aggregator watermark step (LocalSlicingWindowAggOperator: flush the buffer, forward the
@@ -273,7 +279,10 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out);
 
 /* Merge partial accumulators (as produced by fwa_drain_partials on another handle with the same
  * window and aggregate configuration) into this handle's state. slice_ts may be any timestamp inside
- * the slice. Late partials are dropped like records (their counts are added to late_dropped_out). */
+ * the slice. Late partials are dropped like records (their counts are added to late_dropped_out).
+ * acc holds one column per aggregate; a handle with nullable_cols reads fwa_partials.num_hidden more
+ * entries after them, acc[num_aggs + h] = hidden[h] (GlobalAggCombiner merges the nullable buffers,
+ * GlobalAggCombiner.java:77-110). */
 int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_ts, const int64_t* count,
                       const void* const* acc, int64_t n, int32_t flags, int64_t* late_dropped_out);
 
@@ -285,7 +294,8 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
  * (little-endian int64 words): a header (magic "FWASNAP1", window/aggregate configuration,
  * watermark, entry count), a key-group offset table off[max_parallelism + 1] (entries of key group g
  * are [off[g], off[g+1])), then SoA columns key[n], slice_start[n], count[n], acc_j[n] (one per
- * aggregate, same encoding as fwa_partials). Per-key timers are not stored: the engine's timers are
+ * aggregate, same encoding as fwa_partials), then for a handle with nullable_cols one hidden[h][n]
+ * column per hidden non-NULL counter (header word 25 = their number, word 24 = nullable_cols). Per-key timers are not stored: the engine's timers are
  * derived from the live slices and the watermark, as the reference re-registers them from state.
  * SESSION windows: the entries are the in-flight sessions (the MergingWindowSet mapping + window state,
  * WindowOperator.java:224-238) with slice_start = session start and one more column end[n] after the
@@ -306,24 +316,32 @@ void fwa_blob_free(fwa_blob* b);
 int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, int32_t n_blobs);
 
 /* The same keyed state in the byte layout of Flink's heap keyed-state backend (HeapSnapshotStrategy.java:154-175):
- * for each owned key group g = kg_start..kg_end, in order: int g; short 0 (window state), int n, n x (namespace,
- * key, accumulator) (CopyOnWriteStateMapSnapshot.writeState :138-148); [sessions: short 1 (merging-window-set),
- * int k, k x (byte 0 VoidNamespace, key, int size, size x (TimeWindow actual, TimeWindow state)) (ListSerializer)];
- * then the event-time timers: short id, int m, m x (long flipSignBit(ts), key, namespace) (TimerSerializer.serialize
- * :147-152). Big-endian java.io.DataOutput.
- *   DATASTREAM TUMBLE / SESSION (WindowOperator): namespace TimeWindow (long start, long end), key Long, accumulator a
- *     Tuple of Long COUNT(*) then one field per aggregate (Long for COUNT / BIGINT SUM / AVG / MIN / MAX, Double for
- *     floating SUM / AVG / MIN / MAX), timers at window.maxTimestamp() and, with allowed lateness, at the cleanup
- *     time. Each in-flight session is written as its own state window (an equivalent MergingWindowSet mapping).
- *   TABLE TUMBLE / HOP / CUMULATE (SlicingWindowOperator): namespace Long slice end, key BinaryRowData(BIGINT),
- *     accumulator a BinaryRowData of the same fields (BinaryRowDataSerializer); a CUMULATE window's fired slices are
- *     folded into its first slice (the shared state SliceSharedWindowAggProcessor keeps); one timer per (key, first
- *     unfired window end of each live slice) at window end - 1.
+ * for each owned key group g = kg_start..kg_end, in order: int g, then one section per state the reference operator
+ * registers -- short state id, int n, n entries -- with the ids a heap backend gives them (HeapSnapshotResources
+ * .java:100-139: key/value states, then the timer queues, each in java.util.HashMap order of the names; pinned by the
+ * reference's own snapshots, tests/test_heap_reference_cpu.py):
+ *   DATASTREAM TUMBLE  (WindowOperator): 0 "window-contents", 1 "_timer_state/processing_window-timers" (empty),
+ *                      2 "_timer_state/event_window-timers"
+ *   DATASTREAM SESSION (WindowOperator): 0 "window-contents", 1 "merging-window-set", 2 processing timers (empty),
+ *                      3 event timers
+ *   TABLE TUMBLE / HOP / CUMULATE (SlicingWindowOperator): 0 "window-aggs", 1 processing timers (empty), 2 event timers
+ * Key/value entries are (namespace, key, value) (CopyOnWriteStateMapSnapshot.writeState :138-148), timer entries
+ * (long flipSignBit(ts), key, namespace) (TimerSerializer.serialize :147-152); big-endian java.io.DataOutput.
+ *   DataStream: namespace TimeWindow (long start, long end), key Long, value a Tuple of Long COUNT(*) then one field
+ *     per aggregate (Long for COUNT / BIGINT SUM / AVG / MIN / MAX, Double for floating SUM / AVG / MIN / MAX). Timers:
+ *     window.maxTimestamp() while the window has not fired (EventTimeTrigger) and the cleanup time maxTimestamp +
+ *     allowedLateness (WindowOperator.registerCleanupTimer :608-620). Sessions: the merging-window-set holds, per
+ *     key under VoidNamespace (one byte), the List of (actual, state) TimeWindow pairs; each in-flight session is
+ *     written as its own state window.
+ *   Table: namespace Long slice end (local time under a shift time zone), key BinaryRowData(BIGINT), value a
+ *     BinaryRowData of COUNT(*), one field per aggregate (NULL bit set when the aggregate saw only NULLs) and one
+ *     BIGINT per hidden non-NULL counter of a nullable handle; a CUMULATE window's fired slices are folded into its
+ *     first slice (the shared state SliceSharedWindowAggProcessor keeps); one timer per (key, first unfired window
+ *     end of each live slice) at toEpochMillsForTimer(window end - 1) (UTC: window end - 1).
  * kg_offsets[g - kg_start] receives the byte offset of key group g's section (KeyGroupRangeOffsets; the Java shim
  * writes its KeyedBackendSerializationProxy header in front and shifts them), *watermark the operator watermark
- * (union list state, SlicingWindowOperator.java:204-209). DataStream SLIDE / CUMULATE, Table SESSION, a shift time
- * zone, nullable columns or PREHASHED keys: FWA_E_UNSUPPORTED (fwa_snapshot covers them). The blob is freed with
- * fwa_blob_free. */
+ * (union list state, SlicingWindowOperator.java:204-209). DataStream SLIDE / CUMULATE, Table SESSION or PREHASHED
+ * keys: FWA_E_UNSUPPORTED (fwa_snapshot covers them). The blob is freed with fwa_blob_free. */
 int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark);
 
 /* Restore a fresh handle from heap-layout bodies (as written by fwa_snapshot_heap on handles with the same window

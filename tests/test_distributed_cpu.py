@@ -76,7 +76,7 @@ class _OracleFromPartials:
         from oracle.oracle import Oracle
         self.o = Oracle(cfg)
 
-    def push_partials(self, keys, slice_ts, count, accs):
+    def push_partials(self, keys, slice_ts, count, accs, hidden=()):
         rep = np.repeat(np.arange(len(keys)), count)
         first = np.r_[True, rep[1:] != rep[:-1]] if len(rep) else np.zeros(0, bool)
         vals = np.where(first, np.asarray(accs[1])[rep], 0).astype(np.int64)

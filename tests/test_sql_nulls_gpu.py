@@ -124,3 +124,91 @@ def test_nullable_requires_table_semantics(eng_mod):
     cfg = A.make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=1000, aggs=AGGS, nullable_cols=(0,))
     with pytest.raises(eng_mod.EngineError):
         eng_mod.WindowAggregator(cfg)
+
+
+def _batches(stream, nb, delay):
+    keys, ts, cols, nulls = stream
+    n, mx = len(keys), -2**63
+    for b in range(nb + 1):
+        sl = slice(b * n // nb, (b + 1) * n // nb) if b < nb else slice(0, 0)
+        if b < nb:
+            mx = max(mx, int(ts[sl].max()))
+        yield keys[sl], ts[sl], [x[sl] for x in cols], [x[sl] for x in nulls], (mx - delay - 1 if b < nb else A.LONG_MAX)
+
+
+@pytest.mark.parametrize("ci", [0, 2, 3], ids=["TUMBLE", "SLIDE", "CUMULATE"])
+@pytest.mark.parametrize("aggs", [AGGS, AGGS_F], ids=["int", "float"])
+def test_nullable_two_phase_partials_vs_oracle(eng_mod, ci, aggs):
+    """Two-phase plan over nullable columns (LocalSlicingWindowAggOperator -> GlobalAggCombiner, whose nullable
+    buffers merge with their NULL flags, GlobalAggCombiner.java:77-110): two local handles drain (key, slice)
+    partials with the hidden non-NULL counters (fwa_partials.hidden), the owner merges them and fires. Rows, NULL
+    flags and late drops equal one operator over the union of the streams."""
+    from oracle.oracle import Oracle
+    cfg = A.make_config(semantics="TABLE", aggs=aggs, key_capacity=2048, nullable_cols=(0, 1, 2), **CONFIGS[ci])
+    names = A.agg_names(cfg)
+    loc = [eng_mod.WindowAggregator(cfg) for _ in range(2)]
+    glob, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
+    dg = do = 0
+    for k, t, c, z, wm in _batches(_stream(400 + ci, 30_000, 400, 50_000, 1200, 0.25), 8, 1200):
+        do += o.push(k, t, c, nulls=z)
+        for s in range(2):
+            sl = slice(s, None, 2)
+            dg += loc[s].push(k[sl], t[sl], [x[sl] for x in c], nulls=[x[sl] for x in z])
+        for s in range(2):
+            p = loc[s].drain_partials(wm)
+            nh = sum(1 for f in p if f.startswith("hidden"))
+            assert nh == len({col for kind, col in aggs if kind != "COUNT"})
+            dg += glob.push_partials(p["key"], p["slice_start"], p["count"], [p["acc%d" % j] for j in range(len(names))],
+                                     hidden=[p["hidden%d" % h] for h in range(nh)])
+        assert_rows_equal(glob.advance_watermark(wm), o.advance_watermark(wm), names,
+                          rtol=lambda nm: TOL.get(nm, 0.0), ctx="wm=%d" % wm)
+    assert dg == do and do > 0
+    for x in loc + [glob]:
+        x.close()
+    o.close()
+
+
+@pytest.mark.parametrize("ci", range(len(CONFIGS)), ids=[c["window_kind"] + str(i) for i, c in enumerate(CONFIGS)])
+def test_nullable_snapshot_restore_with_rescale(eng_mod, ci):
+    """Checkpoint / restore of nullable handles (FWASNAP1 carries the hidden non-NULL counters after the
+    accumulator columns): two subtasks checkpoint mid-stream, one subtask (scale-in) and then two with a new split
+    restore, and the resumed rows -- NULL flags included -- equal the oracle's uninterrupted run."""
+    from flink_amd import snapshot as S
+    from oracle.oracle import Oracle
+    cfg_kw = dict(semantics="TABLE", aggs=AGGS_F if ci % 2 else AGGS, key_capacity=2048, nullable_cols=(0, 1, 2),
+                  **CONFIGS[ci])
+    cfg = A.make_config(**cfg_kw)
+    names = A.agg_names(cfg)
+    keys, ts, cols, nulls = _stream(500 + ci, 30_000, 400, 50_000, 1000, 0.25)
+    kgs, _ = eng_mod.key_groups(keys, 128, 1, cfg.key_kind)
+    cut = 15_000
+    wm1 = int(ts[:cut].max()) - 1001
+    o = Oracle(cfg)
+    o.push(keys[:cut], ts[:cut], [c[:cut] for c in cols], nulls=[z[:cut] for z in nulls])
+    first = o.advance_watermark(wm1)
+    o.push(keys[cut:], ts[cut:], [c[cut:] for c in cols], nulls=[z[cut:] for z in nulls])
+    final = o.advance_watermark(A.LONG_MAX)
+    blobs, got1 = [], []
+    for lo, hi in ((0, 63), (64, 127)):
+        m = (kgs[:cut] >= lo) & (kgs[:cut] <= hi)
+        g = eng_mod.WindowAggregator(A.make_config(kg_start=lo, kg_end=hi, **cfg_kw))
+        g.push(keys[:cut][m], ts[:cut][m], [c[:cut][m] for c in cols], nulls=[z[:cut][m] for z in nulls])
+        got1.append(g.advance_watermark(wm1))
+        b = g.snapshot()
+        assert S.parse(b)["watermark"] == wm1
+        blobs.append(b)
+        g.close()
+    assert_rows_equal({f: np.concatenate([r[f] for r in got1]) for f in got1[0]}, first, names,
+                      rtol=lambda nm: TOL.get(nm, 0.0))
+    for layout in ([(0, 127)], [(0, 31), (32, 127)]):
+        outs = []
+        for lo, hi in layout:
+            g = eng_mod.WindowAggregator(A.make_config(kg_start=lo, kg_end=hi, **cfg_kw))
+            g.restore(blobs)
+            m = (kgs[cut:] >= lo) & (kgs[cut:] <= hi)
+            g.push(keys[cut:][m], ts[cut:][m], [c[cut:][m] for c in cols], nulls=[z[cut:][m] for z in nulls])
+            outs.append(g.advance_watermark(A.LONG_MAX))
+            g.close()
+        assert_rows_equal({f: np.concatenate([r[f] for r in outs]) for f in outs[0]}, final, names,
+                          rtol=lambda nm: TOL.get(nm, 0.0))
+    o.close()
