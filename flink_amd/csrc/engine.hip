@@ -2337,6 +2337,12 @@ __global__ void reset_slots_kernel(unsigned long long* const* slot_base, const i
     if (blockIdx.x == 0 && threadIdx.x == 0) touched[slot] = 0;
 }
 
+__global__ void to_local_kernel(const int64_t* ts, int64_t* out, int64_t n, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = assign_ts(c, ts[i]);   // TR WindowOperator.processElement :340 toUtcTimestampMills
+}
+
 __global__ void fill_u64_kernel(unsigned long long* p, unsigned long long v, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -2461,6 +2467,8 @@ struct fwa_engine {
     void* o_agg[FWA_MAX_AGGS] = {};
     uint8_t* o_null[FWA_MAX_AGGS] = {};   // SQL NULL flags of the nullable aggregates' output columns
     int64_t* o_hid[FWA_MAX_COLS] = {};    // raw exports of a nullable handle: hidden non-NULL counters
+    int64_t* d_lts = nullptr;             // Table sessions under a shift time zone: the push's local timestamps
+    int64_t lts_cap = 0;
     std::vector<char> h_out;
     FireWindow* d_win = nullptr;
     int32_t win_cap = 0;
@@ -2611,7 +2619,6 @@ int validate(const fwa_config* c) {
     if (c->tz_n < 0 || (c->tz_n > 0 && !c->tz)) return FWA_E_ARG;
     if (c->tz_n > 0) {                       // TIMESTAMP_LTZ rowtime: Table slicing windows only
         if (c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;
-        if (c->window_kind == FWA_SESSION) return FWA_E_UNSUPPORTED;
         for (int32_t i = 1; i < c->tz_n; ++i) if (c->tz[2 * i] <= c->tz[2 * (i - 1)]) return FWA_E_ARG;
     }
     if (c->semantics != FWA_SEM_DATASTREAM && c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;
@@ -2631,6 +2638,25 @@ int64_t slice_start(const fwa_engine* e, int64_t q) { return jm::wadd(e->off, (i
 // toEpochMillsForTimer / isWindowFired :162-183); identity without a shift time zone.
 int64_t trig(const fwa_engine* e, int64_t max_ts) {
     return e->tz.empty() ? max_ts : jm::tz_timer(e->tz.data(), (int)(e->tz.size() / 2), max_ts);
+}
+
+// Table sessions under a shift time zone: every instant the operator compares with the watermark is
+// toEpochMillsForTimer(local) (InternalWindowProcessFunction.isWindowLate :119-123, MergingWindowProcessFunction
+// :137-141, EventTimeTriggers.AfterEndOfWindow), a non-decreasing function of the local time. So trig(x) <= wm
+// <=> x <= local_wm(wm) = the largest local time whose timer instant is <= wm, and the session kernels compare
+// local window times with that local watermark unchanged.
+int64_t local_wm(const fwa_engine* e, int64_t wm) {
+    if (e->tz.empty() || wm == LONG_MAX_J || wm == LONG_MIN_J) return wm;
+    const int64_t kLim = (int64_t)1 << 62;                  // past the zone table: a fixed offset
+    const int64_t thi = trig(e, kLim), tlo = trig(e, -kLim);
+    if (thi <= wm) return jm::wadd(kLim, jm::wsub(wm, thi));
+    if (tlo > wm) return jm::wsub(-kLim, jm::wsub(tlo, wm));
+    int64_t lo = -kLim, hi = kLim;                          // trig(lo) <= wm < trig(hi)
+    while (hi - lo > 1) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (trig(e, mid) <= wm) lo = mid; else hi = mid;
+    }
+    return lo;
 }
 
 int64_t slice_q(const fwa_engine* e, int64_t t) {  // slice number of a timestamp / slice start
@@ -2934,6 +2960,7 @@ void fwa_destroy(fwa_engine* e) {
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_agg[j]) (void)hipFree(e->o_agg[j]);
     for (int j = 0; j < FWA_MAX_AGGS; ++j) if (e->o_null[j]) (void)hipFree(e->o_null[j]);
     for (int h = 0; h < FWA_MAX_COLS; ++h) if (e->o_hid[h]) (void)hipFree(e->o_hid[h]);
+    if (e->d_lts) (void)hipFree(e->d_lts);
     for (void* p : e->chunks) (void)hipFree(p);
     if (e->h_st) (void)hipHostFree(e->h_st);
     if (e->h_arena) (void)hipHostFree(e->h_arena);
@@ -3555,11 +3582,22 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     memset(&s, 0, sizeof(s));
     s.keys = a.keys;
     s.ts = a.ts;
+    if (!e->tz.empty() && n > 0) {                        // Table GROUP BY SESSION over a TIMESTAMP_LTZ rowtime:
+        if (n > e->lts_cap) {                             // sessions are formed on local wall-clock time
+            if (e->d_lts) HIPCHK(e, hipFree(e->d_lts));
+            e->d_lts = nullptr;
+            HIPCHK(e, hipMalloc(&e->d_lts, 8 * (size_t)n));
+            e->lts_cap = n;
+        }
+        to_local_kernel<<<grid_for(n), kBlock, 0, e->stream>>>(a.ts, e->d_lts, n, e->d_ec);
+        HIPCHK(e, hipGetLastError());
+        s.ts = e->d_lts;
+    }
     for (int c = 0; c < FWA_MAX_COLS; ++c) s.cols[c] = a.cols[c];
     s.key_hash = a.key_hash;
     s.gapc = (e->cfg.flags & FWA_CFG_DYNAMIC_GAP) ? (const int64_t*)a.cols[e->cfg.gap_col] : nullptr;
     s.n = n;
-    s.wm = e->wm;
+    s.wm = local_wm(e, e->wm);
     s.gap = e->cfg.gap_ms;
     s.lateness = e->lateness;
     s.key_table = e->d_keys;
@@ -3712,8 +3750,8 @@ static int fire_sessions(fwa_engine* e, int64_t wm, int64_t* nrows) {
     f.in = e->ss[e->ss_cur];
     f.out = e->ss[e->ss_cur ^ 1];
     f.n_in = n_in;
-    f.prev_wm = e->wm;
-    f.wm = wm;
+    f.prev_wm = local_wm(e, e->wm);
+    f.wm = local_wm(e, wm);
     f.lateness = e->lateness;
     f.key_table = e->d_keys;
     f.capacity = e->capacity;

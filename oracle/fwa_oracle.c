@@ -448,7 +448,7 @@ int or_create(const fwa_config* c, or_engine** out) {
     if (c->window_kind == FWA_CUMULATE && (c->semantics != FWA_SEM_TABLE || c->size_ms <= 0 || c->slide_ms <= 0 || c->size_ms % c->slide_ms)) return FWA_E_ARG;
     if (c->window_kind == FWA_SESSION && c->gap_ms <= 0 && !(c->flags & FWA_CFG_DYNAMIC_GAP)) return FWA_E_ARG;
     if (c->semantics == FWA_SEM_TABLE && c->allowed_lateness_ms != 0) return FWA_E_ARG;
-    if (c->tz_n < 0 || (c->tz_n > 0 && (!c->tz || c->semantics != FWA_SEM_TABLE || c->window_kind == FWA_SESSION))) return FWA_E_ARG;
+    if (c->tz_n < 0 || (c->tz_n > 0 && (!c->tz || c->semantics != FWA_SEM_TABLE))) return FWA_E_ARG;
     or_engine* e = (or_engine*)calloc(1, sizeof(or_engine));
     e->c = *c;
     if (c->tz_n > 0) {                                 /* own copy of the shift-time-zone table */
@@ -552,12 +552,20 @@ static void wl_put(or_engine* e, int64_t key, int64_t ws, int64_t we, int64_t sw
 typedef struct { int64_t s, e; } tw;
 static int tw_cmp(const void* a, const void* b) { const tw* x = (const tw*)a; const tw* y = (const tw*)b; return x->s < y->s ? -1 : x->s > y->s; }
 
+/* Table GROUP BY SESSION over a TIMESTAMP_LTZ rowtime: windows are formed on the local wall-clock timestamp
+ * (TR WindowOperator.processElement :340 toUtcTimestampMills) and every event-time instant the operator compares with
+ * the watermark or registers as a timer is toEpochMillsForTimer of it (InternalWindowProcessFunction.isWindowLate
+ * :119-123, MergingWindowProcessFunction :137-141, EventTimeTriggers.AfterEndOfWindow, registerCleanupTimer :422-429).
+ * UTC / DataStream: the instant itself. */
+static int64_t ev_time(or_engine* e, int64_t local) { return e->c.tz_n ? or_tz_timer(&e->c, local) : local; }
+
 /* MergingWindowSet.addWindow :153-236 + TimeWindow.mergeWindows :208-254 + the MergeFunction of
  * WindowOperator.processElement :292-349, then the per-window body :352-386. */
 static int ds_process_element_session(or_engine* e, int64_t key, int64_t ts, const void* const* cols, int64_t i, int* skipped) {
     /* EventTimeSessionWindows.assignWindows :61-63; DynamicEventTimeSessionWindows.assignWindows :57-68 */
     const int64_t gap = (e->c.flags & FWA_CFG_DYNAMIC_GAP) ? ((const int64_t*)cols[e->c.gap_col])[i] : e->c.gap_ms;
     if (gap <= 0) return set_err(e, FWA_E_ARG, "Dynamic session time gap must satisfy 0 < gap");
+    if (e->c.tz_n) ts = or_to_local(&e->c, ts);
     const int64_t nws = ts, nwe = jladd(ts, gap);
     int64_t cnt = 0;
     for (int64_t j = *wl_headp(e, key); j >= 0; j = e->wl_next[j]) cnt++;
@@ -601,19 +609,19 @@ static int ds_process_element_session(or_engine* e, int64_t key, int64_t ts, con
             self_only = self_only && nrem == 1;
             if (!self_only) {
                 /* MergeFunction.merge: lateness check, onMerge, clear merged triggers, mergeNamespaces */
-                if (jladd(jlsub(ce, 1), e->c.allowed_lateness_ms) <= e->wm) {
+                if (jladd(ev_time(e, jlsub(ce, 1)), e->c.allowed_lateness_ms) <= e->wm) {
                     free(ws);
                     return set_err(e, FWA_E_MERGE_LATE, "The end timestamp of an event-time window cannot become earlier than the current watermark by merging.");
                 }
-                if (jlsub(ce, 1) > e->wm) th_add(&e->timers, jlsub(ce, 1), key, cs, ce);   /* EventTimeTrigger.onMerge */
+                if (ev_time(e, jlsub(ce, 1)) > e->wm) th_add(&e->timers, ev_time(e, jlsub(ce, 1)), key, cs, ce);   /* EventTimeTrigger.onMerge */
             }
             for (int64_t q = g0; q < g1; q++) {
                 int64_t a, b;
                 if (!wl_get_state_window(e, key, ws[q].s, ws[q].e, &a, &b)) continue;       /* the new window */
                 if (!self_only) {
-                    th_del(&e->timers, jlsub(ws[q].e, 1), key, ws[q].s, ws[q].e);         /* trigger.clear */
+                    th_del(&e->timers, ev_time(e, jlsub(ws[q].e, 1)), key, ws[q].s, ws[q].e);   /* trigger.clear */
                     int64_t ct = cleanup_time(e, ws[q].s, ws[q].e);                       /* deleteCleanupTimer */
-                    if (ct != J_LONG_MAX) th_del(&e->timers, ct, key, ws[q].s, ws[q].e);
+                    if (ct != J_LONG_MAX) th_del(&e->timers, ev_time(e, ct), key, ws[q].s, ws[q].e);
                     if (!(a == sws && b == swe)) {
                         aval* src = ds_state(e, key, a, b, 0);
                         if (src) { aval* dst = ds_state(e, key, sws, swe, 1); src = ds_state(e, key, a, b, 0); acc_merge(e, dst, src); ds_clear_state(e, key, a, b); }
@@ -627,17 +635,17 @@ static int ds_process_element_session(or_engine* e, int64_t key, int64_t ts, con
     }
     free(ws);
     if (!any_merge || (res_s == nws && res_e == nwe && !merged_new)) wl_put(e, key, nws, nwe, nws, nwe);
-    if (cleanup_time(e, res_s, res_e) <= e->wm) { wl_remove(e, key, res_s, res_e); return FWA_OK; }   /* retireWindow */
+    if (ev_time(e, cleanup_time(e, res_s, res_e)) <= e->wm) { wl_remove(e, key, res_s, res_e); return FWA_OK; }   /* retireWindow */
     *skipped = 0;
     int64_t sws, swe;
     if (!wl_get_state_window(e, key, res_s, res_e, &sws, &swe)) return set_err(e, FWA_E_STATE, "Window is not in in-flight window set.");
     aval* a = ds_state(e, key, sws, swe, 1);
     acc_add(e, a, cols, i);
-    int64_t max_ts = jlsub(res_e, 1);
+    int64_t max_ts = ev_time(e, jlsub(res_e, 1));
     if (max_ts <= e->wm) emit(e, key, res_s, res_e, a);           /* EventTimeTrigger.onElement FIRE */
     else th_add(&e->timers, max_ts, key, res_s, res_e);
     int64_t ct = cleanup_time(e, res_s, res_e);
-    if (ct != J_LONG_MAX) th_add(&e->timers, ct, key, res_s, res_e);
+    if (ct != J_LONG_MAX) th_add(&e->timers, ev_time(e, ct), key, res_s, res_e);
     return FWA_OK;
 }
 
@@ -648,10 +656,10 @@ static void ds_on_event_time(or_engine* e, const timer_t_* t) {   /* WindowOpera
         if (!wl_get_state_window(e, key, ws, we, &sws, &swe)) return;
     }
     aval* a = ds_state(e, key, sws, swe, 0);
-    if (t->ts == jlsub(we, 1) && a) emit(e, key, ws, we, a);     /* EventTimeTrigger.onEventTime FIRE */
-    if (t->ts == cleanup_time(e, ws, we)) {                        /* clearAllState :537-548 */
+    if (t->ts == ev_time(e, jlsub(we, 1)) && a) emit(e, key, ws, we, a);   /* EventTimeTrigger.onEventTime FIRE */
+    if (t->ts == ev_time(e, cleanup_time(e, ws, we))) {            /* clearAllState :537-548 */
         ds_clear_state(e, key, sws, swe);
-        th_del(&e->timers, jlsub(we, 1), key, ws, we);
+        th_del(&e->timers, ev_time(e, jlsub(we, 1)), key, ws, we);
         if (e->c.window_kind == FWA_SESSION) wl_remove(e, key, ws, we);
     }
 }

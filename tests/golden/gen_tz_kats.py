@@ -153,14 +153,16 @@ def timer_cases():
 
 
 def shanghai_operator_kats(utc_kats):
-    """SlicingWindowAggOperatorTest is parameterised by shiftTimeZone (UTC, Asia/Shanghai): inputs are the same
-    epoch rowtimes and watermarks; expected window bounds are localMills(x) = toUtcTimestampMills(x, zone)
-    (SlicingWindowAggOperatorTest.java:116-222, 345-460, 596-692)."""
+    """SlicingWindowAggOperatorTest and the Table WindowOperatorTest (legacy GROUP BY SESSION) are parameterised by
+    shiftTimeZone (UTC, Asia/Shanghai): inputs are the same epoch rowtimes and watermarks; expected window bounds are
+    localMills(x) = toUtcTimestampMills(x, zone) (SlicingWindowAggOperatorTest.java:116-222, 345-460, 596-692;
+    table WindowOperatorTest.java:89-100 parameters, :1401-1514 testEventTimeSessionWindows, localMills :2066-2068)."""
     z = ZoneInfo("Asia/Shanghai")
     tz = transitions("Asia/Shanghai")
     out = []
     for c in utc_kats:
-        if not c["name"].startswith("SlicingWindowAggOperatorTest"):
+        if not (c["name"].startswith("SlicingWindowAggOperatorTest") or
+                c["name"].startswith("TableWindowOperatorTest.testEventTimeSessionWindows")):
             continue
         d = json.loads(json.dumps(c))
         d["name"] = c["name"].replace("(UTC)", "(Asia/Shanghai)")

@@ -484,6 +484,33 @@ def test_shift_time_zone_streams_vs_oracle(eng_mod, zone, kind, size, slide):
     run_pair(cfg, batches, eng_mod.WindowAggregator, Oracle, names)
 
 
+@pytest.mark.parametrize("zone", ["America/Los_Angeles", "Asia/Shanghai"])
+@pytest.mark.parametrize("gap", [300_000, 1_800_000])
+def test_shift_time_zone_sessions_vs_oracle(eng_mod, zone, gap):
+    """Table GROUP BY SESSION over a TIMESTAMP_LTZ rowtime (TR WindowOperator.processElement :340): sessions are
+    formed on local wall-clock time and every watermark comparison / timer is toEpochMillsForTimer of the local
+    instant (InternalWindowProcessFunction.isWindowLate :119-123, MergingWindowProcessFunction :137-141). Streams
+    cross the 2021 America/Los_Angeles DST changes (a 23 h and a 25 h day), with late records."""
+    from oracle.oracle import Oracle
+    tzk = {c["zone"]: c["tz"] for c in TZ_KATS["timer"]}
+    cfg = A.make_config(window_kind="SESSION", semantics="TABLE", gap_ms=gap, tz=tzk[zone],
+                        aggs=[("COUNT", 0), ("SUM_I64", 0), ("MAX_I64", 0)], key_capacity=2048)
+    names = A.agg_names(cfg)
+    rng = np.random.default_rng(29 + gap)
+    batches = []
+    for t0 in (1615593600000, 1636156800000):         # 2021-03-13 and 2021-11-06, 00:00 UTC
+        n = 20_000
+        base = t0 + np.sort(rng.integers(0, 2 * 86_400_000, n)).astype(np.int64)
+        ts = base - rng.integers(0, 900_000, n)
+        keys = rng.integers(0, 200, n).astype(np.int64)
+        vi = rng.integers(-1000, 1000, n).astype(np.int64)
+        for b in range(10):
+            sl = slice(b * n // 10, (b + 1) * n // 10)
+            batches.append((keys[sl], ts[sl], [vi[sl]], int(ts[sl].max()) - 600_001))
+    batches.append((batches[0][0][:0], batches[0][1][:0], [batches[0][2][0][:0]], A.LONG_MAX))
+    run_pair(cfg, batches, eng_mod.WindowAggregator, Oracle, names)
+
+
 @pytest.mark.parametrize("ci", range(len(CONFIGS)))
 def test_late_record_indices_vs_oracle(eng_mod, ci):
     """FWA_CFG_LATE_INDICES: per push, exactly the records the reference drops as late (the ones WindowOperator
