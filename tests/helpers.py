@@ -26,6 +26,34 @@ def load_kats():
         return json.load(f)
 
 
+def load_pyflink_kats():
+    """Operator sequences produced by the reference's own Python WindowOperator (tests/golden/gen_pyflink_kats.py)."""
+    with open(os.path.join(GOLDEN, "pyflink_kats.json")) as f:
+        return json.load(f)
+
+
+def load_session_kats():
+    """EventTimeSessionWindowsTest / TimeWindowTest vectors (tests/golden/gen_session_kats.py)."""
+    with open(os.path.join(GOLDEN, "session_kats.json")) as f:
+        return json.load(f)
+
+
+def assigner_windows_by_rows(case, make_engine):
+    """Window assignment seen through an engine: one record per timestamp (key = its index), fired at
+    Long.MAX_VALUE; returns {ts: [(start, end)]}."""
+    cfg = A.make_config(window_kind=case["kind"], size_ms=case["size"], slide_ms=case.get("slide", 0),
+                        offset_ms=case["offset"], gap_ms=case.get("gap", 0), aggs=[("COUNT", 0)])
+    eng = make_engine(cfg)
+    ts = np.array([c[0] for c in case["cases"]], np.int64)
+    eng.push(np.arange(len(ts), dtype=np.int64), ts, [])
+    rows = eng.advance_watermark((1 << 63) - 1)
+    eng.close()
+    got = {}
+    for i in range(len(rows["key"])):
+        got.setdefault(int(ts[rows["key"][i]]), []).append((int(rows["win_start"][i]), int(rows["win_end"][i])))
+    return {k: sorted(v) for k, v in got.items()}
+
+
 def load_tz_kats():
     """Shift-time-zone KATs (tests/golden/gen_tz_kats.py)."""
     with open(os.path.join(GOLDEN, "tz_kats.json")) as f:

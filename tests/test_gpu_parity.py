@@ -8,12 +8,14 @@ import numpy as np
 import pytest
 
 from flink_amd import _abi as A
-from helpers import assert_rows_equal, load_kats, load_tz_kats, replay_kat
+from helpers import assert_rows_equal, assigner_windows_by_rows, load_kats, load_pyflink_kats, load_session_kats, load_tz_kats, replay_kat
 
 pytestmark = pytest.mark.gpu
 
 KATS = load_kats()
 TZ_KATS = load_tz_kats()
+PY_KATS = load_pyflink_kats()
+SESSION_KATS = load_session_kats()
 
 # Relative tolerances per aggregate (absolute floor equal to the same number, values are O(1..1e3)).
 #  SUM_F32: reference accumulates in float32 sequentially: |err| <= n * 2^-24 * sum|x|; n <= ~2e3 here.
@@ -36,6 +38,35 @@ def eng_mod():
 @pytest.mark.parametrize("case", KATS["operators"], ids=lambda c: c["name"].split(" ")[0])
 def test_reference_kats_on_gpu(eng_mod, case):
     replay_kat(case, eng_mod.WindowAggregator)
+
+
+@pytest.mark.parametrize("case", PY_KATS["operators"], ids=lambda c: c["name"].split(" ", 1)[1])
+def test_pyflink_window_operator_sequences_on_gpu(eng_mod, case):
+    """Random tumbling / sliding / session / dynamic-gap streams with lateness and late records, expected rows
+    and drop counts produced by the reference's own Python WindowOperator (tests/golden/gen_pyflink_kats.py)."""
+    replay_kat(case, eng_mod.WindowAggregator)
+
+
+@pytest.mark.parametrize("case", SESSION_KATS["operators"], ids=lambda c: c["name"].split(" ")[0])
+def test_session_merge_kats_on_gpu(eng_mod, case):
+    """EventTimeSessionWindowsTest mergeWindows / TimeWindowTest.testIntersect as session sequences."""
+    replay_kat(case, eng_mod.WindowAggregator)
+
+
+@pytest.mark.parametrize("case", KATS["assigners"] + SESSION_KATS["assigners"], ids=lambda c: c["src"].split("/")[-1])
+def test_assigner_kats_on_gpu(eng_mod, case):
+    """Assigner / TimeWindowTest window starts as the windows the engine fires."""
+    got = assigner_windows_by_rows(case, eng_mod.WindowAggregator)
+    for ts, exp in case["cases"]:
+        assert got[ts] == sorted(tuple(w) for w in exp), (ts, got[ts], exp)
+
+
+@pytest.mark.parametrize("gap", SESSION_KATS["invalid_gaps"]["gaps"])
+def test_session_invalid_gap_on_gpu(eng_mod, gap):
+    """EventTimeSessionWindowsTest.testInvalidParameters: a gap <= 0 is rejected at create."""
+    with pytest.raises(eng_mod.EngineError) as ei:
+        eng_mod.WindowAggregator(A.make_config(window_kind="SESSION", gap_ms=gap, size_ms=0))
+    assert ei.value.code == -1
 
 
 @pytest.mark.parametrize("case", TZ_KATS["operators"], ids=lambda c: c["name"].split(" ")[0])

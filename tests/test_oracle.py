@@ -6,16 +6,18 @@ import pytest
 
 from flink_amd import _abi as A
 from oracle import oracle as O
-from helpers import load_kats, load_sql_kats, load_tz_kats, replay_kat, replay_sql_kat
+from helpers import load_kats, load_pyflink_kats, load_session_kats, load_sql_kats, load_tz_kats, replay_kat, replay_sql_kat
 
 KATS = load_kats()
 TZ_KATS = load_tz_kats()
+PY_KATS = load_pyflink_kats()
+SESSION_KATS = load_session_kats()
 
 
-@pytest.mark.parametrize("case", KATS["assigners"], ids=lambda c: c["src"].split("/")[-1])
+@pytest.mark.parametrize("case", KATS["assigners"] + SESSION_KATS["assigners"], ids=lambda c: c["src"].split("/")[-1])
 def test_assigner_kats(case):
     cfg = A.make_config(window_kind=case["kind"], size_ms=case["size"], slide_ms=case.get("slide", 0),
-                        offset_ms=case["offset"])
+                        offset_ms=case["offset"], gap_ms=case.get("gap", 0))
     for ts, exp in case["cases"]:
         starts = np.zeros(64, np.int64)
         ends = np.zeros(64, np.int64)
@@ -35,6 +37,27 @@ def test_slice_end_kats(case):
 @pytest.mark.parametrize("case", KATS["operators"], ids=lambda c: c["name"].split(" ")[0])
 def test_operator_kats(case):
     replay_kat(case, O.Oracle)
+
+
+@pytest.mark.parametrize("case", PY_KATS["operators"], ids=lambda c: c["name"].split(" ", 1)[1])
+def test_pyflink_window_operator_sequences(case):
+    """The oracle against the reference's own Python WindowOperator run over random streams
+    (tests/golden/gen_pyflink_kats.py): every watermark's rows and the drop count."""
+    replay_kat(case, O.Oracle)
+
+
+@pytest.mark.parametrize("case", SESSION_KATS["operators"], ids=lambda c: c["name"].split(" ")[0])
+def test_session_merge_kats(case):
+    """EventTimeSessionWindowsTest mergeWindows / TimeWindowTest.testIntersect as session sequences."""
+    replay_kat(case, O.Oracle)
+
+
+@pytest.mark.parametrize("gap", SESSION_KATS["invalid_gaps"]["gaps"])
+def test_session_invalid_gap(gap):
+    """EventTimeSessionWindowsTest.testInvalidParameters: a gap <= 0 is rejected."""
+    with pytest.raises(O.OracleError) as ei:
+        O.Oracle(A.make_config(window_kind="SESSION", gap_ms=gap, size_ms=0))
+    assert ei.value.code == -1
 
 
 def test_murmur_properties():

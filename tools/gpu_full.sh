@@ -1,16 +1,16 @@
 #!/bin/bash
-# Full default bench (C2 workload, with cpu_baseline) + rocprofv3 kernel stats of the same command.
+# Whole GPU suite + smoke, then the per-dispatch trace of the driver's bench command (tools/gpu_trace.sh).
+# TAG names the outputs (default full). SKIP_TESTS=1 runs only the trace.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-R=$PWD
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 TAG=${TAG:-full}
-timeout -k 10 600 python -u bench.py $BENCH_ARGS > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.log; rc=$?
-echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json; tail -3 gpurun_out/bench_$TAG.log
-[ $rc -ne 0 ] && exit $rc
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $R/gpurun_out/rocprof_$TAG -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline $BENCH_ARGS > $R/gpurun_out/prof_$TAG.log 2>&1; rc=$?
-echo "rocprof rc=$rc"; tail -1 $R/gpurun_out/prof_$TAG.log
-f=$(find $R/gpurun_out/rocprof_$TAG -name "*kernel_stats.csv" | head -1)
-[ -n "$f" ] && cut -d, -f1-7 "$f" | head -12
-exit 0
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests \
+    > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" gpurun_out/${TAG}_pytest.log | tail -15
+  [ $rc -ne 0 ] && exit $rc
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { cat gpurun_out/${TAG}_smoke.log; exit 1; }
+  tail -2 gpurun_out/${TAG}_smoke.log
+fi
+TAG=$TAG bash tools/gpu_trace.sh
