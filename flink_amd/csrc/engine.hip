@@ -1814,7 +1814,12 @@ struct Sess2Args {
     int32_t tb;                  // bits of (start - base) in the sort key (kid << tb | start - base)
     int32_t all_sp;              // 1: route everything through the arrival-order path
     unsigned long long* bkey;    // [nb] sort keys (then sorted)
-    uint32_t* bval;              // [nb] payload: record index, or session index | 0x80000000
+    uint32_t* bval;              // [nb] payload: bulk position, | 0x80000000 when its end is in pe (sessions,
+                                 // dynamic gaps)
+    unsigned long long* pk;      // [nb][pkw] the element's COUNT + accumulator words, in bulk order (one row per
+                                 // element gathered once after the sort, not one value column per accumulator)
+    int64_t* pe;                 // [nb] end of a flagged element
+    int32_t pkw, pad_pk;
     int64_t* bend;               // [nb] window / session end per sorted element
     int64_t* bmax;               // [nb] inclusive max of bend over the key so far (segmented scan)
     uint32_t* bcid;              // [nb] head flags, then 1-based cluster ids (inclusive sum)
@@ -1927,7 +1932,7 @@ __device__ __forceinline__ void route_elem(const Sess2Args& a, int64_t t, bool& 
     }
 }
 
-__global__ void __launch_bounds__(kBlock) sess2_route_kernel(Sess2Args a) {
+__global__ void __launch_bounds__(kBlock) sess2_route_kernel(Sess2Args a, const EngineConst* __restrict__ cp) {
     constexpr int kW = kBlock / 64;
     __shared__ uint32_t s_wb[kW], s_ws[kW];
     __shared__ unsigned long long s_base[2];
@@ -1955,7 +1960,27 @@ __global__ void __launch_bounds__(kBlock) sess2_route_kernel(Sess2Args a) {
         bool valid, sp; unsigned long long bk, sk; uint32_t pay;
         route_elem(a, c0 + (int64_t)j * kBlock + threadIdx.x, valid, sp, bk, sk, pay);
         const unsigned long long mb = __ballot(valid && !sp), ms = __ballot(valid && sp);
-        if (valid && !sp) { const unsigned long long o = pb + __popcll(mb & lt); a.bkey[o] = bk; a.bval[o] = pay; }
+        if (valid && !sp) {
+            const unsigned long long o = pb + __popcll(mb & lt);
+            a.bkey[o] = bk;
+            const bool sess = (pay & 0x80000000u) != 0;
+            const bool flag = sess || a.gapc;
+            a.bval[o] = (uint32_t)o | (flag ? 0x80000000u : 0u);
+            unsigned long long* row = a.pk + (int64_t)o * a.pkw;
+            const int64_t x = (int64_t)(pay & 0x7fffffffu);
+            if (sess) {
+                for (int cc = 0; cc < a.pkw; ++cc) row[cc] = a.in.acc[(int64_t)cc * a.in.stride + x];
+                a.pe[o] = a.in.end[x];
+            } else {
+                const EngineConst& c = *cp;
+                row[0] = 1ull;
+                for (int cc = 1; cc < a.pkw; ++cc) {
+                    const AggDesc& d = c.agg[a.col_owner[cc]];
+                    row[cc] = acc_input(d, a.cols[d.col], x, a.nulls[d.col]);
+                }
+                if (a.gapc) a.pe[o] = jm::wadd(a.ts[x], a.gapc[x]);
+            }
+        }
         if (valid && sp) { const unsigned long long o = ps + __popcll(ms & lt); a.skey[o] = sk; a.sval[o] = pay; }
         pb += __popcll(mb);
         ps += __popcll(ms);
@@ -1968,7 +1993,7 @@ __global__ void __launch_bounds__(kBlock) sess2_ends_kernel(Sess2Args a) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.nb; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t p = a.bval[i];
         const int64_t start = a.base + (int64_t)(a.bkey[i] & smask);
-        a.bend[i] = (p & 0x80000000u) ? a.in.end[p & 0x7fffffffu] : jm::wadd(start, a.gapc ? a.gapc[p] : a.gap);
+        a.bend[i] = (p & 0x80000000u) ? a.pe[p & 0x7fffffffu] : jm::wadd(start, a.gap);
     }
 }
 
@@ -1985,12 +2010,6 @@ __global__ void __launch_bounds__(kBlock) sess2_heads_kernel(Sess2Args a) {
     }
 }
 
-__device__ __forceinline__ unsigned long long sess_acc_of(const Sess2Args& a, const EngineConst& c, int cc, uint32_t p) {
-    if (p & 0x80000000u) return a.in.acc[(int64_t)cc * a.in.stride + (p & 0x7fffffffu)];
-    if (cc == 0) return 1ull;
-    const AggDesc& d = c.agg[a.col_owner[cc]];
-    return acc_input(d, a.cols[d.col], (int64_t)p, a.nulls[d.col]);
-}
 
 __device__ __forceinline__ void acc_atomic(int acc_kind, unsigned long long* p, unsigned long long v) {
     switch (acc_kind) {
@@ -2038,7 +2057,7 @@ __global__ void __launch_bounds__(kBlock) sess2_reduce_kernel(Sess2Args a, const
         if (last) a.out.end[cl] = a.bmax[i];
         for (int cc = 0; cc < c.nacc; ++cc) {
             const int ak = cc == 0 ? ACC_ADD_I64 : c.acc_kind[cc];
-            unsigned long long v = act ? sess_acc_of(a, c, cc, p) : 0ull;
+            unsigned long long v = act ? a.pk[(int64_t)(p & 0x7fffffffu) * a.pkw + cc] : 0ull;
             for (int d = 1; d < 64; d <<= 1) {
                 const unsigned long long y = __shfl_up(v, d);
                 const int64_t yc = __shfl_up(cid, d);
@@ -2518,6 +2537,8 @@ struct fwa_engine {
     unsigned long long* d_skey[4] = {};   // bulk in/out, ordered in/out
     uint32_t* d_sval[4] = {};
     int64_t* d_send2 = nullptr;
+    unsigned long long* d_spk = nullptr;   // session bulk rows (Sess2Args::pk)
+    int64_t* d_spe = nullptr;
     int64_t* d_smax = nullptr;
     uint32_t* d_scid = nullptr;
     int64_t sc_cap = 0;                // ordered-path scratch session lists
@@ -2647,7 +2668,7 @@ int64_t trig(const fwa_engine* e, int64_t max_ts) {
 // local window times with that local watermark unchanged.
 int64_t local_wm(const fwa_engine* e, int64_t wm) {
     if (e->tz.empty() || wm == LONG_MAX_J || wm == LONG_MIN_J) return wm;
-    const int64_t kLim = (int64_t)1 << 62;                  // past the zone table: a fixed offset
+    const int64_t kLim = (int64_t)1 << 61;                  // past the zone table: a fixed offset (hi - lo fits int64)
     const int64_t thi = trig(e, kLim), tlo = trig(e, -kLim);
     if (thi <= wm) return jm::wadd(kLim, jm::wsub(wm, thi));
     if (tlo > wm) return jm::wsub(-kLim, jm::wsub(tlo, wm));
@@ -2952,7 +2973,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -3566,7 +3587,7 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
             if ((rc = re((void**)&e->d_sval[q], 4))) return rc;
         }
         if ((rc = re((void**)&e->d_send2, 8)) || (rc = re((void**)&e->d_smax, 8)) || (rc = re((void**)&e->d_scid, 4)) ||
-            (rc = re((void**)&e->d_rkid, 4)))
+            (rc = re((void**)&e->d_rkid, 4)) || (rc = re((void**)&e->d_spk, 8 * (size_t)e->nacc)) || (rc = re((void**)&e->d_spe, 8)))
             return rc;
         e->sb_cap = cap;
     }
@@ -3638,10 +3659,13 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     if (s.all_sp) s.tb = 0;
     s.bkey = e->d_skey[0];
     s.bval = e->d_sval[0];
+    s.pk = e->d_spk;
+    s.pe = e->d_spe;
+    s.pkw = e->nacc;
     s.skey = e->d_skey[2];
     s.sval = e->d_sval[2];
     sess2_route_kernel<<<(unsigned)((n + n_in + (int64_t)kBlock * kRouteItems - 1) / ((int64_t)kBlock * kRouteItems)), kBlock, 0,
-                         e->stream>>>(s);
+                         e->stream>>>(s, e->d_ec);
     HIPCHK(e, hipGetLastError());
     if ((rc = read_sess_ctr(e))) return rc;
     const int64_t nb = (int64_t)e->h_sctr->n_bulk, nsp = (int64_t)e->h_sctr->n_sp;

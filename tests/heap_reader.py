@@ -197,16 +197,20 @@ def s64(x):
 def parse_engine_heap(body, offsets, ds, naggs, sess=False, first_kg=0):
     """The engine's fwa_snapshot_heap body (the layout the Java shim puts behind its own proxy header):
     DataStream: 0 window-contents (TimeWindow, Long, Tuple of 1 + naggs longs), [sessions: 1 merging-window-set
-    (VoidNamespace, Long, List<Tuple2<TimeWindow, TimeWindow>>)], last = event timers (Long key, TimeWindow);
-    Table: 0 window state (Long slice end, BinaryRowData key, BinaryRowData acc), 1 timers (BinaryRowData key, Long).
+    (VoidNamespace, Long, List<Tuple2<TimeWindow, TimeWindow>>)], then processing and event timers (Long key,
+    TimeWindow); Table: 0 window state (Long slice end, BinaryRowData key, BinaryRowData acc), 1 processing and 2 event
+    timers (BinaryRowData key, Long). The ids are the heap backend's (heap_snapshot.cpp ids_of).
     Returns (key group -> [(key, start, end, acc fields, null flags)], timers, merging sets)."""
     if ds:
         lay = {0: ("kv", ser_time_window, ser_long, ser_tuple(*[ser_ulong] * (1 + naggs)))}
         if sess:
             lay[1] = ("kv", ser_void, ser_long, ser_list(ser_tuple(ser_time_window, ser_time_window)))
-        lay[2 if sess else 1] = ("pq", ser_long, ser_time_window)
+        nxt = 2 if sess else 1
+        lay[nxt] = ("pq", ser_long, ser_time_window)             # processing-time timers (none on this path)
+        lay[nxt + 1] = ("pq", ser_long, ser_time_window)         # event-time timers
     else:
-        lay = {0: ("kv", ser_long, ser_binrow(1), ser_binrow(1 + naggs)), 1: ("pq", ser_binrow(1), ser_long)}
+        lay = {0: ("kv", ser_long, ser_binrow(1), ser_binrow(1 + naggs)), 1: ("pq", ser_binrow(1), ser_long),
+               2: ("pq", ser_binrow(1), ser_long)}
     secs = read_key_groups(body, offsets, first_kg, lay)
     ents, timers, msets = {}, {}, {}
     tid = max(lay)

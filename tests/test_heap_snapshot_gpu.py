@@ -387,7 +387,7 @@ def test_restore_reference_reduce_snapshot():
     body = bytearray(struct.pack(">i", 0))
     body += struct.pack(">hi", 0, len(sec[0]))
     for (st, en), key, (_, v) in sec[0]:
-        body += struct.pack(">qqqqq", st, en, ids[key], 1, v)
+        body += struct.pack(">qqqqqq", st, en, ids[key], 1, 1, v)   # ACC tuple: COUNT(*), COUNT, SUM
     body += struct.pack(">hi", 1, 0)
     body += struct.pack(">hi", 2, len(sec[2]))
     for ts_, key, (st, en) in sec[2]:

@@ -198,3 +198,49 @@ def test_record_lists_snapshot_restore_rescale():
             outs.append(g.advance_watermark(A.LONG_MAX))
             g.close()
         assert_rows_equal({f: np.concatenate([r[f] for r in outs]) for f in outs[0]}, final, names, rtol=1e-9)
+
+
+def record_lists_compaction_check():
+    """Few distinct keys, many records per window, a small FWA_SP_BUDGET (set by the caller): the growing windows'
+    lists are folded into pre-aggregated runs, results still equal the oracle's, device memory stays bounded."""
+    import torch
+    rng = np.random.default_rng(29)
+    batches, wms = [], []
+    for b in range(30):
+        n = 100_000
+        keys = rng.integers(0, 500, n).astype(np.int64)
+        ts = rng.integers(0, 1_900_000, n).astype(np.int64) + (100_000 if b >= 20 else 0)
+        vi = rng.integers(-2**40, 2**40, n).astype(np.int64)
+        vf = rng.random(n).astype(np.float32)
+        vd = rng.random(n) - 0.5
+        batches.append((keys, ts, [vi, vf, vd]))
+        wms.append(999_999 if b == 24 else (A.LONG_MAX if b == 29 else -1))
+    from flink_amd import engine
+    from oracle.oracle import Oracle
+    kw = dict(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=1_000_000)
+    g = engine.WindowAggregator(A.make_config(aggs=AGGS, record_lists=True, **kw))
+    o = Oracle(A.make_config(aggs=AGGS, **kw))
+    names = A.agg_names(A.make_config(aggs=AGGS, **kw))
+    free0 = None
+    for b, ((k, t, cols), wm) in enumerate(zip(batches, wms)):
+        assert g.push(k, t, cols) == o.push(k, t, cols)
+        if b == 4:
+            free0 = torch.cuda.mem_get_info()[0]
+        if b == 19:   # 15 more batches (~100 MB of entries without compaction) in the same two windows
+            grew = free0 - torch.cuda.mem_get_info()[0]
+            assert grew < 48 << 20, "record lists grew by %d bytes" % grew
+        if wm != -1:
+            assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), names, rtol=1e-9, ctx="batch %d" % b)
+    st = g.stats()
+    assert st.records_in == 30 * 100_000 and st.live_slices == 0
+    g.close()
+
+
+def test_record_lists_compaction_bounds_memory():
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "from test_record_lists_gpu import record_lists_compaction_check\n"
+            "record_lists_compaction_check()\n"
+            "print('ok')\n") % (ROOT, os.path.join(ROOT, "tests"))
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "FWA_SP_BUDGET": str(4 << 20)},
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 TAG=${TAG:-full}
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests \
+  timeout -k 10 900 python -u -m pytest --maxfail 20 -v --timeout 120 --timeout-method thread -m gpu tests \
     > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?
   echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" gpurun_out/${TAG}_pytest.log | tail -15
   [ $rc -ne 0 ] && exit $rc
