@@ -27,7 +27,12 @@
 // MIN, MAX, DOUBLE for floating SUM / AVG / MIN / MAX (the AggregateFunction's ACC type in the shim).
 // Table rows carry SQL NULLs as BinaryRowData null bits (an aggregate whose column held only NULLs) and one more
 // BIGINT field per hidden non-NULL counter; Table timers under a shift time zone are toEpochMillsForTimer(end - 1).
-// DataStream SLIDE / CUMULATE, Table SESSION and PREHASHED keys: FWA_E_UNSUPPORTED (FWASNAP1 covers them).
+//   DATASTREAM SLIDE   WindowOperator per-window state (window = merge of the engine's slices inside it); the restore
+//                      rebuilds slices whose merges equal every restored window (slide_windows_to_slices).
+//   TABLE SESSION      legacy Table WindowOperator: 0 session-window-mapping (MapSerializer of TimeWindow pairs under
+//                      VoidNamespace), 1 window-aggs (TimeWindow namespace, BinaryRowData key and accumulator), timers
+//                      at toEpochMillsForTimer(maxTimestamp) per in-flight session.
+// PREHASHED keys: FWA_E_UNSUPPORTED (FWASNAP1 covers them).
 #include <algorithm>
 #include <cstdint>
 #include <map>
@@ -133,10 +138,13 @@ struct In {
 // (SlicingWindowOperator: per-slice state, so the engine's slices map 1:1), Table shift time zones and SQL NULLs.
 bool supported(const fwa_config& c) {
     if (c.key_kind == FWA_KEY_PREHASHED) return false;
-    if (c.semantics == FWA_SEM_DATASTREAM) return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SESSION;
-    return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SLIDE || c.window_kind == FWA_CUMULATE;
+    if (c.semantics == FWA_SEM_DATASTREAM)
+        return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SESSION || c.window_kind == FWA_SLIDE;
+    return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SLIDE || c.window_kind == FWA_CUMULATE ||
+           c.window_kind == FWA_SESSION;
 }
-const char* kUnsupported = "heap layout: DataStream TUMBLE / SESSION and Table TUMBLE / HOP / CUMULATE with a computable key hash";
+const char* kUnsupported = "heap layout: DataStream TUMBLE / SLIDE / SESSION and Table TUMBLE / HOP / CUMULATE / SESSION "
+                           "with a computable key hash";
 
 int64_t gcd64(int64_t a, int64_t b) { while (b) { const int64_t t = a % b; a = b; b = t; } return a; }
 
@@ -202,10 +210,96 @@ int64_t timer_of(const fwa_config& c, int64_t max_ts) { return c.tz_n ? jm::tz_t
 //   DataStream TUMBLE  (WindowOperator):        0 window-contents, 1 processing timers, 2 event timers
 //   DataStream SESSION (WindowOperator):        0 window-contents, 1 merging-window-set, 2 processing, 3 event timers
 //   Table (SlicingWindowOperator, window-aggs): 0 window-aggs, 1 processing timers, 2 event timers
+//   Table SESSION (TR WindowOperator :254-286):  0 session-window-mapping, 1 window-aggs, 2 processing, 3 event timers
+//     (String.hashCode buckets of a 16-slot HashMap: "session-window-mapping" 6 < "window-aggs" 8)
 struct Ids { int contents, mset, proc, event, n; };
 Ids ids_of(const fwa_config& c) {
-    if (c.semantics == FWA_SEM_DATASTREAM && c.window_kind == FWA_SESSION) return Ids{0, 1, 2, 3, 4};
+    if (c.window_kind == FWA_SESSION) return c.semantics == FWA_SEM_DATASTREAM ? Ids{0, 1, 2, 3, 4} : Ids{1, 0, 2, 3, 4};
     return Ids{0, -1, 1, 2, 3};
+}
+
+bool is_min(int64_t kind) { return kind == FWA_MIN_I64 || kind == FWA_MIN_F32 || kind == FWA_MIN_F64; }
+bool is_max(int64_t kind) { return kind == FWA_MAX_I64 || kind == FWA_MAX_F32 || kind == FWA_MAX_F64; }
+bool is_fsum(int64_t kind) { return kind == FWA_SUM_F32 || kind == FWA_SUM_F64 || kind == FWA_AVG_F32 || kind == FWA_AVG_F64; }
+
+// WindowOperator.cleanupTime (:647-654): maxTimestamp + allowedLateness, Long.MAX_VALUE on overflow
+int64_t cleanup_of(int64_t max_ts, int64_t late) { return max_ts > INT64_MAX - late ? INT64_MAX : max_ts + late; }
+
+// TimeWindow.getWindowStartWithOffset (:264-272)
+int64_t wstart(int64_t ts, int64_t off, int64_t size) {
+    const int64_t r = (ts - off) % size;
+    return r < 0 ? ts - (r + size) : ts - r;
+}
+
+// DataStream SLIDE restore: WindowOperator holds one accumulator per (key, window) and windows overlap, the engine one
+// per (key, slice of width g = gcd(size, slide)). Slices whose window merges equal every restored window are built per
+// key: a window k covers slices q_k .. q_k + m - 1 (m = size / g), the next window starts r = slide / g slices later.
+//  * additive words (COUNT(*), integer / floating sums, hidden counters): windows from the highest restored one down
+//    to the lowest uncleaned one that overlaps them, each setting its first slice to its value minus the slices above
+//    it (already set; none above the highest window) -- every such window then sums to its value, an uncleaned window
+//    without state to 0 (no record reached it, so none can be in its slices);
+//  * MIN (MAX): each slice takes the largest (smallest) value of the uncleaned windows containing it, the identity for
+//    one without state -- every window's MIN (MAX) is then reached at the slice where its true minimum lies.
+// Future fires of the uncleaned windows (the only ones that can still fire) equal the reference's; floating sums are
+// reassociated (within the DataStream tolerance).
+using Words = std::vector<uint64_t>;
+void slide_windows_to_slices(const fwa_config& c, int64_t wm, const std::map<int64_t, Words>& win, int nw,
+                             std::vector<std::pair<int64_t, Words>>& out) {
+    out.clear();
+    if (win.empty()) return;
+    const int64_t g = gcd64(c.size_ms, c.slide_ms), m = c.size_ms / g, r = c.slide_ms / g;
+    const int na = c.num_aggs;
+    const int64_t kmin = win.begin()->first, kmax = win.rbegin()->first;
+    int64_t lo = kmin;                                          // lowest uncleaned window overlapping the restored ones
+    while (lo - c.slide_ms > kmin - c.size_ms &&
+           (wm == INT64_MIN || cleanup_of(lo - c.slide_ms + c.size_ms - 1, c.allowed_lateness_ms) > wm))
+        lo -= c.slide_ms;
+    auto qof = [&](int64_t t) { return floor_div(t - c.offset_ms, g); };
+    const int64_t q0 = qof(lo), q1 = qof(kmax) + m - 1;
+    const size_t ns = (size_t)(q1 - q0 + 1);
+    std::vector<Words> x(ns, Words((size_t)nw, 0));
+    auto kind_of = [&](int w) -> int64_t { return (w >= 1 && w <= na) ? c.aggs[w - 1].kind : FWA_COUNT; };
+    for (int w = 0; w < nw; ++w) {
+        const int64_t k = kind_of(w);
+        if (is_min(k) || is_max(k)) {
+            for (size_t i = 0; i < ns; ++i) {
+                const int64_t q = q0 + (int64_t)i;
+                uint64_t y = is_min(k) ? 0ull : ~0ull;
+                // windows containing slice q: starts on the slide grid in (t - size, t], t = the slice start
+                const int64_t t = c.offset_ms + q * g;
+                for (int64_t st = wstart(t, c.offset_ms, c.slide_ms); st > t - c.size_ms; st -= c.slide_ms) {
+                    if (st < lo) break;
+                    auto it = win.find(st);
+                    const uint64_t v = it == win.end() ? identity_word(k) : it->second[(size_t)w];
+                    y = is_min(k) ? std::max(y, v) : std::min(y, v);
+                }
+                x[i][(size_t)w] = y;
+            }
+            continue;
+        }
+        const bool fl = is_fsum(k);
+        for (int64_t st = kmax; st >= lo; st -= c.slide_ms) {
+            const int64_t qa = qof(st) - q0;
+            auto it = win.find(st);
+            const uint64_t sv = it == win.end() ? 0ull : it->second[(size_t)w];
+            if (fl) {
+                double a, hsum = 0;
+                memcpy(&a, &sv, 8);
+                for (int64_t q = qa + r; q <= qa + m - 1; ++q) { double h; memcpy(&h, &x[(size_t)q][(size_t)w], 8); hsum += h; }
+                a -= hsum;
+                memcpy(&x[(size_t)qa][(size_t)w], &a, 8);
+            } else {
+                uint64_t hsum = 0;
+                for (int64_t q = qa + r; q <= qa + m - 1; ++q) hsum += x[(size_t)q][(size_t)w];
+                x[(size_t)qa][(size_t)w] = sv - hsum;
+            }
+        }
+    }
+    for (size_t i = 0; i < ns; ++i) {
+        bool any = false;
+        for (int w = 0; w < nw; ++w) any = any || x[i][(size_t)w] != (w >= 1 && w <= na ? identity_word(kind_of(w)) : 0ull);
+        if (any) out.push_back({c.offset_ms + (q0 + (int64_t)i) * g, x[i]});
+    }
 }
 
 }  // namespace
@@ -229,11 +323,12 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
     if (!parse(snap.data, snap.size, &s)) { fwa_blob_free(&snap); return fwa_set_error(e, FWA_E_STATE, "bad FWASNAP1 blob"); }
     const bool ds = c.semantics == FWA_SEM_DATASTREAM;
     const bool sess = c.window_kind == FWA_SESSION;
+    const bool ds_slide = ds && c.window_kind == FWA_SLIDE;
     const Ids id = ids_of(c);
     int hid[FWA_MAX_AGGS];
     const int nh = hidden_map(c, hid);
     const int na = (int)s.naggs, arity = 1 + na + nh;
-    const int64_t n = s.n, g = ds ? s.size : slice_width(c);
+    const int64_t n = s.n, g = ds ? (ds_slide ? gcd64(c.size_ms, c.slide_ms) : s.size) : slice_width(c);
     auto end_of = [&](int64_t i) { return sess ? s.col[(3 + na + nh) * n + i] : s.col[n + i] + g; };
     const bool fired_any = s.wm != INT64_MIN;
     Out o;
@@ -241,6 +336,11 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
     std::vector<uint8_t> fnull((size_t)arity);
     struct Row { int64_t key, start, end; uint64_t w[1 + FWA_MAX_AGGS + FWA_MAX_COLS]; };
     std::vector<Row> rows;
+    auto merge_into = [&](Row& a, const Row& b) {
+        a.w[0] += b.w[0];
+        for (int j = 0; j < na; ++j) a.w[1 + j] = merge_word(s.agg[j], a.w[1 + j], b.w[1 + j]);
+        for (int h = 0; h < nh; ++h) a.w[1 + na + h] += b.w[1 + na + h];
+    };
     for (int64_t kg = c.kg_start; kg <= c.kg_end; ++kg) {
         kg_offsets[kg - c.kg_start] = (int64_t)o.b.size();
         o.i32(kg);
@@ -254,6 +354,27 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
             r.w[0] = (uint64_t)s.col[2 * n + i];
             for (int j = 0; j < na + nh; ++j) r.w[1 + j] = (uint64_t)s.col[(3 + j) * n + i];
             rows.push_back(r);
+        }
+        if (ds_slide) {
+            // WindowOperator keeps one state per (key, window) (SlidingEventTimeWindows.assignWindows :70-82): a window's
+            // contents are the merge of the engine's slices inside it; windows past cleanup (isWindowLate) are gone and a
+            // window holds state iff a record reached it
+            std::map<std::pair<int64_t, int64_t>, Row> win;
+            for (const Row& r : rows)
+                for (int64_t st = wstart(r.start, c.offset_ms, c.slide_ms); st > r.start - c.size_ms; st -= c.slide_ms) {
+                    if (fired_any && cleanup_of(st + c.size_ms - 1, s.late) <= s.wm) continue;
+                    auto it = win.find({r.key, st});
+                    if (it == win.end()) {
+                        Row w = r;
+                        w.start = st;
+                        w.end = st + c.size_ms;
+                        win.emplace(std::make_pair(r.key, st), w);
+                    } else {
+                        merge_into(it->second, r);
+                    }
+                }
+            rows.clear();
+            for (auto& kv : win) if ((int64_t)kv.second.w[0] > 0) rows.push_back(kv.second);
         }
         if (!ds && c.window_kind == FWA_CUMULATE && fired_any) {
             std::map<std::pair<int64_t, int64_t>, Row> first;          // (key, window start) -> folded first slice
@@ -270,71 +391,83 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
                     m.end = ws + g;
                     first.emplace(std::make_pair(r.key, ws), m);
                 } else {
-                    it->second.w[0] += r.w[0];
-                    for (int j = 0; j < na; ++j) it->second.w[1 + j] = merge_word(s.agg[j], it->second.w[1 + j], r.w[1 + j]);
-                    for (int h = 0; h < nh; ++h) it->second.w[1 + na + h] += r.w[1 + na + h];
+                    merge_into(it->second, r);
                 }
             }
             rows.clear();
             for (auto& kv : first) rows.push_back(kv.second);
             rows.insert(rows.end(), keep.begin(), keep.end());
         }
-        o.i16(id.contents);                                            // window contents / window-aggs
-        o.i32((int64_t)rows.size());
-        for (const Row& r : rows) {
-            const int64_t key = r.key, start = r.start, end = r.end;
-            f[0] = r.w[0];
-            fnull[0] = 0;
-            for (int j = 0; j < na; ++j) {
-                f[1 + j] = acc_to_field(s.agg[j], r.w[1 + j]);
-                // SQL: an aggregate whose input column held only NULLs has a NULL buffer (Sum/Min/MaxAggFunction);
-                // COUNT(col) is the counter itself
-                fnull[1 + j] = hid[j] >= 0 && s.agg[j] != FWA_COUNT_COL && r.w[1 + na + hid[j]] == 0;
+        auto contents = [&]() {                                        // window contents / window-aggs
+            o.i16(id.contents);
+            o.i32((int64_t)rows.size());
+            for (const Row& r : rows) {
+                const int64_t key = r.key, start = r.start, end = r.end;
+                f[0] = r.w[0];
+                fnull[0] = 0;
+                for (int j = 0; j < na; ++j) {
+                    f[1 + j] = acc_to_field(s.agg[j], r.w[1 + j]);
+                    // SQL: an aggregate whose input column held only NULLs has a NULL buffer (Sum/Min/MaxAggFunction);
+                    // COUNT(col) is the counter itself
+                    fnull[1 + j] = hid[j] >= 0 && s.agg[j] != FWA_COUNT_COL && r.w[1 + na + hid[j]] == 0;
+                }
+                for (int h = 0; h < nh; ++h) { f[1 + na + h] = r.w[1 + na + h]; fnull[1 + na + h] = 0; }
+                if (ds) {
+                    o.i64((uint64_t)start); o.i64((uint64_t)end);          // TimeWindow.Serializer
+                    o.i64((uint64_t)key);                                  // LongSerializer
+                    for (int k = 0; k < arity; ++k) o.i64(f[k]);           // TupleSerializer of the ACC fields
+                } else {
+                    if (sess) { o.i64((uint64_t)start); o.i64((uint64_t)end); }   // TR TimeWindow.Serializer :169-172
+                    else o.i64((uint64_t)end);                              // slice end (LongSerializer)
+                    const uint64_t kf = (uint64_t)key;
+                    o.row(&kf, 1);                                         // key row
+                    bool nl[1 + FWA_MAX_AGGS + FWA_MAX_COLS];
+                    for (int k = 0; k < arity; ++k) nl[k] = fnull[k] != 0;
+                    o.row(f.data(), arity, nl);                            // accumulator row
+                }
             }
-            for (int h = 0; h < nh; ++h) { f[1 + na + h] = r.w[1 + na + h]; fnull[1 + na + h] = 0; }
-            if (ds) {
-                o.i64((uint64_t)start); o.i64((uint64_t)end);          // TimeWindow.Serializer
-                o.i64((uint64_t)key);                                  // LongSerializer
-                for (int k = 0; k < arity; ++k) o.i64(f[k]);           // TupleSerializer of the ACC fields
-            } else {
-                o.i64((uint64_t)end);                                  // slice end (LongSerializer)
-                const uint64_t kf = (uint64_t)key;
-                o.row(&kf, 1);                                         // key row
-                bool nl[1 + FWA_MAX_AGGS + FWA_MAX_COLS];
-                for (int k = 0; k < arity; ++k) nl[k] = fnull[k] != 0;
-                o.row(f.data(), arity, nl);                            // accumulator row
-            }
-        }
-        if (ds && sess) {                                              // merging-window-set: each in-flight session
-            std::map<int64_t, std::vector<int64_t>> by_key;            // maps to itself as its state window
-            for (int64_t i = lo; i < hi; ++i) by_key[s.col[i]].push_back(i);
+        };
+        auto mset = [&]() {                                            // merging-window-set / session-window-mapping:
+            std::map<int64_t, std::vector<int64_t>> by_key;            // each in-flight session maps to itself as its
+            for (int64_t i = lo; i < hi; ++i) by_key[s.col[i]].push_back(i);   // state window
             o.i16(id.mset);
             o.i32((int64_t)by_key.size());
             for (auto& kv : by_key) {
                 o.u8(0);                                               // VoidNamespaceSerializer: one byte
-                o.i64((uint64_t)kv.first);
-                o.i32((int64_t)kv.second.size());                      // ListSerializer: size, then the elements
-                for (int64_t i : kv.second) {
+                if (ds) o.i64((uint64_t)kv.first);
+                else { const uint64_t kf = (uint64_t)kv.first; o.row(&kf, 1); }
+                o.i32((int64_t)kv.second.size());                      // ListSerializer / MapSerializer: size, then
+                for (int64_t i : kv.second) {                          // (actual, state) TimeWindow pairs
                     const int64_t st = s.col[n + i], en = end_of(i);
-                    o.i64((uint64_t)st); o.i64((uint64_t)en); o.i64((uint64_t)st); o.i64((uint64_t)en);
+                    o.i64((uint64_t)st); o.i64((uint64_t)en);
+                    if (!ds) o.u8(0);                                  // MapSerializer: value not null
+                    o.i64((uint64_t)st); o.i64((uint64_t)en);
                 }
             }
-        }
+        };
+        if (sess && id.mset < id.contents) { mset(); contents(); }     // sections in state-id order
+        else { contents(); if (sess) mset(); }
         o.i16(id.proc);                                                // processing-time timers: none on this path
         o.i32(0);
-        // event-time timers. DataStream: window.maxTimestamp() while the window has not fired
-        // (EventTimeTrigger.onElement / onEventTime: a fired window keeps no trigger timer, a late element within
-        // allowed lateness FIREs at once) and always the cleanup timer maxTimestamp + allowedLateness
-        // (WindowOperator.registerCleanupTimer :608-620, cleanupTime :647-654; the same timer when the lateness is 0).
-        // Table: toEpochMillsForTimer(end - 1) of the first unfired window containing each slice, one per
-        // (key, window) (AbstractWindowAggProcessor.processElement :160-164, SliceSharedWindowAggProcessor.fireWindow :76-84).
+        // event-time timers. DataStream (per (key, window) of the state written above): window.maxTimestamp() while
+        // the window has not fired (EventTimeTrigger.onElement / onEventTime: a fired window keeps no trigger timer, a
+        // late element within allowed lateness FIREs at once) and always the cleanup timer maxTimestamp +
+        // allowedLateness (WindowOperator.registerCleanupTimer :608-620, cleanupTime :647-654; the same timer when the
+        // lateness is 0). Table sessions: toEpochMillsForTimer(maxTimestamp) per in-flight session (the trigger and the
+        // cleanup timer coincide, TR WindowOperator :421-446). Table slices: toEpochMillsForTimer(end - 1) of the first
+        // unfired window containing each slice, one per (key, window) (AbstractWindowAggProcessor.processElement
+        // :160-164, SliceSharedWindowAggProcessor.fireWindow :76-84).
         std::set<std::tuple<int64_t, int64_t, int64_t, int64_t>> timers;   // (ts, key, ns start, ns end)
-        for (int64_t i = lo; i < hi; ++i) {
-            const int64_t key = s.col[i], start = s.col[n + i], end = end_of(i);
-            if (ds) {
-                if (!fired_any || end - 1 > s.wm) timers.insert({end - 1, key, start, end});
-                timers.insert({(end - 1 > INT64_MAX - s.late) ? INT64_MAX : end - 1 + s.late, key, start, end});
-            } else {
+        if (ds) {
+            for (const Row& r : rows) {
+                if (!fired_any || r.end - 1 > s.wm) timers.insert({r.end - 1, r.key, r.start, r.end});
+                timers.insert({cleanup_of(r.end - 1, s.late), r.key, r.start, r.end});
+            }
+        } else if (sess) {
+            for (const Row& r : rows) timers.insert({timer_of(c, r.end - 1), r.key, r.start, r.end});
+        } else {
+            for (int64_t i = lo; i < hi; ++i) {
+                const int64_t key = s.col[i], end = end_of(i);
                 int64_t we = first_window_end(c, end);
                 while (fired_any && timer_of(c, we - 1) <= s.wm) we += (c.window_kind == FWA_SLIDE ? c.slide_ms : g);
                 timers.insert({timer_of(c, we - 1), key, 0, we});
@@ -346,7 +479,12 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
             o.i64((uint64_t)std::get<0>(t) ^ 0x8000000000000000ull);   // MathUtils.flipSignBit
             const int64_t key = std::get<1>(t);
             if (ds) { o.i64((uint64_t)key); o.i64((uint64_t)std::get<2>(t)); o.i64((uint64_t)std::get<3>(t)); }
-            else { const uint64_t kf = (uint64_t)key; o.row(&kf, 1); o.i64((uint64_t)std::get<3>(t)); }
+            else {
+                const uint64_t kf = (uint64_t)key;
+                o.row(&kf, 1);
+                if (sess) o.i64((uint64_t)std::get<2>(t));             // TimeWindow namespace
+                o.i64((uint64_t)std::get<3>(t));
+            }
         }
     }
     *watermark = s.wm;
@@ -367,6 +505,7 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
     if (!supported(c)) return fwa_set_error(e, FWA_E_UNSUPPORTED, kUnsupported);
     const bool ds = c.semantics == FWA_SEM_DATASTREAM;
     const bool sess = c.window_kind == FWA_SESSION;
+    const bool ds_slide = ds && c.window_kind == FWA_SLIDE;
     const Ids id = ids_of(c);
     int hid[FWA_MAX_AGGS];
     const int nh = hidden_map(c, hid);
@@ -392,6 +531,8 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
                 v.push_back((int64_t)(fnull[1 + j] ? identity_word(c.aggs[j].kind) : field_to_acc(c.aggs[j].kind, f[1 + j])));
             for (int h = 0; h < nh; ++h) v.push_back((int64_t)f[1 + na + h]);
         };
+        std::map<int64_t, std::map<int64_t, Words>> slide_win;    // DataStream SLIDE: key -> window start -> words
+        std::vector<std::pair<int64_t, Words>> slices;
         while (in.ok && in.at < in.n) {
             const int64_t kg = in.i32();
             if (!in.ok || kg < 0 || kg >= maxp) return fwa_set_error(e, FWA_E_ARG, "heap body: bad key group id");
@@ -402,14 +543,20 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
                 for (int64_t i = 0; i < cnt && in.ok; ++i) {
                     if (sid == id.proc || sid == id.event) {           // timers: re-derived from the window state
                         in.i64();
-                        if (ds) { in.i64(); in.i64(); in.i64(); } else { uint64_t k; in.row(&k, 1); in.i64(); }
+                        if (ds) { in.i64(); in.i64(); in.i64(); }
+                        else { uint64_t k; in.row(&k, 1); in.i64(); if (sess) in.i64(); }
                         continue;
                     }
                     if (sid == id.mset) {                              // merging-window-set: (actual, state) pairs
                         in.get(1);                                     // MergingWindowSet(...) :83-87
-                        const int64_t key = in.i64(), m = in.i32();
+                        int64_t key;
+                        if (ds) key = in.i64();
+                        else { uint64_t kf; in.row(&kf, 1); key = (int64_t)kf; }
+                        const int64_t m = in.i32();
                         for (int64_t q = 0; q < m && in.ok; ++q) {
-                            const int64_t as = in.i64(), ae = in.i64(), ss = in.i64(), se = in.i64();
+                            const int64_t as = in.i64(), ae = in.i64();
+                            if (!ds && in.get(1) != 0) in.ok = false;      // MapSerializer: null value flag
+                            const int64_t ss = in.i64(), se = in.i64();
                             actual[std::make_tuple(key, ss, se)] = std::make_pair(as, ae);
                         }
                         continue;
@@ -418,13 +565,20 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
                     for (int k = 0; k < arity; ++k) fnull[k] = false;
                     if (ds) { start = in.i64(); end = in.i64(); key = in.i64(); for (int k = 0; k < arity; ++k) f[k] = (uint64_t)in.i64(); }
                     else {
+                        start = sess ? in.i64() : 0;                   // Table sessions: TimeWindow namespace
                         end = in.i64();
                         uint64_t kf;
                         in.row(&kf, 1);
                         key = (int64_t)kf;
                         in.row(f.data(), arity, fnull);
                         if (fnull[0]) in.ok = false;                   // COUNT(*) is never NULL
-                        start = end - g;
+                        if (!sess) start = end - g;
+                    }
+                    if (ds_slide) {                                    // per-window state: slices built below
+                        std::vector<int64_t> v;
+                        words(v);
+                        slide_win[key][start] = Words(v.begin(), v.end());
+                        continue;
                     }
                     if (sess) {                                        // resolved against the mapping below
                         Pending p{kg, key, start, end, {}};
@@ -454,6 +608,17 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
             }
             pend.clear();
             actual.clear();
+            for (auto& kw : slide_win) {
+                slide_windows_to_slices(c, watermarks[b], kw.second, 1 + na + nh, slices);
+                std::vector<int64_t>& v = per[(size_t)kg];
+                for (auto& sl : slices) {
+                    v.push_back(kw.first);
+                    v.push_back(sl.first);
+                    for (uint64_t x : sl.second) v.push_back((int64_t)x);
+                    ++total;
+                }
+            }
+            slide_win.clear();
         }
         if (!in.ok) return fwa_set_error(e, FWA_E_ARG, "heap body: truncated or malformed");
         // the equivalent FWASNAP1 blob (engine.hip snap_header layout)

@@ -103,6 +103,17 @@ def ser_list(elem):
     return rd
 
 
+def ser_map(key, value):
+    """MapSerializer: int size, then per entry the key, a null flag byte and (if not null) the value"""
+    def rd(r):
+        out = []
+        for _ in range(r.get(">i")):
+            k = key(r)
+            out.append((k, None if r.get(">b") else value(r)))
+        return out
+    return rd
+
+
 def ser_binrow(arity):
     """BinaryRowDataSerializer of a row with `arity` fixed-length 8-byte fields -> (RowKind byte, null flags, fields)"""
     def rd(r):
@@ -208,16 +219,21 @@ def parse_engine_heap(body, offsets, ds, naggs, sess=False, first_kg=0):
         nxt = 2 if sess else 1
         lay[nxt] = ("pq", ser_long, ser_time_window)             # processing-time timers (none on this path)
         lay[nxt + 1] = ("pq", ser_long, ser_time_window)         # event-time timers
+    elif sess:                                                   # legacy Table WindowOperator (GROUP BY SESSION)
+        lay = {0: ("kv", ser_void, ser_binrow(1), ser_map(ser_time_window, ser_time_window)),
+               1: ("kv", ser_time_window, ser_binrow(1), ser_binrow(1 + naggs)),
+               2: ("pq", ser_binrow(1), ser_time_window), 3: ("pq", ser_binrow(1), ser_time_window)}
     else:
         lay = {0: ("kv", ser_long, ser_binrow(1), ser_binrow(1 + naggs)), 1: ("pq", ser_binrow(1), ser_long),
                2: ("pq", ser_binrow(1), ser_long)}
     secs = read_key_groups(body, offsets, first_kg, lay)
     ents, timers, msets = {}, {}, {}
     tid = max(lay)
+    cid, mid = (1, 0) if sess and not ds else (0, 1)            # window contents / merging set state ids
     for kg, s in secs.items():
         assert sorted(s) == sorted(lay), "every state section is written, in id order"
         e = []
-        for ns, key, val in s.get(0, []):
+        for ns, key, val in s.get(cid, []):
             if ds:
                 e.append((key, ns[0], ns[1], list(val), [False] * (1 + naggs)))
             else:
@@ -225,12 +241,20 @@ def parse_engine_heap(body, offsets, ds, naggs, sess=False, first_kg=0):
                 assert rk == 0 and not kn[0]                 # RowKind INSERT, non-NULL key
                 vk, vn, vf = val
                 assert vk == 0
-                e.append((kf[0], None, ns, vf, vn))
+                if sess:
+                    e.append((kf[0], ns[0], ns[1], vf, vn))
+                else:
+                    e.append((kf[0], None, ns, vf, vn))
         ents[kg] = e
         if sess:
-            msets[kg] = {key: [(a[0], a[1], b[0], b[1]) for a, b in val] for _, key, val in s.get(1, [])}
+            if ds:
+                msets[kg] = {key: [(a[0], a[1], b[0], b[1]) for a, b in val] for _, key, val in s.get(mid, [])}
+            else:
+                msets[kg] = {key[2][0]: [(a[0], a[1], b[0], b[1]) for a, b in val] for _, key, val in s.get(mid, [])}
         if ds:
             timers[kg] = [(ts, key, ns[0], ns[1]) for ts, key, ns in s.get(tid, [])]
+        elif sess:
+            timers[kg] = [(ts, key[2][0], ns[0], ns[1]) for ts, key, ns in s.get(tid, [])]
         else:
             timers[kg] = [(ts, key[2][0], ns) for ts, key, ns in s.get(tid, [])]
     return ents, timers, msets

@@ -80,6 +80,14 @@ CASES = {
     "table_tumble_tz": dict(window_kind="TUMBLE", semantics="TABLE", size_ms=5000, tz=TZ["Asia/Shanghai"]),
     "table_cumulate_tz": dict(window_kind="CUMULATE", semantics="TABLE", size_ms=20000, slide_ms=5000,
                               tz=TZ["America/Los_Angeles"]),
+    # DataStream sliding windows: per-window state (SlidingEventTimeWindows), from the engine's slices
+    "ds_slide": dict(window_kind="SLIDE", semantics="DATASTREAM", size_ms=15000, slide_ms=5000),
+    "ds_slide_late_odd": dict(window_kind="SLIDE", semantics="DATASTREAM", size_ms=5000, slide_ms=2000, offset_ms=300,
+                              allowed_lateness_ms=2500),
+    # legacy Table WindowOperator (GROUP BY SESSION): session-window-mapping + window-aggs
+    "table_session": dict(window_kind="SESSION", semantics="TABLE", gap_ms=700),
+    "table_session_null": dict(window_kind="SESSION", semantics="TABLE", gap_ms=700, nullable_cols=(0, 1, 2)),
+    "table_session_tz": dict(window_kind="SESSION", semantics="TABLE", gap_ms=700, tz=TZ["Asia/Shanghai"]),
 }
 
 
@@ -131,6 +139,20 @@ def expected_state(case, snap, kg, wm):
     sl = S.entries_of_key_group(snap, kg)
     rows = list(zip(snap["key"][sl].tolist(), snap["slice_start"][sl].tolist(), snap["count"][sl].tolist(),
                     *[a[sl].tolist() for a in snap["acc"]], *[h[sl].tolist() for h in snap["hidden"]]))
+    if c["semantics"] == "DATASTREAM" and c["window_kind"] == "SLIDE":
+        # WindowOperator's per-window state: the merge of the slices inside each window that is not past cleanup
+        size, slide, off, late = c["size_ms"], c["slide_ms"], c.get("offset_ms", 0), c.get("allowed_lateness_ms", 0)
+        kinds = [A.AGG_KINDS[a] for a, _ in aggs_of(case)]
+        win = {}
+        for r in rows:
+            st = r[1] - (r[1] - off) % slide
+            while st > r[1] - size:
+                if wm == A.LONG_MIN or st + size - 1 + late > wm:
+                    w = win.get((r[0], st))
+                    win[(r[0], st)] = list(r[2:]) if w is None else [w[0] + r[2]] + [
+                        merge_words(k, w[1 + j], r[3 + j]) for j, k in enumerate(kinds)]
+                st -= slide
+        return sorted((k, st, *w) for (k, st), w in win.items() if w[0] > 0)
     if c["window_kind"] != "CUMULATE":
         return sorted(rows)
     step, size = c["slide_ms"], c["size_ms"]
@@ -179,7 +201,7 @@ def test_heap_bytes_match_engine_state(case):
     for kg in range(128):                                      # KeyGroupRangeOffsets point at each section
         assert struct.unpack_from(">i", body, int(offs[kg]))[0] == kg
     kinds = [A.AGG_KINDS[a] for a, _ in aggs]
-    width = {"TUMBLE": c.get("size_ms"), "SLIDE": 5000, "CUMULATE": 5000}.get(c["window_kind"])
+    width = {"TUMBLE": c.get("size_ms"), "SLIDE": c.get("size_ms") if ds else 5000, "CUMULATE": 5000}.get(c["window_kind"])
     n = nulled = 0
     for kg in range(128):
         got = []
@@ -205,7 +227,11 @@ def test_heap_bytes_match_engine_state(case):
             assert {s64(k): sorted(v) for k, v in msets[kg].items()} == {k: sorted(v) for k, v in want.items()}
             ends = {(s64(e[0]), e[1]): e[2] for e in ents[kg]}
             assert all(ends[(s64(k), st)] == en for k, v in msets[kg].items() for st, en, _, _ in v)
-        if ds:
+        if sess and not ds:
+            # legacy Table WindowOperator: trigger and cleanup timer coincide at toEpochMillsForTimer(maxTimestamp)
+            want_t = {(tz_timer(case, e[2] - 1), s64(e[0]), e[1], e[2]) for e in ents[kg]}
+            assert sorted((t[0], s64(t[1]), t[2], t[3]) for t in timers[kg]) == sorted(want_t)
+        elif ds:
             # window.maxTimestamp() while unfired (EventTimeTrigger) + the cleanup time, per (key, window)
             want_t = set()
             for e in ents[kg]:
@@ -229,10 +255,10 @@ def test_heap_bytes_match_engine_state(case):
     assert n > 0
     if nh:
         assert nulled > 0                                      # the stream makes some aggregates NULL
-    if CASES[case]["window_kind"] != "CUMULATE":
-        assert n == snap["n"]
-    else:
+    if CASES[case]["window_kind"] == "CUMULATE":
         assert n < snap["n"]                                   # some fired slices were folded
+    elif not (ds and CASES[case]["window_kind"] == "SLIDE"):
+        assert n == snap["n"]
     g.close()
 
 
@@ -331,12 +357,12 @@ def test_heap_restore_resumes_with_rescale(case):
         g.close()
     tol = 1e-6 if "nullable_cols" in CASES[case] else 1e-9
     assert_rows_equal({f: np.concatenate([r[f] for r in got1]) for f in got1[0]}, first, names, rtol=tol)
-    if CASES[case]["window_kind"] == "SESSION":
+    if CASES[case]["window_kind"] == "SESSION" and CASES[case]["semantics"] == "DATASTREAM":
         # a run of the reference names an older window as a merged session's state namespace
         # (MergingWindowSet.addWindow :190-201): rename every state window and check the restore follows the mapping
         renamed = []
-        for b in bodies:
-            ents, timers, msets, _ = parse_heap(b, offsets_of(b), True, len(AGGS), True)
+        for b, (lo, _) in zip(bodies, halves):
+            ents, timers, msets, _ = parse_heap(b, offsets_of(b), True, len(AGGS), True, first_kg=lo)
             for kg in ents:
                 ents[kg] = [(k, st - 7, st + 1, acc) for k, st, en, acc in ents[kg]]
                 msets[kg] = {k: [(a, b_, a - 7, a + 1) for a, b_, _, _ in v] for k, v in msets[kg].items()}
@@ -357,11 +383,12 @@ def test_heap_restore_resumes_with_rescale(case):
             assert_rows_equal({f: np.concatenate([r[f] for r in outs]) for f in outs[0]}, final, names, rtol=tol)
 
 
-@pytest.mark.parametrize("kind", [dict(window_kind="SESSION", semantics="TABLE", gap_ms=700),
+@pytest.mark.parametrize("kind", [dict(window_kind="TUMBLE", semantics="TABLE", size_ms=5000),
                                   dict(window_kind="SLIDE", semantics="DATASTREAM", size_ms=15000, slide_ms=5000)])
 def test_heap_layout_unsupported_kinds(kind):
+    """Host-computed key hashes (FWA_KEY_PREHASHED): the restore could not place a key in its key group."""
     from flink_amd import engine
-    g = engine.WindowAggregator(A.make_config(aggs=AGGS, key_capacity=64, **kind))
+    g = engine.WindowAggregator(A.make_config(aggs=AGGS, key_capacity=64, key_kind=A.KEY_PREHASHED, **kind))
     with pytest.raises(engine.EngineError) as ei:
         g.snapshot_heap()
     assert A.STATUS[ei.value.code] == "E_UNSUPPORTED"
