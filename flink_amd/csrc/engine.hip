@@ -754,11 +754,12 @@ __device__ __noinline__ void pre_apply_global(unsigned long long* table, uint64_
 
 // W16: the tile's columns are read with 16-byte loads (two records per lane per column; 8-byte loads reach
 // roughly 0.6x the 16-byte rate, MI355X_MICROARCH.md): item j of a lane is record 2 * ((j / 2) * THREADS + tid) + j % 2.
-template <int NV, int ITEMS, int THREADS, int VW, int KG, int PRE = 0, int W16 = 0>
+template <int NV, int ITEMS, int THREADS, int VW, int KG, int PRE = 0, int W16 = 0, int EARLY = 0>
 __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
     static_assert(THREADS == kMaxPart && ITEMS <= 8, "one partition cursor per thread; trash area of 8 x kMaxPart");
     static_assert(!PRE || NV <= 1, "pre-aggregation: COUNT [+ one BIGINT sum]");
     static_assert(!W16 || (ITEMS % 2 == 0 && KG != 2 && NV <= 1), "paired loads: even ITEMS, no key-hash column");
+    static_assert(!EARLY || (W16 && !PRE && EARLY <= ITEMS / 2), "early loads: paired, no tile pre-aggregation");
     constexpr int kTile = THREADS * ITEMS;
     constexpr int kHt = 2 * kTile;                     // PRE: (key, slice) hash table, load <= 0.5
     constexpr int kHtLog = __builtin_ctz(kHt);
@@ -785,9 +786,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
     for (int r = tid; r < kRelCap / 4; r += THREADS) ((uint32_t*)s_code)[r] = ((const uint32_t*)a.relcode)[r];
     const int64_t ntiles = (a.n + kTile - 1) / kTile;
     const int sub = blockIdx.x % kSub;
-    unsigned long long r_key[ITEMS], r_v0[ITEMS], r_v1[ITEMS];
-    int64_t r_ts[ITEMS];
-    int32_t r_kh[ITEMS];
+    // one tile's loaded columns
+    struct Regs { unsigned long long key[ITEMS], v0[ITEMS], v1[ITEMS]; int64_t ts[ITEMS]; int32_t kh[ITEMS]; };
     // Column pointers resolved once (uniform, SGPRs): indexing the kernel-argument array per load
     // made hipcc fetch the pointer with a vector load and wait vmcnt(0) before every value load,
     // serialising the tile's loads item by item.
@@ -801,29 +801,33 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
     // every load of a tile is issued before any is used; uniform branches sit outside the item loops
     // (a per-item select between a 4- and an 8-byte load made hipcc wait vmcnt(0) at every join)
     auto xof = [&](int j) -> int { return W16 ? 2 * ((j >> 1) * THREADS + tid) + (j & 1) : j * THREADS + tid; };
-    auto load = [&](int64_t t) {
-        if constexpr (W16) {
-            // pair p = records 2p, 2p+1 of the tile; a pair reaching past n is not loaded (its record n-1, if any,
-            // goes to the slow path below)
+    // W16: pair p = records 2p, 2p+1 of the tile; a pair reaching past n is not loaded (its record n-1, if any, goes
+    // to the slow path below). Pairs [j0, j1) of tile t.
+    auto load_pairs = [&](Regs& R, int64_t t, int j0, int j1) {
 #pragma unroll
             for (int jj = 0; jj < ITEMS / 2; ++jj) {
+                if (jj < j0 || jj >= j1) continue;
                 const int64_t pi = t * (kTile / 2) + (int64_t)jj * THREADS + tid;
                 const int64_t ip = 2 * pi + 1 < n ? pi : 0;
                 const ulonglong2 kk = reinterpret_cast<const ulonglong2*>(pkeys)[ip];
                 const longlong2 tt = reinterpret_cast<const longlong2*>(pts)[ip];
-                r_key[2 * jj] = kk.x; r_key[2 * jj + 1] = kk.y;
-                r_ts[2 * jj] = tt.x; r_ts[2 * jj + 1] = tt.y;
+                R.key[2 * jj] = kk.x; R.key[2 * jj + 1] = kk.y;
+                R.ts[2 * jj] = tt.x; R.ts[2 * jj + 1] = tt.y;
                 if constexpr (NV > 0) {
                     if constexpr (w0) {
                         const ulonglong2 vv = reinterpret_cast<const ulonglong2*>(pc0)[ip];
-                        r_v0[2 * jj] = vv.x; r_v0[2 * jj + 1] = vv.y;
+                        R.v0[2 * jj] = vv.x; R.v0[2 * jj + 1] = vv.y;
                     } else {
                         const uint2 vv = reinterpret_cast<const uint2*>(pc0)[ip];
-                        r_v0[2 * jj] = vv.x; r_v0[2 * jj + 1] = vv.y;
+                        R.v0[2 * jj] = vv.x; R.v0[2 * jj + 1] = vv.y;
                     }
                 }
-                r_kh[2 * jj] = 0; r_kh[2 * jj + 1] = 0;
+                R.kh[2 * jj] = 0; R.kh[2 * jj + 1] = 0;
             }
+    };
+    auto load = [&](Regs& R, int64_t t) {
+        if constexpr (W16) {
+            load_pairs(R, t, 0, ITEMS / 2);
             return;
         }
         int64_t ic[ITEMS];
@@ -833,38 +837,40 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             ic[j] = i < n ? i : 0;
         }
 #pragma unroll
-        for (int j = 0; j < ITEMS; ++j) { r_key[j] = (unsigned long long)pkeys[ic[j]]; r_ts[j] = pts[ic[j]]; }
+        for (int j = 0; j < ITEMS; ++j) { R.key[j] = (unsigned long long)pkeys[ic[j]]; R.ts[j] = pts[ic[j]]; }
         if constexpr (NV > 0) {
             if constexpr (w0) {
 #pragma unroll
-                for (int j = 0; j < ITEMS; ++j) r_v0[j] = ((const unsigned long long*)pc0)[ic[j]];
+                for (int j = 0; j < ITEMS; ++j) R.v0[j] = ((const unsigned long long*)pc0)[ic[j]];
             } else {
 #pragma unroll
-                for (int j = 0; j < ITEMS; ++j) r_v0[j] = ((const uint32_t*)pc0)[ic[j]];
+                for (int j = 0; j < ITEMS; ++j) R.v0[j] = ((const uint32_t*)pc0)[ic[j]];
             }
         }
         if constexpr (NV > 1) {
             if constexpr (w1) {
 #pragma unroll
-                for (int j = 0; j < ITEMS; ++j) r_v1[j] = ((const unsigned long long*)pc1)[ic[j]];
+                for (int j = 0; j < ITEMS; ++j) R.v1[j] = ((const unsigned long long*)pc1)[ic[j]];
             } else {
 #pragma unroll
-                for (int j = 0; j < ITEMS; ++j) r_v1[j] = ((const uint32_t*)pc1)[ic[j]];
+                for (int j = 0; j < ITEMS; ++j) R.v1[j] = ((const uint32_t*)pc1)[ic[j]];
             }
         }
         if constexpr (KG == 2) {
 #pragma unroll
-            for (int j = 0; j < ITEMS; ++j) r_kh[j] = pkh[ic[j]];
+            for (int j = 0; j < ITEMS; ++j) R.kh[j] = pkh[ic[j]];
         } else {
 #pragma unroll
-            for (int j = 0; j < ITEMS; ++j) r_kh[j] = 0;
+            for (int j = 0; j < ITEMS; ++j) R.kh[j] = 0;
         }
     };
     long long pt = clock64();
     long long pacc[6] = {0, 0, 0, 0, 0, 0};
 #define QMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
+    Regs ra;
+    const int64_t G = gridDim.x;
     int64_t tile = blockIdx.x;
-    load(tile < ntiles ? tile : 0);
+    load(ra, tile < ntiles ? tile : 0);
     // the memory operations of one store phase, to the trash area: hipcc's waitcnt analysis merges the
     // loop entry with the back-edge, so an entry without the stores made the header wait vmcnt(0) on
     // every trip (draining the previous tile's stores)
@@ -877,7 +883,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         if (NV > 0) a.b_val0[o] = 0ull;
         if (NV > 1) a.b_val1[o] = 0ull;
     }
-    for (; tile < ntiles; tile += gridDim.x) {
+    // one tile: classify R, scan, reserve, issue the loads of tile `nx` into R, scatter, store
+    auto step = [&](Regs& R, int64_t tile, int64_t nx) {
         for (int i = tid; i < a.np; i += THREADS) hist[i] = 0;
         if constexpr (PRE) for (int i = tid; i < kHt / 4; i += THREADS) ((uint4*)ht)[i] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
@@ -889,17 +896,17 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         // next reuse of that register then waited vmcnt(0) -- draining the stores and the prefetch
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-            consume(r_key[j]);
-            consume(r_ts[j]);
-            if constexpr (NV > 0) consume(r_v0[j]);
-            if constexpr (NV > 1) consume(r_v1[j]);
-            if constexpr (KG == 2) consume(r_kh[j]);
+            consume(R.key[j]);
+            consume(R.ts[j]);
+            if constexpr (NV > 0) consume(R.v0[j]);
+            if constexpr (NV > 1) consume(R.v1[j]);
+            if constexpr (KG == 2) consume(R.kh[j]);
         }
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const int64_t i = t0 + xof(j);
-            const int64_t key = (int64_t)r_key[j];
-            const int64_t ts = r_ts[j];
+            const int64_t key = (int64_t)R.key[j];
+            const int64_t ts = R.ts[j];
             // slice relative to q_base: a timestamp within kRelCap slices of the base takes a 32-bit division
             // (one 32 x 33-bit multiply); anything else (and shift time zones) the exact 64-bit floor division
             uint64_t rel;
@@ -915,7 +922,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             }
             uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
             if constexpr (KG != 0) {
-                const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, r_kh[j]), c.max_par);
+                const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, R.kh[j]), c.max_par);
                 if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;
             }
             if (ds && ts == LONG_MIN_J) code = kCodeSlow;
@@ -949,10 +956,10 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 const uint64_t h = jm::mix64((uint64_t)key);
                 const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
                 const int x = xof(j);
-                x_key[x] = r_key[j];
+                x_key[x] = R.key[j];
                 x_rel[x] = (uint16_t)rel;
-                if (NV > 0) x_val[0][x] = r_v0[j];
-                if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = r_v1[j];
+                if (NV > 0) x_val[0][x] = R.v0[j];
+                if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = R.v1[j];
                 if constexpr (PRE) {
                     x_n[x] = rn;
                     r_pos[j] = a.pcount ? ((p << 16) | atomicAdd(&hist[p], 1u))   // partial rows: no merge
@@ -960,6 +967,9 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 }
                 else r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
             }
+            // EARLY: pair j/2 of this tile is staged; its registers take the next tile's pair now, so loads are in
+            // flight through the classify and the scan (the reservation below then waits for these loads)
+            if constexpr (EARLY > 0) if ((j & 1) && (j >> 1) < EARLY) load_pairs(R, nx < ntiles ? nx : tile, j >> 1, (j >> 1) + 1);
         }
         if constexpr (PRE) {
             __syncthreads();                        // the tile's staged (key, rel) visible to every lane
@@ -967,7 +977,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             for (int j = 0; j < ITEMS; ++j) {
                 if (r_pos[j] == ~0u || !(r_pos[j] & 0x80000000u)) continue;
                 const uint32_t x = (uint32_t)xof(j);
-                const unsigned long long key = r_key[j];
+                const unsigned long long key = R.key[j];
                 const uint32_t rel = x_rel[x];
                 uint32_t hs = ((uint32_t)key * 0x9E3779B1u + (uint32_t)(key >> 32) * 0x85EBCA77u + rel * 0xC2B2AE3Du) >> (32 - kHtLog);
                 for (int probe = 0; probe < kHt; ++probe) {
@@ -980,7 +990,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                     const uint32_t o = old - 1u;
                     if (x_key[o] == key && x_rel[o] == rel) {   // merge into the representative
                         atomicAdd(&x_n[o], 1u);
-                        if constexpr (NV > 0) atomicAdd(&x_val[0][o], r_v0[j]);
+                        if constexpr (NV > 0) atomicAdd(&x_val[0][o], R.v0[j]);
                         r_pos[j] = ~0u;
                         break;
                     }
@@ -1000,7 +1010,9 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         const uint32_t h = p < a.np ? hist[p] : 0u;
         uint32_t g = 0;
         if (h) g = atomicAdd(&a.b_cnt[p * kSub + sub], h);
-        load(tile + gridDim.x < ntiles ? tile + gridDim.x : tile);   // next tile in flight from here on (unconditional)
+        // the next tile in flight from here on (unconditional); EARLY: its first pairs were issued while classifying
+        if constexpr (EARLY) load_pairs(R, nx < ntiles ? nx : tile, EARLY, ITEMS / 2);
+        else load(R, nx < ntiles ? nx : tile);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {               // the LDS scatter does not need the reservation: the
             if (r_pos[j] == ~0u) continue;              // reservation's latency overlaps this loop
@@ -1055,7 +1067,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         QMARK(3);
         __syncthreads();
         QMARK(4);
-    }
+    };
+    for (; tile < ntiles; tile += G) step(ra, tile, tile + G);
     if (a.prof && tid == 0) for (int q = 0; q < 6; ++q) a.prof[(int64_t)blockIdx.x * 8 + q] = pacc[q];
 #undef QMARK
     for (int sh = 32; sh >= 1; sh >>= 1) {
@@ -1819,7 +1832,17 @@ struct Sess2Args {
     unsigned long long* pk;      // [nb][pkw] the element's COUNT + accumulator words, in bulk order (one row per
                                  // element gathered once after the sort, not one value column per accumulator)
     int64_t* pe;                 // [nb] end of a flagged element
-    int32_t pkw, pad_pk;
+    uint32_t* sg_kid;            // segment kernel staging: wave w's clusters at [h0(w), h0(w) + count(w)) (no atomics)
+    int64_t* sg_start;
+    int64_t* sg_end;
+    unsigned long long* sg_acc;  // [nacc][cap]
+    int64_t sg_cap;
+    uint32_t* sg_cnt;            // [nw + 1] clusters per wave
+    uint32_t* sg_off;            // [nw + 1] their exclusive sum
+    int64_t* sg_h0;              // [nw] first owned position per wave
+    int32_t pkw;
+    int32_t seg_out;             // bulk sessions appended on ctr->n_out_sp by sess2_segment_kernel (the arrival-order
+                                 // path appends after them on the same counter)
     int64_t* bend;               // [nb] window / session end per sorted element
     int64_t* bmax;               // [nb] inclusive max of bend over the key so far (segmented scan)
     uint32_t* bcid;              // [nb] head flags, then 1-based cluster ids (inclusive sum)
@@ -1968,18 +1991,19 @@ __global__ void __launch_bounds__(kBlock) sess2_route_kernel(Sess2Args a, const 
             a.bval[o] = (uint32_t)o | (flag ? 0x80000000u : 0u);
             unsigned long long* row = a.pk + (int64_t)o * a.pkw;
             const int64_t x = (int64_t)(pay & 0x7fffffffu);
-            if (sess) {
-                for (int cc = 0; cc < a.pkw; ++cc) row[cc] = a.in.acc[(int64_t)cc * a.in.stride + x];
-                a.pe[o] = a.in.end[x];
-            } else {
-                const EngineConst& c = *cp;
-                row[0] = 1ull;
-                for (int cc = 1; cc < a.pkw; ++cc) {
-                    const AggDesc& d = c.agg[a.col_owner[cc]];
-                    row[cc] = acc_input(d, a.cols[d.col], x, a.nulls[d.col]);
-                }
-                if (a.gapc) a.pe[o] = jm::wadd(a.ts[x], a.gapc[x]);
-            }
+            const EngineConst& c = *cp;
+            auto word = [&](int cc) -> unsigned long long {
+                if (sess) return a.in.acc[(int64_t)cc * a.in.stride + x];
+                if (cc == 0) return 1ull;
+                const AggDesc& d = c.agg[a.col_owner[cc]];
+                return acc_input(d, a.cols[d.col], x, a.nulls[d.col]);
+            };
+            int cc = 0;
+            if ((a.pkw & 1) == 0)                                  // 16-byte stores (rows stay 16-byte aligned)
+                for (; cc < a.pkw; cc += 2) *reinterpret_cast<ulonglong2*>(row + cc) = make_ulonglong2(word(cc), word(cc + 1));
+            for (; cc < a.pkw; ++cc) row[cc] = word(cc);
+            if (sess) a.pe[o] = a.in.end[x];
+            else if (a.gapc) a.pe[o] = jm::wadd(a.ts[x], a.gapc[x]);
         }
         if (valid && sp) { const unsigned long long o = ps + __popcll(ms & lt); a.skey[o] = sk; a.sval[o] = pay; }
         pb += __popcll(mb);
@@ -2071,6 +2095,176 @@ __global__ void __launch_bounds__(kBlock) sess2_reduce_kernel(Sess2Args a, const
     }
 }
 
+// Bulk sessions after the (kid, start) sort in one pass, replacing ends / scan-by-key / heads / cluster-id scan /
+// reduce: wave w owns the keys whose first sorted element lies in positions [64w, 64w + 64) and walks each owned key
+// to its end in 64-element chunks, carrying the open cluster (the session being built) from chunk to chunk. Per chunk:
+// the ends (start + gap, or the element's own end), the key's running max end (segmented shuffle scan; lane 0 joins
+// the carried key), cluster heads (a new key, or a start after every earlier end of the key: TimeWindow.intersects is
+// inclusive, so touching windows merge), the accumulators per cluster (segmented shuffle scans over the packed
+// rows) and the completed clusters appended to the output list (one reservation per wave and chunk).
+template <int NA>
+__global__ void __launch_bounds__(kBlock) sess2_segment_kernel(Sess2Args a, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    const int lane = threadIdx.x & 63;
+    const uint64_t smask = ((uint64_t)1 << a.tb) - 1;              // tb <= 63 - kid bits on this path
+    const int64_t nb = a.nb;
+    const int64_t nw = (nb + 63) >> 6;
+    const int64_t wstride = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    int ak[NA];
+#pragma unroll
+    for (int cc = 0; cc < NA; ++cc) ak[cc] = cc == 0 ? ACC_ADD_I64 : c.acc_kind[cc];
+    const unsigned long long below = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);   // lanes <= this one
+    for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
+        const int64_t p0 = w << 6;
+        // a window of 128 sorted positions (this wave's 64 and the next 64) and the element before, loaded at once:
+        // the heads, the end of the last owned key and the first two chunks come from it (one round trip)
+        const int64_t pa = p0 + lane, pb = p0 + 64 + lane;
+        const unsigned long long kA = pa < nb ? a.bkey[pa] : 0ull, kB = pb < nb ? a.bkey[pb] : 0ull;
+        const uint32_t vA = pa < nb ? a.bval[pa] : 0u, vB = pb < nb ? a.bval[pb] : 0u;
+        const unsigned long long kprev = p0 > 0 ? a.bkey[p0 - 1] : 0ull;
+        const uint32_t kidA = (uint32_t)(kA >> a.tb), kidB = (uint32_t)(kB >> a.tb);
+        const uint32_t kup = __shfl_up(kidA, 1);
+        const bool hd = pa < nb && (lane == 0 ? (p0 == 0 || (uint32_t)(kprev >> a.tb) != kidA) : kidA != kup);
+        const unsigned long long hm = __ballot(hd);
+        if (!hm) {                                                  // inside a key owned by an earlier wave
+            if (lane == 0) a.sg_cnt[w] = 0u;
+            continue;
+        }
+        const int64_t h0 = p0 + (__ffsll((long long)hm) - 1);
+        uint32_t wc = 0;                                            // clusters this wave wrote (staging h0 + i)
+        int64_t h1 = min(p0 + 64, nb);
+        if (h1 < nb) {                                              // the last owned key may run past the range
+            const uint32_t kl = __shfl(kidA, 63);
+            const unsigned long long dm = __ballot(pb >= nb || kidB != kl);
+            if (dm) h1 = p0 + 64 + (__ffsll((long long)dm) - 1);
+            else
+                for (int64_t q = p0 + 128;; q += 64) {
+                    const int64_t pp = q + lane;
+                    const unsigned long long dq = __ballot(pp >= nb || (uint32_t)(a.bkey[pp] >> a.tb) != kl);
+                    if (dq) { h1 = q + (__ffsll((long long)dq) - 1); break; }
+                }
+        }
+        // chunk loads: key, payload, end, accumulator row of position base + lane (window or memory)
+        auto fetch = [&](int64_t base, unsigned long long& bk, uint32_t& pay, int64_t& en, unsigned long long* x) {
+            const int64_t q = base + lane;
+            const int64_t d = q - p0;
+            if (base + 63 - p0 < 128) {                             // inside the window
+                const int src = (int)(d & 63);
+                const unsigned long long ka = __shfl(kA, src), kb = __shfl(kB, src);
+                const uint32_t va = __shfl(vA, src), vb = __shfl(vB, src);
+                bk = d < 64 ? ka : kb;
+                pay = d < 64 ? va : vb;
+            } else {
+                bk = q < h1 ? a.bkey[q] : 0ull;
+                pay = q < h1 ? a.bval[q] : 0u;
+            }
+            const bool v = q < h1;
+            const int64_t st = a.base + (int64_t)(bk & smask);
+            en = !v ? LONG_MIN_J : (pay & 0x80000000u) ? a.pe[pay & 0x7fffffffu] : jm::wadd(st, a.gap);
+            const uint32_t o = pay & 0x7fffffffu;
+#pragma unroll
+            for (int cc = 0; cc < NA; ++cc) x[cc] = v ? a.pk[(int64_t)o * a.pkw + cc] : 0ull;
+        };
+        uint32_t ck = 0u;                                           // the carried open cluster
+        int64_t cmax = LONG_MIN_J, cst = 0;
+        unsigned long long cacc[NA];
+#pragma unroll
+        for (int cc = 0; cc < NA; ++cc) cacc[cc] = 0ull;
+        bool copen = false;
+        unsigned long long nbk, nx[NA];                             // the next chunk, in flight (software pipeline)
+        uint32_t npay;
+        int64_t nen;
+        fetch(h0, nbk, npay, nen, nx);
+        for (int64_t base = h0; base < h1; base += 64) {
+            const int64_t q = base + lane;
+            const bool v = q < h1;
+            const unsigned long long bk = nbk;
+            const int64_t en = nen;
+            unsigned long long acc[NA];
+#pragma unroll
+            for (int cc = 0; cc < NA; ++cc) acc[cc] = nx[cc];
+            if (base + 64 < h1) fetch(base + 64, nbk, npay, nen, nx);
+            const uint32_t kk = (uint32_t)(bk >> a.tb);
+            const int64_t st = a.base + (int64_t)(bk & smask);
+            const uint32_t kp = __shfl_up(kk, 1);
+            const bool kc = v && (lane == 0 ? (!copen || kk != ck) : kk != kp);
+            const unsigned long long km = __ballot(kc) & below;
+            const int ks = km ? 63 - __clzll((long long)km) : 0;   // first lane of this lane's key in the chunk
+            int64_t m = en;                                         // running max end of the key (inclusive)
+            for (int d = 1; d < 64; d <<= 1) {
+                const int64_t y = __shfl_up(m, d);
+                if (lane - d >= ks && y > m) m = y;
+            }
+            if (km == 0 && copen && cmax > m) m = cmax;            // the key continues from the previous chunk
+            int64_t mprev = __shfl_up(m, 1);
+            if (lane == 0) mprev = cmax;
+            const bool head = v && (kc || st > mprev);
+            const unsigned long long hb = __ballot(head) & below;
+            const int cs = hb ? 63 - __clzll((long long)hb) : 0;   // first lane of this lane's cluster in the chunk
+            const bool ccont = hb == 0;                            // still the carried cluster
+            const int64_t hst = __shfl(st, cs);
+            const int64_t cstart = ccont ? cst : hst;
+#pragma unroll
+            for (int cc = 0; cc < NA; ++cc) {
+                unsigned long long x = acc[cc];
+                for (int d = 1; d < 64; d <<= 1) {
+                    const unsigned long long y = __shfl_up(x, d);
+                    if (lane - d >= cs) x = acc_combine(ak[cc], x, y);
+                }
+                if (ccont && copen) x = acc_combine(ak[cc], cacc[cc], x);
+                acc[cc] = x;
+            }
+            const bool nxt = __shfl_down(head ? 1 : 0, 1) != 0;
+            const bool tail = v && (q + 1 == h1 || (lane < 63 && nxt));
+            const bool emit_c = copen && __shfl(head ? 1 : 0, 0) != 0;   // the carried cluster ended before lane 0
+            if (emit_c && lane == 0) {
+                const int64_t sc = h0 + (int64_t)wc;
+                a.sg_kid[sc] = ck;
+                a.sg_start[sc] = cst;
+                a.sg_end[sc] = cmax;
+#pragma unroll
+                for (int cc = 0; cc < NA; ++cc) a.sg_acc[(int64_t)cc * a.sg_cap + sc] = cacc[cc];
+            }
+            wc += emit_c ? 1u : 0u;
+            const unsigned long long tm = __ballot(tail);
+            if (tail) {
+                const int64_t so = h0 + (int64_t)wc + __popcll(tm & ((1ull << lane) - 1ull));
+                a.sg_kid[so] = kk;
+                a.sg_start[so] = cstart;
+                a.sg_end[so] = m;                                   // the key's max end at the cluster's last element
+#pragma unroll
+                for (int cc = 0; cc < NA; ++cc) a.sg_acc[(int64_t)cc * a.sg_cap + so] = acc[cc];
+            }
+            wc += (uint32_t)__popcll(tm);
+            ck = __shfl(kk, 63);
+            cmax = __shfl(m, 63);
+            cst = __shfl(cstart, 63);
+#pragma unroll
+            for (int cc = 0; cc < NA; ++cc) cacc[cc] = __shfl(acc[cc], 63);
+            copen = true;
+        }
+        if (lane == 0) { a.sg_cnt[w] = wc; a.sg_h0[w] = h0; }
+    }
+}
+
+// The segment kernel's clusters, moved from each wave's staging range to the output list at the exclusive sum of the
+// per-wave counts (one thread per wave; the arrival-order path appends after them on ctr->n_out_sp).
+__global__ void __launch_bounds__(kBlock) sess2_compact_kernel(Sess2Args a, int64_t nw, int nacc) {
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t o0 = a.sg_off[w], o1 = a.sg_off[w + 1];
+        if (o1 == o0) continue;
+        const int64_t h0 = a.sg_h0[w];
+        for (uint32_t i = 0; i < o1 - o0; ++i) {
+            const int64_t src = h0 + i, dst = (int64_t)o0 + i;
+            a.out.kid[dst] = a.sg_kid[src];
+            a.out.start[dst] = a.sg_start[src];
+            a.out.end[dst] = a.sg_end[src];
+            for (int cc = 0; cc < nacc; ++cc) a.out.acc[(int64_t)cc * a.out.stride + dst] = a.sg_acc[(int64_t)cc * a.sg_cap + src];
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr->n_out_sp = a.sg_off[nw];
+}
+
 __device__ __forceinline__ int64_t sess_key_of(const unsigned long long* key_table, int64_t capacity, uint32_t kid) {
     return (int64_t)kid < capacity ? (int64_t)key_table[kid] : LONG_MIN_J;   // side slot: the sentinel key
 }
@@ -2082,7 +2276,7 @@ __global__ void __launch_bounds__(kBlock) sess2_ordered_kernel(Sess2Args a, cons
     const EngineConst& c = *cp;
     const int nacc = c.nacc;
     const bool table = c.sem == FWA_SEM_TABLE;
-    const int64_t ncl = a.nb > 0 ? (int64_t)a.bcid[a.nb - 1] : 0;
+    const int64_t ncl = (a.seg_out || a.nb == 0) ? 0 : (int64_t)a.bcid[a.nb - 1];
     unsigned long long dropped = 0;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.nsp; t += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t kid = (uint32_t)(a.skey[t] >> 32);
@@ -2538,6 +2732,8 @@ struct fwa_engine {
     uint32_t* d_sval[4] = {};
     int64_t* d_send2 = nullptr;
     unsigned long long* d_spk = nullptr;   // session bulk rows (Sess2Args::pk)
+    void* d_sg = nullptr;                  // segment kernel staging (Sess2Args::sg_*)
+    int64_t sg_cap = 0, sgw_cap = 0;
     int64_t* d_spe = nullptr;
     int64_t* d_smax = nullptr;
     uint32_t* d_scid = nullptr;
@@ -2973,7 +3169,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -3409,6 +3605,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     const bool kg_all = e->cfg.kg_start == 0 && e->cfg.kg_end == e->cfg.max_parallelism - 1;
     const int kgm = kg_all ? 0 : (e->cfg.key_kind == FWA_KEY_PREHASHED ? 2 : 1);
     static const bool now16 = getenv("FWA_NOW16") != nullptr;  // A/B switch: 8-byte Phase P loads
+    static const int pdb = getenv("FWA_PDB") ? atoi(getenv("FWA_PDB")) : 0;   // A/B: next-tile pairs issued in classify
     auto al16 = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; };
     const bool w16 = !now16 && !p2 && kgm == 0 && al16(pa.keys) && al16(pa.ts) &&
                      (e->nv == 0 || ((uintptr_t)pa.cols[pa.vcol[0]] & ((e->vsize[0] == 8) ? 15 : 7)) == 0);
@@ -3422,6 +3619,9 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else partition3_kernel<NV, 4, 1024, 3, 2, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
     if (pre) { if (e->nv == 0) PRELAUNCH(0); else PRELAUNCH(1); }
     else if (e->nv == 0) P2LAUNCH(0, 8, 3);
+    else if (e->nv == 1 && w16 && (vw & 1) && pdb == 1) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
+    else if (e->nv == 1 && w16 && (vw & 1) && pdb == 2) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
+    else if (e->nv == 1 && w16 && (vw & 1) && pdb == 3) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 3><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1) { if (vw & 1) P2LAUNCH(1, 6, 3); else P2LAUNCH(1, 6, 2); }
@@ -3684,6 +3884,48 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
                                                      (const uint32_t*)e->d_sval[0], e->d_sval[1], (int)nb, 0, e->kid_bits + tb, e->stream));
         s.bkey = e->d_skey[1];
         s.bval = e->d_sval[1];
+    }
+    static const bool scan_path = getenv("FWA_SESS_SCAN") != nullptr;   // A/B: the r02 multi-pass bulk path
+    s.seg_out = (!scan_path && e->nacc <= 5) ? 1 : 0;
+    if (nb > 0 && s.seg_out) {
+        const int64_t nw = (nb + 63) / 64;
+        if (nb > e->sg_cap || nw + 1 > e->sgw_cap) {
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            if (e->d_sg) HIPCHK(e, hipFree(e->d_sg));
+            e->d_sg = nullptr;
+            e->sg_cap = std::max<int64_t>(nb + nb / 4, 1 << 14);
+            e->sgw_cap = (e->sg_cap + 63) / 64 + 1;
+            const size_t bytes = (size_t)e->sg_cap * (4 + 8 + 8 + 8 * (size_t)e->nacc) + (size_t)e->sgw_cap * (4 + 4 + 8) + 1024;
+            HIPCHK(e, hipMalloc(&e->d_sg, bytes));
+        }
+        char* sp = (char*)e->d_sg;
+        s.sg_start = (int64_t*)sp; sp += 8 * (size_t)e->sg_cap;
+        s.sg_end = (int64_t*)sp; sp += 8 * (size_t)e->sg_cap;
+        s.sg_acc = (unsigned long long*)sp; sp += 8 * (size_t)e->sg_cap * e->nacc;
+        s.sg_h0 = (int64_t*)sp; sp += 8 * (size_t)e->sgw_cap;
+        s.sg_kid = (uint32_t*)sp; sp += 4 * (size_t)e->sg_cap;
+        s.sg_cnt = (uint32_t*)sp; sp += 4 * (size_t)e->sgw_cap;
+        s.sg_off = (uint32_t*)sp;
+        s.sg_cap = e->sg_cap;
+        const unsigned sg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nb + 255) / 256, 1 << 16));
+        switch (e->nacc) {
+            case 1: sess2_segment_kernel<1><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
+            case 2: sess2_segment_kernel<2><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
+            case 3: sess2_segment_kernel<3><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
+            case 4: sess2_segment_kernel<4><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
+            default: sess2_segment_kernel<5><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
+        }
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipMemsetAsync(s.sg_cnt + nw, 0, 4, e->stream));
+        size_t bytes = 0;
+        HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s.sg_cnt, s.sg_off, (int)(nw + 1), e->stream));
+        if ((rc = ensure_sort_tmp(e, bytes))) return rc;
+        bytes = e->sort_tmp_bytes;
+        HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(e->d_sort_tmp, bytes, s.sg_cnt, s.sg_off, (int)(nw + 1), e->stream));
+        sess2_compact_kernel<<<grid_for(nw, 256 * 8), kBlock, 0, e->stream>>>(s, nw, e->nacc);
+        HIPCHK(e, hipGetLastError());
+    } else if (nb > 0) {
+        size_t bytes = 0;
         sess2_ends_kernel<<<grid_for(nb, 256 * 32), kBlock, 0, e->stream>>>(s);
         HIPCHK(e, hipGetLastError());
         KidEq eq{tb};
@@ -3743,7 +3985,7 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     HIPCHK(e, hipEventRecord(e->ev[1], e->stream));
     uint32_t ncl = 0;
     unsigned long long lrn = (unsigned long long)e->late_rows;
-    if (nb > 0) HIPCHK(e, hipMemcpyAsync(&ncl, e->d_scid + nb - 1, 4, hipMemcpyDeviceToHost, e->stream));
+    if (nb > 0 && !s.seg_out) HIPCHK(e, hipMemcpyAsync(&ncl, e->d_scid + nb - 1, 4, hipMemcpyDeviceToHost, e->stream));
     if (nsp > 0) HIPCHK(e, hipMemcpyAsync(&lrn, e->d_lr_n, 8, hipMemcpyDeviceToHost, e->stream));
     if ((rc = read_sess_ctr(e))) return rc;
     if ((rc = account_ingest(e))) return rc;

@@ -216,7 +216,17 @@ def test_heap_bytes_match_engine_state(case):
                     assert acc[1 + j] == 0
                     words[j] = IDENT.get(k, 0)
             got.append((s64(key), start, s64(acc[0]), *words, *[s64(x) for x in acc[1 + len(kinds):]]))
-        assert sorted(got) == expected_state(case, snap, kg, wm), kg
+        exp = expected_state(case, snap, kg, wm)
+        if ds and c["window_kind"] == "SLIDE":
+            # a window merges several slices: floating sums are added in another order than the test's (tolerance)
+            fl = [3 + j for j, k in enumerate(kinds) if k in (2, 3, 11, 12)]
+            as_f = lambda w: struct.unpack("<d", struct.pack("<q", w))[0]   # noqa: E731
+            strip = lambda rows: [tuple(x for i, x in enumerate(r) if i not in fl) for r in rows]   # noqa: E731
+            g_, e_ = sorted(got), sorted(exp)
+            assert strip(g_) == strip(e_), kg
+            assert all(np.isclose(as_f(a[i]), as_f(b[i]), rtol=1e-12, atol=1e-12) for a, b in zip(g_, e_) for i in fl), kg
+        else:
+            assert sorted(got) == exp, kg
         n += len(got)
         if sess:                                               # every in-flight session maps to itself
             sl = S.entries_of_key_group(snap, kg)
