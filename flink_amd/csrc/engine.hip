@@ -465,6 +465,11 @@ struct PartArgs {
     int64_t stride;
     DevStatus* st;
     long long* prof;                   // optional per-block phase cycle counters (FWA_PPROF)
+    // flat layout (part_hist_kernel first): block b owns tiles [b * tpb, (b + 1) * tpb) and writes partition p's
+    // records at [flat_off[p * G + b], ...) -- no reservation atomics, no overflow, holes for records not accepted
+    const uint32_t* flat_off;          // [np * G + 1] exclusive sum of the (partition, block) counts, or nullptr
+    int64_t tpb;
+    int64_t flat_cap;
 };
 
 __device__ __forceinline__ bool row_has_null(const PartArgs& a, int64_t i) {
@@ -518,6 +523,36 @@ __device__ __forceinline__ void consume(unsigned long long x) {
 __device__ __forceinline__ void consume(int64_t x) { consume((unsigned long long)x); }
 __device__ __forceinline__ void consume(int32_t x) { asm volatile("" : : "v"(x)); }
 __device__ __forceinline__ void consume(uint32_t x) { asm volatile("" : : "v"(x)); }
+
+// Flat Phase P layout, pass 1: records per (partition, block) over exactly the tiles Phase P gives
+// each block (a contiguous run of tpb tiles), from the keys alone, written partition-major; their exclusive sum is
+// every block's private, contiguous output range per partition. Phase P then needs no reservation atomics (r02
+// clock profile: 43 % of Phase P waited on them) and a partition's entries are contiguous and in time order.
+// skip_last: the record n-1 of an odd n that paired 16-byte loads leave to the replay (no bucket slot).
+__global__ void __launch_bounds__(1024) part_hist_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t tile,
+                                                         int64_t tpb, int part_bits, int np, int skip_last,
+                                                         uint32_t* __restrict__ counts) {
+    __shared__ uint32_t hist[kMaxPart];
+    for (int i = threadIdx.x; i < np; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * tpb * tile;
+    const int64_t i1 = min(i0 + tpb * tile, n - (skip_last ? 1 : 0));
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+        const uint64_t h = jm::mix64((uint64_t)keys[i]);
+        atomicAdd(&hist[part_bits ? (uint32_t)(h >> (64 - part_bits)) : 0u], 1u);
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < np; p += blockDim.x) counts[(int64_t)p * gridDim.x + blockIdx.x] = hist[p];
+}
+
+// The flat layout never overflows; its skew signal is what the sub-bucket layout would have overflowed: entries of a
+// partition past kSub sub-buckets of capacity capb (DevStatus::ovf_n, the PRE switch of push_settle).
+__global__ void flat_skew_kernel(const uint32_t* offs, int np, int g, int64_t lim, DevStatus* st) {
+    for (int p = threadIdx.x; p < np; p += blockDim.x) {
+        const int64_t tot = (int64_t)offs[(int64_t)(p + 1) * g] - (int64_t)offs[(int64_t)p * g];
+        if (tot > lim) atomicAdd(&st->ovf_n, (int32_t)min<int64_t>(tot - lim, INT32_MAX / 4));
+    }
+}
 
 // partition2: Phase P with the next tile's loads in flight while the current tile is scanned,
 // reserved and stored (r01 ablation: without its bucket stores Phase P still took 0.58 ms per 2^26
@@ -869,8 +904,15 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
 #define QMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
     Regs ra;
     const int64_t G = gridDim.x;
-    int64_t tile = blockIdx.x;
-    load(ra, tile < ntiles ? tile : 0);
+    const bool flat = a.flat_off != nullptr;
+    int64_t tile = blockIdx.x, tstep = G, tend = ntiles;            // tiles of this block
+    if (flat) {
+        tile = (int64_t)blockIdx.x * a.tpb;
+        tstep = 1;
+        tend = min(ntiles, tile + a.tpb);
+        for (int q = tid; q < a.np; q += THREADS) sbase[q] = a.flat_off[(int64_t)q * G + blockIdx.x];   // cursors
+    }
+    load(ra, tile < tend ? tile : 0);
     // the memory operations of one store phase, to the trash area: hipcc's waitcnt analysis merges the
     // loop entry with the back-edge, so an entry without the stores made the header wait vmcnt(0) on
     // every trip (draining the previous tile's stores)
@@ -966,10 +1008,21 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                                         : (0x80000000u | p);                        // bucketed after the merge
                 }
                 else r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
+            } else if (!PRE && flat && i < a.n && !(W16 && i == a.n - 1 && (a.n & 1))) {
+                // flat layout: every record the histogram counted takes its slot; one not accepted leaves a hole
+                // (rel 0xFFFF, skipped by Phase A)
+                const uint64_t h = jm::mix64((uint64_t)key);
+                const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
+                const int x = xof(j);
+                x_key[x] = R.key[j];
+                x_rel[x] = 0xFFFF;
+                if (NV > 0) x_val[0][x] = 0ull;
+                if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = 0ull;
+                r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
             }
             // EARLY: pair j/2 of this tile is staged; its registers take the next tile's pair now, so loads are in
             // flight through the classify and the scan (the reservation below then waits for these loads)
-            if constexpr (EARLY > 0) if ((j & 1) && (j >> 1) < EARLY) load_pairs(R, nx < ntiles ? nx : tile, j >> 1, (j >> 1) + 1);
+            if constexpr (EARLY > 0) if ((j & 1) && (j >> 1) < EARLY) load_pairs(R, nx < tend ? nx : tile, j >> 1, (j >> 1) + 1);
         }
         if constexpr (PRE) {
             __syncthreads();                        // the tile's staged (key, rel) visible to every lane
@@ -1009,10 +1062,11 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         const int p = tid;
         const uint32_t h = p < a.np ? hist[p] : 0u;
         uint32_t g = 0;
-        if (h) g = atomicAdd(&a.b_cnt[p * kSub + sub], h);
+        if (flat) { if (p < a.np) { g = sbase[p]; sbase[p] = g + h; } }   // the block's own cursor
+        else if (h) g = atomicAdd(&a.b_cnt[p * kSub + sub], h);
         // the next tile in flight from here on (unconditional); EARLY: its first pairs were issued while classifying
-        if constexpr (EARLY) load_pairs(R, nx < ntiles ? nx : tile, EARLY, ITEMS / 2);
-        else load(R, nx < ntiles ? nx : tile);
+        if constexpr (EARLY) load_pairs(R, nx < tend ? nx : tile, EARLY, ITEMS / 2);
+        else load(R, nx < tend ? nx : tile);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {               // the LDS scatter does not need the reservation: the
             if (r_pos[j] == ~0u) continue;              // reservation's latency overlaps this loop
@@ -1027,7 +1081,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             // per (tile, overflowing partition) -- a per-wave reservation on the single spill counter
             // serialised ~100 K same-address device atomics per push under Zipf(1.1)
             const uint64_t end = (uint64_t)g + h;
-            if (end > (uint64_t)a.capb) {
+            if (!flat && end > (uint64_t)a.capb) {
                 const uint32_t ov = (uint32_t)(end - std::max<uint64_t>(g, (uint64_t)a.capb));
                 atomicAdd(&a.st->ovf_n, (int32_t)ov);
                 if constexpr (!PRE) sbase[p] = (uint32_t)atomicAdd(&a.st->spill_n, (int32_t)ov);
@@ -1045,8 +1099,9 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             const uint32_t p = valid ? s_part[sidx] : 0u;
             const uint32_t x = valid ? s_src[sidx] : 0u;
             const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
-            const bool inb = valid && dst < (uint64_t)a.capb;
-            if (valid && !inb) {                // sub-bucket full (skewed keys)
+            const bool inb = valid && dst < (uint64_t)(flat ? a.flat_cap : a.capb);
+            if (flat && valid && !inb) raise_error(a.st, FWA_E_STATE);   // cannot happen: sized by the histogram
+            else if (valid && !inb) {           // sub-bucket full (skewed keys)
                 if constexpr (PRE) {            // a merged entry has no record index to replay: apply it now
                     const int32_t slot = a.rel2slot[x_rel[x]];
                     if (slot >= 0)
@@ -1057,7 +1112,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                     put_idx(a.spill, (int64_t)sbase[p] + (int64_t)(dst - first), a.spill_cap, (int32_t)(t0 + x), a.st);
                 }
             }
-            const uint64_t o = inb ? ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst : a.trash + (uint64_t)(jj * THREADS + tid);
+            const uint64_t o = !inb ? a.trash + (uint64_t)(jj * THREADS + tid)
+                             : flat ? dst : ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
             a.b_key[o] = x_key[x];
             a.b_rel[o] = x_rel[x];
             if constexpr (PRE) a.b_n[o] = (uint16_t)x_n[x];
@@ -1068,7 +1124,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         __syncthreads();
         QMARK(4);
     };
-    for (; tile < ntiles; tile += G) step(ra, tile, tile + G);
+    for (; tile < tend; tile += tstep) step(ra, tile, tile + tstep);
     if (a.prof && tid == 0) for (int q = 0; q < 6; ++q) a.prof[(int64_t)blockIdx.x * 8 + q] = pacc[q];
 #undef QMARK
     for (int sh = 32; sh >= 1; sh >>= 1) {
@@ -1107,6 +1163,8 @@ struct CombineArgs {
     int32_t abl;                       // ablation bits (timing experiments only)
     DevStatus* st;
     long long* prof;                   // optional per-block phase cycle counters (FWA_APROF)
+    const uint32_t* flat_off;          // flat layout: partition p = [flat_off[p * G], flat_off[(p + 1) * G]), or nullptr
+    int32_t flat_g, pad_f;
 };
 
 __device__ __forceinline__ unsigned long long ident_of(int acc_kind) { return acc_kind == ACC_MIN_ORD ? ~0ull : 0ull; }
@@ -1218,10 +1276,17 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         const unsigned long long id = LAYOUT == 1 ? 0ull : ident_of(s_desc[cc] & 0xff);
         for (int i = tid; i < SL * seg; i += TH) lacc[(size_t)(cc - 1) * SL * seg + i] = id;
     }
-    const int64_t my_cnt = min((int64_t)a.b_cnt[p * kSub + sub], a.capb);
-    const int64_t boff = ((int64_t)p * kSub + sub) * a.capb;
+    constexpr int64_t kChunk = (int64_t)IT * LPS;
+    const bool flat = a.flat_off != nullptr;
+    // sub-buckets: this wave's own list; flat layout: the partition's contiguous range, each chunk of
+    // kSub * kChunk entries split across the waves (all waves stay in the same stretch of event time)
+    const int64_t flo = flat ? (int64_t)a.flat_off[(int64_t)p * a.flat_g] : 0;
+    const int64_t flen = flat ? (int64_t)a.flat_off[(int64_t)(p + 1) * a.flat_g] - flo : 0;
+    const int64_t my_cnt = flat ? flen : min((int64_t)a.b_cnt[p * kSub + sub], a.capb);
+    const int64_t boff = flat ? flo : ((int64_t)p * kSub + sub) * a.capb;
     int64_t cnt = 0;
-    for (int s2 = 0; s2 < kSub; ++s2) cnt = max(cnt, min((int64_t)a.b_cnt[p * kSub + s2], a.capb));
+    if (flat) cnt = (flen + kSub * kChunk - 1) / (kSub * kChunk) * kChunk;
+    else for (int s2 = 0; s2 < kSub; ++s2) cnt = max(cnt, min((int64_t)a.b_cnt[p * kSub + s2], a.capb));
     const gc_u64_ptr bk = (const gc_u64_ptr)(a.b_key + boff);
     const gc_u64_ptr bv0 = a.b_val0 ? (const gc_u64_ptr)(a.b_val0 + boff) : nullptr;
     const gc_u64_ptr bv1 = a.b_val1 ? (const gc_u64_ptr)(a.b_val1 + boff) : nullptr;
@@ -1288,18 +1353,19 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
     int nrel[IT];
     uint32_t nnn[IT];                   // PRE: records per entry
     auto load_chunk = [&](int64_t cb) {
+        const int64_t cbase = flat ? (cb / kChunk) * (kSub * kChunk) + sub * kChunk : cb;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
-            const int64_t i = cb + (int64_t)j * LPS + li;
+            const int64_t i = cbase + (int64_t)j * LPS + li;
             const bool ok = i < my_cnt;
             nkey[j] = ok ? bk[i] : 0ull;
             nx0[j] = (NV > 0 && ok) ? bv0[i] : 0ull;
             nx1[j] = (NV > 1 && ok) ? bv1[i] : 0ull;
-            nrel[j] = ok ? (int)br[i] : -1;
+            const int r = ok ? (int)br[i] : -1;
+            nrel[j] = r == 0xFFFF ? -1 : r;                 // flat layout: a hole (record not accepted)
             nnn[j] = PRE ? (ok ? (uint32_t)bn[i] : 0u) : 1u;
         }
     };
-    constexpr int64_t kChunk = (int64_t)IT * LPS;
     load_chunk(0);
     PMARK(0);
     int it = 0;
@@ -2733,6 +2799,8 @@ struct fwa_engine {
     int64_t* d_send2 = nullptr;
     unsigned long long* d_spk = nullptr;   // session bulk rows (Sess2Args::pk)
     void* d_sg = nullptr;                  // segment kernel staging (Sess2Args::sg_*)
+    uint32_t* d_flat = nullptr;            // flat Phase P layout: (partition, block) counts | their exclusive sum
+    int64_t flat_cap = 0;
     int64_t sg_cap = 0, sgw_cap = 0;
     int64_t* d_spe = nullptr;
     int64_t* d_smax = nullptr;
@@ -3169,7 +3237,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_flat};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -3494,6 +3562,7 @@ static int ensure_v2_buffers(fwa_engine* e, int64_t n, bool need_bn) {
 
 // Two-phase ingest. Sets *ran = false (and leaves no state change besides key insertions) when the
 // batch must take the v1 path instead (bucket overflow on skewed keys).
+static int ensure_sort_tmp(fwa_engine* e, size_t bytes);
 static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     *ran = false;
     // combiner accumulator layout (compile-time in combine3) and the skew mode (PRE, partition3)
@@ -3609,6 +3678,38 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     auto al16 = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; };
     const bool w16 = !now16 && !p2 && kgm == 0 && al16(pa.keys) && al16(pa.ts) &&
                      (e->nv == 0 || ((uintptr_t)pa.cols[pa.vcol[0]] & ((e->vsize[0] == 8) ? 15 : 7)) == 0);
+    // flat bucket layout (part_hist_kernel, then reservation-free Phase P): an A/B option, off by default -- measured
+    // slower on C2 (Phase P 1.30 vs 0.81 ms: 512 open runs per block leave partial lines in L2)
+    static const int flat_env = getenv("FWA_FLAT") ? atoi(getenv("FWA_FLAT")) : 0;     // A/B: 1 = flat layout
+    const bool flat = flat_env != 0 && !pre && !p2;
+    if (flat) {
+        const int64_t ntiles = (a.n + tile - 1) / tile;
+        const int64_t tpb = (ntiles + grid - 1) / grid;
+        const int64_t ncnt = (int64_t)e->np * grid + 1;
+        if (ncnt > e->flat_cap) {
+            if (e->d_flat) HIPCHK(e, hipFree(e->d_flat));
+            e->d_flat = nullptr;
+            e->flat_cap = std::max<int64_t>(ncnt, (int64_t)kMaxPart * 256 + 1);
+            HIPCHK(e, hipMalloc(&e->d_flat, 2 * sizeof(uint32_t) * (size_t)e->flat_cap));
+        }
+        uint32_t* cnts = e->d_flat;
+        uint32_t* offs = e->d_flat + e->flat_cap;
+        const bool w16k = w16 && e->nv == 1;          // the paired-load kernel below (it leaves an odd n's last record
+        part_hist_kernel<<<grid, 1024, 0, e->stream>>>(pa.keys, a.n, tile, tpb, e->part_bits, e->np,   // to the replay)
+                                                       (w16k && (a.n & 1)) ? 1 : 0, cnts);
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipMemsetAsync(cnts + ncnt - 1, 0, 4, e->stream));
+        size_t bytes = 0;
+        HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnts, offs, (int)ncnt, e->stream));
+        if (int rc2 = ensure_sort_tmp(e, bytes)) return rc2;
+        bytes = e->sort_tmp_bytes;
+        HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(e->d_sort_tmp, bytes, cnts, offs, (int)ncnt, e->stream));
+        flat_skew_kernel<<<1, 1024, 0, e->stream>>>(offs, e->np, grid, e->capb * kSub, e->d_st);
+        HIPCHK(e, hipGetLastError());
+        pa.flat_off = offs;
+        pa.tpb = tpb;
+        pa.flat_cap = e->capb * e->np * kSub;
+    }
 #define P2LAUNCH(NV, IT, VW) do { if (p2) partition2_kernel<NV, IT, 1024, 1, VW><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else if (kgm == 0) partition3_kernel<NV, IT, 1024, VW, 0><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else if (kgm == 1) partition3_kernel<NV, IT, 1024, VW, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
@@ -3661,6 +3762,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.slot_base = e->d_slot_base;
     ca.stride = e->stride;
     ca.st = e->d_st;
+    ca.flat_off = pa.flat_off;
+    ca.flat_g = grid;
     static const int aabl = getenv("FWA_AABL") ? atoi(getenv("FWA_AABL")) : 0;
     ca.abl = aabl;
     static const int aprof = getenv("FWA_APROF") ? atoi(getenv("FWA_APROF")) : 0;
