@@ -16,7 +16,7 @@ WINDOW_KINDS = {"TUMBLE": TUMBLE, "SLIDE": SLIDE, "HOP": SLIDE, "CUMULATE": CUMU
 SEM_DATASTREAM, SEM_TABLE = 0, 1
 SEMANTICS = {"DATASTREAM": SEM_DATASTREAM, "TABLE": SEM_TABLE}
 # enum fwa_key_kind
-KEY_JAVA_LONG, KEY_BINROW_BIGINT, KEY_PREHASHED = 0, 1, 2
+KEY_JAVA_LONG, KEY_BINROW_BIGINT, KEY_PREHASHED, KEY_GROUP_PREFIXED = 0, 1, 2, 3
 
 AGG_KINDS = {
     "COUNT": 0, "SUM_I64": 1, "SUM_F32": 2, "SUM_F64": 3, "MIN_I64": 4, "MAX_I64": 5,

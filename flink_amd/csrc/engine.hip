@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const Engi
         const int64_t key = a.keys[i];
         const int64_t ts = a.ts[i];
         // key-group ownership (StateTable.getMapForKeyGroup :300-307)
-        const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0), c.max_par);
+        const int32_t kg = jm::key_group_of(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0, c.max_par);
         if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }
         if (c.sem == FWA_SEM_DATASTREAM && ts == LONG_MIN_J) { raise_error(a.st, FWA_E_TS_MIN); continue; }
         // slice number q = floor((ts - off) / g), Java wrap arithmetic (TimeWindow.java:264-272)
@@ -660,7 +660,7 @@ __global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, c
             const uint64_t rel = (uint64_t)(q - a.q_base);
             uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
             if (!kg_all) {
-                const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, r_kh[j]), c.max_par);
+                const int32_t kg = jm::key_group_of(key, c.key_kind, r_kh[j], c.max_par);
                 if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;
             }
             if (ds && ts == LONG_MIN_J) code = kCodeSlow;
@@ -964,7 +964,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             }
             uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
             if constexpr (KG != 0) {
-                const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, R.kh[j]), c.max_par);
+                const int32_t kg = jm::key_group_of(key, c.key_kind, R.kh[j], c.max_par);
                 if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;
             }
             if (ds && ts == LONG_MIN_J) code = kCodeSlow;
@@ -1956,7 +1956,7 @@ __global__ void __launch_bounds__(kBlock) sess2_classify_kernel(Sess2Args a, con
         const int64_t key = a.keys[i];
         const int64_t ts = a.ts[i];
         a.rkid[i] = 0xffffffffu;
-        const int32_t kg = jm::key_group(jm::key_hash(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0), c.max_par);
+        const int32_t kg = jm::key_group_of(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0, c.max_par);
         if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }   // StateTable :300-307
         const int64_t gap = a.gapc ? a.gapc[i] : a.gap;
         if (gap <= 0) { raise_error(a.st, FWA_E_ARG); continue; }   // DynamicEventTimeSessionWindows.java:60-64
@@ -2629,7 +2629,7 @@ __global__ void fill_u64_kernel(unsigned long long* p, unsigned long long v, int
 __global__ void key_groups_kernel(const int64_t* keys, const int32_t* kh, int64_t n, int32_t kind, int32_t maxp,
                                   int32_t par, int32_t* kg_out, int32_t* op_out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t kg = jm::key_group(jm::key_hash(keys[i], kind, kh ? kh[i] : 0), maxp);
+        const int32_t kg = jm::key_group_of(keys[i], kind, kh ? kh[i] : 0, maxp);
         kg_out[i] = kg;
         if (op_out) op_out[i] = jm::operator_index(maxp, par, kg);
     }
@@ -2909,7 +2909,7 @@ int validate(const fwa_config* c) {
     if (c->semantics != FWA_SEM_DATASTREAM && c->semantics != FWA_SEM_TABLE) return FWA_E_ARG;
     if (c->semantics == FWA_SEM_TABLE && c->allowed_lateness_ms != 0) return FWA_E_ARG;
     if (c->allowed_lateness_ms < 0) return FWA_E_ARG;
-    if (c->key_kind < 0 || c->key_kind > 2) return FWA_E_ARG;
+    if (c->key_kind < 0 || c->key_kind > 3) return FWA_E_ARG;
     if (c->max_parallelism <= 0 || c->max_parallelism > 32768) return FWA_E_ARG;
     if (c->kg_start < 0 || c->kg_end >= c->max_parallelism || c->kg_start > c->kg_end) return FWA_E_ARG;
     return FWA_OK;
@@ -4751,7 +4751,7 @@ static int snapshot_sessions(fwa_engine* e, fwa_blob* out) {
     std::vector<int64_t> off((size_t)maxp + 1, 0), key((size_t)n);
     for (int64_t i = 0; i < n; ++i) {
         key[i] = (int64_t)kid[i] < e->capacity ? (int64_t)table[kid[i]] : LONG_MIN_J;
-        kg[i] = jm::key_group(jm::key_hash(key[i], e->cfg.key_kind, 0), maxp);
+        kg[i] = jm::key_group_of(key[i], e->cfg.key_kind, 0, maxp);
         off[kg[i] + 1]++;
     }
     for (int g = 0; g < maxp; ++g) off[g + 1] += off[g];
@@ -4905,7 +4905,7 @@ int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
     std::vector<int32_t> kg((size_t)n);
     std::vector<int64_t> off((size_t)maxp + 1, 0);
     for (int64_t i = 0; i < n; ++i) {
-        kg[i] = jm::key_group(jm::key_hash(cols[i], e->cfg.key_kind, 0), maxp);
+        kg[i] = jm::key_group_of(cols[i], e->cfg.key_kind, 0, maxp);
         off[kg[i] + 1]++;
     }
     for (int g = 0; g < maxp; ++g) off[g + 1] += off[g];
@@ -5257,7 +5257,7 @@ int fwa_set_input_stream(fwa_engine* e, void* stream) {
 
 int fwa_key_groups(const int64_t* keys, const int32_t* key_hash, int64_t n, int32_t key_kind, int32_t max_par,
                    int32_t par, int32_t* kg_out, int32_t* op_out, int32_t flags, int32_t device) {
-    if (n < 0 || max_par <= 0 || par <= 0 || par > max_par || key_kind < 0 || key_kind > 2) return FWA_E_ARG;
+    if (n < 0 || max_par <= 0 || par <= 0 || par > max_par || key_kind < 0 || key_kind > 3) return FWA_E_ARG;
     if (key_kind == FWA_KEY_PREHASHED && n > 0 && !key_hash) return FWA_E_ARG;
     if (n == 0) return FWA_OK;
     if (hipSetDevice(device) != hipSuccess) return FWA_E_DEVICE;

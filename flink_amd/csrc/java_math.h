@@ -75,11 +75,35 @@ JM_HD int32_t binrow_bigint_hash(int64_t v) {
     return bit_mix((int32_t)h);  // MurmurHashUtils.fmix(int) == MathUtils.bitMix
 }
 
-// key_kind: 0 JAVA_LONG, 1 BINROW_BIGINT, 2 PREHASHED (hash supplied)
+// BinaryRowData of `arity` fixed-length fields (BinaryRowData.java:68-123): an 8-byte header (byte 0 = RowKind
+// INSERT = 0, then one null bit per field from bit 8 on) and one 8-byte little-endian slot per field (BIGINT, DOUBLE
+// raw bits; INT in the low 4 bytes; a NULL field's slot zeroed, BinaryRowWriter.setNullAt); hashCode() =
+// MurmurHashUtils.hashBytesByWords(row, 8 + 8 * arity bytes, seed 42) (:92-170): every 4-byte little-endian word
+// mixed in order, then fmix(h ^ length). `slots[i]` is field i's slot, `nullbits` bit i = field i is NULL (arity <= 56).
+JM_HD int32_t binrow_hash(const uint64_t* slots, int arity, uint64_t nullbits) {
+    uint32_t h = 42u;
+    const uint64_t hdr = nullbits << 8;                   // RowKind byte 0, null bits from bit 8
+    h = mh_h1(h, mh_k1((uint32_t)hdr));
+    h = mh_h1(h, mh_k1((uint32_t)(hdr >> 32)));
+    for (int i = 0; i < arity; ++i) {
+        const uint64_t v = (nullbits >> i) & 1 ? 0ull : slots[i];
+        h = mh_h1(h, mh_k1((uint32_t)v));
+        h = mh_h1(h, mh_k1((uint32_t)(v >> 32)));
+    }
+    h ^= (uint32_t)(8 + 8 * arity);
+    return bit_mix((int32_t)h);
+}
+
+// key_kind: 0 JAVA_LONG, 1 BINROW_BIGINT, 2 PREHASHED (hash supplied), 3 GROUP_PREFIXED (key ids of a key
+// dictionary, fwa_keydict: the key group in the top 16 bits)
 JM_HD int32_t key_hash(int64_t key, int key_kind, int32_t supplied) {
     return key_kind == 0 ? long_hash(key) : (key_kind == 1 ? binrow_bigint_hash(key) : supplied);
 }
 JM_HD int32_t key_group(int32_t hash, int32_t max_par) { return murmur_hash(hash) % max_par; }
+JM_HD int32_t key_group_of(int64_t key, int key_kind, int32_t supplied, int32_t max_par) {
+    if (key_kind == 3) return (int32_t)((uint64_t)key >> 48);
+    return key_group(key_hash(key, key_kind, supplied), max_par);
+}
 JM_HD int32_t operator_index(int32_t max_par, int32_t par, int32_t kg) { return kg * par / max_par; }
 
 // ---- 64-bit unsigned division by a runtime constant -------------------------------------------

@@ -1,0 +1,333 @@
+// keydict.hip -- the key dictionary of include/flink_amd.h (multi-column Table keys).
+//
+// A key row of `arity` fixed-length fields becomes the 8-byte slots of its BinaryRowData (BinaryRowData.java:68-123):
+// BIGINT as is, INT zero-extended (the low 4 bytes of its slot), DOUBLE as its raw bits, a NULL field as 0 with its
+// null bit set. hashCode() is jm::binrow_hash (MurmurHashUtils.hashBytesByWords over those bytes); its key group is
+// KeyGroupRangeAssignment.assignToKeyGroup (murmur % maxParallelism). The row's identity is a 64-bit hash of the same
+// bytes; an encode runs three passes, each a kernel, so a pass only reads what an earlier launch finished writing:
+//   kd_insert_kernel  every row claims or finds its identity in the open-addressing table (one CAS per row);
+//   kd_assign_kernel  the rows that claimed a slot take a sequence number (one reservation per wave), store the
+//                     row's slots and publish id = key group << 48 | sequence in the table;
+//   kd_lookup_kernel  every row reads its id, checks its slots against the stored row (a different row with the
+//                     same 64-bit hash raises FWA_E_STATE) and writes its id and hash.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/flink_amd.h"
+#include "java_math.h"
+
+namespace {
+
+constexpr int kBlockKd = 256;
+constexpr uint64_t kKdEmpty = 0ull;
+constexpr uint64_t kSeqMask = (1ull << 48) - 1;
+
+struct KdCols {
+    const void* col[FWA_KEYDICT_MAX_ARITY];
+    const uint8_t* nul[FWA_KEYDICT_MAX_ARITY];
+    int32_t type[FWA_KEYDICT_MAX_ARITY];
+    int32_t arity;
+};
+
+struct KdDev {
+    unsigned long long* ht_key;    // [cap] row identity (0 = empty)
+    long long* ht_id;              // [cap] id, published by the assign pass
+    uint32_t* ht_rep;              // [cap] the row that claimed the slot (this encode only)
+    unsigned long long* fslot;     // [arity][max_rows] stored slots
+    unsigned long long* fnull;     // [max_rows] stored null bits
+    unsigned long long* nrows;     // distinct rows so far
+    uint32_t* pos;                 // [n] per row: table slot | 0x80000000 when the row claimed it
+    int32_t* status;               // FWA_E_* of the kernels (0 = ok)
+    uint64_t mask;                 // table capacity - 1
+    int64_t max_rows;
+    int32_t max_par;
+};
+
+__device__ __forceinline__ void row_of(const KdCols& k, int64_t i, uint64_t* slots, uint64_t* nullbits) {
+    uint64_t nb = 0;
+    for (int c = 0; c < FWA_KEYDICT_MAX_ARITY; ++c) {
+        if (c >= k.arity) break;
+        const bool isnull = k.nul[c] && k.nul[c][i];
+        uint64_t v = 0;
+        if (!isnull) {
+            if (k.type[c] == FWA_KEY_FIELD_INT) v = (uint64_t)(uint32_t)((const int32_t*)k.col[c])[i];
+            else v = ((const uint64_t*)k.col[c])[i];   // BIGINT, DOUBLE raw bits
+        }
+        nb |= (uint64_t)isnull << c;
+        slots[c] = v;
+    }
+    *nullbits = nb;
+}
+
+__device__ __forceinline__ uint64_t row_identity(const uint64_t* slots, int arity, uint64_t nullbits) {
+    uint64_t h = jm::mix64(nullbits ^ 0x9E3779B97F4A7C15ull ^ (uint64_t)arity);
+    for (int c = 0; c < FWA_KEYDICT_MAX_ARITY; ++c) {
+        if (c >= arity) break;
+        h = jm::mix64(h ^ slots[c] ^ ((uint64_t)(c + 1) << 56));
+    }
+    return h == kKdEmpty ? 1ull : h;
+}
+
+__global__ void __launch_bounds__(kBlockKd) kd_hash_kernel(KdCols k, int64_t n, int32_t* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t slots[FWA_KEYDICT_MAX_ARITY], nb;
+        row_of(k, i, slots, &nb);
+        out[i] = jm::binrow_hash(slots, k.arity, nb);
+    }
+}
+
+__global__ void __launch_bounds__(kBlockKd) kd_insert_kernel(KdCols k, KdDev d, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t slots[FWA_KEYDICT_MAX_ARITY], nb;
+        row_of(k, i, slots, &nb);
+        const uint64_t h = row_identity(slots, k.arity, nb);
+        uint64_t s = (h * 0x9E3779B97F4A7C15ull) & d.mask;
+        uint32_t got = 0xffffffffu;
+        for (uint64_t probe = 0; probe <= d.mask; ++probe) {
+            const unsigned long long old = atomicCAS(&d.ht_key[s], kKdEmpty, (unsigned long long)h);
+            if (old == kKdEmpty) { d.ht_rep[s] = (uint32_t)i; got = (uint32_t)s | 0x80000000u; break; }
+            if (old == h) { got = (uint32_t)s; break; }
+            s = (s + 1) & d.mask;
+        }
+        if (got == 0xffffffffu) atomicCAS(d.status, 0, FWA_E_OOM);
+        d.pos[i] = got;
+    }
+}
+
+__global__ void __launch_bounds__(kBlockKd) kd_assign_kernel(KdCols k, KdDev d, int64_t n) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < n; t0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t0 + threadIdx.x;
+        const uint32_t ps = i < n ? d.pos[i] : 0xffffffffu;
+        const bool win = ps != 0xffffffffu && (ps & 0x80000000u);
+        const unsigned long long m = __ballot(win);
+        if (!m) continue;
+        const int ld = __ffsll((long long)m) - 1;
+        unsigned long long base = 0;
+        if (lane == ld) base = atomicAdd(d.nrows, (unsigned long long)__popcll(m));
+        base = __shfl(base, ld);
+        if (!win) continue;
+        const unsigned long long seq = base + __popcll(m & ((1ull << lane) - 1ull));
+        const uint64_t s = ps & 0x7fffffffu;
+        if ((int64_t)seq >= d.max_rows) { atomicCAS(d.status, 0, FWA_E_OOM); continue; }
+        uint64_t slots[FWA_KEYDICT_MAX_ARITY], nb;
+        row_of(k, i, slots, &nb);
+        for (int c = 0; c < FWA_KEYDICT_MAX_ARITY; ++c) {
+            if (c >= k.arity) break;
+            d.fslot[(int64_t)c * d.max_rows + (int64_t)seq] = slots[c];
+        }
+        d.fnull[seq] = nb;
+        const int32_t kg = jm::key_group(jm::binrow_hash(slots, k.arity, nb), d.max_par);
+        d.ht_id[s] = (long long)(((uint64_t)kg << 48) | (seq & kSeqMask));
+    }
+}
+
+__global__ void __launch_bounds__(kBlockKd) kd_lookup_kernel(KdCols k, KdDev d, int64_t n, int64_t* ids, int32_t* hashes) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t ps = d.pos[i];
+        if (ps == 0xffffffffu) continue;
+        const int64_t id = d.ht_id[ps & 0x7fffffffu];
+        const uint64_t seq = (uint64_t)id & kSeqMask;
+        uint64_t slots[FWA_KEYDICT_MAX_ARITY], nb;
+        row_of(k, i, slots, &nb);
+        bool same = (int64_t)seq < d.max_rows && d.fnull[seq] == nb;
+        for (int c = 0; c < FWA_KEYDICT_MAX_ARITY; ++c) {
+            if (c >= k.arity) break;
+            same = same && d.fslot[(int64_t)c * d.max_rows + (int64_t)seq] == slots[c];
+        }
+        if (!same) atomicCAS(d.status, 0, FWA_E_STATE);    // two rows with one 64-bit identity
+        ids[i] = id;
+        if (hashes) hashes[i] = jm::binrow_hash(slots, k.arity, nb);
+    }
+}
+
+__global__ void __launch_bounds__(kBlockKd) kd_decode_kernel(KdDev d, KdCols k, int64_t n, const int64_t* ids,
+                                                              void* const* cols, uint8_t* const* nul, int has_nul) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t seq = (uint64_t)ids[i] & kSeqMask;
+        if ((int64_t)seq >= d.max_rows) { atomicCAS(d.status, 0, FWA_E_ARG); continue; }
+        const uint64_t nb = d.fnull[seq];
+        for (int c = 0; c < FWA_KEYDICT_MAX_ARITY; ++c) {
+            if (c >= k.arity) break;
+            const uint64_t v = d.fslot[(int64_t)c * d.max_rows + (int64_t)seq];
+            if (k.type[c] == FWA_KEY_FIELD_INT) ((int32_t*)cols[c])[i] = (int32_t)(uint32_t)v;
+            else ((uint64_t*)cols[c])[i] = v;
+            if (has_nul && nul[c]) nul[c][i] = (uint8_t)((nb >> c) & 1);
+        }
+    }
+}
+
+int grid_kd(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlockKd - 1) / kBlockKd, 8192)); }
+
+}  // namespace
+
+struct fwa_keydict {
+    int32_t arity = 0, device = 0;
+    int32_t types[FWA_KEYDICT_MAX_ARITY] = {};
+    KdDev d{};
+    int64_t cap = 0;                 // table slots
+    int64_t pos_cap = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    void** d_colptr = nullptr;       // decode: device copies of the column / null pointer arrays
+};
+
+namespace {
+int kd_fail(fwa_keydict* d, int code, const char* msg) { d->err = msg; return code; }
+#define KDCHK(d, call) do { hipError_t _e = (call); if (_e != hipSuccess) return kd_fail(d, FWA_E_DEVICE, hipGetErrorString(_e)); } while (0)
+
+bool cols_of(const fwa_keydict* d, const void* const* cols, const uint8_t* const* nulls, KdCols* k) {
+    memset(k, 0, sizeof(*k));
+    k->arity = d->arity;
+    for (int c = 0; c < d->arity; ++c) {
+        if (!cols[c]) return false;
+        k->col[c] = cols[c];
+        k->nul[c] = nulls ? nulls[c] : nullptr;
+        k->type[c] = d->types[c];
+    }
+    return true;
+}
+
+int read_status(fwa_keydict* d) {
+    int32_t st = 0;
+    KDCHK(d, hipMemcpyAsync(&st, d->d.status, 4, hipMemcpyDeviceToHost, d->stream));
+    KDCHK(d, hipStreamSynchronize(d->stream));
+    if (st == FWA_E_OOM) return kd_fail(d, st, "key dictionary full (capacity)");
+    if (st == FWA_E_STATE) return kd_fail(d, st, "two key rows with one 64-bit identity");
+    if (st) return kd_fail(d, st, "bad key id");
+    return FWA_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int fwa_keydict_create(int32_t arity, const int32_t* field_types, int32_t max_parallelism, int64_t capacity,
+                       int32_t device, fwa_keydict** out) {
+    if (!out || arity < 1 || arity > FWA_KEYDICT_MAX_ARITY || !field_types || max_parallelism <= 0 ||
+        max_parallelism > 32768 || capacity <= 0 || capacity > ((int64_t)1 << 31))
+        return FWA_E_ARG;
+    for (int c = 0; c < arity; ++c)
+        if (field_types[c] < FWA_KEY_FIELD_BIGINT || field_types[c] > FWA_KEY_FIELD_DOUBLE) return FWA_E_ARG;
+    fwa_keydict* d = new fwa_keydict();
+    d->arity = arity;
+    d->device = device;
+    for (int c = 0; c < arity; ++c) d->types[c] = field_types[c];
+    int64_t cap = 1024;
+    while (cap < 2 * capacity) cap <<= 1;
+    d->cap = cap;
+    d->d.mask = (uint64_t)cap - 1;
+    d->d.max_rows = capacity;
+    d->d.max_par = max_parallelism;
+    int rc = FWA_OK;
+    do {
+        if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        if (hipMalloc(&d->d.ht_key, 8 * cap) != hipSuccess || hipMalloc(&d->d.ht_id, 8 * cap) != hipSuccess ||
+            hipMalloc(&d->d.ht_rep, 4 * cap) != hipSuccess ||
+            hipMalloc(&d->d.fslot, 8 * (size_t)arity * (size_t)capacity) != hipSuccess ||
+            hipMalloc(&d->d.fnull, 8 * (size_t)capacity) != hipSuccess || hipMalloc(&d->d.nrows, 8) != hipSuccess ||
+            hipMalloc(&d->d.status, 4) != hipSuccess || hipMalloc(&d->d_colptr, 2 * sizeof(void*) * FWA_KEYDICT_MAX_ARITY) != hipSuccess) {
+            rc = FWA_E_OOM; break;
+        }
+        if (hipMemsetAsync(d->d.ht_key, 0, 8 * cap, d->stream) != hipSuccess || hipMemsetAsync(d->d.nrows, 0, 8, d->stream) != hipSuccess ||
+            hipMemsetAsync(d->d.status, 0, 4, d->stream) != hipSuccess || hipStreamSynchronize(d->stream) != hipSuccess) {
+            rc = FWA_E_DEVICE; break;
+        }
+    } while (0);
+    if (rc) { fwa_keydict_destroy(d); return rc; }
+    *out = d;
+    return FWA_OK;
+}
+
+void fwa_keydict_destroy(fwa_keydict* d) {
+    if (!d) return;
+    (void)hipSetDevice(d->device);
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
+    for (void* p : {(void*)d->d.ht_key, (void*)d->d.ht_id, (void*)d->d.ht_rep, (void*)d->d.fslot, (void*)d->d.fnull,
+                    (void*)d->d.nrows, (void*)d->d.pos, (void*)d->d.status, (void*)d->d_colptr})
+        if (p) (void)hipFree(p);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
+const char* fwa_keydict_last_error(const fwa_keydict* d) { return d ? d->err.c_str() : "null key dictionary"; }
+
+int64_t fwa_keydict_size(const fwa_keydict* d) {
+    if (!d) return -1;
+    unsigned long long n = 0;
+    if (hipSetDevice(d->device) != hipSuccess) return -1;
+    if (hipMemcpyAsync(&n, d->d.nrows, 8, hipMemcpyDeviceToHost, d->stream) != hipSuccess) return -1;
+    if (hipStreamSynchronize(d->stream) != hipSuccess) return -1;
+    return (int64_t)std::min<unsigned long long>(n, (unsigned long long)d->d.max_rows);
+}
+
+int fwa_keydict_encode(fwa_keydict* d, const void* const* cols, const uint8_t* const* nulls, int64_t n, int64_t* ids,
+                       int32_t* hashes) {
+    if (!d) return FWA_E_ARG;
+    if (n < 0 || (n > 0 && (!cols || !ids)) || n > INT32_MAX) return kd_fail(d, FWA_E_ARG, "fwa_keydict_encode: bad arguments");
+    if (n == 0) return FWA_OK;
+    KdCols k;
+    if (!cols_of(d, cols, nulls, &k)) return kd_fail(d, FWA_E_ARG, "fwa_keydict_encode: null key column");
+    KDCHK(d, hipSetDevice(d->device));
+    if (n > d->pos_cap) {
+        KDCHK(d, hipStreamSynchronize(d->stream));
+        if (d->d.pos) KDCHK(d, hipFree(d->d.pos));
+        d->d.pos = nullptr;
+        d->pos_cap = std::max<int64_t>(n + n / 4, 1 << 16);
+        KDCHK(d, hipMalloc(&d->d.pos, 4 * (size_t)d->pos_cap));
+    }
+    KDCHK(d, hipMemsetAsync(d->d.status, 0, 4, d->stream));
+    kd_insert_kernel<<<grid_kd(n), kBlockKd, 0, d->stream>>>(k, d->d, n);
+    kd_assign_kernel<<<grid_kd(n), kBlockKd, 0, d->stream>>>(k, d->d, n);
+    kd_lookup_kernel<<<grid_kd(n), kBlockKd, 0, d->stream>>>(k, d->d, n, ids, hashes);
+    KDCHK(d, hipGetLastError());
+    return read_status(d);
+}
+
+int fwa_keydict_decode(fwa_keydict* d, const int64_t* ids, int64_t n, void* const* cols, uint8_t* const* nulls) {
+    if (!d) return FWA_E_ARG;
+    if (n < 0 || (n > 0 && (!ids || !cols))) return kd_fail(d, FWA_E_ARG, "fwa_keydict_decode: bad arguments");
+    if (n == 0) return FWA_OK;
+    KDCHK(d, hipSetDevice(d->device));
+    void* h[2 * FWA_KEYDICT_MAX_ARITY] = {};
+    for (int c = 0; c < d->arity; ++c) {
+        if (!cols[c]) return kd_fail(d, FWA_E_ARG, "fwa_keydict_decode: null key column");
+        h[c] = cols[c];
+        h[FWA_KEYDICT_MAX_ARITY + c] = nulls ? (void*)nulls[c] : nullptr;
+    }
+    KDCHK(d, hipMemcpyAsync(d->d_colptr, h, sizeof(h), hipMemcpyHostToDevice, d->stream));
+    KDCHK(d, hipMemsetAsync(d->d.status, 0, 4, d->stream));
+    KdCols k;
+    memset(&k, 0, sizeof(k));
+    k.arity = d->arity;
+    for (int c = 0; c < d->arity; ++c) k.type[c] = d->types[c];
+    kd_decode_kernel<<<grid_kd(n), kBlockKd, 0, d->stream>>>(d->d, k, n, ids, d->d_colptr,
+                                                             (uint8_t* const*)(d->d_colptr + FWA_KEYDICT_MAX_ARITY),
+                                                             nulls ? 1 : 0);
+    KDCHK(d, hipGetLastError());
+    return read_status(d);
+}
+
+int fwa_binrow_hash(int32_t arity, const int32_t* field_types, const void* const* cols, const uint8_t* const* nulls,
+                    int64_t n, int32_t* out, int32_t device) {
+    if (arity < 1 || arity > FWA_KEYDICT_MAX_ARITY || !field_types || n < 0 || (n > 0 && (!cols || !out))) return FWA_E_ARG;
+    if (n == 0) return FWA_OK;
+    KdCols k;
+    memset(&k, 0, sizeof(k));
+    k.arity = arity;
+    for (int c = 0; c < arity; ++c) {
+        if (!cols[c] || field_types[c] < FWA_KEY_FIELD_BIGINT || field_types[c] > FWA_KEY_FIELD_DOUBLE) return FWA_E_ARG;
+        k.col[c] = cols[c];
+        k.nul[c] = nulls ? nulls[c] : nullptr;
+        k.type[c] = field_types[c];
+    }
+    if (hipSetDevice(device) != hipSuccess) return FWA_E_DEVICE;
+    kd_hash_kernel<<<grid_kd(n), kBlockKd>>>(k, n, out);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return FWA_E_DEVICE;
+    return FWA_OK;
+}
+
+}  // extern "C"

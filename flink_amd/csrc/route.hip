@@ -42,7 +42,7 @@ struct RouteArgs {
 };
 
 __device__ __forceinline__ int32_t dest_of(const RouteArgs& a, int64_t i) {
-    const int32_t kg = jm::key_group(jm::key_hash(a.keys[i], a.key_kind, a.key_hash ? a.key_hash[i] : 0), a.maxp);
+    const int32_t kg = jm::key_group_of(a.keys[i], a.key_kind, a.key_hash ? a.key_hash[i] : 0, a.maxp);
     return jm::operator_index(a.maxp, a.par, kg);
 }
 

@@ -70,7 +70,8 @@ enum fwa_semantics { FWA_SEM_DATASTREAM = 0, FWA_SEM_TABLE = 1 };
  *                 = MurmurHashUtils.hashBytesByWords over [0, 0, lo32, hi32], seed 42
  * PREHASHED:      the caller passes key.hashCode() in the low 32 bits of a separate column
  *                 (fwa_push key_hash argument); the int64 key is an opaque dictionary id. */
-enum fwa_key_kind { FWA_KEY_JAVA_LONG = 0, FWA_KEY_BINROW_BIGINT = 1, FWA_KEY_PREHASHED = 2 };
+enum fwa_key_kind { FWA_KEY_JAVA_LONG = 0, FWA_KEY_BINROW_BIGINT = 1, FWA_KEY_PREHASHED = 2,
+                    FWA_KEY_GROUP_PREFIXED = 3 /* ids of a key dictionary (fwa_keydict): bits 48-63 = key group */ };
 
 /* Aggregates. Result column type in brackets. */
 enum fwa_agg_kind {
@@ -381,6 +382,36 @@ int fwa_route_rows(const int64_t* keys, const int32_t* key_hash, int64_t n, int3
 
 /* The receive side of that exchange: rows[n][ncols] (int64 cells) -> cols[c][n], device pointers, on `stream`. */
 int fwa_unpack_rows(const int64_t* rows, int64_t n, int32_t ncols, int64_t* const* cols, int32_t device, void* stream);
+
+/* ---- key dictionary: multi-column Table keys ----
+ * A Table job keyed by several columns has BinaryRowData keys of `arity` fixed-length fields whose hashCode()
+ * (BinaryRowData.java:452-454 -> MurmurHashUtils.hashBytesByWords :92-170) places them in key groups
+ * (KeyGroupRangeAssignment.assignToKeyGroup :63-77). The dictionary computes that hash on the GPU and maps each
+ * distinct key row to a 64-bit id whose bits 48-63 are the row's key group and bits 0-47 a dense sequence number;
+ * an engine created with key_kind FWA_KEY_GROUP_PREFIXED runs on those ids -- key-group ownership, partials,
+ * FWASNAP1 snapshots and rescaling work unchanged (the key group is read from the id) -- and fired rows are mapped
+ * back to the key columns with fwa_keydict_decode. Rows are equal iff their bytes are (BinaryRowData.equals), so
+ * -0.0 and 0.0 are different DOUBLE keys, as in the reference. Identity is a 64-bit hash of the row's bytes checked
+ * against the stored row: two rows with the same 64-bit hash (never observed) fail the encode with FWA_E_STATE
+ * instead of merging. One dictionary serves one engine handle (ids are local to it). */
+enum fwa_key_field_type { FWA_KEY_FIELD_BIGINT = 0, FWA_KEY_FIELD_INT = 1, FWA_KEY_FIELD_DOUBLE = 2 };
+#define FWA_KEYDICT_MAX_ARITY 8
+typedef struct fwa_keydict fwa_keydict;
+/* capacity: the most distinct key rows the dictionary will hold (FWA_E_OOM past it) */
+int fwa_keydict_create(int32_t arity, const int32_t* field_types, int32_t max_parallelism, int64_t capacity,
+                       int32_t device, fwa_keydict** out);
+void fwa_keydict_destroy(fwa_keydict* d);
+const char* fwa_keydict_last_error(const fwa_keydict* d);
+int64_t fwa_keydict_size(const fwa_keydict* d);            /* distinct rows so far */
+/* Device pointers: cols[c][i] is field c of row i (int64 BIGINT, int32 INT, double DOUBLE); nulls[c] (or nulls
+ * itself) may be NULL = no NULLs in field c. Writes ids[i] and, if hashes != NULL, hashes[i] = the row's hashCode(). */
+int fwa_keydict_encode(fwa_keydict* d, const void* const* cols, const uint8_t* const* nulls, int64_t n, int64_t* ids,
+                       int32_t* hashes);
+/* Device pointers: the key columns (and NULL flags, if nulls != NULL) of n ids from this dictionary. */
+int fwa_keydict_decode(fwa_keydict* d, const int64_t* ids, int64_t n, void* const* cols, uint8_t* const* nulls);
+/* BinaryRowData.hashCode() of n rows of fixed-length fields, device pointers (no dictionary). */
+int fwa_binrow_hash(int32_t arity, const int32_t* field_types, const void* const* cols, const uint8_t* const* nulls,
+                    int64_t n, int32_t* out, int32_t device);
 
 /* ---- bench / test support (synthetic streams of SURVEY.md §8(d), generated in HBM) ---- */
 typedef struct fwa_gen_params {

@@ -86,8 +86,27 @@ int32_t or_binrow_bigint_hash(int64_t v) {
     return mh_fmix(h1 ^ 16);
 }
 
+/* BinaryRowData.hashCode of a row of `arity` fixed-length fields (BinaryRowData.java:68-123, 452-454;
+   MurmurHashUtils.hashBytesByWords :92-170): bytes = 8-byte header (RowKind INSERT 0, null bit of field i at bit
+   8 + i, BinaryRowData.setNullAt) + one little-endian 8-byte slot per field (BIGINT / DOUBLE bits; INT in the low 4
+   bytes; a NULL field's slot zeroed, BinaryRowWriter.setNullAt); the row's 4-byte words mixed in order from seed 42,
+   then fmix(h ^ length). slots[i] = field i's 8 slot bytes as a little-endian integer. */
+int32_t or_binrow_hash(const int64_t* slots, int32_t arity, uint64_t nullbits) {
+    int32_t h1 = 42;
+    const uint64_t hdr = nullbits << 8;
+    h1 = mh_mix_h1(h1, mh_mix_k1((int32_t)(uint32_t)(hdr & 0xffffffffu)));
+    h1 = mh_mix_h1(h1, mh_mix_k1((int32_t)(uint32_t)(hdr >> 32)));
+    for (int32_t i = 0; i < arity; i++) {
+        const uint64_t v = ((nullbits >> i) & 1) ? 0 : (uint64_t)slots[i];
+        h1 = mh_mix_h1(h1, mh_mix_k1((int32_t)(uint32_t)(v & 0xffffffffu)));
+        h1 = mh_mix_h1(h1, mh_mix_k1((int32_t)(uint32_t)(v >> 32)));
+    }
+    return mh_fmix(h1 ^ (8 + 8 * arity));
+}
+
 int32_t or_key_group(int64_t key, int32_t key_kind, int32_t key_hash, int32_t max_par) {
     int32_t h;
+    if (key_kind == 3) return (int32_t)((uint64_t)key >> 48);   /* key-dictionary ids carry their key group */
     if (key_kind == FWA_KEY_JAVA_LONG) h = or_long_hash(key);
     else if (key_kind == FWA_KEY_BINROW_BIGINT) h = or_binrow_bigint_hash(key);
     else h = key_hash;

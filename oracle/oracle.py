@@ -37,6 +37,8 @@ def lib():
         L.or_long_hash.restype = C.c_int32
         L.or_binrow_bigint_hash.argtypes = [C.c_int64]
         L.or_binrow_bigint_hash.restype = C.c_int32
+        L.or_binrow_hash.argtypes = [C.c_void_p, C.c_int32, C.c_uint64]
+        L.or_binrow_hash.restype = C.c_int32
         L.or_key_group.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32]
         L.or_key_group.restype = C.c_int32
         L.or_operator_index.argtypes = [C.c_int32, C.c_int32, C.c_int32]
