@@ -136,8 +136,10 @@ struct In {
 
 // Layouts this file writes: DataStream TUMBLE and SESSION (WindowOperator), Table TUMBLE / HOP / CUMULATE
 // (SlicingWindowOperator: per-slice state, so the engine's slices map 1:1), Table shift time zones and SQL NULLs.
-bool supported(const fwa_config& c) {
+bool supported(const fwa_config& c, bool dict = false) {
     if (c.key_kind == FWA_KEY_PREHASHED) return false;
+    if ((c.key_kind == FWA_KEY_GROUP_PREFIXED) != dict) return false;   // dictionary ids <=> a key dictionary
+    if (dict && c.semantics != FWA_SEM_TABLE) return false;            // BinaryRowData keys: Table only
     if (c.semantics == FWA_SEM_DATASTREAM)
         return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SESSION || c.window_kind == FWA_SLIDE;
     return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SLIDE || c.window_kind == FWA_CUMULATE ||
@@ -199,6 +201,15 @@ int hidden_map(const fwa_config& c, int* hid) {
     }
     return nh;
 }
+
+// Key rows of a key dictionary (fwa_keydict, multi-column Table keys): the slots and null bits of every row so far,
+// read back from the device (keydict.hip fwa_keydict_host_rows); id bits 0-47 index them.
+struct DictRows {
+    int arity = 0;
+    int32_t types[FWA_KEYDICT_MAX_ARITY] = {};
+    std::vector<uint64_t> slots;     // [row][arity]
+    std::vector<uint64_t> nulls;     // [row]
+};
 
 // Event-time timer of a window end under the shift time zone (TimeWindowUtil.toEpochMillsForTimer :67-100; UTC:
 // the end - 1 itself)
@@ -309,14 +320,32 @@ extern "C" {
 // engine-side accessors (engine.hip)
 int fwa_get_config(const fwa_engine* e, fwa_config* out);
 int fwa_set_error(fwa_engine* e, int code, const char* msg);
+// keydict.hip (internal): the dictionary's rows on the host, and an encode of host rows
+int fwa_keydict_host_rows(fwa_keydict* d, int32_t* arity, int32_t* types, std::vector<uint64_t>* slots,
+                          std::vector<uint64_t>* nulls);
+int fwa_keydict_encode_host(fwa_keydict* d, const uint64_t* slots, const uint64_t* nulls, int64_t n, int64_t* ids);
 
-int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark) {
+static int snapshot_heap_impl(fwa_engine* e, fwa_keydict* dict, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark) {
     if (!e) return FWA_E_ARG;
     if (!out || !kg_offsets || !watermark) return fwa_set_error(e, FWA_E_ARG, "fwa_snapshot_heap: null output pointer");
     fwa_config c;
     int rc = fwa_get_config(e, &c);
     if (rc) return rc;
-    if (!supported(c)) return fwa_set_error(e, FWA_E_UNSUPPORTED, kUnsupported);
+    if (!supported(c, dict != nullptr)) return fwa_set_error(e, FWA_E_UNSUPPORTED, kUnsupported);
+    DictRows dr;
+    if (dict && (rc = fwa_keydict_host_rows(dict, &dr.arity, dr.types, &dr.slots, &dr.nulls)))
+        return fwa_set_error(e, rc, "key dictionary rows");
+    // the key as a BinaryRowData: one BIGINT field, or the dictionary row of an id
+    auto key_row = [&](Out& o, int64_t key) -> bool {
+        if (!dict) { const uint64_t kf = (uint64_t)key; o.row(&kf, 1); return true; }
+        const uint64_t seq = (uint64_t)key & ((1ull << 48) - 1);
+        if (seq >= dr.nulls.size()) return false;
+        bool nl[FWA_KEYDICT_MAX_ARITY];
+        for (int i = 0; i < dr.arity; ++i) nl[i] = (dr.nulls[seq] >> i) & 1;
+        o.row(&dr.slots[seq * (size_t)dr.arity], dr.arity, nl);
+        return true;
+    };
+    bool keys_ok = true;
     fwa_blob snap{nullptr, 0};
     if ((rc = fwa_snapshot(e, &snap))) return rc;
     Snap s;
@@ -419,8 +448,7 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
                 } else {
                     if (sess) { o.i64((uint64_t)start); o.i64((uint64_t)end); }   // TR TimeWindow.Serializer :169-172
                     else o.i64((uint64_t)end);                              // slice end (LongSerializer)
-                    const uint64_t kf = (uint64_t)key;
-                    o.row(&kf, 1);                                         // key row
+                    keys_ok = key_row(o, key) && keys_ok;                  // key row
                     bool nl[1 + FWA_MAX_AGGS + FWA_MAX_COLS];
                     for (int k = 0; k < arity; ++k) nl[k] = fnull[k] != 0;
                     o.row(f.data(), arity, nl);                            // accumulator row
@@ -435,7 +463,7 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
             for (auto& kv : by_key) {
                 o.u8(0);                                               // VoidNamespaceSerializer: one byte
                 if (ds) o.i64((uint64_t)kv.first);
-                else { const uint64_t kf = (uint64_t)kv.first; o.row(&kf, 1); }
+                else keys_ok = key_row(o, kv.first) && keys_ok;
                 o.i32((int64_t)kv.second.size());                      // ListSerializer / MapSerializer: size, then
                 for (int64_t i : kv.second) {                          // (actual, state) TimeWindow pairs
                     const int64_t st = s.col[n + i], en = end_of(i);
@@ -480,8 +508,7 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
             const int64_t key = std::get<1>(t);
             if (ds) { o.i64((uint64_t)key); o.i64((uint64_t)std::get<2>(t)); o.i64((uint64_t)std::get<3>(t)); }
             else {
-                const uint64_t kf = (uint64_t)key;
-                o.row(&kf, 1);
+                keys_ok = key_row(o, key) && keys_ok;
                 if (sess) o.i64((uint64_t)std::get<2>(t));             // TimeWindow namespace
                 o.i64((uint64_t)std::get<3>(t));
             }
@@ -489,6 +516,7 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
     }
     *watermark = s.wm;
     fwa_blob_free(&snap);
+    if (!keys_ok) return fwa_set_error(e, FWA_E_ARG, "a key id is not in the key dictionary");
     out->size = (int64_t)o.b.size();
     out->data = malloc(o.b.size() ? o.b.size() : 1);
     if (!out->data) return fwa_set_error(e, FWA_E_OOM, "heap snapshot allocation failed");
@@ -496,13 +524,19 @@ int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t
     return FWA_OK;
 }
 
-int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* sizes, const int64_t* watermarks,
-                     int32_t n_bodies) {
+static int restore_heap_impl(fwa_engine* e, fwa_keydict* dict, const void* const* bodies, const int64_t* sizes,
+                             const int64_t* watermarks, int32_t n_bodies) {
     if (!e || n_bodies <= 0 || !bodies || !sizes || !watermarks) return FWA_E_ARG;
     fwa_config c;
     int rc = fwa_get_config(e, &c);
     if (rc) return rc;
-    if (!supported(c)) return fwa_set_error(e, FWA_E_UNSUPPORTED, kUnsupported);
+    if (!supported(c, dict != nullptr)) return fwa_set_error(e, FWA_E_UNSUPPORTED, kUnsupported);
+    int32_t darity = 1;
+    if (dict) {
+        int32_t types[FWA_KEYDICT_MAX_ARITY];
+        std::vector<uint64_t> tmp_s, tmp_n;
+        if ((rc = fwa_keydict_host_rows(dict, &darity, types, &tmp_s, &tmp_n))) return fwa_set_error(e, rc, "key dictionary");
+    }
     const bool ds = c.semantics == FWA_SEM_DATASTREAM;
     const bool sess = c.window_kind == FWA_SESSION;
     const bool ds_slide = ds && c.window_kind == FWA_SLIDE;
@@ -533,6 +567,26 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
         };
         std::map<int64_t, std::map<int64_t, Words>> slide_win;    // DataStream SLIDE: key -> window start -> words
         std::vector<std::pair<int64_t, Words>> slices;
+        // dictionary keys: each distinct key row read gets a placeholder key (its index), encoded to ids at the end
+        std::map<std::vector<uint64_t>, int64_t> comp_idx;
+        std::vector<uint64_t> comp_slots, comp_nulls;
+        auto read_key = [&](In& in) -> int64_t {
+            if (!dict) { uint64_t kf; in.row(&kf, 1); return (int64_t)kf; }
+            uint64_t f[FWA_KEYDICT_MAX_ARITY];
+            bool nl[FWA_KEYDICT_MAX_ARITY];
+            in.row(f, darity, nl);
+            std::vector<uint64_t> k(f, f + darity);
+            uint64_t nb = 0;
+            for (int i = 0; i < darity; ++i) nb |= (uint64_t)nl[i] << i;
+            k.push_back(nb);
+            auto it = comp_idx.find(k);
+            if (it != comp_idx.end()) return it->second;
+            const int64_t idx = (int64_t)comp_nulls.size();
+            comp_idx.emplace(k, idx);
+            comp_slots.insert(comp_slots.end(), f, f + darity);
+            comp_nulls.push_back(nb);
+            return idx;
+        };
         while (in.ok && in.at < in.n) {
             const int64_t kg = in.i32();
             if (!in.ok || kg < 0 || kg >= maxp) return fwa_set_error(e, FWA_E_ARG, "heap body: bad key group id");
@@ -544,14 +598,14 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
                     if (sid == id.proc || sid == id.event) {           // timers: re-derived from the window state
                         in.i64();
                         if (ds) { in.i64(); in.i64(); in.i64(); }
-                        else { uint64_t k; in.row(&k, 1); in.i64(); if (sess) in.i64(); }
+                        else { read_key(in); in.i64(); if (sess) in.i64(); }
                         continue;
                     }
                     if (sid == id.mset) {                              // merging-window-set: (actual, state) pairs
                         in.get(1);                                     // MergingWindowSet(...) :83-87
                         int64_t key;
                         if (ds) key = in.i64();
-                        else { uint64_t kf; in.row(&kf, 1); key = (int64_t)kf; }
+                        else key = read_key(in);
                         const int64_t m = in.i32();
                         for (int64_t q = 0; q < m && in.ok; ++q) {
                             const int64_t as = in.i64(), ae = in.i64();
@@ -567,9 +621,7 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
                     else {
                         start = sess ? in.i64() : 0;                   // Table sessions: TimeWindow namespace
                         end = in.i64();
-                        uint64_t kf;
-                        in.row(&kf, 1);
-                        key = (int64_t)kf;
+                        key = read_key(in);
                         in.row(f.data(), arity, fnull);
                         if (fnull[0]) in.ok = false;                   // COUNT(*) is never NULL
                         if (!sess) start = end - g;
@@ -621,6 +673,20 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
             slide_win.clear();
         }
         if (!in.ok) return fwa_set_error(e, FWA_E_ARG, "heap body: truncated or malformed");
+        if (dict && !comp_nulls.empty()) {                            // placeholder keys -> dictionary ids
+            std::vector<int64_t> ids(comp_nulls.size());
+            if ((rc = fwa_keydict_encode_host(dict, comp_slots.data(), comp_nulls.data(), (int64_t)ids.size(), ids.data())))
+                return fwa_set_error(e, rc, "key dictionary encode");
+            for (int kg = 0; kg < maxp; ++kg) {
+                std::vector<int64_t>& v = per[(size_t)kg];
+                for (size_t r = 0; r < v.size(); r += (size_t)ncols) {
+                    const int64_t id = ids[(size_t)v[r]];
+                    if ((int64_t)((uint64_t)id >> 48) != kg)
+                        return fwa_set_error(e, FWA_E_ARG, "heap body: a key row outside its key group (maxParallelism?)");
+                    v[r] = id;
+                }
+            }
+        }
         // the equivalent FWASNAP1 blob (engine.hip snap_header layout)
         std::vector<int64_t>& w = blobs[(size_t)b];
         w.assign((size_t)(kHdr + maxp + 1 + total * ncols), 0);
@@ -645,6 +711,26 @@ int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* si
         bsz.push_back((int64_t)w.size() * 8);
     }
     return fwa_restore(e, ptrs.data(), bsz.data(), n_bodies);
+}
+
+int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark) {
+    return snapshot_heap_impl(e, nullptr, out, kg_offsets, watermark);
+}
+
+int fwa_restore_heap(fwa_engine* e, const void* const* bodies, const int64_t* sizes, const int64_t* watermarks,
+                     int32_t n_bodies) {
+    return restore_heap_impl(e, nullptr, bodies, sizes, watermarks, n_bodies);
+}
+
+int fwa_snapshot_heap_keys(fwa_engine* e, fwa_keydict* dict, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark) {
+    if (!dict) return e ? fwa_set_error(e, FWA_E_ARG, "fwa_snapshot_heap_keys: null key dictionary") : FWA_E_ARG;
+    return snapshot_heap_impl(e, dict, out, kg_offsets, watermark);
+}
+
+int fwa_restore_heap_keys(fwa_engine* e, fwa_keydict* dict, const void* const* bodies, const int64_t* sizes,
+                          const int64_t* watermarks, int32_t n_bodies) {
+    if (!dict) return e ? fwa_set_error(e, FWA_E_ARG, "fwa_restore_heap_keys: null key dictionary") : FWA_E_ARG;
+    return restore_heap_impl(e, dict, bodies, sizes, watermarks, n_bodies);
 }
 
 }  // extern "C"

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/flink_amd.h"
 #include "java_math.h"
@@ -309,6 +310,61 @@ int fwa_keydict_decode(fwa_keydict* d, const int64_t* ids, int64_t n, void* cons
                                                              nulls ? 1 : 0);
     KDCHK(d, hipGetLastError());
     return read_status(d);
+}
+
+// internal (heap_snapshot.cpp): every row of the dictionary on the host -- slots [row][arity] and null bits
+int fwa_keydict_host_rows(fwa_keydict* d, int32_t* arity, int32_t* types, std::vector<uint64_t>* slots,
+                          std::vector<uint64_t>* nulls) {
+    if (!d) return FWA_E_ARG;
+    *arity = d->arity;
+    for (int c = 0; c < d->arity; ++c) types[c] = d->types[c];
+    const int64_t n = fwa_keydict_size(d);
+    if (n < 0) return FWA_E_DEVICE;
+    std::vector<uint64_t> cols((size_t)n * d->arity);
+    nulls->assign((size_t)n, 0);
+    KDCHK(d, hipSetDevice(d->device));
+    for (int c = 0; c < d->arity && n > 0; ++c)
+        KDCHK(d, hipMemcpyAsync(cols.data() + (size_t)c * n, d->d.fslot + (size_t)c * d->d.max_rows, 8 * (size_t)n,
+                                hipMemcpyDeviceToHost, d->stream));
+    if (n > 0) KDCHK(d, hipMemcpyAsync(nulls->data(), d->d.fnull, 8 * (size_t)n, hipMemcpyDeviceToHost, d->stream));
+    KDCHK(d, hipStreamSynchronize(d->stream));
+    slots->assign((size_t)n * d->arity, 0);
+    for (int64_t r = 0; r < n; ++r)
+        for (int c = 0; c < d->arity; ++c) (*slots)[(size_t)r * d->arity + c] = cols[(size_t)c * n + r];
+    return FWA_OK;
+}
+
+// internal (heap_snapshot.cpp): encode n rows given on the host as slots [row][arity] + null bits; ids to the host
+int fwa_keydict_encode_host(fwa_keydict* d, const uint64_t* slots, const uint64_t* nulls, int64_t n, int64_t* ids) {
+    if (!d || n < 0) return FWA_E_ARG;
+    if (n == 0) return FWA_OK;
+    KDCHK(d, hipSetDevice(d->device));
+    const int a = d->arity;
+    std::vector<uint64_t> cols((size_t)n * a);
+    std::vector<uint8_t> nul((size_t)n * a);
+    for (int64_t r = 0; r < n; ++r)
+        for (int c = 0; c < a; ++c) {
+            const uint64_t v = slots[(size_t)r * a + c];
+            if (d->types[c] == FWA_KEY_FIELD_INT) reinterpret_cast<int32_t*>(cols.data() + (size_t)c * n)[r] = (int32_t)(uint32_t)v;
+            else cols[(size_t)c * n + r] = v;
+            nul[(size_t)c * n + r] = (uint8_t)((nulls[r] >> c) & 1);
+        }
+    char* buf = nullptr;
+    const size_t bc = 8 * (size_t)n * a, bn = (size_t)n * a, bi = 8 * (size_t)n;
+    KDCHK(d, hipMalloc(&buf, bc + bn + bi + 64));
+    int rc = FWA_OK;
+    do {
+        if (hipMemcpyAsync(buf, cols.data(), bc, hipMemcpyHostToDevice, d->stream) != hipSuccess ||
+            hipMemcpyAsync(buf + bc, nul.data(), bn, hipMemcpyHostToDevice, d->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        const void* cp[FWA_KEYDICT_MAX_ARITY];
+        const uint8_t* np_[FWA_KEYDICT_MAX_ARITY];
+        for (int c = 0; c < a; ++c) { cp[c] = buf + 8 * (size_t)c * n; np_[c] = (const uint8_t*)(buf + bc + (size_t)c * n); }
+        int64_t* did = (int64_t*)(buf + ((bc + bn + 7) & ~(size_t)7));
+        if ((rc = fwa_keydict_encode(d, cp, np_, n, did, nullptr))) break;
+        if (hipMemcpy(ids, did, bi, hipMemcpyDeviceToHost) != hipSuccess) rc = FWA_E_DEVICE;
+    } while (0);
+    (void)hipFree(buf);
+    return rc;
 }
 
 int fwa_binrow_hash(int32_t arity, const int32_t* field_types, const void* const* cols, const uint8_t* const* nulls,

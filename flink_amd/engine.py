@@ -60,6 +60,11 @@ def lib():
     L.fwa_restore_heap.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                    C.c_int32]
     L.fwa_restore_heap.restype = C.c_int
+    L.fwa_snapshot_heap_keys.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(Blob), C.c_void_p, C.POINTER(C.c_int64)]
+    L.fwa_snapshot_heap_keys.restype = C.c_int
+    L.fwa_restore_heap_keys.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64),
+                                        C.POINTER(C.c_int64), C.c_int32]
+    L.fwa_restore_heap_keys.restype = C.c_int
     L.fwa_flush.argtypes = [C.c_void_p]
     L.fwa_get_config.argtypes = [C.c_void_p, C.POINTER(A.Config)]
     L.fwa_get_config.restype = C.c_int
@@ -276,14 +281,18 @@ class WindowAggregator:
         self._settled()
         _check(rc, self.h)
 
-    def snapshot_heap(self):
+    def snapshot_heap(self, keydict=None):
         """Keyed window state in Flink's heap-backend key-group byte layout (fwa_snapshot_heap): returns
-        (body bytes, per-key-group section offsets, watermark)."""
+        (body bytes, per-key-group section offsets, watermark). keydict: the flink_amd.keydict.KeyDictionary of an
+        engine on dictionary ids (key rows written as its multi-column BinaryRowData rows)."""
         b = Blob()
         nkg = self.cfg.kg_end - self.cfg.kg_start + 1
         offs = np.zeros(nkg, np.int64)
         wm = C.c_int64(0)
-        rc = lib().fwa_snapshot_heap(self.h, C.byref(b), offs.ctypes.data_as(C.c_void_p), C.byref(wm))
+        if keydict is not None:
+            rc = lib().fwa_snapshot_heap_keys(self.h, keydict.h, C.byref(b), offs.ctypes.data_as(C.c_void_p), C.byref(wm))
+        else:
+            rc = lib().fwa_snapshot_heap(self.h, C.byref(b), offs.ctypes.data_as(C.c_void_p), C.byref(wm))
         self._settled()
         _check(rc, self.h)
         try:
@@ -291,12 +300,15 @@ class WindowAggregator:
         finally:
             lib().fwa_blob_free(C.byref(b))
 
-    def restore_heap(self, bodies, watermarks):
+    def restore_heap(self, bodies, watermarks, keydict=None):
         bufs = [C.create_string_buffer(bytes(b), max(1, len(b))) for b in bodies]
         ptrs = (C.c_void_p * len(bufs))(*[C.cast(b, C.c_void_p).value for b in bufs])
         sizes = (C.c_int64 * len(bufs))(*[len(b) for b in bodies])
         wms = (C.c_int64 * len(bufs))(*[int(w) for w in watermarks])
-        rc = lib().fwa_restore_heap(self.h, ptrs, sizes, wms, len(bufs))
+        if keydict is not None:
+            rc = lib().fwa_restore_heap_keys(self.h, keydict.h, ptrs, sizes, wms, len(bufs))
+        else:
+            rc = lib().fwa_restore_heap(self.h, ptrs, sizes, wms, len(bufs))
         self._settled()
         _check(rc, self.h)
 

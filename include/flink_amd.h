@@ -409,6 +409,11 @@ int fwa_keydict_encode(fwa_keydict* d, const void* const* cols, const uint8_t* c
                        int32_t* hashes);
 /* Device pointers: the key columns (and NULL flags, if nulls != NULL) of n ids from this dictionary. */
 int fwa_keydict_decode(fwa_keydict* d, const int64_t* ids, int64_t n, void* const* cols, uint8_t* const* nulls);
+/* fwa_snapshot_heap / fwa_restore_heap for an engine on dictionary ids (Table semantics): key rows are written and
+ * read as the dictionary's BinaryRowData rows of `arity` fields (restored rows are encoded into `dict`). */
+int fwa_snapshot_heap_keys(fwa_engine* e, fwa_keydict* dict, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark);
+int fwa_restore_heap_keys(fwa_engine* e, fwa_keydict* dict, const void* const* bodies, const int64_t* sizes,
+                          const int64_t* watermarks, int32_t n_bodies);
 /* BinaryRowData.hashCode() of n rows of fixed-length fields, device pointers (no dictionary). */
 int fwa_binrow_hash(int32_t arity, const int32_t* field_types, const void* const* cols, const uint8_t* const* nulls,
                     int64_t n, int32_t* out, int32_t device);

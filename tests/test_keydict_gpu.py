@@ -241,3 +241,67 @@ def test_dictionary_ids_key_group_ownership_partials_and_rescale():
     assert_rows_equal(g.advance_watermark(A.LONG_MAX), final, names, rtol=1e-9)
     g.close()
     d.close()
+
+
+def test_heap_layout_with_multi_column_key_rows():
+    """fwa_snapshot_heap_keys: the window state of an engine on dictionary ids in Flink's heap layout with the key as
+    its multi-column BinaryRowData row (read back with tests/heap_reader.py); restored by two subtasks into fresh
+    dictionaries (rescaling), the run resumes exactly like the oracle."""
+    import heap_reader as H
+    from flink_amd import engine
+    from flink_amd.keydict import KeyDictionary
+    from oracle.oracle import Oracle
+    d, ids, ts, cols = multi_key_stream(13, 30_000, 1200, 40_000, 1000)
+    base = dict(window_kind="SLIDE", semantics="TABLE", size_ms=10_000, slide_ms=5000, aggs=AGGS,
+                key_kind=A.KEY_GROUP_PREFIXED, key_capacity=8192)
+    names = A.agg_names(A.make_config(**base))
+    cut = 18_000
+    wm1 = int(ts[:cut].max()) - 1001
+    o = Oracle(A.make_config(**base))
+    o.push(ids[:cut], ts[:cut], [c[:cut] for c in cols])
+    o.advance_watermark(wm1)
+    g = engine.WindowAggregator(A.make_config(**base))
+    g.push(ids[:cut], ts[:cut], [c[:cut] for c in cols])
+    g.advance_watermark(wm1)
+    body, offs, wm = g.snapshot_heap(keydict=d)
+    g.close()
+    # the key rows are the dictionary's 2-field rows (INT, BIGINT)
+    lay = {0: ("kv", H.ser_long, H.ser_binrow(2), H.ser_binrow(1 + len(AGGS))), 1: ("pq", H.ser_binrow(2), H.ser_long),
+           2: ("pq", H.ser_binrow(2), H.ser_long)}
+    secs = H.read_key_groups(body, offs, 0, lay)
+    seen = set()
+    for kg, sec in secs.items():
+        for _, key, _ in sec.get(0, []):
+            rk, nl, f = key
+            assert rk == 0
+            seen.add((kg, tuple(nl), tuple(f)))
+    dec, dn = d.decode(np.unique(ids[:cut]))
+    assert len(seen) > 0 and len({s[1:] for s in seen}) <= len(dec[0])
+    # restore into two new subtasks, each with its own dictionary, and finish the run
+    o.push(ids[cut:], ts[cut:], [c[cut:] for c in cols])
+    final = o.advance_watermark(A.LONG_MAX)
+    rows_dec = []
+    for klo, khi in [(0, 50), (51, 127)]:
+        d2 = KeyDictionary(["INT", "BIGINT"], max_parallelism=128, capacity=8192)
+        g2 = engine.WindowAggregator(A.make_config(kg_start=klo, kg_end=khi, **base))
+        g2.restore_heap([body], [wm], keydict=d2)
+        # the rest of the stream, re-keyed through the new dictionary (the same rows, new ids)
+        (kc, kn) = d.decode(ids[cut:])
+        nid = d2.encode(kc, [z.astype(np.uint8) for z in kn]).cpu().numpy()
+        m = ((nid >> 48) >= klo) & ((nid >> 48) <= khi)
+        g2.push(nid[m], ts[cut:][m], [c[cut:][m] for c in cols])
+        r = g2.advance_watermark(A.LONG_MAX)
+        kc2, kn2 = d2.decode(r["key"]) if len(r["key"]) else ([np.zeros(0, np.int32), np.zeros(0, np.int64)], None)
+        rows_dec.append((r, kc2, kn2))
+        g2.close()
+        d2.close()
+    # compare with the oracle's final rows through the original dictionary's rows
+    fk, _ = d.decode(final["key"])
+    exp = sorted(zip(fk[0].tolist(), fk[1].tolist(), final["win_start"].tolist(), final["win_end"].tolist(),
+                     *[final["agg%d" % j].tolist() for j in range(3)]))
+    got = []
+    for r, kc2, _ in rows_dec:
+        got += list(zip(kc2[0].tolist(), kc2[1].tolist(), r["win_start"].tolist(), r["win_end"].tolist(),
+                        *[r["agg%d" % j].tolist() for j in range(3)]))
+    assert sorted(got) == exp
+    d.close()
