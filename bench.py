@@ -203,14 +203,20 @@ def main():
     e2e_bytes = rec_bytes * recs_timed + row_bytes * rows_all   # whole-job algorithmic bytes incl. emitted rows
     # HBM traffic per ingest launch (Phase P + Phase A) from the committed rocprofv3 PMC passes of this
     # same workload (counters need their own runs: tools/gpu_pmc.sh); null for other shapes
-    traffic, traffic_src = None, None
-    pmc_path = os.path.join(ROOT, "profiles", "r02_pmc_%s.json" % args.config)
-    if world == 1 and os.path.exists(pmc_path):
+    traffic, traffic_src, traffic_bounds = None, None, None
+    for tag in ("r03", "r02"):
+        pmc_path = os.path.join(ROOT, "profiles", "%s_pmc_%s.json" % (tag, args.config))
+        if world != 1 or not os.path.exists(pmc_path):
+            continue
         pmc = json.load(open(pmc_path))
         if pmc["config"]["batch"] == B:
             traffic = pmc["ingest_bytes_per_launch"]
-            traffic_src = ("profiles/r02_pmc_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the ingest kernels per "
-                           "timed step, tools/gpu_pmc_all.sh)" % args.config)
+            traffic_bounds = pmc.get("ingest_bytes_per_launch_bounds")
+            traffic_src = ("profiles/%s_pmc_%s.json (rocprofv3 FETCH_SIZE + WRITE_SIZE of the ingest kernels per timed "
+                           "step, tools/gpu_pmc_all.sh; FETCH_SIZE x2 %s)"
+                           % (tag, args.config, "for the wide streaming readers only, raw / all-x2 bounds beside"
+                              if traffic_bounds else "for every kernel"))
+        break
     if args.config == "c3":
         metric = "records/sec aggregated (C3: HOP 60s/1s, Zipf(1.1) keys over %d items)" % args.keys
         workload = ("C3: Table HOP 60s/1s (1s slices) COUNT+SUM(long), Zipf(1.1) over %d keys, %d records/GPU "
@@ -255,7 +261,7 @@ def main():
             "bound": "hbm", "kernel": ingest_kernels(args, eng),
             "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_unit": "bytes per launch",
-            "traffic_source": traffic_src, "alg_bytes_per_launch": rec_bytes * B,
+            "traffic_source": traffic_src, "traffic_bounds": traffic_bounds, "alg_bytes_per_launch": rec_bytes * B,
             "alg_bytes_per_record": rec_bytes, "launches": st.ingest_launches,
             "avg_launch_ms": st.ingest_ms / max(1, st.ingest_launches),
         },

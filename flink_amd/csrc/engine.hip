@@ -1859,7 +1859,7 @@ struct SessCtr {                 // per-push device counters (zeroed by the host
     unsigned long long n_bulk, n_sp;     // elements routed to the bulk / the arrival-order path
     unsigned long long n_out_sp;         // sessions written by the arrival-order path
     unsigned long long n_keep;           // fire: sessions kept
-    unsigned long long pad;
+    unsigned long long n_redo;           // cell path: elements outside the cell range (the push is redone)
 };
 
 struct SessList {                // one in-flight session list (SoA)
@@ -1907,6 +1907,7 @@ struct Sess2Args {
     uint32_t* sg_off;            // [nw + 1] their exclusive sum
     int64_t* sg_h0;              // [nw] first owned position per wave
     int32_t pkw;
+    jm::UDiv64 gap_div;          // cell path: cell = (start - base) / gap, base = ctr->ts_min
     int32_t seg_out;             // bulk sessions appended on ctr->n_out_sp by sess2_segment_kernel (the arrival-order
                                  // path appends after them on the same counter)
     int64_t* bend;               // [nb] window / session end per sorted element
@@ -2329,6 +2330,363 @@ __global__ void __launch_bounds__(kBlock) sess2_compact_kernel(Sess2Args a, int6
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr->n_out_sp = a.sg_off[nw];
+}
+
+// ---- Cell path: fixed gap, every record of the push order-free ------------------------------------------------------
+// The time axis is cut into cells of width gap starting at base = the smallest start of the push. Two windows whose
+// starts lie in one cell intersect (s2 - s1 < gap <= end1 - s1, TimeWindow.intersects), so the elements of one
+// (kid, cell) group end in one session whatever their order: sorting by the 32-bit key kid << cb | cell (cb = 32 -
+// kid_bits) replaces the (kid, start) sort (4 one-byte passes over 8-byte pairs instead of 5 over 12-byte pairs), and
+// the segment walk reduces each group (min start, max end, accumulators) before chaining the key's groups in cell
+// order. Records go to the sort at their input position (no compaction); a record that is not order-free or a start
+// outside the cell range is counted and the host redoes the push on the general path (sess2_*).
+constexpr uint32_t kCellSent = 0xffffffffu;        // sorts last; its kid (all ones in kid_bits) is never a real kid
+
+__global__ void __launch_bounds__(kBlock) sess3_min_kernel(Sess2Args a) {
+    __shared__ unsigned long long s_lo[kBlock / 64];
+    unsigned long long lo = ~0ull;
+    const int64_t tot = a.n + a.n_in;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long o = jm::ord_i64(t < a.n ? a.ts[t] : a.in.start[t - a.n]);
+        lo = o < lo ? o : lo;
+    }
+    for (int sh = 32; sh >= 1; sh >>= 1) { const unsigned long long y = __shfl_xor(lo, sh); lo = y < lo ? y : lo; }
+    if ((threadIdx.x & 63) == 0) s_lo[threadIdx.x >> 6] = lo;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) lo = s_lo[w] < lo ? s_lo[w] : lo;
+        if (lo != ~0ull) atomicMin(&a.ctr->ts_min, lo);
+    }
+}
+
+// Records (t < n, sort position = input position) and in-flight sessions (t >= n): key-group check, kid, 32-bit cell
+// key, payload (record index, or session index | 0x80000000), and the record's packed row [ts, acc_1 .. acc_{nacc-1}]
+// (COUNT is 1 for a record; a session's words are read from the in-flight list by the segment walk).
+__global__ void __launch_bounds__(kBlock) sess3_route_kernel(Sess2Args a, const EngineConst* __restrict__ cp) {
+    __shared__ uint32_t s_c[2];
+    const EngineConst& c = *cp;
+    if (threadIdx.x == 0) { s_c[0] = 0u; s_c[1] = 0u; }
+    __syncthreads();
+    const int cb = a.tb;
+    const uint64_t ncell = (uint64_t)1 << cb;
+    const uint64_t base = (uint64_t)jm::unord_i64(a.ctr->ts_min);
+    uint32_t nsp = 0, nredo = 0;
+    const int64_t tot = a.n + a.n_in;
+    uint32_t* bkey = reinterpret_cast<uint32_t*>(a.bkey);
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t k32 = kCellSent, pay;
+        if (t < a.n) {
+            const int64_t key = a.keys[t];
+            const int64_t ts = a.ts[t];
+            pay = (uint32_t)t;
+            const int32_t kg = jm::key_group_of(key, c.key_kind, a.key_hash ? a.key_hash[t] : 0, c.max_par);
+            if (kg < c.kg_lo || kg > c.kg_hi) {
+                raise_error(a.st, FWA_E_KEYGROUP);                     // StateTable :300-307
+            } else {
+                const int64_t kid = key_slot(a.key_table, a.key_mask, a.seg_log, a.part_bits, key, a.st);
+                if (kid < 0) {
+                    a.st->key_full = 1;
+                    raise_error(a.st, FWA_E_OOM);
+                } else if (jm::wsub(jm::wadd(ts, a.gap), 1) <= a.wm) {  // order-sensitive: the general path
+                    a.kflag[kid] = 1;
+                    ++nsp;
+                } else {
+                    const uint64_t cell = jm::udiv64((uint64_t)ts - base, a.gap_div);
+                    if (cell >= ncell) ++nredo;
+                    else k32 = ((uint32_t)kid << cb) | (uint32_t)cell;
+                    unsigned long long* row = a.pk + t * a.pkw;
+                    auto word = [&](int cc) -> unsigned long long {
+                        if (cc == 0) return (unsigned long long)ts;
+                        const AggDesc& d = c.agg[a.col_owner[cc]];
+                        return acc_input(d, a.cols[d.col], t, a.nulls[d.col]);
+                    };
+                    int cc = 0;
+                    if ((a.pkw & 1) == 0)
+                        for (; cc < a.pkw; cc += 2) *reinterpret_cast<ulonglong2*>(row + cc) = make_ulonglong2(word(cc), word(cc + 1));
+                    for (; cc < a.pkw; ++cc) row[cc] = word(cc);
+                }
+            }
+        } else {
+            const int64_t j = t - a.n;
+            pay = (uint32_t)j | 0x80000000u;
+            const uint64_t cell = jm::udiv64((uint64_t)a.in.start[j] - base, a.gap_div);
+            if (cell >= ncell) ++nredo;
+            else k32 = (a.in.kid[j] << cb) | (uint32_t)cell;
+        }
+        bkey[t] = k32;
+        a.bval[t] = pay;
+    }
+    for (int sh = 32; sh >= 1; sh >>= 1) { nsp += __shfl_xor(nsp, sh); nredo += __shfl_xor(nredo, sh); }
+    if ((threadIdx.x & 63) == 0 && (nsp | nredo)) { atomicAdd(&s_c[0], nsp); atomicAdd(&s_c[1], nredo); }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_c[0]) atomicAdd(&a.ctr->n_special, (unsigned long long)s_c[0]);
+    if (threadIdx.x == 0 && s_c[1]) atomicAdd(&a.ctr->n_redo, (unsigned long long)s_c[1]);
+}
+
+__device__ __forceinline__ uint32_t perm32(int dst4, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_permute(dst4, (int)v); }
+__device__ __forceinline__ unsigned long long perm64(int dst4, unsigned long long v) {
+    const uint32_t lo = perm32(dst4, (uint32_t)v), hi = perm32(dst4, (uint32_t)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// Cross-lane moves on the VALU (DPP) instead of the LDS crossbar: row_shr:n = 0x110 + n, row_bcast:15 = 0x142,
+// row_bcast:31 = 0x143, wave_shl:1 = 0x130, wave_shr:1 = 0x138 (lanes without a source get 0)
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xf, false);
+}
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ unsigned long long dpp64(unsigned long long v) {
+    return ((unsigned long long)dpp32<CTRL, RM>((uint32_t)(v >> 32)) << 32) | dpp32<CTRL, RM>((uint32_t)v);
+}
+__device__ __forceinline__ unsigned long long rdlane64(unsigned long long v, int l) {   // wave-uniform l
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t rdlane32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+
+// Segmented inclusive scan: lane L combines the lanes [gs(L), L] (gs = first lane of L's segment), f(x, earlier).
+// Hillis-Steele inside rows of 16 (row_shr 1, 2, 4, 8), then the row totals (row_bcast 15 / 31).
+template <class F>
+__device__ __forceinline__ unsigned long long seg_scan64(unsigned long long x, int lane, int gs, F f) {
+    unsigned long long y;
+    y = dpp64<0x111>(x); if ((lane & 15) >= 1 && lane - 1 >= gs) x = f(x, y);
+    y = dpp64<0x112>(x); if ((lane & 15) >= 2 && lane - 2 >= gs) x = f(x, y);
+    y = dpp64<0x114>(x); if ((lane & 15) >= 4 && lane - 4 >= gs) x = f(x, y);
+    y = dpp64<0x118>(x); if ((lane & 15) >= 8 && lane - 8 >= gs) x = f(x, y);
+    y = dpp64<0x142, 0xa>(x); if ((lane & 16) != 0 && gs < (lane & ~15)) x = f(x, y);
+    y = dpp64<0x143, 0xc>(x); if (lane >= 32 && gs < 32) x = f(x, y);
+    return x;
+}
+__device__ __forceinline__ int64_t seg_min64(int64_t x, int lane, int gs) {
+    return (int64_t)seg_scan64((unsigned long long)x, lane, gs, [](unsigned long long p, unsigned long long q) {
+        return (int64_t)q < (int64_t)p ? q : p; });
+}
+__device__ __forceinline__ int64_t seg_max64(int64_t x, int lane, int gs) {
+    return (int64_t)seg_scan64((unsigned long long)x, lane, gs, [](unsigned long long p, unsigned long long q) {
+        return (int64_t)q > (int64_t)p ? q : p; });
+}
+
+// The cell-sorted elements in one pass. Ownership as in sess2_segment_kernel (wave w owns the keys whose first sorted
+// element lies in [64w, 64w + 64) and walks each to its end). Per 64-element chunk: (1) segmented scans over the
+// (kid, cell) groups -- min start, max end, accumulators -- joined with the group carried from the previous chunk;
+// (2) the groups that end in the chunk are packed to the low lanes (ds_permute) and chained as sess2_segment_kernel
+// chains elements: a group opens a session if it starts a key or starts after the key's running max end.
+template <int NA>
+__global__ void __launch_bounds__(kBlock) sess3_segment_kernel(Sess2Args a, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    const int lane = threadIdx.x & 63;
+    const int cb = a.tb;
+    const uint32_t* bkey = reinterpret_cast<const uint32_t*>(a.bkey);
+    const int64_t nb = a.nb;
+    const int64_t nw = (nb + 63) >> 6;
+    const int64_t wstride = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    int ak[NA];
+    unsigned long long idn[NA];
+#pragma unroll
+    for (int cc = 0; cc < NA; ++cc) { ak[cc] = cc == 0 ? ACC_ADD_I64 : c.acc_kind[cc]; idn[cc] = ident_of(ak[cc]); }
+    const unsigned long long below = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);   // lanes <= this one
+    const unsigned long long before = (1ull << lane) - 1ull;                          // lanes < this one
+    for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
+        const int64_t p0 = w << 6;
+        const int64_t pa = p0 + lane, pb = p0 + 64 + lane;
+        const uint32_t kA = pa < nb ? bkey[pa] : kCellSent, kB = pb < nb ? bkey[pb] : kCellSent;
+        const uint32_t vA = pa < nb ? a.bval[pa] : 0u, vB = pb < nb ? a.bval[pb] : 0u;
+        const uint32_t kprev = p0 > 0 ? bkey[p0 - 1] : kCellSent;
+        const uint32_t kidA = kA >> cb;
+        const uint32_t kup = __shfl_up(kidA, 1);
+        const bool okA = kA != kCellSent;
+        const bool hd = okA && (lane == 0 ? (p0 == 0 || (kprev >> cb) != kidA) : kidA != kup);
+        const unsigned long long hm = __ballot(hd);
+        if (!hm) {
+            if (lane == 0) a.sg_cnt[w] = 0u;
+            continue;
+        }
+        const int64_t h0 = p0 + (__ffsll((long long)hm) - 1);
+        int64_t h1;
+        const unsigned long long sa = __ballot(!okA);               // sentinels / the end inside this range
+        if (sa) {
+            h1 = p0 + (__ffsll((long long)sa) - 1);
+        } else {                                                    // the last owned key may run past the range
+            const uint32_t kl = __shfl(kidA, 63);
+            const unsigned long long dm = __ballot((kB >> cb) != kl);   // a sentinel's kid differs from every kid
+            if (dm) h1 = p0 + 64 + (__ffsll((long long)dm) - 1);
+            else
+                for (int64_t q = p0 + 128;; q += 64) {
+                    const int64_t pp = q + lane;
+                    const uint32_t kq = pp < nb ? bkey[pp] : kCellSent;
+                    const unsigned long long dq = __ballot((kq >> cb) != kl);
+                    if (dq) { h1 = q + (__ffsll((long long)dq) - 1); break; }
+                }
+        }
+        auto fetch = [&](int64_t base, uint32_t& bk, int64_t& st, int64_t& en, unsigned long long* x) {
+            const int64_t q = base + lane;
+            const int64_t d = q - p0;
+            uint32_t pay;
+            if (base + 63 - p0 < 128) {                             // inside the loaded window
+                const int src = (int)(d & 63);
+                const uint32_t ka = __shfl(kA, src), kb = __shfl(kB, src);
+                const uint32_t va = __shfl(vA, src), vb = __shfl(vB, src);
+                bk = d < 64 ? ka : kb;
+                pay = d < 64 ? va : vb;
+            } else {
+                bk = q < h1 ? bkey[q] : kCellSent;
+                pay = q < h1 ? a.bval[q] : 0u;
+            }
+            const uint32_t o = pay & 0x7fffffffu;
+            if (q >= h1) {
+                bk = kCellSent;
+                st = LONG_MAX_J;
+                en = LONG_MIN_J;
+#pragma unroll
+                for (int cc = 0; cc < NA; ++cc) x[cc] = idn[cc];
+            } else if (pay & 0x80000000u) {                         // in-flight session
+                st = a.in.start[o];
+                en = a.in.end[o];
+#pragma unroll
+                for (int cc = 0; cc < NA; ++cc) x[cc] = a.in.acc[(int64_t)cc * a.in.stride + o];
+            } else {                                                // record: packed row [ts, acc_1 ..]
+                const unsigned long long* row = a.pk + (int64_t)o * NA;
+                unsigned long long wv[NA];
+                if constexpr ((NA & 1) == 0) {
+#pragma unroll
+                    for (int cc = 0; cc < NA; cc += 2) {
+                        const ulonglong2 p = reinterpret_cast<const ulonglong2*>(row)[cc >> 1];
+                        wv[cc] = p.x;
+                        wv[cc + 1] = p.y;
+                    }
+                } else {
+#pragma unroll
+                    for (int cc = 0; cc < NA; ++cc) wv[cc] = row[cc];
+                }
+                st = (int64_t)wv[0];
+                en = jm::wadd(st, a.gap);
+                x[0] = 1ull;
+#pragma unroll
+                for (int cc = 1; cc < NA; ++cc) x[cc] = wv[cc];
+            }
+        };
+        // carried group and carried session: wave-uniform (readlane results, held in SGPRs)
+        bool gopen = false, copen = false;
+        uint32_t gkey = 0u, ck = 0u;
+        int64_t gmin = 0, gmax = 0, cmaxe = LONG_MIN_J, cst = 0;
+        unsigned long long gacc[NA], cacc[NA];
+#pragma unroll
+        for (int cc = 0; cc < NA; ++cc) { gacc[cc] = 0ull; cacc[cc] = 0ull; }
+        uint32_t wc = 0;                                            // sessions this wave wrote (staging h0 + i)
+        uint32_t nbk;
+        int64_t nst, nen;
+        unsigned long long nx[NA];
+        fetch(h0, nbk, nst, nen, nx);
+        for (int64_t base = h0; base < h1; base += 64) {
+            const int64_t q = base + lane;
+            const bool v = q < h1;
+            const uint32_t bk = nbk;
+            int64_t st = nst, en = nen;
+            unsigned long long x[NA];
+#pragma unroll
+            for (int cc = 0; cc < NA; ++cc) x[cc] = nx[cc];
+            const bool more = base + 64 < h1;
+            if (more) fetch(base + 64, nbk, nst, nen, nx);
+            // (1) groups
+            const uint32_t gup = dpp32<0x138>(bk);                  // lane - 1
+            const bool gf = v && (lane == 0 ? !(gopen && bk == gkey) : bk != gup);
+            const unsigned long long gm = __ballot(gf) & below;
+            const int gs = gm ? 63 - __clzll((long long)gm) : 0;
+            st = seg_min64(st, lane, gs);
+            en = seg_max64(en, lane, gs);
+#pragma unroll
+            for (int cc = 0; cc < NA; ++cc) {
+                const int k = ak[cc];
+                x[cc] = seg_scan64(x[cc], lane, gs, [k](unsigned long long p, unsigned long long y) { return acc_combine(k, p, y); });
+            }
+            if (gm == 0 && gopen) {                                 // lanes continuing the carried group
+                st = gmin < st ? gmin : st;
+                en = gmax > en ? gmax : en;
+#pragma unroll
+                for (int cc = 0; cc < NA; ++cc) x[cc] = acc_combine(ak[cc], gacc[cc], x[cc]);
+            }
+            const uint32_t nk0 = rdlane32(nbk, 0);                  // the next chunk's first key (when `more`)
+            const uint32_t gdn = dpp32<0x130>(bk);                  // lane + 1
+            const bool gt = v && (q + 1 == h1 || (lane < 63 ? gdn != bk : nk0 != bk));   // the group's last element
+            const int lv = (int)min<int64_t>(63, h1 - 1 - base);   // last valid lane
+            const unsigned long long P = __ballot(gt);
+            if (((P >> lv) & 1ull) == 0) {                          // the last group continues in the next chunk
+                gopen = true;
+                gkey = rdlane32(bk, lv);
+                gmin = (int64_t)rdlane64((unsigned long long)st, lv);
+                gmax = (int64_t)rdlane64((unsigned long long)en, lv);
+#pragma unroll
+                for (int cc = 0; cc < NA; ++cc) gacc[cc] = rdlane64(x[cc], lv);
+            } else {
+                gopen = false;
+            }
+            if (!P) continue;
+            // (2) pack the ended groups to lanes [0, np) in order, then chain them
+            const int np = __popcll(P);
+            const int dst = gt ? __popcll(P & before) : np + __popcll(~P & before);
+            const uint32_t kk = perm32(dst * 4, bk >> cb);
+            const int64_t gst = (int64_t)perm64(dst * 4, (unsigned long long)st);
+            const int64_t gen = (int64_t)perm64(dst * 4, (unsigned long long)en);
+            unsigned long long acc[NA];
+#pragma unroll
+            for (int cc = 0; cc < NA; ++cc) acc[cc] = perm64(dst * 4, x[cc]);
+            const bool range_end = base + lv + 1 == h1;             // the last packed group closes the walk
+            const bool pv = lane < np;
+            const uint32_t kp = dpp32<0x138>(kk);
+            const bool kc = pv && (lane == 0 ? (!copen || kk != ck) : kk != kp);
+            const unsigned long long km = __ballot(kc) & below;
+            const int ks = km ? 63 - __clzll((long long)km) : 0;
+            int64_t m = seg_max64(pv ? gen : LONG_MIN_J, lane, ks);   // running max end of the key (inclusive)
+            if (km == 0 && copen && cmaxe > m) m = cmaxe;           // the key continues from the carried session
+            int64_t mprev = (int64_t)dpp64<0x138>((unsigned long long)m);
+            if (lane == 0) mprev = cmaxe;
+            const bool head = pv && (kc || gst > mprev);
+            const unsigned long long H = __ballot(head);
+            const unsigned long long hb = H & below;
+            const int cs = hb ? 63 - __clzll((long long)hb) : 0;
+            const bool ccont = hb == 0;                             // still the carried session
+            const int64_t hst = __shfl(gst, cs);
+            const int64_t cstart = ccont ? cst : hst;
+#pragma unroll
+            for (int cc = 0; cc < NA; ++cc) {
+                const int k = ak[cc];
+                unsigned long long xx = seg_scan64(acc[cc], lane, cs, [k](unsigned long long p, unsigned long long y) { return acc_combine(k, p, y); });
+                if (ccont && copen) xx = acc_combine(ak[cc], cacc[cc], xx);
+                acc[cc] = xx;
+            }
+            const bool nxt = lane < 63 && ((H >> (lane + 1)) & 1ull) != 0;
+            const bool tail = pv && (lane == np - 1 ? range_end : nxt);
+            const bool emit_c = copen && (H & 1ull) != 0;           // the carried session ended before lane 0
+            if (emit_c && lane == 0) {
+                const int64_t sc = h0 + (int64_t)wc;
+                a.sg_kid[sc] = ck;
+                a.sg_start[sc] = cst;
+                a.sg_end[sc] = cmaxe;
+#pragma unroll
+                for (int cc = 0; cc < NA; ++cc) a.sg_acc[(int64_t)cc * a.sg_cap + sc] = cacc[cc];
+            }
+            wc += emit_c ? 1u : 0u;
+            const unsigned long long tm = __ballot(tail);
+            if (tail) {
+                const int64_t so = h0 + (int64_t)wc + __popcll(tm & before);
+                a.sg_kid[so] = kk;
+                a.sg_start[so] = cstart;
+                a.sg_end[so] = m;
+#pragma unroll
+                for (int cc = 0; cc < NA; ++cc) a.sg_acc[(int64_t)cc * a.sg_cap + so] = acc[cc];
+            }
+            wc += (uint32_t)__popcll(tm);
+            ck = rdlane32(kk, np - 1);
+            cmaxe = (int64_t)rdlane64((unsigned long long)m, np - 1);
+            cst = (int64_t)rdlane64((unsigned long long)cstart, np - 1);
+#pragma unroll
+            for (int cc = 0; cc < NA; ++cc) cacc[cc] = rdlane64(acc[cc], np - 1);
+            copen = true;
+        }
+        if (lane == 0) { a.sg_cnt[w] = wc; a.sg_h0[w] = h0; }
+    }
 }
 
 __device__ __forceinline__ int64_t sess_key_of(const unsigned long long* key_table, int64_t capacity, uint32_t kid) {
@@ -2802,6 +3160,7 @@ struct fwa_engine {
     uint32_t* d_flat = nullptr;            // flat Phase P layout: (partition, block) counts | their exclusive sum
     int64_t flat_cap = 0;
     int64_t sg_cap = 0, sgw_cap = 0;
+    int32_t cell_skip = 0;          // sessions: pushes left before the cell path is tried again after a redo
     int64_t* d_spe = nullptr;
     int64_t* d_smax = nullptr;
     uint32_t* d_scid = nullptr;
@@ -3872,6 +4231,49 @@ static int read_sess_ctr(fwa_engine* e) {
     return sync_status(e);
 }
 
+// Staging buffers, the segment walk (sess2_segment_kernel, or sess3_segment_kernel over cell keys), the scan of the
+// per-wave counts and the compaction into s.out.
+static int launch_segments(fwa_engine* e, Sess2Args& s, int64_t nb, bool cells) {
+    const int64_t nw = (nb + 63) / 64;
+    if (nb > e->sg_cap || nw + 1 > e->sgw_cap) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (e->d_sg) HIPCHK(e, hipFree(e->d_sg));
+        e->d_sg = nullptr;
+        e->sg_cap = std::max<int64_t>(nb + nb / 4, 1 << 14);
+        e->sgw_cap = (e->sg_cap + 63) / 64 + 1;
+        const size_t bytes = (size_t)e->sg_cap * (4 + 8 + 8 + 8 * (size_t)e->nacc) + (size_t)e->sgw_cap * (4 + 4 + 8) + 1024;
+        HIPCHK(e, hipMalloc(&e->d_sg, bytes));
+    }
+    char* sp = (char*)e->d_sg;
+    s.sg_start = (int64_t*)sp; sp += 8 * (size_t)e->sg_cap;
+    s.sg_end = (int64_t*)sp; sp += 8 * (size_t)e->sg_cap;
+    s.sg_acc = (unsigned long long*)sp; sp += 8 * (size_t)e->sg_cap * e->nacc;
+    s.sg_h0 = (int64_t*)sp; sp += 8 * (size_t)e->sgw_cap;
+    s.sg_kid = (uint32_t*)sp; sp += 4 * (size_t)e->sg_cap;
+    s.sg_cnt = (uint32_t*)sp; sp += 4 * (size_t)e->sgw_cap;
+    s.sg_off = (uint32_t*)sp;
+    s.sg_cap = e->sg_cap;
+    const unsigned sg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nb + 255) / 256, 1 << 16));
+    switch (e->nacc) {
+        case 1: if (cells) sess3_segment_kernel<1><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); else sess2_segment_kernel<1><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
+        case 2: if (cells) sess3_segment_kernel<2><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); else sess2_segment_kernel<2><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
+        case 3: if (cells) sess3_segment_kernel<3><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); else sess2_segment_kernel<3><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
+        case 4: if (cells) sess3_segment_kernel<4><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); else sess2_segment_kernel<4><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
+        default: if (cells) sess3_segment_kernel<5><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); else sess2_segment_kernel<5><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
+    }
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipMemsetAsync(s.sg_cnt + nw, 0, 4, e->stream));
+    size_t bytes = 0;
+    HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s.sg_cnt, s.sg_off, (int)(nw + 1), e->stream));
+    int rc = ensure_sort_tmp(e, bytes);
+    if (rc) return rc;
+    bytes = e->sort_tmp_bytes;
+    HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(e->d_sort_tmp, bytes, s.sg_cnt, s.sg_off, (int)(nw + 1), e->stream));
+    sess2_compact_kernel<<<grid_for(nw, 256 * 8), kBlock, 0, e->stream>>>(s, nw, e->nacc);
+    HIPCHK(e, hipGetLastError());
+    return FWA_OK;
+}
+
 static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     const int64_t n = a.n;
     const int64_t n_in = e->n_ss;
@@ -3941,6 +4343,65 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     s.ctr = e->d_sctr;
     s.dropidx = a.dropidx;
     s.st = e->d_st;
+    static const bool scan_path = getenv("FWA_SESS_SCAN") != nullptr;   // A/B: the r02 multi-pass bulk path
+    // cell path (sess3_*): fixed gap, 32-bit cell keys; redone on the general path below when a record is not
+    // order-free or a start falls outside the cell range (then not tried again for 8 pushes)
+    const char* cell_s = getenv("FWA_SESS_CELL");         // A/B switch, read per push (tests toggle it)
+    const int cell_env = cell_s ? atoi(cell_s) : 1;
+    const int cb = 32 - e->kid_bits;
+    if (cell_env != 0 && !s.gapc && cb >= 1 && e->nacc <= 5 && !scan_path && n > 0 && e->cell_skip <= 0 &&
+        n + n_in < ((int64_t)1 << 31)) {
+        Sess2Args t = s;
+        t.tb = cb;
+        t.gap_div = jm::udiv64_make((uint64_t)e->cfg.gap_ms);
+        t.nb = n + n_in;
+        t.bkey = e->d_skey[0];
+        t.bval = e->d_sval[0];
+        t.pk = e->d_spk;
+        t.pkw = e->nacc;
+        t.seg_out = 1;
+        HIPCHK(e, hipEventRecord(e->ev[0], e->stream));
+        sess3_min_kernel<<<grid_for(n + n_in, 1024), kBlock, 0, e->stream>>>(t);
+        sess3_route_kernel<<<grid_for(n + n_in, 256 * 32), kBlock, 0, e->stream>>>(t, e->d_ec);
+        HIPCHK(e, hipGetLastError());
+        size_t bytes = 0;
+        const uint32_t* k0 = (const uint32_t*)e->d_skey[0];
+        uint32_t* k1 = (uint32_t*)e->d_skey[1];
+        HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k0, k1, (const uint32_t*)e->d_sval[0], e->d_sval[1],
+                                                     (int)t.nb, 0, 32, e->stream));
+        if ((rc = ensure_sort_tmp(e, bytes))) return rc;
+        bytes = e->sort_tmp_bytes;
+        HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(e->d_sort_tmp, bytes, k0, k1, (const uint32_t*)e->d_sval[0], e->d_sval[1],
+                                                     (int)t.nb, 0, 32, e->stream));
+        t.bkey = e->d_skey[1];
+        t.bval = e->d_sval[1];
+        if ((rc = launch_segments(e, t, t.nb, true))) return rc;
+        HIPCHK(e, hipEventRecord(e->ev[1], e->stream));
+        if ((rc = read_sess_ctr(e))) return rc;
+        if (e->h_st->error) return FWA_OK;                // reported by the caller
+        if (getenv("FWA_DEBUG_CELL"))
+            fprintf(stderr, "[cell] n %lld n_in %lld kid_bits %d cb %d base %lld special %llu redo %llu out %llu\n",
+                    (long long)n, (long long)n_in, e->kid_bits, cb, (long long)jm::unord_i64(e->h_sctr->ts_min),
+                    e->h_sctr->n_special, e->h_sctr->n_redo, e->h_sctr->n_out_sp);
+        if (e->h_sctr->n_special == 0 && e->h_sctr->n_redo == 0) {
+            if ((rc = account_ingest(e))) return rc;
+            e->ingest_launches++;
+            e->ingest_records += n;
+            e->n_ss = (int64_t)e->h_sctr->n_out_sp;
+            e->ss_cur ^= 1;
+            *dropped_out = (int64_t)e->h_st->dropped;
+            return FWA_OK;
+        }
+        e->cell_skip = 8;                                 // the general path redoes the push (key inserts are idempotent)
+        e->replay_records += n;
+        memset(&z, 0, sizeof(z));
+        z.ts_min = ~0ull;
+        if ((rc = upload(e, e->d_sctr, &z, sizeof(z)))) return rc;
+        HIPCHK(e, hipMemsetAsync(e->d_kflag, 0, (size_t)e->capacity + 1, e->stream));
+        if ((rc = reset_push_status(e))) return rc;
+    } else if (e->cell_skip > 0) {
+        --e->cell_skip;
+    }
     HIPCHK(e, hipEventRecord(e->ev[0], e->stream));
     if (n > 0) sess2_classify_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(s, e->d_ec);
     if (n_in > 0) sess2_range_kernel<<<grid_for(n_in, 256 * 32), kBlock, 0, e->stream>>>(s);
@@ -3988,45 +4449,9 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
         s.bkey = e->d_skey[1];
         s.bval = e->d_sval[1];
     }
-    static const bool scan_path = getenv("FWA_SESS_SCAN") != nullptr;   // A/B: the r02 multi-pass bulk path
     s.seg_out = (!scan_path && e->nacc <= 5) ? 1 : 0;
     if (nb > 0 && s.seg_out) {
-        const int64_t nw = (nb + 63) / 64;
-        if (nb > e->sg_cap || nw + 1 > e->sgw_cap) {
-            HIPCHK(e, hipStreamSynchronize(e->stream));
-            if (e->d_sg) HIPCHK(e, hipFree(e->d_sg));
-            e->d_sg = nullptr;
-            e->sg_cap = std::max<int64_t>(nb + nb / 4, 1 << 14);
-            e->sgw_cap = (e->sg_cap + 63) / 64 + 1;
-            const size_t bytes = (size_t)e->sg_cap * (4 + 8 + 8 + 8 * (size_t)e->nacc) + (size_t)e->sgw_cap * (4 + 4 + 8) + 1024;
-            HIPCHK(e, hipMalloc(&e->d_sg, bytes));
-        }
-        char* sp = (char*)e->d_sg;
-        s.sg_start = (int64_t*)sp; sp += 8 * (size_t)e->sg_cap;
-        s.sg_end = (int64_t*)sp; sp += 8 * (size_t)e->sg_cap;
-        s.sg_acc = (unsigned long long*)sp; sp += 8 * (size_t)e->sg_cap * e->nacc;
-        s.sg_h0 = (int64_t*)sp; sp += 8 * (size_t)e->sgw_cap;
-        s.sg_kid = (uint32_t*)sp; sp += 4 * (size_t)e->sg_cap;
-        s.sg_cnt = (uint32_t*)sp; sp += 4 * (size_t)e->sgw_cap;
-        s.sg_off = (uint32_t*)sp;
-        s.sg_cap = e->sg_cap;
-        const unsigned sg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nb + 255) / 256, 1 << 16));
-        switch (e->nacc) {
-            case 1: sess2_segment_kernel<1><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
-            case 2: sess2_segment_kernel<2><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
-            case 3: sess2_segment_kernel<3><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
-            case 4: sess2_segment_kernel<4><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
-            default: sess2_segment_kernel<5><<<sg, kBlock, 0, e->stream>>>(s, e->d_ec); break;
-        }
-        HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipMemsetAsync(s.sg_cnt + nw, 0, 4, e->stream));
-        size_t bytes = 0;
-        HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s.sg_cnt, s.sg_off, (int)(nw + 1), e->stream));
-        if ((rc = ensure_sort_tmp(e, bytes))) return rc;
-        bytes = e->sort_tmp_bytes;
-        HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(e->d_sort_tmp, bytes, s.sg_cnt, s.sg_off, (int)(nw + 1), e->stream));
-        sess2_compact_kernel<<<grid_for(nw, 256 * 8), kBlock, 0, e->stream>>>(s, nw, e->nacc);
-        HIPCHK(e, hipGetLastError());
+        if ((rc = launch_segments(e, s, nb, false))) return rc;
     } else if (nb > 0) {
         size_t bytes = 0;
         sess2_ends_kernel<<<grid_for(nb, 256 * 32), kBlock, 0, e->stream>>>(s);

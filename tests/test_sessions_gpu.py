@@ -136,3 +136,72 @@ def test_session_late_firings_mixed_with_bulk(eng_mod):
     ]
     batches = [(kk, tt, [tt * 3, tt * 3, (tt * 0.5).astype(np.float64)], wm) for kk, tt, wm in pushes]
     _run(eng_mod, cfg, batches)
+
+
+# ---- cell path (sess3_*: fixed gap, every record of the push order-free) ---------------------------
+# A stream without late records batched as _batches does is order-free in every push (each record's window ends after
+# the previous watermark), so these pushes run on the cell path; FWA_SESS_CELL=0 forces the general path on the same
+# stream. replay_records counts the records of pushes the cell path had to hand back to the general path.
+CELL_AGGS = {
+    1: [("COUNT", 0)],
+    2: [("COUNT", 0), ("SUM_I64", 0)],
+    3: [("COUNT", 0), ("SUM_I64", 0), ("MAX_I64", 0)],
+    4: [("COUNT", 0), ("SUM_I64", 0), ("MIN_I64", 0), ("MAX_F64", 2)],
+    5: AGGS,
+}
+
+
+@pytest.mark.parametrize("cell", ["1", "0"])
+@pytest.mark.parametrize("nacc", [1, 2, 3, 4, 5])
+def test_cell_path_order_free_vs_oracle(eng_mod, monkeypatch, nacc, cell):
+    monkeypatch.setenv("FWA_SESS_CELL", cell)
+    keys, ts, vi, vd = _stream(100 + nacc, 200_000, 3000, 400_000, 300, 0.0)
+    cfg = A.make_config(window_kind="SESSION", gap_ms=700, aggs=CELL_AGGS[nacc], key_capacity=8192)
+    dropped, st = _run(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 12, 300))
+    assert dropped == 0
+    assert st.replay_records == 0
+
+
+def test_cell_path_groups_span_many_chunks(eng_mod):
+    """10 keys, ~1000 records per (key, cell): groups run over many 64-element chunks and wave ranges; holes in event
+    time split sessions inside and across pushes."""
+    rng = np.random.default_rng(21)
+    n = 1 << 20
+    keys = rng.integers(0, 10, n).astype(np.int64)
+    base = np.sort(rng.integers(0, 500_000, n)).astype(np.int64)
+    keep = (base % 97_000) > 8_000                               # 8 s holes: a new session after each
+    keys, base = keys[keep], base[keep]
+    ts = base - rng.integers(0, 200, len(base))
+    vi = rng.integers(-2**40, 2**40, len(base)).astype(np.int64)
+    vd = rng.random(len(base)) * 100.0
+    cfg = A.make_config(window_kind="SESSION", gap_ms=5000, aggs=AGGS, key_capacity=64)
+    _, st = _run(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 5, 200))
+    assert st.replay_records == 0
+
+
+def test_cell_path_table_session_vs_oracle(eng_mod):
+    keys, ts, vi, vd = _stream(23, 100_000, 1500, 300_000, 250, 0.0)
+    cfg = A.make_config(window_kind="SESSION", semantics="TABLE", gap_ms=900, aggs=AGGS, key_capacity=4096)
+    _, st = _run(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 8, 250))
+    assert st.replay_records == 0
+
+
+def test_cell_range_overflow_is_redone(eng_mod):
+    """A large key table leaves few bits for the cell (2^23 slots: 8 cell bits); a push spanning more than 256 gaps is
+    handed back to the general path, with the same results."""
+    keys, ts, vi, vd = _stream(29, 50_000, 500, 100_000, 5, 0.0)
+    cfg = A.make_config(window_kind="SESSION", gap_ms=10, aggs=AGGS, key_capacity=1 << 22)
+    _, st = _run(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 3, 5))
+    assert st.replay_records > 0
+
+
+def test_cell_path_redo_on_order_sensitive_records(eng_mod):
+    """Late records in a push hand it back to the general path (arrival-order walk for their keys); the pushes after
+    the skip window take the cell path again."""
+    keys, ts, vi, vd = _stream(31, 120_000, 800, 200_000, 400, 0.0)
+    ts = ts.copy()
+    ts[30_000:30_050] -= 20_000                                  # late records in the third push only
+    cfg = A.make_config(window_kind="SESSION", gap_ms=1000, allowed_lateness_ms=500, aggs=AGGS, key_capacity=2048)
+    dropped, st = _run(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 24, 400))
+    assert dropped > 0
+    assert 0 < st.replay_records < len(keys)

@@ -1,9 +1,15 @@
 """Summarise tools/gpu_pmc_all.sh output into profiles/<tag>_pmc_<cfg>.json.
 
-Per kernel: FETCH_SIZE (x2, the gfx950 correction of MI355X_MICROARCH.md: FETCH_SIZE reports half the bytes of a
-wide coalesced read) and WRITE_SIZE per dispatch. Per timed step: the bytes of the ingest kernels (everything but
-the fire, generator, torch and runtime-copy kernels) over the last `steps` steps' share of the dispatches,
-against the algorithmic bytes of the step (24 B per record, 28 B for the C5 float columns).
+Per kernel: FETCH_SIZE and WRITE_SIZE per dispatch, as reported. MI355X_MICROARCH.md (HBM section) calibrates
+FETCH_SIZE only for wide coalesced streaming reads (16 B per lane), where it reports exactly half the bytes; other
+access widths are uncalibrated. So the per-step traffic is given three ways:
+  raw       FETCH_SIZE + WRITE_SIZE as reported (lower bound),
+  estimate  FETCH_SIZE x2 only for the kernels in WIDE (their bulk reads are 16 B/lane streaming loads,
+            as noted at WIDE) + WRITE_SIZE -- this is `ingest_bytes_per_launch`, the bench's `traffic`,
+  upper     FETCH_SIZE x2 for every kernel + WRITE_SIZE (upper bound).
+Per timed step: the ingest kernels (everything but the fire, generator, torch and runtime-copy kernels) over the
+last `steps` steps' dispatches, against the algorithmic bytes of the step (24 B per record, 28 B
+for the C5 float columns).
 """
 import csv
 import glob
@@ -14,6 +20,13 @@ import sys
 
 EXCLUDE = re.compile(r"fire|sp_refine|sp_agg|generate_kernel|reduce_kernel|elementwise|rocclr|reset|fill_u64|push_reset|wire_")
 FIRE = re.compile(r"fire|sp_agg")   # one per step: marks the timed region
+# kernels whose bulk reads are 16 B-per-lane coalesced streaming loads (the calibrated case)
+WIDE = {
+    "partition3_kernel",   # engine.hip load_pairs: ulonglong2 / longlong2 key, ts, value loads
+    "sp_agg_kernel",       # sparse.inc: 16-byte entry loads over contiguous bucket runs
+    "wire_scan_kernel",    # wire.hip: 16-byte chunk loads
+    "wire_decode_kernel",
+}
 
 
 def short(name):
@@ -52,33 +65,40 @@ def main(root, tag, steps=3):
         # timed steps = the dispatches after the last warm-up step's fire (one fire kernel per step)
         fires = sorted(d for k, v in fe.items() if FIRE.search(k) for d, _ in v)
         bound = fires[len(fires) - steps - 1] if len(fires) > steps else -1
-        res, step_bytes = {}, 0.0
+        res = {}
+        tot = {"raw": 0.0, "estimate": 0.0, "upper": 0.0}
         for k in sorted(set(fe) | set(wr)):
-            f = [(d, v * 1024 * 2) for d, v in fe.get(k, [])]   # KB -> bytes, x2 gfx950 correction
+            f = [(d, v * 1024) for d, v in fe.get(k, [])]   # KB -> bytes, as reported
             w = [(d, v * 1024) for d, v in wr.get(k, [])]
-            res[k] = {"dispatches": max(len(f), len(w)), "fetch_bytes_x2_per_dispatch": [v for _, v in f],
-                      "write_bytes_per_dispatch": [v for _, v in w]}
+            res[k] = {"dispatches": max(len(f), len(w)), "fetch_bytes_raw_per_dispatch": [v for _, v in f],
+                      "write_bytes_per_dispatch": [v for _, v in w], "wide_streaming_reads": k in WIDE}
             if not EXCLUDE.search(k):
-                tf = [v for d, v in f if d > bound]
-                tw = [v for d, v in w if d > bound]
-                sb = (sum(tf) + sum(tw)) / steps
-                res[k]["bytes_per_timed_step"] = sb
-                res[k]["timed_dispatches"] = len(tf)
-                step_bytes += sb
+                tf = sum(v for d, v in f if d > bound) / steps
+                tw = sum(v for d, v in w if d > bound) / steps
+                b = {"raw": tf + tw, "estimate": tf * (2 if k in WIDE else 1) + tw, "upper": 2 * tf + tw}
+                res[k]["bytes_per_timed_step"] = b
+                res[k]["timed_dispatches"] = len([1 for d, _ in f if d > bound])
+                for x in tot:
+                    tot[x] += b[x]
+        step_bytes = tot["estimate"]
         batch = 1 << 26
         rec = 28 if cfg in ("c5", "c5s") else 24
         doc = {"note": "rocprofv3 --pmc FETCH_SIZE; WRITE_SIZE in separate runs (tools/gpu_pmc_all.sh), bench.py "
-                       "--config %s --steps %d --warmup %d; FETCH_SIZE x2 (gfx950), WRITE_SIZE as reported; "
+                       "--config %s --steps %d --warmup %d; FETCH_SIZE x2 only for the WIDE kernels (gfx950 calibration), "
+                       "WRITE_SIZE as reported; raw and upper bounds beside the estimate; "
                        "ingest = every kernel except fire (incl. the record-list refine / aggregate) / generator / torch / runtime copies, dispatched after the warm-up's last fire (%d timed steps)"
                        % (cfg, steps, warm, steps),
                "config": {"workload": cfg, "batch": batch}, "per_kernel": res,
-               "ingest_bytes_per_launch": step_bytes, "alg_bytes_per_launch": rec * batch,
-               "traffic_over_alg": step_bytes / (rec * batch)}
+               "wide_kernels": sorted(WIDE), "ingest_bytes_per_launch": step_bytes,
+               "ingest_bytes_per_launch_bounds": {"raw": tot["raw"], "upper": tot["upper"]},
+               "alg_bytes_per_launch": rec * batch, "traffic_over_alg": step_bytes / (rec * batch),
+               "traffic_over_alg_bounds": {"raw": tot["raw"] / (rec * batch), "upper": tot["upper"] / (rec * batch)}}
         with open(os.path.join(out_dir, "%s_pmc_%s.json" % (tag, cfg)), "w") as fh:
             json.dump(doc, fh, indent=1)
-        print(cfg, "ingest bytes/step %.3g" % step_bytes, "x alg %.2f" % (step_bytes / (rec * batch)),
-              {k: round(v.get("bytes_per_timed_step", 0) / 1e6) for k, v in res.items() if "bytes_per_timed_step" in v})
+        print(cfg, "ingest bytes/step %.3g" % step_bytes, "x alg %.2f (raw %.2f, upper %.2f)"
+              % (step_bytes / (rec * batch), tot["raw"] / (rec * batch), tot["upper"] / (rec * batch)),
+              {k: round(v["bytes_per_timed_step"]["estimate"] / 1e6) for k, v in res.items() if "bytes_per_timed_step" in v})
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmca", sys.argv[2] if len(sys.argv) > 2 else "r02")
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmca", sys.argv[2] if len(sys.argv) > 2 else "r03")
