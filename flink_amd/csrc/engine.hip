@@ -2359,68 +2359,149 @@ __global__ void __launch_bounds__(kBlock) sess3_min_kernel(Sess2Args a) {
     }
 }
 
-// Records (t < n, sort position = input position) and in-flight sessions (t >= n): key-group check, kid, 32-bit cell
-// key, payload (record index, or session index | 0x80000000), and the record's packed row [ts, acc_1 .. acc_{nacc-1}]
-// (COUNT is 1 for a record; a session's words are read from the in-flight list by the segment walk).
-__global__ void __launch_bounds__(kBlock) sess3_route_kernel(Sess2Args a, const EngineConst* __restrict__ cp) {
+// Row buckets: a record's packed row goes to the region of its key's hash bucket (the top `bb` bits of mix64(key), i.e.
+// the top bits of its kid: kid = segment << seg_log | offset, segment = top part_bits of the hash), so that the segment
+// walk, which visits the rows in kid order, gathers from a few MB of rows at a time instead of the whole batch.
+constexpr int kRowBucketBits = 6;
+__device__ __forceinline__ uint32_t row_bucket(int64_t key, int bb) {
+    if ((uint64_t)key == kEmptyKey) return 1u << bb;               // the side slot (kid = capacity) sorts last
+    return bb ? (uint32_t)(jm::mix64((uint64_t)key) >> (64 - bb)) : 0u;
+}
+
+// Per block (a contiguous chunk of `chunk` records): row count per bucket, stored bucket-major (hist[bucket * G + b]).
+__global__ void __launch_bounds__(kBlock) sess3_hist_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t chunk,
+                                                           int bb, uint32_t* hist) {
+    __shared__ uint32_t h[(1 << kRowBucketBits) + 1];
+    const int nbk = (1 << bb) + 1;
+    for (int i = threadIdx.x; i < nbk; i += blockDim.x) h[i] = 0u;
+    __syncthreads();
+    const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(n, r0 + chunk);
+    for (int64_t t = r0 + threadIdx.x; t < r1; t += blockDim.x) atomicAdd(&h[row_bucket(keys[t], bb)], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nbk; i += blockDim.x) hist[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
+}
+
+// Probe of the key's first 8-slot bucket (one 64-byte read); -1 when the key is not there (then key_slot, which also
+// inserts). Loads only: the caller issues several before using any.
+__device__ __forceinline__ int64_t key_probe8(const unsigned long long* table, int seg_log, int part_bits, int64_t key,
+                                             ulonglong2 (&bk)[4], uint64_t& i0) {
+    const uint64_t h = jm::mix64((uint64_t)key);
+    const uint64_t smask = ((uint64_t)1 << seg_log) - 1;
+    i0 = seg_base(h, seg_log, part_bits) | (h & smask & ~(uint64_t)(kBucket - 1));
+    const ulonglong2* p = reinterpret_cast<const ulonglong2*>(table + i0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bk[j] = p[j];
+    return 0;
+}
+__device__ __forceinline__ int64_t key_probe8_find(const ulonglong2 (&bk)[4], uint64_t i0, int64_t key) {
+    const unsigned long long k = (unsigned long long)key;
+    int64_t r = -1;
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {
+        if (bk[j].y == k) r = (int64_t)(i0 + 2 * j + 1);
+        if (bk[j].x == k) r = (int64_t)(i0 + 2 * j);
+    }
+    return r;
+}
+
+// Records: block b routes its chunk [b * chunk, (b + 1) * chunk) (the chunks of sess3_hist_kernel): key-group check,
+// kid (U records' bucket probes in flight at once), 32-bit cell key and payload (the row position) at the record's
+// input position, and the packed row [ts, acc_1 .. acc_{nacc-1}] (COUNT is 1 for a record) in its bucket's region.
+template <int U>
+__global__ void __launch_bounds__(kBlock) sess3_route_kernel(Sess2Args a, const EngineConst* __restrict__ cp,
+                                                            const uint32_t* __restrict__ off, int64_t chunk, int bb) {
+    __shared__ uint32_t cur[(1 << kRowBucketBits) + 1];
     __shared__ uint32_t s_c[2];
     const EngineConst& c = *cp;
+    const int nbk = (1 << bb) + 1;
+    if (off) for (int i = threadIdx.x; i < nbk; i += blockDim.x) cur[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
     if (threadIdx.x == 0) { s_c[0] = 0u; s_c[1] = 0u; }
     __syncthreads();
     const int cb = a.tb;
     const uint64_t ncell = (uint64_t)1 << cb;
     const uint64_t base = (uint64_t)jm::unord_i64(a.ctr->ts_min);
     uint32_t nsp = 0, nredo = 0;
-    const int64_t tot = a.n + a.n_in;
     uint32_t* bkey = reinterpret_cast<uint32_t*>(a.bkey);
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
-        uint32_t k32 = kCellSent, pay;
-        if (t < a.n) {
-            const int64_t key = a.keys[t];
-            const int64_t ts = a.ts[t];
-            pay = (uint32_t)t;
-            const int32_t kg = jm::key_group_of(key, c.key_kind, a.key_hash ? a.key_hash[t] : 0, c.max_par);
+    const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(a.n, r0 + chunk);
+    for (int64_t t0 = r0 + threadIdx.x; t0 < r1; t0 += (int64_t)blockDim.x * U) {
+        int64_t key[U], ts[U], kid[U];
+        ulonglong2 bk[U][4];
+        uint64_t i0[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t t = t0 + (int64_t)u * blockDim.x;
+            key[u] = t < r1 ? a.keys[t] : 0;
+            ts[u] = t < r1 ? a.ts[t] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) key_probe8(a.key_table, a.seg_log, a.part_bits, key[u], bk[u], i0[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t t = t0 + (int64_t)u * blockDim.x;
+            if (t >= r1) continue;
+            uint32_t k32 = kCellSent;
+            kid[u] = -1;
+            const int32_t kg = jm::key_group_of(key[u], c.key_kind, a.key_hash ? a.key_hash[t] : 0, c.max_par);
             if (kg < c.kg_lo || kg > c.kg_hi) {
                 raise_error(a.st, FWA_E_KEYGROUP);                     // StateTable :300-307
             } else {
-                const int64_t kid = key_slot(a.key_table, a.key_mask, a.seg_log, a.part_bits, key, a.st);
-                if (kid < 0) {
+                kid[u] = (uint64_t)key[u] == kEmptyKey ? -1 : key_probe8_find(bk[u], i0[u], key[u]);
+                if (kid[u] < 0) kid[u] = key_slot(a.key_table, a.key_mask, a.seg_log, a.part_bits, key[u], a.st);
+                if (kid[u] < 0) {
                     a.st->key_full = 1;
                     raise_error(a.st, FWA_E_OOM);
-                } else if (jm::wsub(jm::wadd(ts, a.gap), 1) <= a.wm) {  // order-sensitive: the general path
-                    a.kflag[kid] = 1;
+                } else if (jm::wsub(jm::wadd(ts[u], a.gap), 1) <= a.wm) {   // order-sensitive: the general path
+                    a.kflag[kid[u]] = 1;
                     ++nsp;
                 } else {
-                    const uint64_t cell = jm::udiv64((uint64_t)ts - base, a.gap_div);
+                    const uint64_t cell = jm::udiv64((uint64_t)ts[u] - base, a.gap_div);
                     if (cell >= ncell) ++nredo;
-                    else k32 = ((uint32_t)kid << cb) | (uint32_t)cell;
-                    unsigned long long* row = a.pk + t * a.pkw;
-                    auto word = [&](int cc) -> unsigned long long {
-                        if (cc == 0) return (unsigned long long)ts;
-                        const AggDesc& d = c.agg[a.col_owner[cc]];
-                        return acc_input(d, a.cols[d.col], t, a.nulls[d.col]);
-                    };
-                    int cc = 0;
-                    if ((a.pkw & 1) == 0)
-                        for (; cc < a.pkw; cc += 2) *reinterpret_cast<ulonglong2*>(row + cc) = make_ulonglong2(word(cc), word(cc + 1));
-                    for (; cc < a.pkw; ++cc) row[cc] = word(cc);
+                    else k32 = ((uint32_t)kid[u] << cb) | (uint32_t)cell;
                 }
             }
-        } else {
-            const int64_t j = t - a.n;
-            pay = (uint32_t)j | 0x80000000u;
-            const uint64_t cell = jm::udiv64((uint64_t)a.in.start[j] - base, a.gap_div);
-            if (cell >= ncell) ++nredo;
-            else k32 = (a.in.kid[j] << cb) | (uint32_t)cell;
+            uint32_t pos = 0u;
+            if (k32 != kCellSent) {
+                pos = off ? atomicAdd(&cur[row_bucket(key[u], bb)], 1u) : (uint32_t)t;
+                unsigned long long* row = a.pk + (int64_t)pos * a.pkw;
+                const int64_t tsu = ts[u];
+                auto word = [&](int cc) -> unsigned long long {
+                    if (cc == 0) return (unsigned long long)tsu;
+                    const AggDesc& d = c.agg[a.col_owner[cc]];
+                    return acc_input(d, a.cols[d.col], t, a.nulls[d.col]);
+                };
+                int cc = 0;
+                if ((a.pkw & 1) == 0)
+                    for (; cc < a.pkw; cc += 2) *reinterpret_cast<ulonglong2*>(row + cc) = make_ulonglong2(word(cc), word(cc + 1));
+                for (; cc < a.pkw; ++cc) row[cc] = word(cc);
+            }
+            bkey[t] = k32;
+            a.bval[t] = pos;
         }
-        bkey[t] = k32;
-        a.bval[t] = pay;
     }
     for (int sh = 32; sh >= 1; sh >>= 1) { nsp += __shfl_xor(nsp, sh); nredo += __shfl_xor(nredo, sh); }
     if ((threadIdx.x & 63) == 0 && (nsp | nredo)) { atomicAdd(&s_c[0], nsp); atomicAdd(&s_c[1], nredo); }
     __syncthreads();
     if (threadIdx.x == 0 && s_c[0]) atomicAdd(&a.ctr->n_special, (unsigned long long)s_c[0]);
     if (threadIdx.x == 0 && s_c[1]) atomicAdd(&a.ctr->n_redo, (unsigned long long)s_c[1]);
+}
+
+// In-flight sessions at sort positions n + j: cell key of their start, payload j | 0x80000000.
+__global__ void __launch_bounds__(kBlock) sess3_route_sessions_kernel(Sess2Args a) {
+    const int cb = a.tb;
+    const uint64_t ncell = (uint64_t)1 << cb;
+    const uint64_t base = (uint64_t)jm::unord_i64(a.ctr->ts_min);
+    uint32_t* bkey = reinterpret_cast<uint32_t*>(a.bkey);
+    uint32_t nredo = 0;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.n_in; j += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t cell = jm::udiv64((uint64_t)a.in.start[j] - base, a.gap_div);
+        uint32_t k32 = kCellSent;
+        if (cell >= ncell) ++nredo;
+        else k32 = (a.in.kid[j] << cb) | (uint32_t)cell;
+        bkey[a.n + j] = k32;
+        a.bval[a.n + j] = (uint32_t)j | 0x80000000u;
+    }
+    for (int sh = 32; sh >= 1; sh >>= 1) nredo += __shfl_xor(nredo, sh);
+    if ((threadIdx.x & 63) == 0 && nredo) atomicAdd(&a.ctr->n_redo, (unsigned long long)nredo);
 }
 
 __device__ __forceinline__ uint32_t perm32(int dst4, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_permute(dst4, (int)v); }
@@ -2446,26 +2527,43 @@ __device__ __forceinline__ unsigned long long rdlane64(unsigned long long v, int
 }
 __device__ __forceinline__ uint32_t rdlane32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 
-// Segmented inclusive scan: lane L combines the lanes [gs(L), L] (gs = first lane of L's segment), f(x, earlier).
-// Hillis-Steele inside rows of 16 (row_shr 1, 2, 4, 8), then the row totals (row_bcast 15 / 31).
-template <class F>
-__device__ __forceinline__ unsigned long long seg_scan64(unsigned long long x, int lane, int gs, F f) {
-    unsigned long long y;
-    y = dpp64<0x111>(x); if ((lane & 15) >= 1 && lane - 1 >= gs) x = f(x, y);
-    y = dpp64<0x112>(x); if ((lane & 15) >= 2 && lane - 2 >= gs) x = f(x, y);
-    y = dpp64<0x114>(x); if ((lane & 15) >= 4 && lane - 4 >= gs) x = f(x, y);
-    y = dpp64<0x118>(x); if ((lane & 15) >= 8 && lane - 8 >= gs) x = f(x, y);
-    y = dpp64<0x142, 0xa>(x); if ((lane & 16) != 0 && gs < (lane & ~15)) x = f(x, y);
-    y = dpp64<0x143, 0xc>(x); if (lane >= 32 && gs < 32) x = f(x, y);
+// Segmented inclusive scans: lane L combines the lanes [gs(L), L] (gs = first lane of L's segment) with the earlier
+// part as the second operand. Hillis-Steele inside rows of 16 (row_shr 1, 2, 4, 8), then the row totals (row_bcast 15
+// / 31); one accumulator kind per scan, branch-free (selects; the kind switch is taken once per scan, not per step).
+template <int K>
+__device__ __forceinline__ unsigned long long comb_k(unsigned long long x, unsigned long long y) {
+    if constexpr (K == ACC_ADD_I64) return x + y;
+    else if constexpr (K == ACC_ADD_F64)
+        return (unsigned long long)__double_as_longlong(__longlong_as_double((long long)x) + __longlong_as_double((long long)y));
+    else if constexpr (K == ACC_MIN_ORD) return y < x ? y : x;
+    else if constexpr (K == ACC_MAX_ORD) return y > x ? y : x;
+    else return x;
+}
+template <int K>
+__device__ __forceinline__ unsigned long long seg_scan_k(unsigned long long x, int lane, int gs) {
+    unsigned long long y, r;
+    y = dpp64<0x111>(x); r = comb_k<K>(x, y); x = ((lane & 15) >= 1 && lane - 1 >= gs) ? r : x;
+    y = dpp64<0x112>(x); r = comb_k<K>(x, y); x = ((lane & 15) >= 2 && lane - 2 >= gs) ? r : x;
+    y = dpp64<0x114>(x); r = comb_k<K>(x, y); x = ((lane & 15) >= 4 && lane - 4 >= gs) ? r : x;
+    y = dpp64<0x118>(x); r = comb_k<K>(x, y); x = ((lane & 15) >= 8 && lane - 8 >= gs) ? r : x;
+    y = dpp64<0x142, 0xa>(x); r = comb_k<K>(x, y); x = ((lane & 16) != 0 && gs < (lane & ~15)) ? r : x;
+    y = dpp64<0x143, 0xc>(x); r = comb_k<K>(x, y); x = (lane >= 32 && gs < 32) ? r : x;
     return x;
 }
-__device__ __forceinline__ int64_t seg_min64(int64_t x, int lane, int gs) {
-    return (int64_t)seg_scan64((unsigned long long)x, lane, gs, [](unsigned long long p, unsigned long long q) {
-        return (int64_t)q < (int64_t)p ? q : p; });
+__device__ __forceinline__ unsigned long long seg_scan_acc(int k, unsigned long long x, int lane, int gs) {
+    switch (k) {
+        case ACC_ADD_I64: return seg_scan_k<ACC_ADD_I64>(x, lane, gs);
+        case ACC_ADD_F64: return seg_scan_k<ACC_ADD_F64>(x, lane, gs);
+        case ACC_MIN_ORD: return seg_scan_k<ACC_MIN_ORD>(x, lane, gs);
+        case ACC_MAX_ORD: return seg_scan_k<ACC_MAX_ORD>(x, lane, gs);
+        default: return x;
+    }
+}
+__device__ __forceinline__ int64_t seg_min64(int64_t x, int lane, int gs) {   // ord encoding: unsigned min
+    return jm::unord_i64(seg_scan_k<ACC_MIN_ORD>(jm::ord_i64(x), lane, gs));
 }
 __device__ __forceinline__ int64_t seg_max64(int64_t x, int lane, int gs) {
-    return (int64_t)seg_scan64((unsigned long long)x, lane, gs, [](unsigned long long p, unsigned long long q) {
-        return (int64_t)q > (int64_t)p ? q : p; });
+    return jm::unord_i64(seg_scan_k<ACC_MAX_ORD>(jm::ord_i64(x), lane, gs));
 }
 
 // The cell-sorted elements in one pass. Ownership as in sess2_segment_kernel (wave w owns the keys whose first sorted
@@ -2597,10 +2695,7 @@ __global__ void __launch_bounds__(kBlock) sess3_segment_kernel(Sess2Args a, cons
             st = seg_min64(st, lane, gs);
             en = seg_max64(en, lane, gs);
 #pragma unroll
-            for (int cc = 0; cc < NA; ++cc) {
-                const int k = ak[cc];
-                x[cc] = seg_scan64(x[cc], lane, gs, [k](unsigned long long p, unsigned long long y) { return acc_combine(k, p, y); });
-            }
+            for (int cc = 0; cc < NA; ++cc) x[cc] = seg_scan_acc(ak[cc], x[cc], lane, gs);
             if (gm == 0 && gopen) {                                 // lanes continuing the carried group
                 st = gmin < st ? gmin : st;
                 en = gmax > en ? gmax : en;
@@ -2651,8 +2746,7 @@ __global__ void __launch_bounds__(kBlock) sess3_segment_kernel(Sess2Args a, cons
             const int64_t cstart = ccont ? cst : hst;
 #pragma unroll
             for (int cc = 0; cc < NA; ++cc) {
-                const int k = ak[cc];
-                unsigned long long xx = seg_scan64(acc[cc], lane, cs, [k](unsigned long long p, unsigned long long y) { return acc_combine(k, p, y); });
+                unsigned long long xx = seg_scan_acc(ak[cc], acc[cc], lane, cs);
                 if (ccont && copen) xx = acc_combine(ak[cc], cacc[cc], xx);
                 acc[cc] = xx;
             }
@@ -3160,7 +3254,9 @@ struct fwa_engine {
     uint32_t* d_flat = nullptr;            // flat Phase P layout: (partition, block) counts | their exclusive sum
     int64_t flat_cap = 0;
     int64_t sg_cap = 0, sgw_cap = 0;
-    int32_t cell_skip = 0;          // sessions: pushes left before the cell path is tried again after a redo
+    int32_t cell_skip = 0;
+    uint32_t* d_rh = nullptr;       // sessions cell path: per-block row-bucket counts and their exclusive sum
+    int64_t rh_cap = 0;          // sessions: pushes left before the cell path is tried again after a redo
     int64_t* d_spe = nullptr;
     int64_t* d_smax = nullptr;
     uint32_t* d_scid = nullptr;
@@ -3596,7 +3692,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_flat};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_flat, e->d_rh};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -4362,9 +4458,34 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
         t.seg_out = 1;
         HIPCHK(e, hipEventRecord(e->ev[0], e->stream));
         sess3_min_kernel<<<grid_for(n + n_in, 1024), kBlock, 0, e->stream>>>(t);
-        sess3_route_kernel<<<grid_for(n + n_in, 256 * 32), kBlock, 0, e->stream>>>(t, e->d_ec);
-        HIPCHK(e, hipGetLastError());
+        const int bb = std::min<int>(e->part_bits, kRowBucketBits);
+        const int nbk = (1 << bb) + 1;
+        const int G = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 2047) / 2048));
+        const int64_t chunk = ((n + G - 1) / G + 255) / 256 * 256;
+        const int64_t nh = (int64_t)nbk * G;
+        if (nh + 1 > e->rh_cap) {
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            if (e->d_rh) HIPCHK(e, hipFree(e->d_rh));
+            e->d_rh = nullptr;
+            e->rh_cap = nh + 1;
+            HIPCHK(e, hipMalloc(&e->d_rh, 2 * sizeof(uint32_t) * (size_t)e->rh_cap));
+        }
+        uint32_t* rh = e->d_rh;
+        uint32_t* roff = nullptr;                         // rows at the input position unless bucketed (A/B: FWA_ROWB=1)
         size_t bytes = 0;
+        if (getenv("FWA_ROWB") && atoi(getenv("FWA_ROWB")) != 0) {
+            roff = e->d_rh + e->rh_cap;
+            sess3_hist_kernel<<<G, kBlock, 0, e->stream>>>(t.keys, n, chunk, bb, rh);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, rh, roff, (int)nh, e->stream));
+            if ((rc = ensure_sort_tmp(e, bytes))) return rc;
+            bytes = e->sort_tmp_bytes;
+            HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(e->d_sort_tmp, bytes, rh, roff, (int)nh, e->stream));
+        }
+        sess3_route_kernel<2><<<G, kBlock, 0, e->stream>>>(t, e->d_ec, roff, chunk, bb);
+        if (n_in > 0) sess3_route_sessions_kernel<<<grid_for(n_in, 256 * 16), kBlock, 0, e->stream>>>(t);
+        HIPCHK(e, hipGetLastError());
+        bytes = 0;
         const uint32_t* k0 = (const uint32_t*)e->d_skey[0];
         uint32_t* k1 = (uint32_t*)e->d_skey[1];
         HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k0, k1, (const uint32_t*)e->d_sval[0], e->d_sval[1],
