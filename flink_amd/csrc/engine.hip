@@ -2665,7 +2665,8 @@ __global__ void __launch_bounds__(kBlock) sess3_segment_kernel(Sess2Args a, cons
                 for (int cc = 1; cc < NA; ++cc) x[cc] = wv[cc];
             }
         };
-        // carried group and carried session: wave-uniform (readlane results, held in SGPRs)
+        // Carries (wave-uniform): the pending group (its last element not seen yet: its session is undecided) and the
+        // open session (every group before the pending one that belongs to it).
         bool gopen = false, copen = false;
         uint32_t gkey = 0u, ck = 0u;
         int64_t gmin = 0, gmax = 0, cmaxe = LONG_MIN_J, cst = 0;
@@ -2687,72 +2688,77 @@ __global__ void __launch_bounds__(kBlock) sess3_segment_kernel(Sess2Args a, cons
             for (int cc = 0; cc < NA; ++cc) x[cc] = nx[cc];
             const bool more = base + 64 < h1;
             if (more) fetch(base + 64, nbk, nst, nen, nx);
-            // (1) groups
+            // (1) groups: min start / max end per (kid, cell) run, joined with the pending group at lane 0
             const uint32_t gup = dpp32<0x138>(bk);                  // lane - 1
-            const bool gf = v && (lane == 0 ? !(gopen && bk == gkey) : bk != gup);
-            const unsigned long long gm = __ballot(gf) & below;
+            const bool cont0 = gopen && rdlane32(bk, 0) == gkey;    // lane 0 continues the pending group
+            const bool gf = v && (lane == 0 ? !cont0 : bk != gup);
+            const unsigned long long GF = __ballot(gf);
+            const unsigned long long gm = GF & below;
             const int gs = gm ? 63 - __clzll((long long)gm) : 0;
             st = seg_min64(st, lane, gs);
             en = seg_max64(en, lane, gs);
-#pragma unroll
-            for (int cc = 0; cc < NA; ++cc) x[cc] = seg_scan_acc(ak[cc], x[cc], lane, gs);
-            if (gm == 0 && gopen) {                                 // lanes continuing the carried group
+            if (gm == 0 && cont0) {
                 st = gmin < st ? gmin : st;
                 en = gmax > en ? gmax : en;
-#pragma unroll
-                for (int cc = 0; cc < NA; ++cc) x[cc] = acc_combine(ak[cc], gacc[cc], x[cc]);
             }
             const uint32_t nk0 = rdlane32(nbk, 0);                  // the next chunk's first key (when `more`)
             const uint32_t gdn = dpp32<0x130>(bk);                  // lane + 1
             const bool gt = v && (q + 1 == h1 || (lane < 63 ? gdn != bk : nk0 != bk));   // the group's last element
             const int lv = (int)min<int64_t>(63, h1 - 1 - base);   // last valid lane
             const unsigned long long P = __ballot(gt);
-            if (((P >> lv) & 1ull) == 0) {                          // the last group continues in the next chunk
-                gopen = true;
-                gkey = rdlane32(bk, lv);
-                gmin = (int64_t)rdlane64((unsigned long long)st, lv);
-                gmax = (int64_t)rdlane64((unsigned long long)en, lv);
-#pragma unroll
-                for (int cc = 0; cc < NA; ++cc) gacc[cc] = rdlane64(x[cc], lv);
-            } else {
-                gopen = false;
-            }
-            if (!P) continue;
-            // (2) pack the ended groups to lanes [0, np) in order, then chain them
+            const bool pend = ((P >> lv) & 1ull) == 0;              // the last group continues in the next chunk
+            // (2) chain the groups that end here, packed to lanes [0, np): heads and session tails
             const int np = __popcll(P);
-            const int dst = gt ? __popcll(P & before) : np + __popcll(~P & before);
-            const uint32_t kk = perm32(dst * 4, bk >> cb);
-            const int64_t gst = (int64_t)perm64(dst * 4, (unsigned long long)st);
-            const int64_t gen = (int64_t)perm64(dst * 4, (unsigned long long)en);
-            unsigned long long acc[NA];
-#pragma unroll
-            for (int cc = 0; cc < NA; ++cc) acc[cc] = perm64(dst * 4, x[cc]);
-            const bool range_end = base + lv + 1 == h1;             // the last packed group closes the walk
-            const bool pv = lane < np;
-            const uint32_t kp = dpp32<0x138>(kk);
-            const bool kc = pv && (lane == 0 ? (!copen || kk != ck) : kk != kp);
-            const unsigned long long km = __ballot(kc) & below;
-            const int ks = km ? 63 - __clzll((long long)km) : 0;
-            int64_t m = seg_max64(pv ? gen : LONG_MIN_J, lane, ks);   // running max end of the key (inclusive)
-            if (km == 0 && copen && cmaxe > m) m = cmaxe;           // the key continues from the carried session
-            int64_t mprev = (int64_t)dpp64<0x138>((unsigned long long)m);
-            if (lane == 0) mprev = cmaxe;
-            const bool head = pv && (kc || gst > mprev);
-            const unsigned long long H = __ballot(head);
-            const unsigned long long hb = H & below;
-            const int cs = hb ? 63 - __clzll((long long)hb) : 0;
-            const bool ccont = hb == 0;                             // still the carried session
-            const int64_t hst = __shfl(gst, cs);
-            const int64_t cstart = ccont ? cst : hst;
+            uint32_t kk = 0u;
+            int64_t gst = 0, m = LONG_MIN_J, cstart = 0;
+            bool head = false, ptail = false;
+            unsigned long long H = 0ull;
+            if (np) {
+                const int dst = gt ? __popcll(P & before) : np + __popcll(~P & before);
+                kk = perm32(dst * 4, bk >> cb);
+                gst = (int64_t)perm64(dst * 4, (unsigned long long)st);
+                const int64_t gen = (int64_t)perm64(dst * 4, (unsigned long long)en);
+                const bool range_end = base + lv + 1 == h1;         // the last packed group closes the walk
+                const bool pv = lane < np;
+                const uint32_t kp = dpp32<0x138>(kk);
+                const bool kc = pv && (lane == 0 ? (!copen || kk != ck) : kk != kp);
+                const unsigned long long km = __ballot(kc) & below;
+                const int ks = km ? 63 - __clzll((long long)km) : 0;
+                m = seg_max64(pv ? gen : LONG_MIN_J, lane, ks);     // running max end of the key (inclusive)
+                if (km == 0 && copen && cmaxe > m) m = cmaxe;       // the key continues from the open session
+                int64_t mprev = (int64_t)dpp64<0x138>((unsigned long long)m);
+                if (lane == 0) mprev = cmaxe;
+                head = pv && (kc || gst > mprev);
+                H = __ballot(head);
+                const unsigned long long hb = H & below;
+                const int cs = hb ? 63 - __clzll((long long)hb) : 0;
+                const int64_t hst = __shfl(gst, cs);
+                cstart = hb == 0 ? cst : hst;
+                ptail = pv && (lane == np - 1 ? range_end : (lane < 63 && ((H >> ((lane + 1) & 63)) & 1ull) != 0));
+            }
+            // (3) accumulators once, per element, segmented by session: a segment starts at lane 0, at the first
+            // element of every head group, and at the first element of the pending group
+            const unsigned long long Pge = P & ~before;             // groups ending at or after this lane
+            const int tl = Pge ? __ffsll((long long)Pge) - 1 : 64;  // this lane's group tail (64: pending group)
+            const int rk = __popcll(P & ((tl < 64) ? ((1ull << tl) - 1ull) : ~0ull));   // its packed rank
+            const bool ghead = tl < 64 && ((H >> rk) & 1ull) != 0;
+            const unsigned long long SS = __ballot(v && gf && (tl == 64 || ghead)) | 1ull;
+            const unsigned long long sm = SS & below;
+            const int ss = 63 - __clzll((long long)sm);
+            // prefix of the first segment: the open session unless its first group is a head, then the pending group
+            // that lane 0 continues
+            const bool g0end = (P & ~0ull) != 0;                    // the group at lane 0 ends in this chunk
+            const bool pre_c = copen && g0end && (H & 1ull) == 0;
+            const bool pre_g = cont0;
 #pragma unroll
             for (int cc = 0; cc < NA; ++cc) {
-                unsigned long long xx = seg_scan_acc(ak[cc], acc[cc], lane, cs);
-                if (ccont && copen) xx = acc_combine(ak[cc], cacc[cc], xx);
-                acc[cc] = xx;
+                unsigned long long xx = seg_scan_acc(ak[cc], x[cc], lane, ss);
+                if (ss == 0 && pre_g) xx = acc_combine(ak[cc], xx, gacc[cc]);
+                if (ss == 0 && pre_c) xx = acc_combine(ak[cc], xx, cacc[cc]);
+                x[cc] = xx;
             }
-            const bool nxt = lane < 63 && ((H >> (lane + 1)) & 1ull) != 0;
-            const bool tail = pv && (lane == np - 1 ? range_end : nxt);
-            const bool emit_c = copen && (H & 1ull) != 0;           // the carried session ended before lane 0
+            // the open session ended before the first group here
+            const bool emit_c = copen && np > 0 && (H & 1ull) != 0;
             if (emit_c && lane == 0) {
                 const int64_t sc = h0 + (int64_t)wc;
                 a.sg_kid[sc] = ck;
@@ -2762,22 +2768,40 @@ __global__ void __launch_bounds__(kBlock) sess3_segment_kernel(Sess2Args a, cons
                 for (int cc = 0; cc < NA; ++cc) a.sg_acc[(int64_t)cc * a.sg_cap + sc] = cacc[cc];
             }
             wc += emit_c ? 1u : 0u;
-            const unsigned long long tm = __ballot(tail);
-            if (tail) {
+            // sessions ending at an element lane (the tail of a packed group whose session ends)
+            const int rsrc = gt ? __popcll(P & before) : 0;
+            const int ptl = __shfl(ptail ? 1 : 0, rsrc);           // every lane takes part in the shuffle
+            const bool etail = gt && ptl != 0;
+            const int64_t e_start = __shfl(cstart, rsrc);
+            const int64_t e_end = __shfl(m, rsrc);
+            const unsigned long long tm = __ballot(etail);
+            if (etail) {
                 const int64_t so = h0 + (int64_t)wc + __popcll(tm & before);
-                a.sg_kid[so] = kk;
-                a.sg_start[so] = cstart;
-                a.sg_end[so] = m;
+                a.sg_kid[so] = bk >> cb;
+                a.sg_start[so] = e_start;
+                a.sg_end[so] = e_end;
 #pragma unroll
-                for (int cc = 0; cc < NA; ++cc) a.sg_acc[(int64_t)cc * a.sg_cap + so] = acc[cc];
+                for (int cc = 0; cc < NA; ++cc) a.sg_acc[(int64_t)cc * a.sg_cap + so] = x[cc];
             }
             wc += (uint32_t)__popcll(tm);
-            ck = rdlane32(kk, np - 1);
-            cmaxe = (int64_t)rdlane64((unsigned long long)m, np - 1);
-            cst = (int64_t)rdlane64((unsigned long long)cstart, np - 1);
+            // carries
+            if (np) {
+                const int tlast = 63 - __clzll((long long)P);       // element lane of the last ended group
+                ck = rdlane32(kk, np - 1);
+                cmaxe = (int64_t)rdlane64((unsigned long long)m, np - 1);
+                cst = (int64_t)rdlane64((unsigned long long)cstart, np - 1);
 #pragma unroll
-            for (int cc = 0; cc < NA; ++cc) cacc[cc] = rdlane64(acc[cc], np - 1);
-            copen = true;
+                for (int cc = 0; cc < NA; ++cc) cacc[cc] = rdlane64(x[cc], tlast);
+                copen = true;
+            }
+            gopen = pend;
+            if (pend) {
+                gkey = rdlane32(bk, lv);
+                gmin = (int64_t)rdlane64((unsigned long long)st, lv);
+                gmax = (int64_t)rdlane64((unsigned long long)en, lv);
+#pragma unroll
+                for (int cc = 0; cc < NA; ++cc) gacc[cc] = rdlane64(x[cc], lv);
+            }
         }
         if (lane == 0) { a.sg_cnt[w] = wc; a.sg_h0[w] = h0; }
     }
@@ -4460,7 +4484,7 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
         sess3_min_kernel<<<grid_for(n + n_in, 1024), kBlock, 0, e->stream>>>(t);
         const int bb = std::min<int>(e->part_bits, kRowBucketBits);
         const int nbk = (1 << bb) + 1;
-        const int G = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 2047) / 2048));
+        const int G = (int)std::max<int64_t>(1, std::min<int64_t>(8192, (n + 2047) / 2048));   // >= 32 waves per CU (latency-bound probes)
         const int64_t chunk = ((n + G - 1) / G + 255) / 256 * 256;
         const int64_t nh = (int64_t)nbk * G;
         if (nh + 1 > e->rh_cap) {
