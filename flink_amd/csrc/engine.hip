@@ -73,6 +73,8 @@ struct DevStatus {
     unsigned long long drop_n;     // FWA_CFG_LATE_INDICES: entries in the dropped-record index list this push
     int32_t ovf_n;                 // Phase P: bucket entries past their sub-bucket's end this push (skew signal)
     int32_t strag_n;               // Phase A: entries older than their combiner's LDS window this push
+    int32_t wide_n;                // Phase P narrow entries: accepted records whose key or value needs 64 bits (replayed)
+    int32_t pad3;
 };
 
 // FWA_CFG_LATE_INDICES: record index of a late-dropped record (lateDataOutputTag / lateRecordsDroppedRate),
@@ -789,12 +791,15 @@ __device__ __noinline__ void pre_apply_global(unsigned long long* table, uint64_
 
 // W16: the tile's columns are read with 16-byte loads (two records per lane per column; 8-byte loads reach
 // roughly 0.6x the 16-byte rate, MI355X_MICROARCH.md): item j of a lane is record 2 * ((j / 2) * THREADS + tid) + j % 2.
-template <int NV, int ITEMS, int THREADS, int VW, int KG, int PRE = 0, int W16 = 0, int EARLY = 0>
+template <int NV, int ITEMS, int THREADS, int VW, int KG, int PRE = 0, int W16 = 0, int EARLY = 0, int NW = 0>
 __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
     static_assert(THREADS == kMaxPart && ITEMS <= 8, "one partition cursor per thread; trash area of 8 x kMaxPart");
     static_assert(!PRE || NV <= 1, "pre-aggregation: COUNT [+ one BIGINT sum]");
     static_assert(!W16 || (ITEMS % 2 == 0 && KG != 2 && NV <= 1), "paired loads: even ITEMS, no key-hash column");
     static_assert(!EARLY || (W16 && !PRE && EARLY <= ITEMS / 2), "early loads: paired, no tile pre-aggregation");
+    // NW: narrow bucket entries -- key and BIGINT value as two sign-extended 32-bit halves of one u64 (10 instead of
+    // 18 bytes per entry with the u16 slice); a record whose key or value needs 64 bits takes the v1 replay
+    static_assert(!NW || (NV == 1 && !PRE && (VW & 1)), "narrow entries: one 8-byte value column, no pre-aggregation");
     constexpr int kTile = THREADS * ITEMS;
     constexpr int kHt = 2 * kTile;                     // PRE: (key, slice) hash table, load <= 0.5
     constexpr int kHtLog = __builtin_ctz(kHt);
@@ -815,7 +820,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
     __shared__ uint32_t x_n[PRE ? kTile : 1];          // PRE: records merged into the representative
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    unsigned dropped = 0;
+    unsigned dropped = 0, wide = 0;
     uint32_t relmax = 0, relmin = ~0u;
     const bool ds = c.sem == FWA_SEM_DATASTREAM;
     for (int r = tid; r < kRelCap / 4; r += THREADS) ((uint32_t*)s_code)[r] = ((const uint32_t*)a.relcode)[r];
@@ -922,7 +927,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         a.b_key[o] = 0ull;
         a.b_rel[o] = 0;
         if constexpr (PRE) a.b_n[o] = 0;
-        if (NV > 0) a.b_val0[o] = 0ull;
+        if (NV > 0 && !NW) a.b_val0[o] = 0ull;
         if (NV > 1) a.b_val1[o] = 0ull;
     }
     // one tile: classify R, scan, reserve, issue the loads of tile `nx` into R, scatter, store
@@ -977,6 +982,12 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                     const unsigned long long pc = a.pcount[i];
                     rn = (uint32_t)pc;
                     if (pc == 0 || pc > 0xFFFFull) code = kCodeSlow;  // does not fit a bucket's u16 count
+                }
+            }
+            if constexpr (NW) {
+                if (code == kCodeAccept && ((int64_t)(int32_t)key != key || (int64_t)(int32_t)R.v0[j] != (int64_t)R.v0[j])) {
+                    code = kCodeSlow;
+                    ++wide;
                 }
             }
             if (i >= a.n) code = 0xff;
@@ -1114,10 +1125,11 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             }
             const uint64_t o = !inb ? a.trash + (uint64_t)(jj * THREADS + tid)
                              : flat ? dst : ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
-            a.b_key[o] = x_key[x];
+            if constexpr (NW) a.b_key[o] = (x_key[x] & 0xffffffffull) | (x_val[0][x] << 32);
+            else a.b_key[o] = x_key[x];
             a.b_rel[o] = x_rel[x];
             if constexpr (PRE) a.b_n[o] = (uint16_t)x_n[x];
-            if (NV > 0) a.b_val0[o] = x_val[0][x];
+            if (NV > 0 && !NW) a.b_val0[o] = x_val[0][x];
             if (NV > 1) a.b_val1[o] = x_val[NV > 1 ? 1 : 0][x];
         }
         QMARK(3);
@@ -1129,11 +1141,13 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
 #undef QMARK
     for (int sh = 32; sh >= 1; sh >>= 1) {
         dropped += __shfl_xor(dropped, sh);
+        if constexpr (NW) wide += __shfl_xor(wide, sh);
         relmax = max(relmax, (uint32_t)__shfl_xor((int)relmax, sh));
         relmin = min(relmin, (uint32_t)__shfl_xor((int)relmin, sh));
     }
     if (lane == 0) {
         if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
+        if (NW && wide) atomicAdd(&a.st->wide_n, (int32_t)wide);
         if (relmin != ~0u) {
             atomicMax(&a.st->max_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmax));
             atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
@@ -1234,7 +1248,7 @@ typedef const __attribute__((address_space(1))) unsigned long long* gc_u64_ptr;
 // 2 = COUNT only; 0 = generic (descriptor table in LDS, one column per loop trip).
 // MP: window passes (below) for chunks spanning more slices than the window; chosen per handle once a push
 // saw many stragglers (small HOP/CUMULATE slices), since the passes cost registers the common case needs.
-template <int IT, int SL, int NV, int TH, int LAYOUT, int PRE = 0, int MP = 0>
+template <int IT, int SL, int NV, int TH, int LAYOUT, int PRE = 0, int MP = 0, int NW = 0>
 __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int kWaves = TH / 64;
@@ -1358,8 +1372,14 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         for (int j = 0; j < IT; ++j) {
             const int64_t i = cbase + (int64_t)j * LPS + li;
             const bool ok = i < my_cnt;
-            nkey[j] = ok ? bk[i] : 0ull;
-            nx0[j] = (NV > 0 && ok) ? bv0[i] : 0ull;
+            if constexpr (NW) {                             // narrow entry: sign-extended key | value halves
+                const unsigned long long e = ok ? bk[i] : 0ull;
+                nkey[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)e;
+                nx0[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)(e >> 32);
+            } else {
+                nkey[j] = ok ? bk[i] : 0ull;
+                nx0[j] = (NV > 0 && ok) ? bv0[i] : 0ull;
+            }
             nx1[j] = (NV > 1 && ok) ? bv1[i] : 0ull;
             const int r = ok ? (int)br[i] : -1;
             nrel[j] = r == 0xFFFF ? -1 : r;                 // flat layout: a hole (record not accepted)
@@ -3069,7 +3089,7 @@ __global__ void push_reset_kernel(DevStatus* st, unsigned long long* want, int32
     const int32_t nt = gridDim.x * blockDim.x;
     if (t == 0) {
         st->error = 0; st->spill_n = 0; st->want_n = 0; st->key_full = 0;
-        st->dropped = 0; st->late_fire = 0; st->max_q = 0; st->min_q = ~0ull; st->ovf_n = 0; st->strag_n = 0;
+        st->dropped = 0; st->late_fire = 0; st->max_q = 0; st->min_q = ~0ull; st->ovf_n = 0; st->strag_n = 0; st->wide_n = 0;
     }
     for (int32_t i = t; i < nwant; i += nt) want[i] = 0ull;
     for (int32_t i = t; i < nbcnt; i += nt) bcnt[i] = 0u;
@@ -3279,6 +3299,7 @@ struct fwa_engine {
     int64_t flat_cap = 0;
     int64_t sg_cap = 0, sgw_cap = 0;
     int32_t cell_skip = 0;
+    bool narrow = true, narrow_used = false;   // Phase P / A narrow bucket entries (sticky off after a wide push)
     uint32_t* d_rh = nullptr;       // sessions cell path: per-block row-bucket counts and their exclusive sum
     int64_t rh_cap = 0;          // sessions: pushes left before the cell path is tried again after a redo
     int64_t* d_spe = nullptr;
@@ -4161,6 +4182,13 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     // slower on C2 (Phase P 1.30 vs 0.81 ms: 512 open runs per block leave partial lines in L2)
     static const int flat_env = getenv("FWA_FLAT") ? atoi(getenv("FWA_FLAT")) : 0;     // A/B: 1 = flat layout
     const bool flat = flat_env != 0 && !pre && !p2;
+    // narrow bucket entries (partition3 / combine3 NW): COUNT + one BIGINT SUM over an 8-byte column, the paired-load
+    // kernel; on by default until a push finds more than 1/64 of its records needing 64-bit keys or values
+    const char* narrow_s = getenv("FWA_NARROW");                  // A/B: 0 never, 1 always (read per push)
+    const int narrow_env = narrow_s ? atoi(narrow_s) : -1;
+    const bool narrow = narrow_env != 0 && (narrow_env == 1 || e->narrow) && layout == 1 && e->nv == 1 && (vw & 1) &&
+                        w16 && !pre && !flat && !p2 && pdb == 0 && !a.pcount;
+    e->narrow_used = narrow;
     if (flat) {
         const int64_t ntiles = (a.n + tile - 1) / tile;
         const int64_t tpb = (ntiles + grid - 1) / grid;
@@ -4202,6 +4230,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     else if (e->nv == 1 && w16 && (vw & 1) && pdb == 1) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1) && pdb == 2) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1) && pdb == 3) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 3><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
+    else if (e->nv == 1 && w16 && (vw & 1) && narrow) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1) { if (vw & 1) P2LAUNCH(1, 6, 3); else P2LAUNCH(1, 6, 2); }
@@ -4262,7 +4291,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else if (layout == 1) C3M(IT, TH, NV, 1, 0); \
         else if (layout == 2) C3M(IT, TH, NV, 2, 0); \
         else C3M(IT, TH, NV, 0, 0); } while (0)
-    if (e->nv == 0) C3L(4, 1024, 0);
+    if (narrow) {
+        if (mp) combine3_kernel<4, 2, 1, 1024, 1, 0, 1, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        else combine3_kernel<4, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+    } else if (e->nv == 0) C3L(4, 1024, 0);
     else if (e->nv == 1) C3L(4, 1024, 1);
     else C3L(4, 1024, 2);
 #undef C3L
@@ -4959,6 +4991,7 @@ static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, boo
         const DevStatus st = *e->h_st;
         if (ran_v2 && round == 0 && (int64_t)st.ovf_n * 64 > n) e->pre = true;   // skewed keys: PRE from the next push
         if (ran_v2 && round == 0 && (int64_t)st.strag_n * 64 > n) e->mp = true;  // wide chunks: window passes
+        if (ran_v2 && round == 0 && e->narrow_used && (int64_t)st.wide_n * 64 > n) e->narrow = false;   // 64-bit keys / values
         if (st.error) {
             const char* m = st.error == FWA_E_KEYGROUP ? "Key group is not in the owned KeyGroupRange (StateTable.getMapForKeyGroup)"
                           : st.error == FWA_E_TS_MIN ? "Record has Long.MIN_VALUE timestamp (= no timestamp marker)."
