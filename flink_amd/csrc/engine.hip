@@ -1372,10 +1372,8 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         for (int j = 0; j < IT; ++j) {
             const int64_t i = cbase + (int64_t)j * LPS + li;
             const bool ok = i < my_cnt;
-            if constexpr (NW) {                             // narrow entry: sign-extended key | value halves
-                const unsigned long long e = ok ? bk[i] : 0ull;
-                nkey[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)e;
-                nx0[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)(e >> 32);
+            if constexpr (NW) {                             // narrow entry (key | value << 32), unpacked at use
+                nkey[j] = ok ? bk[i] : 0ull;
             } else {
                 nkey[j] = ok ? bk[i] : 0ull;
                 nx0[j] = (NV > 0 && ok) ? bv0[i] : 0ull;
@@ -1396,7 +1394,13 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         int rmin = 0x7fffffff, rmax = -1;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
-            key[j] = nkey[j]; x0[j] = nx0[j]; x1[j] = nx1[j]; rel[j] = nrel[j]; nr[j] = nnn[j];
+            if constexpr (NW) {
+                key[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)nkey[j];
+                x0[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)(nkey[j] >> 32);
+            } else {
+                key[j] = nkey[j]; x0[j] = nx0[j];
+            }
+            x1[j] = nx1[j]; rel[j] = nrel[j]; nr[j] = nnn[j];
             if (rel[j] >= 0) { rmin = min(rmin, rel[j]); rmax = max(rmax, rel[j]); }
         }
         PMARK(1);
@@ -4291,8 +4295,11 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else if (layout == 1) C3M(IT, TH, NV, 1, 0); \
         else if (layout == 2) C3M(IT, TH, NV, 2, 0); \
         else C3M(IT, TH, NV, 0, 0); } while (0)
+    static const int nit_env = getenv("FWA_NIT") ? atoi(getenv("FWA_NIT")) : 8;   // A/B: entries per lane and chunk (8: measured best)
     if (narrow) {
         if (mp) combine3_kernel<4, 2, 1, 1024, 1, 0, 1, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        else if (nit_env == 8) combine3_kernel<8, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        else if (nit_env == 6) combine3_kernel<6, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
         else combine3_kernel<4, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
     } else if (e->nv == 0) C3L(4, 1024, 0);
     else if (e->nv == 1) C3L(4, 1024, 1);
