@@ -924,8 +924,9 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
 #pragma unroll
     for (int jj = 0; jj < ITEMS; ++jj) {
         const uint64_t o = a.trash + (uint64_t)(jj * THREADS + tid);   // distinct: not merged by the compiler
-        a.b_key[o] = 0ull;
-        a.b_rel[o] = 0;
+        if constexpr (NW == 2) reinterpret_cast<uint3*>(a.b_key)[o] = make_uint3(0u, 0u, 0u);
+        else a.b_key[o] = 0ull;
+        if constexpr (NW != 2) a.b_rel[o] = 0;
         if constexpr (PRE) a.b_n[o] = 0;
         if (NV > 0 && !NW) a.b_val0[o] = 0ull;
         if (NV > 1) a.b_val1[o] = 0ull;
@@ -1074,6 +1075,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         const uint32_t h = p < a.np ? hist[p] : 0u;
         uint32_t g = 0;
         if (flat) { if (p < a.np) { g = sbase[p]; sbase[p] = g + h; } }   // the block's own cursor
+        else if (a.abl & 1) g = 0;                      // timing ablation only (FWA_PABL=1: wrong results)
         else if (h) g = atomicAdd(&a.b_cnt[p * kSub + sub], h);
         // the next tile in flight from here on (unconditional); EARLY: its first pairs were issued while classifying
         if constexpr (EARLY) load_pairs(R, nx < tend ? nx : tile, EARLY, ITEMS / 2);
@@ -1125,9 +1127,11 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             }
             const uint64_t o = !inb ? a.trash + (uint64_t)(jj * THREADS + tid)
                              : flat ? dst : ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
-            if constexpr (NW) a.b_key[o] = (x_key[x] & 0xffffffffull) | (x_val[0][x] << 32);
+            if constexpr (NW == 2)                       // 12-byte entry {key, value, slice}: one store
+                reinterpret_cast<uint3*>(a.b_key)[o] = make_uint3((uint32_t)x_key[x], (uint32_t)x_val[0][x], x_rel[x]);
+            else if constexpr (NW) a.b_key[o] = (x_key[x] & 0xffffffffull) | (x_val[0][x] << 32);
             else a.b_key[o] = x_key[x];
-            a.b_rel[o] = x_rel[x];
+            if constexpr (NW != 2) a.b_rel[o] = x_rel[x];
             if constexpr (PRE) a.b_n[o] = (uint16_t)x_n[x];
             if (NV > 0 && !NW) a.b_val0[o] = x_val[0][x];
             if (NV > 1) a.b_val1[o] = x_val[NV > 1 ? 1 : 0][x];
@@ -1372,14 +1376,25 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         for (int j = 0; j < IT; ++j) {
             const int64_t i = cbase + (int64_t)j * LPS + li;
             const bool ok = i < my_cnt;
-            if constexpr (NW) {                             // narrow entry (key | value << 32), unpacked at use
+            int r;
+            if constexpr (NW == 2) {                        // 12-byte entry {key, value, slice}: one load
+                uint3 q = make_uint3(0u, 0u, 0u);
+                if (ok) {
+                    const __attribute__((address_space(1))) uint32_t* qp =
+                        (const __attribute__((address_space(1))) uint32_t*)a.b_key + 3 * (boff + i);   // 12-byte entries
+                    q = make_uint3(qp[0], qp[1], qp[2]);
+                }
+                nkey[j] = (unsigned long long)q.x | ((unsigned long long)q.y << 32);
+                r = ok ? (int)q.z : -1;
+            } else if constexpr (NW) {                      // narrow entry (key | value << 32), unpacked at use
                 nkey[j] = ok ? bk[i] : 0ull;
+                r = ok ? (int)br[i] : -1;
             } else {
                 nkey[j] = ok ? bk[i] : 0ull;
                 nx0[j] = (NV > 0 && ok) ? bv0[i] : 0ull;
+                r = ok ? (int)br[i] : -1;
             }
             nx1[j] = (NV > 1 && ok) ? bv1[i] : 0ull;
-            const int r = ok ? (int)br[i] : -1;
             nrel[j] = r == 0xFFFF ? -1 : r;                 // flat layout: a hole (record not accepted)
             nnn[j] = PRE ? (ok ? (uint32_t)bn[i] : 0u) : 1u;
         }
@@ -4051,7 +4066,7 @@ static int ensure_v2_buffers(fwa_engine* e, int64_t n, bool need_bn) {
         e->d_bn = nullptr;
         e->d_bval[0] = e->d_bval[1] = nullptr;
         const int64_t ent = capb * e->np * kSub + 8 * kMaxPart;  // + a trash area (partition3's masked stores)
-        HIPCHK(e, hipMalloc(&e->d_bkey, 8 * ent));
+        HIPCHK(e, hipMalloc(&e->d_bkey, (e->nv == 1 ? 12 : 8) * ent));   // 12: narrow {key, value, slice} entries
         HIPCHK(e, hipMalloc(&e->d_brel, 2 * ent));
         for (int v = 0; v < e->nv; ++v) HIPCHK(e, hipMalloc(&e->d_bval[v], 8 * ent));
         e->capb = capb;
@@ -4193,6 +4208,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     const bool narrow = narrow_env != 0 && (narrow_env == 1 || e->narrow) && layout == 1 && e->nv == 1 && (vw & 1) &&
                         w16 && !pre && !flat && !p2 && pdb == 0 && !a.pcount;
     e->narrow_used = narrow;
+    const char* n12_s = getenv("FWA_NARROW12");                   // A/B: 12-byte AoS entries (one store / load each)
+    const bool n12 = n12_s && atoi(n12_s) != 0;
     if (flat) {
         const int64_t ntiles = (a.n + tile - 1) / tile;
         const int64_t tpb = (ntiles + grid - 1) / grid;
@@ -4234,6 +4251,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     else if (e->nv == 1 && w16 && (vw & 1) && pdb == 1) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1) && pdb == 2) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1) && pdb == 3) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 3><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
+    else if (e->nv == 1 && w16 && (vw & 1) && narrow && n12) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 0, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1) && narrow) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
@@ -4297,7 +4315,9 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else C3M(IT, TH, NV, 0, 0); } while (0)
     static const int nit_env = getenv("FWA_NIT") ? atoi(getenv("FWA_NIT")) : 8;   // A/B: entries per lane and chunk (8: measured best)
     if (narrow) {
-        if (mp) combine3_kernel<4, 2, 1, 1024, 1, 0, 1, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        if (mp && n12) combine3_kernel<4, 2, 1, 1024, 1, 0, 1, 2><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        else if (mp) combine3_kernel<4, 2, 1, 1024, 1, 0, 1, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        else if (n12) combine3_kernel<8, 2, 1, 1024, 1, 0, 0, 2><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
         else if (nit_env == 8) combine3_kernel<8, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
         else if (nit_env == 6) combine3_kernel<6, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
         else combine3_kernel<4, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
