@@ -799,7 +799,10 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
     static_assert(!EARLY || (W16 && !PRE && EARLY <= ITEMS / 2), "early loads: paired, no tile pre-aggregation");
     // NW: narrow bucket entries -- key and BIGINT value as two sign-extended 32-bit halves of one u64 (10 instead of
     // 18 bytes per entry with the u16 slice); a record whose key or value needs 64 bits takes the v1 replay
-    static_assert(!NW || (NV == 1 && !PRE && (VW & 1)), "narrow entries: one 8-byte value column, no pre-aggregation");
+    // NW 3: the first value column is a 4-byte column (FLOAT / INT raw bits, zero-extended as in the 64-bit entries): the
+    // key's low half and those 32 bits share the u64, any second column keeps its own stream
+    static_assert(!NW || (NW == 3 ? (NV >= 1 && !PRE && !(VW & 1)) : (NV == 1 && !PRE && (VW & 1))),
+                  "narrow entries: one 8-byte value column (NW 1, 2), or a 4-byte first column (NW 3); no pre-aggregation");
     constexpr int kTile = THREADS * ITEMS;
     constexpr int kHt = 2 * kTile;                     // PRE: (key, slice) hash table, load <= 0.5
     constexpr int kHtLog = __builtin_ctz(kHt);
@@ -986,7 +989,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 }
             }
             if constexpr (NW) {
-                if (code == kCodeAccept && ((int64_t)(int32_t)key != key || (int64_t)(int32_t)R.v0[j] != (int64_t)R.v0[j])) {
+                if (code == kCodeAccept && ((int64_t)(int32_t)key != key ||
+                                            (NW != 3 && (int64_t)(int32_t)R.v0[j] != (int64_t)R.v0[j]))) {
                     code = kCodeSlow;
                     ++wide;
                 }
@@ -1409,7 +1413,10 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         int rmin = 0x7fffffff, rmax = -1;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
-            if constexpr (NW) {
+            if constexpr (NW == 3) {                        // 4-byte first column: raw bits, zero-extended
+                key[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)nkey[j];
+                x0[j] = nkey[j] >> 32;
+            } else if constexpr (NW) {
                 key[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)nkey[j];
                 x0[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)(nkey[j] >> 32);
             } else {
@@ -4207,7 +4214,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     const int narrow_env = narrow_s ? atoi(narrow_s) : -1;
     const bool narrow = narrow_env != 0 && (narrow_env == 1 || e->narrow) && layout == 1 && e->nv == 1 && (vw & 1) &&
                         w16 && !pre && !flat && !p2 && pdb == 0 && !a.pcount;
-    e->narrow_used = narrow;
+    // NW 3: a 4-byte first value column (C5's FLOAT) packed with the 32-bit key, generic accumulator layout
+    const bool narrow3 = narrow_env != 0 && (narrow_env == 1 || e->narrow) && e->nv == 2 && vw == 2 && layout == 0 &&
+                         kgm == 0 && !pre && !flat && !p2 && !a.pcount;
+    e->narrow_used = narrow || narrow3;
     const char* n12_s = getenv("FWA_NARROW12");                   // A/B: 12-byte AoS entries (one store / load each)
     const bool n12 = n12_s && atoi(n12_s) != 0;
     if (flat) {
@@ -4256,6 +4266,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1) { if (vw & 1) P2LAUNCH(1, 6, 3); else P2LAUNCH(1, 6, 2); }
+    else if (narrow3) partition3_kernel<2, 4, 1024, 2, 0, 0, 0, 0, 3><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (vw == 3) P2LAUNCH(2, 4, 3); else if (vw == 2) P2LAUNCH(2, 4, 2);
     else if (vw == 1) P2LAUNCH(2, 4, 1); else P2LAUNCH(2, 4, 0);
 #undef P2LAUNCH
@@ -4321,6 +4332,11 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else if (nit_env == 8) combine3_kernel<8, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
         else if (nit_env == 6) combine3_kernel<6, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
         else combine3_kernel<4, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+    } else if (narrow3) {
+        static const int nit3 = getenv("FWA_NIT3") ? atoi(getenv("FWA_NIT3")) : 4;   // A/B: entries per lane and chunk
+        if (mp) combine3_kernel<4, 2, 2, 1024, 0, 0, 1, 3><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        else if (nit3 == 8) combine3_kernel<8, 2, 2, 1024, 0, 0, 0, 3><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        else combine3_kernel<4, 2, 2, 1024, 0, 0, 0, 3><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
     } else if (e->nv == 0) C3L(4, 1024, 0);
     else if (e->nv == 1) C3L(4, 1024, 1);
     else C3L(4, 1024, 2);
