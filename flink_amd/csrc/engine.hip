@@ -4215,8 +4215,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     const bool narrow = narrow_env != 0 && (narrow_env == 1 || e->narrow) && layout == 1 && e->nv == 1 && (vw & 1) &&
                         w16 && !pre && !flat && !p2 && pdb == 0 && !a.pcount;
     // NW 3: a 4-byte first value column (C5's FLOAT) packed with the 32-bit key, generic accumulator layout
-    const bool narrow3 = narrow_env != 0 && (narrow_env == 1 || e->narrow) && e->nv == 2 && vw == 2 && layout == 0 &&
-                         kgm == 0 && !pre && !flat && !p2 && !a.pcount;
+    // (opt-in, FWA_NARROW3=1: measured 2-6 % slower on C5, whose Phase P is bound by 4-record partition runs)
+    const char* n3_s = getenv("FWA_NARROW3");
+    const bool narrow3 = n3_s && atoi(n3_s) != 0 && narrow_env != 0 && (narrow_env == 1 || e->narrow) && e->nv == 2 &&
+                         vw == 2 && layout == 0 && kgm == 0 && !pre && !flat && !p2 && !a.pcount;
     e->narrow_used = narrow || narrow3;
     const char* n12_s = getenv("FWA_NARROW12");                   // A/B: 12-byte AoS entries (one store / load each)
     const bool n12 = n12_s && atoi(n12_s) != 0;

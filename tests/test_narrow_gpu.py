@@ -86,11 +86,12 @@ C5_AGGS = [("COUNT", 0), ("SUM_F64", 1), ("AVG_F64", 1), ("MAX_F32", 0), ("MAX_F
 
 
 @pytest.mark.parametrize("wide_keys", [False, True], ids=["keys32", "keys64"])
-def test_narrow_float_column_entries_vs_oracle(eng_mod, wide_keys):
+def test_narrow_float_column_entries_vs_oracle(eng_mod, monkeypatch, wide_keys):
     """C5's shape: FLOAT + DOUBLE columns; the FLOAT's raw bits share the u64 with the 32-bit key (NW 3). With 64-bit
     keys (some, then most) the records are replayed and the handle switches back; rows equal the oracle's within the
     float-sum tolerance."""
     from oracle.oracle import Oracle
+    monkeypatch.setenv("FWA_NARROW3", "1")
     rng = np.random.default_rng(11)
     n = 1 << 20
     keys = rng.integers(-30_000, 30_000, n).astype(np.int64)
