@@ -1782,8 +1782,14 @@ struct FireSlideArgs {
     void* o_agg[FWA_MAX_AGGS];
     int64_t out_cap;                         // rows past it are counted, not written (host grows, relaunches)
     DevStatus* st;
+    int32_t abl;                             // timing ablation bits (0 in production)
+    unsigned long long* abl_ctr;             // ablation: 64 scratch counters (the push's want-set buffer)
 };
 
+// NA = the handle's accumulator count (compile time: the running sums and the next window's slice values stay in
+// registers). The slices entering / leaving window w + 1 are loaded before window w's rows are reserved and written,
+// so their latency overlaps the ballot, the row reservation and the stores.
+template <int NA>
 __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
     constexpr int kWaves = kBlock / 64;
@@ -1792,19 +1798,18 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
     __shared__ unsigned long long s_base;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     for (int i = tid; i < f.m; i += kBlock) s_u[i] = f.upos[i];
-    const int nacc = c.nacc;
     const int64_t nk = f.capacity + 1;
     const int64_t k0 = (int64_t)blockIdx.x * kBlock * kSlideJ;
     unsigned long long kv[kSlideJ];
     bool present[kSlideJ];
-    unsigned long long S[kSlideJ][kSlideAcc];
+    unsigned long long S[kSlideJ][NA];
 #pragma unroll
     for (int j = 0; j < kSlideJ; ++j) {
         const int64_t k = k0 + (int64_t)j * kBlock + tid;
         kv[j] = k < nk ? f.key_table[k] : kEmptyKey;
         present[j] = k < nk && ((k < f.capacity) ? (kv[j] != kEmptyKey) : (kv[j] == 1ull));
 #pragma unroll
-        for (int a = 0; a < kSlideAcc; ++a) S[j][a] = 0;
+        for (int a = 0; a < NA; ++a) S[j][a] = 0;
     }
     __syncthreads();
     // window 0: the sum of its L slices
@@ -1816,12 +1821,46 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
             if (!present[j]) continue;
             const int64_t k = k0 + (int64_t)j * kBlock + tid;
 #pragma unroll
-            for (int a = 0; a < kSlideAcc; ++a) if (a < nacc) S[j][a] += b[(int64_t)a * f.stride + k];
+            for (int a = 0; a < NA; ++a) S[j][a] += b[(int64_t)a * f.stride + k];
         }
     }
+    // the next window's entering minus leaving values, prefetched when they fit the registers (NA <= 2)
+    constexpr bool PF = false;   // measured slower with the prefetch (153 VGPRs for NA = 2, C3 fire 2.64 vs 2.0 ms)
+    unsigned long long D[PF ? kSlideJ : 1][NA];
+    auto load_delta = [&](int w1) {   // S(w1) = S(w1 - 1) + D
+        if constexpr (PF) {
+#pragma unroll
+            for (int j = 0; j < kSlideJ; ++j)
+#pragma unroll
+                for (int a = 0; a < NA; ++a) D[j][a] = 0;
+            if (w1 >= f.nw) return;
+            for (int t = 0; t < f.r; ++t) {
+                const unsigned long long* bin = s_u[(w1 - 1) * f.r + f.L + t];
+                const unsigned long long* bout = s_u[(w1 - 1) * f.r + t];
+#pragma unroll
+                for (int j = 0; j < kSlideJ; ++j) {
+                    if (!present[j]) continue;
+                    const int64_t k = k0 + (int64_t)j * kBlock + tid;
+#pragma unroll
+                    for (int a = 0; a < NA; ++a) {
+                        const unsigned long long xin = bin ? bin[(int64_t)a * f.stride + k] : 0ull;
+                        const unsigned long long xout = bout ? bout[(int64_t)a * f.stride + k] : 0ull;
+                        D[j][a] += xin - xout;
+                    }
+                }
+            }
+        }
+    };
+    if (PF) load_delta(1);
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (int w = 0; w < f.nw; ++w) {
-        if (w > 0) {
+        if (w > 0 && PF) {
+#pragma unroll
+            for (int j = 0; j < kSlideJ; ++j)
+#pragma unroll
+                for (int a = 0; a < NA; ++a) S[j][a] += D[PF ? j : 0][a];
+            load_delta(w + 1);                      // in flight while this window's rows are reserved and written
+        } else if (w > 0) {                         // S(w) = S(w - 1) + entering - leaving, in place
             for (int t = 0; t < f.r; ++t) {
                 const unsigned long long* bin = s_u[(w - 1) * f.r + f.L + t];
                 const unsigned long long* bout = s_u[(w - 1) * f.r + t];
@@ -1830,8 +1869,7 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
                     if (!present[j]) continue;
                     const int64_t k = k0 + (int64_t)j * kBlock + tid;
 #pragma unroll
-                    for (int a = 0; a < kSlideAcc; ++a) {
-                        if (a >= nacc) continue;
+                    for (int a = 0; a < NA; ++a) {
                         const unsigned long long xin = bin ? bin[(int64_t)a * f.stride + k] : 0ull;
                         const unsigned long long xout = bout ? bout[(int64_t)a * f.stride + k] : 0ull;
                         S[j][a] = S[j][a] + xin - xout;
@@ -1850,7 +1888,9 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
             uint32_t run = 0;
             for (int j = 0; j < kSlideJ; ++j)
                 for (int v = 0; v < kWaves; ++v) { const uint32_t t = woff[j][v]; woff[j][v] = run; run += t; }
-            s_base = run ? atomicAdd(&f.st->rows, (unsigned long long)run) : 0ull;
+            // timing ablation only (FWA_FSABL=1: the reservation spread over 64 scratch counters -- wrong rows)
+            unsigned long long* ctr = f.abl ? f.abl_ctr + 16 * (blockIdx.x & 63) : &f.st->rows;
+            s_base = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
         }
         __syncthreads();
         const int64_t ws = f.start0 + (int64_t)w * f.slide;
@@ -1867,7 +1907,7 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
                 const AggDesc d = c.agg[a];
                 unsigned long long x = 0;
 #pragma unroll
-                for (int q = 1; q < kSlideAcc; ++q) if (q == d.acc) x = S[j][q];
+                for (int q = 1; q < NA; ++q) if (q == d.acc) x = S[j][q];
                 write_agg(d, S[j][0], x, 0, f.o_agg[a], nullptr, row);
             }
         }
@@ -3123,10 +3163,11 @@ __global__ void push_reset_kernel(DevStatus* st, unsigned long long* want, int32
 
 // Restore the identities of a list of slots (every accumulator column; MIN columns 0xFF..) and clear
 // their touched flags: one launch for all slices a watermark retires (was 3 memsets per slot).
-__global__ void reset_slots_kernel(unsigned long long* const* slot_base, const int32_t* list, int64_t stride,
+struct SlotList { int32_t n, id[15]; };   // up to 15 slot ids by value (no upload); more: the device list
+__global__ void reset_slots_kernel(unsigned long long* const* slot_base, const int32_t* list, SlotList inl, int64_t stride,
                                    int32_t* touched, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
-    const int32_t slot = list[blockIdx.y];
+    const int32_t slot = inl.n ? inl.id[blockIdx.y] : list[blockIdx.y];
     unsigned long long* base = slot_base[slot];
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
     for (int col = 0; col < c.nacc; ++col) {
@@ -3234,6 +3275,7 @@ struct fwa_engine {
     std::vector<int32_t> touched;     // host mirror
     // slice directory
     DirEntry* d_dir = nullptr;
+    bool dir_dirty = false;         // the host directory changed since the last publish (published before v1 ingest)
     uint32_t dir_cap = 0;
     std::map<int64_t, int32_t> live;  // slice number -> slot (allocated slices)
     std::set<int64_t> negative;       // slices known late during the current push (published with slot -1)
@@ -3586,10 +3628,17 @@ int flush_resets(fwa_engine* e) {
         e->reset_cap = std::max<int32_t>(64, 2 * n);
         HIPCHK(e, hipMalloc(&e->d_reset_list, sizeof(int32_t) * e->reset_cap));
     }
-    int rc = upload(e, e->d_reset_list, e->pending_reset.data(), sizeof(int32_t) * n);
-    if (rc) return rc;
+    SlotList inl;
+    memset(&inl, 0, sizeof(inl));
+    if (n <= 15) {                                  // slot ids in the kernel arguments: no upload, no copy on the stream
+        inl.n = n;
+        for (int32_t i = 0; i < n; ++i) inl.id[i] = e->pending_reset[i];
+    } else {
+        int rc = upload(e, e->d_reset_list, e->pending_reset.data(), sizeof(int32_t) * n);
+        if (rc) return rc;
+    }
     const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 1024 / n), (e->stride / 2 + 1023) / 1024);
-    reset_slots_kernel<<<dim3((unsigned)blocks, (unsigned)n), 1024, 0, e->stream>>>(e->d_slot_base, e->d_reset_list,
+    reset_slots_kernel<<<dim3((unsigned)blocks, (unsigned)n), 1024, 0, e->stream>>>(e->d_slot_base, e->d_reset_list, inl,
                                                                                    e->stride, e->d_touched, e->d_ec);
     HIPCHK(e, hipGetLastError());
     e->pending_reset.clear();
@@ -3636,6 +3685,7 @@ int publish_dir(fwa_engine* e) {
         d.flags = 1 | (always ? 2 : 0);
         d.first_maxts = LONG_MAX_J;
     }
+    e->dir_dirty = false;
     return upload(e, e->d_dir, h.data(), sizeof(DirEntry) * h.size());
 }
 
@@ -3761,7 +3811,7 @@ void fwa_destroy(fwa_engine* e) {
     if (e->d_late) (void)hipFree(e->d_late);
     if (e->d_lr_n) (void)hipFree(e->d_lr_n);
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
-                    e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_win_slots, e->d_bkey, e->d_brel, e->d_bn,
+                    e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos,
                     e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_flat, e->d_rh};
     for (void* p : bufs) if (p) (void)hipFree(p);
@@ -4030,6 +4080,7 @@ static int wait_input_stream(fwa_engine* e) {
 }
 
 static int launch_ingest(fwa_engine* e, IngestArgs& a, bool replay) {
+    if (e->dir_dirty) { int rc = publish_dir(e); if (rc) return rc; }
     a.spill_cap = e->spill_cap;
     a.key_table = e->d_keys;
     a.key_mask = (uint64_t)e->capacity - 1;
@@ -4801,21 +4852,19 @@ static int fire_sessions(fwa_engine* e, int64_t wm, int64_t* nrows) {
 static int emit_late_rows(fwa_engine* e);
 static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const std::vector<int32_t>& hs, int raw,
                        int64_t* nrows, int64_t row0 = 0) {
-    if ((int32_t)hw.size() > e->win_cap) {
+    // windows and their slot list in one buffer: one upload
+    if ((int32_t)hw.size() > e->win_cap || (int32_t)hs.size() > e->win_slots_cap) {
         if (e->d_win) HIPCHK(e, hipFree(e->d_win));
         e->d_win = nullptr;
-        e->win_cap = (int32_t)hw.size() * 2;
-        HIPCHK(e, hipMalloc(&e->d_win, sizeof(FireWindow) * e->win_cap));
+        e->win_cap = std::max<int32_t>(e->win_cap, (int32_t)hw.size() * 2);
+        e->win_slots_cap = std::max<int32_t>(e->win_slots_cap, (int32_t)hs.size() * 2);
+        HIPCHK(e, hipMalloc(&e->d_win, sizeof(FireWindow) * e->win_cap + sizeof(int32_t) * e->win_slots_cap));
+        e->d_win_slots = (int32_t*)(e->d_win + e->win_cap);
     }
-    if ((int32_t)hs.size() > e->win_slots_cap) {
-        if (e->d_win_slots) HIPCHK(e, hipFree(e->d_win_slots));
-        e->d_win_slots = nullptr;
-        e->win_slots_cap = (int32_t)hs.size() * 2;
-        HIPCHK(e, hipMalloc(&e->d_win_slots, sizeof(int32_t) * e->win_slots_cap));
-    }
-    int rc = upload(e, e->d_win, hw.data(), sizeof(FireWindow) * hw.size());
-    if (rc) return rc;
-    rc = upload(e, e->d_win_slots, hs.data(), sizeof(int32_t) * hs.size());
+    std::vector<char> wbuf(sizeof(FireWindow) * e->win_cap + sizeof(int32_t) * hs.size());
+    memcpy(wbuf.data(), hw.data(), sizeof(FireWindow) * hw.size());
+    memcpy(wbuf.data() + sizeof(FireWindow) * e->win_cap, hs.data(), sizeof(int32_t) * hs.size());
+    int rc = upload(e, e->d_win, wbuf.data(), wbuf.size());
     if (rc) return rc;
     // rows <= windows x distinct keys; n_keys is current: every push ends with a status sync
     const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
@@ -4914,6 +4963,7 @@ static int process_late(fwa_engine* e, const IngestArgs& a0, std::vector<int32_t
     if (rc0) return rc0;
     if (!e->d_lr_n) HIPCHK(e, hipMalloc(&e->d_lr_n, 8));
     HIPCHK(e, hipMemcpyAsync(e->d_lr_n, &e->late_rows, 8, hipMemcpyHostToDevice, e->stream));
+    if (e->dir_dirty) { int rc = publish_dir(e); if (rc) return rc; }
     LateArgs L;
     memset(&L, 0, sizeof(L));
     L.in = a0;
@@ -5091,7 +5141,7 @@ static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, boo
         for (int64_t q = e->max_q + 1; q <= e->max_q + la; ++q)
             if (!e->live.count(q)) { rc = alloc_slice(e, q); if (rc) return rc; republish = true; }
     }
-    if (republish) { rc = publish_dir(e); if (rc) return rc; }
+    if (republish) e->dir_dirty = true;
     if (a.dropidx) { rc = collect_late_indices(e); if (rc) return rc; }
     e->records_in += n;
     e->late_dropped += dropped;
@@ -5267,7 +5317,7 @@ static int retire_slices(fwa_engine* e, int64_t wm) {
         e->live.erase(q);
     }
     if (int rc = flush_resets(e)) return rc;
-    if (!dead.empty()) return publish_dir(e);
+    if (!dead.empty()) e->dir_dirty = true;           // published lazily, before a kernel that reads it
     return FWA_OK;
 }
 
@@ -5688,9 +5738,17 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
     f.out_cap = e->out_cap;
     f.st = e->d_st;
+    static const int fsabl = getenv("FWA_FSABL") ? atoi(getenv("FWA_FSABL")) : 0;   // timing ablation (wrong rows)
+    f.abl = fsabl && e->d_want && kWantCap >= 1024 ? fsabl : 0;
+    f.abl_ctr = e->d_want;
     const int64_t grid = (e->capacity + 1 + (int64_t)kBlock * kSlideJ - 1) / ((int64_t)kBlock * kSlideJ);
     HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
-    fire_slide_kernel<<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
+    switch (e->nacc) {
+        case 1: fire_slide_kernel<1><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec); break;
+        case 2: fire_slide_kernel<2><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec); break;
+        case 3: fire_slide_kernel<3><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec); break;
+        default: fire_slide_kernel<4><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec); break;
+    }
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
     rc = sync_status(e);
@@ -5735,9 +5793,12 @@ static int speculative_fire(fwa_engine* e, int64_t wm, int64_t* nrows, bool* ok)
         if (rc) return rc;
     }
     const DevStatus st = *e->h_st;
+    *ok = hw.empty() ? false : (st.spill_n == 0 && st.late_fire == 0 && st.error == 0 && e->late_rows == 0);
+    // the speculation held: the fired slices retire now, so their resets run on the GPU while the host settles the push
+    // (fwa_advance_watermark's own retire_slices then finds nothing left)
+    if (*ok && (rc = retire_slices(e, wm))) return rc;
     rc = settle_pending(e);
     if (rc) return rc;
-    *ok = hw.empty() ? false : (st.spill_n == 0 && st.late_fire == 0 && st.error == 0 && e->late_rows == 0);
     return FWA_OK;
 }
 
