@@ -812,7 +812,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
     __shared__ uint32_t gbase[kMaxPart];
     __shared__ uint32_t sbase[kMaxPart];   // spill-list base of the tile's overflow records, per partition
     __shared__ unsigned long long x_key[kTile];
-    __shared__ unsigned long long x_val[NV > 0 ? NV : 1][NV > 0 ? kTile : 1];
+    // NW 1: x_key holds the packed entry (key | value << 32) and x_val is not used (half the staging LDS)
+    __shared__ unsigned long long x_val[NV > 0 && NW != 1 ? NV : 1][NV > 0 && NW != 1 ? kTile : 1];
     __shared__ uint16_t x_rel[kTile];
     __shared__ uint16_t s_part[kTile];
     __shared__ uint16_t s_src[kTile];
@@ -1016,7 +1017,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 const int x = xof(j);
                 x_key[x] = R.key[j];
                 x_rel[x] = (uint16_t)rel;
-                if (NV > 0) x_val[0][x] = R.v0[j];
+                if constexpr (NW == 1) x_key[x] = (R.key[j] & 0xffffffffull) | (R.v0[j] << 32);
+                else if (NV > 0) x_val[0][x] = R.v0[j];
                 if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = R.v1[j];
                 if constexpr (PRE) {
                     x_n[x] = rn;
@@ -1133,6 +1135,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                              : flat ? dst : ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
             if constexpr (NW == 2)                       // 12-byte entry {key, value, slice}: one store
                 reinterpret_cast<uint3*>(a.b_key)[o] = make_uint3((uint32_t)x_key[x], (uint32_t)x_val[0][x], x_rel[x]);
+            else if constexpr (NW == 1) a.b_key[o] = x_key[x];    // packed at staging
             else if constexpr (NW) a.b_key[o] = (x_key[x] & 0xffffffffull) | (x_val[0][x] << 32);
             else a.b_key[o] = x_key[x];
             if constexpr (NW != 2) a.b_rel[o] = x_rel[x];
@@ -3342,7 +3345,7 @@ struct fwa_engine {
     size_t combine_lds = 0;
     int32_t partition_grid = 256;
     // kernel timing (HIP events on this handle's stream)
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[10] = {};
     double partition_ms = 0, combine_ms = 0;
     int64_t ingest_launches = 0, ingest_records = 0, replay_records = 0, fire_launches = 0, fire_rows = 0;
     // producer stream of device inputs (fwa_set_input_stream): every push waits for it (stream order)
@@ -4271,6 +4274,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     const bool narrow3 = n3_s && atoi(n3_s) != 0 && narrow_env != 0 && (narrow_env == 1 || e->narrow) && e->nv == 2 &&
                          vw == 2 && layout == 0 && kgm == 0 && !pre && !flat && !p2 && !a.pcount;
     e->narrow_used = narrow || narrow3;
+    static const bool nitems8 = getenv("FWA_NITEMS8") && atoi(getenv("FWA_NITEMS8")) != 0;   // A/B: 8192-record tiles
+    const int grid8 = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + 8191) / 8192, 256));
     const char* n12_s = getenv("FWA_NARROW12");                   // A/B: 12-byte AoS entries (one store / load each)
     const bool n12 = n12_s && atoi(n12_s) != 0;
     if (flat) {
@@ -4315,6 +4320,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     else if (e->nv == 1 && w16 && (vw & 1) && pdb == 2) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1) && pdb == 3) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 3><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1) && narrow && n12) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 0, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
+    else if (e->nv == 1 && w16 && (vw & 1) && narrow && nitems8) partition3_kernel<1, 8, 1024, 3, 0, 0, 1, 0, 1><<<grid8, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1) && narrow) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
