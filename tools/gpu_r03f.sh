@@ -8,8 +8,6 @@ tail -3 gpurun_out/r03f_sess.log
 timeout -k 10 300 python bench.py --config c5s --steps 5 --warmup 1 --no-cpu-baseline --no-pcie --no-wire > gpurun_out/r03f_c5s.json 2> gpurun_out/r03f_c5s.log || { tail -20 gpurun_out/r03f_c5s.log; exit 1; }
 python -c "
 import json; d=json.load(open('gpurun_out/r03f_c5s.json')); print('c5s', round(d['value']/1e9,2), d['ms_per_step'])"
-FWA_ROWB=1 timeout -k 10 300 python bench.py --config c5s --steps 5 --warmup 1 --no-cpu-baseline --no-pcie --no-wire > gpurun_out/r03f_c5s_rowb.json 2>> gpurun_out/r03f_c5s.log && python -c "
-import json; d=json.load(open('gpurun_out/r03f_c5s_rowb.json')); print('c5s rowb', round(d['value']/1e9,2), d['ms_per_step'])"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r03f_prof -o run --output-format csv -- python3 $R/bench.py --config c5s --steps 5 --warmup 1 --no-cpu-baseline --no-pcie --no-wire > $R/gpurun_out/r03f_prof.log 2>&1 || { tail -20 $R/gpurun_out/r03f_prof.log; exit 1; }
 python3 - <<'P'
