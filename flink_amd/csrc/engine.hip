@@ -2393,20 +2393,24 @@ __global__ void __launch_bounds__(kBlock) sess2_segment_kernel(Sess2Args a, cons
 
 // The segment kernel's clusters, moved from each wave's staging range to the output list at the exclusive sum of the
 // per-wave counts (one thread per wave; the arrival-order path appends after them on ctr->n_out_sp).
+// One thread per output session (coalesced stores): the staging wave w that owns output dst is the last one with
+// sg_off[w] <= dst (a binary search over the scanned counts, which stay cache-resident); a thread per wave copying its
+// ~1.4 clusters serially took 0.24 ms per C5s push.
 __global__ void __launch_bounds__(kBlock) sess2_compact_kernel(Sess2Args a, int64_t nw, int nacc) {
-    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t o0 = a.sg_off[w], o1 = a.sg_off[w + 1];
-        if (o1 == o0) continue;
-        const int64_t h0 = a.sg_h0[w];
-        for (uint32_t i = 0; i < o1 - o0; ++i) {
-            const int64_t src = h0 + i, dst = (int64_t)o0 + i;
-            a.out.kid[dst] = a.sg_kid[src];
-            a.out.start[dst] = a.sg_start[src];
-            a.out.end[dst] = a.sg_end[src];
-            for (int cc = 0; cc < nacc; ++cc) a.out.acc[(int64_t)cc * a.out.stride + dst] = a.sg_acc[(int64_t)cc * a.sg_cap + src];
+    const int64_t tot = a.sg_off[nw];
+    for (int64_t dst = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; dst < tot; dst += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = nw;                          // invariant: sg_off[lo] <= dst < sg_off[hi]
+        while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)a.sg_off[mid] <= dst) lo = mid; else hi = mid;
         }
+        const int64_t src = a.sg_h0[lo] + (dst - (int64_t)a.sg_off[lo]);
+        a.out.kid[dst] = a.sg_kid[src];
+        a.out.start[dst] = a.sg_start[src];
+        a.out.end[dst] = a.sg_end[src];
+        for (int cc = 0; cc < nacc; ++cc) a.out.acc[(int64_t)cc * a.out.stride + dst] = a.sg_acc[(int64_t)cc * a.sg_cap + src];
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr->n_out_sp = a.sg_off[nw];
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr->n_out_sp = (unsigned long long)tot;
 }
 
 // ---- Cell path: fixed gap, every record of the push order-free ------------------------------------------------------
@@ -4544,7 +4548,7 @@ static int launch_segments(fwa_engine* e, Sess2Args& s, int64_t nb, bool cells) 
     if (rc) return rc;
     bytes = e->sort_tmp_bytes;
     HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(e->d_sort_tmp, bytes, s.sg_cnt, s.sg_off, (int)(nw + 1), e->stream));
-    sess2_compact_kernel<<<grid_for(nw, 256 * 8), kBlock, 0, e->stream>>>(s, nw, e->nacc);
+    sess2_compact_kernel<<<1024, kBlock, 0, e->stream>>>(s, nw, e->nacc);
     HIPCHK(e, hipGetLastError());
     return FWA_OK;
 }
