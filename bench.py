@@ -53,6 +53,8 @@ def main():
                          "c4: tumbling 10s COUNT+SUM(long), 100M uniform keys, maxParallelism 128; "
                          "c5: Table TUMBLE 10s TVF COUNT, SUM(double), AVG(double), MAX(float), MAX(double); "
                          "c5s: DataStream session windows (gap 5s), same float aggregates")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="fwa_set_option on the measured engine(s) (flink_amd.engine.OPTIONS), e.g. profile=1")
     ap.add_argument("--exchange", choices=["partials", "raw"], default="partials",
                     help="N>1 keyBy plan: two-phase partial accumulators (default) or raw records")
     args = ap.parse_args()
@@ -62,6 +64,9 @@ def main():
 
     from flink_amd import _abi as A
     from flink_amd import engine as E
+    for o in args.option:                           # A/B and diagnostic options, every handle of this run
+        k, v = o.split("=", 1)
+        E.DEFAULT_OPTIONS[k] = int(v)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -453,7 +453,6 @@ struct PartArgs {
     int32_t part_bits, np;
     int32_t vcol[2];
     int32_t vsize[2];                  // 4 or 8 bytes
-    int32_t abl;                       // ablation bits (timing experiments only; 0 in production)
     int32_t* dropidx;                  // FWA_CFG_LATE_INDICES list (nullptr: not collected)
     const uint8_t* nulls[FWA_MAX_COLS];   // SQL NULL flags of the push (records with a NULL take the v1 path)
     int32_t any_null;                  // some nulls[] is set
@@ -466,12 +465,7 @@ struct PartArgs {
     unsigned long long* const* slot_base;
     int64_t stride;
     DevStatus* st;
-    long long* prof;                   // optional per-block phase cycle counters (FWA_PPROF)
-    // flat layout (part_hist_kernel first): block b owns tiles [b * tpb, (b + 1) * tpb) and writes partition p's
-    // records at [flat_off[p * G + b], ...) -- no reservation atomics, no overflow, holes for records not accepted
-    const uint32_t* flat_off;          // [np * G + 1] exclusive sum of the (partition, block) counts, or nullptr
-    int64_t tpb;
-    int64_t flat_cap;
+    long long* prof;                   // optional per-block phase cycle counters (FWA_OPT_PROFILE)
 };
 
 __device__ __forceinline__ bool row_has_null(const PartArgs& a, int64_t i) {
@@ -526,255 +520,11 @@ __device__ __forceinline__ void consume(int64_t x) { consume((unsigned long long
 __device__ __forceinline__ void consume(int32_t x) { asm volatile("" : : "v"(x)); }
 __device__ __forceinline__ void consume(uint32_t x) { asm volatile("" : : "v"(x)); }
 
-// Flat Phase P layout, pass 1: records per (partition, block) over exactly the tiles Phase P gives
-// each block (a contiguous run of tpb tiles), from the keys alone, written partition-major; their exclusive sum is
-// every block's private, contiguous output range per partition. Phase P then needs no reservation atomics (r02
-// clock profile: 43 % of Phase P waited on them) and a partition's entries are contiguous and in time order.
-// skip_last: the record n-1 of an odd n that paired 16-byte loads leave to the replay (no bucket slot).
-__global__ void __launch_bounds__(1024) part_hist_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t tile,
-                                                         int64_t tpb, int part_bits, int np, int skip_last,
-                                                         uint32_t* __restrict__ counts) {
-    __shared__ uint32_t hist[kMaxPart];
-    for (int i = threadIdx.x; i < np; i += blockDim.x) hist[i] = 0;
-    __syncthreads();
-    const int64_t i0 = (int64_t)blockIdx.x * tpb * tile;
-    const int64_t i1 = min(i0 + tpb * tile, n - (skip_last ? 1 : 0));
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        const uint64_t h = jm::mix64((uint64_t)keys[i]);
-        atomicAdd(&hist[part_bits ? (uint32_t)(h >> (64 - part_bits)) : 0u], 1u);
-    }
-    __syncthreads();
-    for (int p = threadIdx.x; p < np; p += blockDim.x) counts[(int64_t)p * gridDim.x + blockIdx.x] = hist[p];
-}
-
-// The flat layout never overflows; its skew signal is what the sub-bucket layout would have overflowed: entries of a
-// partition past kSub sub-buckets of capacity capb (DevStatus::ovf_n, the PRE switch of push_settle).
-__global__ void flat_skew_kernel(const uint32_t* offs, int np, int g, int64_t lim, DevStatus* st) {
-    for (int p = threadIdx.x; p < np; p += blockDim.x) {
-        const int64_t tot = (int64_t)offs[(int64_t)(p + 1) * g] - (int64_t)offs[(int64_t)p * g];
-        if (tot > lim) atomicAdd(&st->ovf_n, (int32_t)min<int64_t>(tot - lim, INT32_MAX / 4));
-    }
-}
-
-// partition2: Phase P with the next tile's loads in flight while the current tile is scanned,
-// reserved and stored (r01 ablation: without its bucket stores Phase P still took 0.58 ms per 2^26
-// records, twice the streaming time of its 1.6 GB of input -- one tile in flight per CU left every
-// latency in the tile's chain exposed). The tile is staged in LDS in arrival order (x_*), the
-// counting sort only writes a permutation (s_src) and the store loop gathers through it, so the
-// load registers are free as soon as the tile is classified.
-// VW: value-column widths, bit v set = carried value column v is 8 bytes (else 4): a compile-time
-// width keeps the tile's loads branch-free, so none waits for another.
-template <int NV, int ITEMS, int THREADS, int MINW = 1, int VW = 3>
-__global__ void __launch_bounds__(THREADS, MINW) partition2_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
-    constexpr int kTile = THREADS * ITEMS;
-    const EngineConst& c = *cp;
-    __shared__ uint32_t hist[kMaxPart];
-    __shared__ uint32_t toff[kMaxPart];
-    __shared__ uint32_t gbase[kMaxPart];
-    __shared__ uint32_t sbase[kMaxPart];   // spill-list base of the tile's overflow records, per partition
-    __shared__ unsigned long long x_key[kTile];
-    __shared__ unsigned long long x_val[NV > 0 ? NV : 1][NV > 0 ? kTile : 1];
-    __shared__ uint16_t x_rel[kTile];
-    __shared__ uint16_t s_part[kTile];
-    __shared__ uint16_t s_src[kTile];
-    __shared__ uint32_t wsum[THREADS / 64];
-    __shared__ uint32_t s_total;
-    __shared__ uint8_t s_code[kRelCap];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    unsigned dropped = 0;
-    uint32_t relmax = 0, relmin = ~0u;
-    const bool kg_all = c.kg_lo == 0 && c.kg_hi == c.max_par - 1;
-    const bool ds = c.sem == FWA_SEM_DATASTREAM;
-    for (int r = tid; r < kRelCap / 4; r += THREADS) ((uint32_t*)s_code)[r] = ((const uint32_t*)a.relcode)[r];
-    const int64_t ntiles = (a.n + kTile - 1) / kTile;
-    const int sub = blockIdx.x % kSub;
-    unsigned long long r_key[ITEMS], r_v0[ITEMS], r_v1[ITEMS];
-    int64_t r_ts[ITEMS];
-    int32_t r_kh[ITEMS];
-    // Column pointers resolved once (uniform, SGPRs): indexing the kernel-argument array per load
-    // made hipcc fetch the pointer with a vector load and wait vmcnt(0) before every value load,
-    // serialising the tile's loads item by item.
-    const int64_t* __restrict__ pkeys = a.keys;
-    const int64_t* __restrict__ pts = a.ts;
-    const void* pc0 = NV > 0 ? a.cols[a.vcol[0]] : nullptr;
-    const void* pc1 = NV > 1 ? a.cols[a.vcol[1]] : nullptr;
-    constexpr bool w0 = (VW & 1) != 0, w1 = (VW & 2) != 0;
-    const int32_t* __restrict__ pkh = a.key_hash;
-    const int64_t n = a.n;
-    // every load of a tile is issued before any is used; uniform branches sit outside the item loops
-    // (a per-item select between a 4- and an 8-byte load made hipcc wait vmcnt(0) at every join)
-    auto load = [&](int64_t t) {
-        int64_t ic[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const int64_t i = t * kTile + (int64_t)j * THREADS + tid;
-            ic[j] = i < n ? i : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) { r_key[j] = (unsigned long long)pkeys[ic[j]]; r_ts[j] = pts[ic[j]]; }
-        if constexpr (NV > 0) {
-            if constexpr (w0) {
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j) r_v0[j] = ((const unsigned long long*)pc0)[ic[j]];
-            } else {
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j) r_v0[j] = ((const uint32_t*)pc0)[ic[j]];
-            }
-        }
-        if constexpr (NV > 1) {
-            if constexpr (w1) {
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j) r_v1[j] = ((const unsigned long long*)pc1)[ic[j]];
-            } else {
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j) r_v1[j] = ((const uint32_t*)pc1)[ic[j]];
-            }
-        }
-        if (pkh) {
-#pragma unroll
-            for (int j = 0; j < ITEMS; ++j) r_kh[j] = pkh[ic[j]];
-        } else {
-#pragma unroll
-            for (int j = 0; j < ITEMS; ++j) r_kh[j] = 0;
-        }
-    };
-    long long pt = clock64();
-    long long pacc[6] = {0, 0, 0, 0, 0, 0};
-#define QMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
-    int64_t tile = blockIdx.x;
-    if (tile < ntiles) load(tile);
-    for (; tile < ntiles; tile += gridDim.x) {
-        for (int i = tid; i < a.np; i += THREADS) hist[i] = 0;
-        __syncthreads();
-        QMARK(5);
-        const int64_t t0 = tile * kTile;
-        uint32_t r_pos[ITEMS];   // (p << 16 | rank) or ~0u when the record does not go to a bucket
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const int64_t i = t0 + (int64_t)j * THREADS + tid;
-            const int64_t key = (int64_t)r_key[j];
-            const int64_t ts = r_ts[j];
-            const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
-            const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
-            const uint64_t uq = jm::udiv64(ud, c.g_div);
-            const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
-            const uint64_t rel = (uint64_t)(q - a.q_base);
-            uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
-            if (!kg_all) {
-                const int32_t kg = jm::key_group_of(key, c.key_kind, r_kh[j], c.max_par);
-                if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;
-            }
-            if (ds && ts == LONG_MIN_J) code = kCodeSlow;
-            if (a.any_null && i < a.n && row_has_null(a, i)) code = kCodeSlow;   // SQL NULLs: the v1 path
-            if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
-            if (i >= a.n) code = 0xff;
-            dropped += code == kCodeDrop;
-            note_drop(a.dropidx, a.st, code == kCodeDrop, i);
-            const bool slow = code == kCodeSlow;
-            const unsigned long long mk = __ballot(slow);
-            if (mk) {
-                const int leader = __ffsll((long long)mk) - 1;
-                int32_t sb = 0;
-                if (lane == leader) sb = atomicAdd(&a.st->spill_n, __popcll(mk));
-                sb = __shfl(sb, leader);
-                if (slow) put_idx(a.spill, sb + __popcll(mk & ((1ull << lane) - 1)), a.spill_cap, (int32_t)i, a.st);
-            }
-            r_pos[j] = ~0u;
-            if (code == kCodeAccept) {
-                relmax = max(relmax, (uint32_t)rel);
-                relmin = min(relmin, (uint32_t)rel);
-                const uint64_t h = jm::mix64((uint64_t)key);
-                const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
-                const int x = j * THREADS + tid;
-                x_key[x] = r_key[j];
-                x_rel[x] = (uint16_t)rel;
-                if (NV > 0) x_val[0][x] = r_v0[j];
-                if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = r_v1[j];
-                r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
-            }
-        }
-        QMARK(0);
-        if (tile + gridDim.x < ntiles) load(tile + gridDim.x);   // next tile in flight from here on
-        __syncthreads();
-        block_scan_np<THREADS>(hist, toff, wsum, a.np, &s_total);
-        __syncthreads();
-        QMARK(1);
-        for (int p = tid; p < a.np; p += THREADS) {
-            const uint32_t h = hist[p];
-            const uint32_t g = h ? atomicAdd(&a.b_cnt[p * kSub + sub], h) : 0u;
-            gbase[p] = g;
-            // records past the sub-bucket's end (skewed keys) go to the v1 replay: one spill reservation
-            // per (tile, overflowing partition) -- a per-wave reservation on the single spill counter
-            // serialised ~100 K same-address device atomics per push under Zipf(1.1)
-            const uint64_t end = (uint64_t)g + h;
-            if (end > (uint64_t)a.capb) {
-                const uint32_t ov = (uint32_t)(end - std::max<uint64_t>(g, (uint64_t)a.capb));
-                sbase[p] = (uint32_t)atomicAdd(&a.st->spill_n, (int32_t)ov);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            if (r_pos[j] == ~0u) continue;
-            const uint32_t p = r_pos[j] >> 16;
-            const uint32_t sidx = toff[p] + (r_pos[j] & 0xffffu);
-            s_part[sidx] = (uint16_t)p;
-            s_src[sidx] = (uint16_t)(j * THREADS + tid);
-        }
-        __syncthreads();
-        QMARK(2);
-        const uint32_t total = s_total;
-        for (uint32_t sidx = tid; sidx < total; sidx += THREADS) {
-            const uint32_t p = s_part[sidx];
-            const uint32_t x = s_src[sidx];
-            const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
-            if (dst >= (uint64_t)a.capb) {      // sub-bucket full (skewed keys): the v1 replay takes it
-                const uint64_t first = std::max<uint64_t>(gbase[p], (uint64_t)a.capb);
-                put_idx(a.spill, (int64_t)sbase[p] + (int64_t)(dst - first), a.spill_cap, (int32_t)(t0 + x), a.st);
-                continue;
-            }
-            const uint64_t o = ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
-            a.b_key[o] = x_key[x];
-            a.b_rel[o] = x_rel[x];
-            if (NV > 0) a.b_val0[o] = x_val[0][x];
-            if (NV > 1) a.b_val1[o] = x_val[NV > 1 ? 1 : 0][x];
-        }
-        QMARK(3);
-        __syncthreads();
-        QMARK(4);
-    }
-    if (a.prof && tid == 0) for (int q = 0; q < 6; ++q) a.prof[(int64_t)blockIdx.x * 8 + q] = pacc[q];
-#undef QMARK
-    for (int sh = 32; sh >= 1; sh >>= 1) {
-        dropped += __shfl_xor(dropped, sh);
-        relmax = max(relmax, (uint32_t)__shfl_xor((int)relmax, sh));
-        relmin = min(relmin, (uint32_t)__shfl_xor((int)relmin, sh));
-    }
-    if (lane == 0) {
-        if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
-        if (relmin != ~0u) {
-            atomicMax(&a.st->max_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmax));
-            atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
-        }
-    }
-    if (relmin != ~0u)
-        for (uint32_t r = relmin + (uint32_t)lane; r <= relmax; r += 64) {
-            const int32_t slot = a.rel2slot[r];
-            if (slot >= 0 && a.touched[slot] == 0) a.touched[slot] = 1;
-        }
-}
-
-// partition3: partition2 with the reservation/prefetch order fixed (below) and the key-group check
-// and key-hash loads compiled in only when needed (KG: 0 whole range owned, 1 hash of the key, 2 supplied
-// key.hashCode()).
-// partition2: Phase P with the next tile's loads in flight while the current tile is scanned,
-// reserved and stored (r01 ablation: without its bucket stores Phase P still took 0.58 ms per 2^26
-// records, twice the streaming time of its 1.6 GB of input -- one tile in flight per CU left every
-// latency in the tile's chain exposed). The tile is staged in LDS in arrival order (x_*), the
-// counting sort only writes a permutation (s_src) and the store loop gathers through it, so the
-// load registers are free as soon as the tile is classified.
-// VW: value-column widths, bit v set = carried value column v is 8 bytes (else 4): a compile-time
-// width keeps the tile's loads branch-free, so none waits for another.
+// partition3 (Phase P): the tile is staged in LDS in arrival order (x_*), a counting sort by partition writes only a
+// permutation (s_src) and the store loop gathers through it, so the load registers are free for the next tile's
+// loads as soon as the tile is classified; the run reservations are issued before those loads (below). The
+// key-group check and key-hash loads are compiled in only when needed (KG: 0 whole range owned, 1 hash of the key,
+// 2 supplied key.hashCode()).
 // PRE (skewed keys, COUNT [+ one BIGINT SUM] layouts): equal (key, slice) records of a tile are first merged
 // in an LDS hash table -- the wavefront/workgroup hot-key reduction of Flink's local pre-aggregation
 // (LocalSlicingWindowAggOperator) -- so a Zipf head key costs one bucket entry per tile instead of one
@@ -791,18 +541,14 @@ __device__ __noinline__ void pre_apply_global(unsigned long long* table, uint64_
 
 // W16: the tile's columns are read with 16-byte loads (two records per lane per column; 8-byte loads reach
 // roughly 0.6x the 16-byte rate, MI355X_MICROARCH.md): item j of a lane is record 2 * ((j / 2) * THREADS + tid) + j % 2.
-template <int NV, int ITEMS, int THREADS, int VW, int KG, int PRE = 0, int W16 = 0, int EARLY = 0, int NW = 0>
+// NW: narrow bucket entries -- key and BIGINT value as two sign-extended 32-bit halves of one u64 (10 instead of 18
+// bytes per entry with the u16 slice); a record whose key or value needs 64 bits takes the v1 replay.
+template <int NV, int ITEMS, int THREADS, int VW, int KG, int PRE = 0, int W16 = 0, int NW = 0>
 __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
     static_assert(THREADS == kMaxPart && ITEMS <= 8, "one partition cursor per thread; trash area of 8 x kMaxPart");
     static_assert(!PRE || NV <= 1, "pre-aggregation: COUNT [+ one BIGINT sum]");
     static_assert(!W16 || (ITEMS % 2 == 0 && KG != 2 && NV <= 1), "paired loads: even ITEMS, no key-hash column");
-    static_assert(!EARLY || (W16 && !PRE && EARLY <= ITEMS / 2), "early loads: paired, no tile pre-aggregation");
-    // NW: narrow bucket entries -- key and BIGINT value as two sign-extended 32-bit halves of one u64 (10 instead of
-    // 18 bytes per entry with the u16 slice); a record whose key or value needs 64 bits takes the v1 replay
-    // NW 3: the first value column is a 4-byte column (FLOAT / INT raw bits, zero-extended as in the 64-bit entries): the
-    // key's low half and those 32 bits share the u64, any second column keeps its own stream
-    static_assert(!NW || (NW == 3 ? (NV >= 1 && !PRE && !(VW & 1)) : (NV == 1 && !PRE && (VW & 1))),
-                  "narrow entries: one 8-byte value column (NW 1, 2), or a 4-byte first column (NW 3); no pre-aggregation");
+    static_assert(!NW || (NV == 1 && !PRE && (VW & 1) && W16), "narrow entries: one 8-byte value column, paired loads");
     constexpr int kTile = THREADS * ITEMS;
     constexpr int kHt = 2 * kTile;                     // PRE: (key, slice) hash table, load <= 0.5
     constexpr int kHtLog = __builtin_ctz(kHt);
@@ -812,8 +558,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
     __shared__ uint32_t gbase[kMaxPart];
     __shared__ uint32_t sbase[kMaxPart];   // spill-list base of the tile's overflow records, per partition
     __shared__ unsigned long long x_key[kTile];
-    // NW 1: x_key holds the packed entry (key | value << 32) and x_val is not used (half the staging LDS)
-    __shared__ unsigned long long x_val[NV > 0 && NW != 1 ? NV : 1][NV > 0 && NW != 1 ? kTile : 1];
+    // NW: x_key holds the packed entry (key | value << 32) and x_val is not used (half the staging LDS)
+    __shared__ unsigned long long x_val[NV > 0 && !NW ? NV : 1][NV > 0 && !NW ? kTile : 1];
     __shared__ uint16_t x_rel[kTile];
     __shared__ uint16_t s_part[kTile];
     __shared__ uint16_t s_src[kTile];
@@ -845,12 +591,10 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
     // every load of a tile is issued before any is used; uniform branches sit outside the item loops
     // (a per-item select between a 4- and an 8-byte load made hipcc wait vmcnt(0) at every join)
     auto xof = [&](int j) -> int { return W16 ? 2 * ((j >> 1) * THREADS + tid) + (j & 1) : j * THREADS + tid; };
-    // W16: pair p = records 2p, 2p+1 of the tile; a pair reaching past n is not loaded (its record n-1, if any, goes
-    // to the slow path below). Pairs [j0, j1) of tile t.
-    auto load_pairs = [&](Regs& R, int64_t t, int j0, int j1) {
-#pragma unroll
+    auto load = [&](Regs& R, int64_t t) {
+        if constexpr (W16) {   // pair p = records 2p, 2p+1 of the tile; a pair reaching past n is not loaded (its
+#pragma unroll                 // record n-1, if any, goes to the slow path below)
             for (int jj = 0; jj < ITEMS / 2; ++jj) {
-                if (jj < j0 || jj >= j1) continue;
                 const int64_t pi = t * (kTile / 2) + (int64_t)jj * THREADS + tid;
                 const int64_t ip = 2 * pi + 1 < n ? pi : 0;
                 const ulonglong2 kk = reinterpret_cast<const ulonglong2*>(pkeys)[ip];
@@ -868,10 +612,6 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 }
                 R.kh[2 * jj] = 0; R.kh[2 * jj + 1] = 0;
             }
-    };
-    auto load = [&](Regs& R, int64_t t) {
-        if constexpr (W16) {
-            load_pairs(R, t, 0, ITEMS / 2);
             return;
         }
         int64_t ic[ITEMS];
@@ -913,24 +653,15 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
 #define QMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
     Regs ra;
     const int64_t G = gridDim.x;
-    const bool flat = a.flat_off != nullptr;
-    int64_t tile = blockIdx.x, tstep = G, tend = ntiles;            // tiles of this block
-    if (flat) {
-        tile = (int64_t)blockIdx.x * a.tpb;
-        tstep = 1;
-        tend = min(ntiles, tile + a.tpb);
-        for (int q = tid; q < a.np; q += THREADS) sbase[q] = a.flat_off[(int64_t)q * G + blockIdx.x];   // cursors
-    }
-    load(ra, tile < tend ? tile : 0);
+    load(ra, blockIdx.x < ntiles ? (int64_t)blockIdx.x : 0);
     // the memory operations of one store phase, to the trash area: hipcc's waitcnt analysis merges the
     // loop entry with the back-edge, so an entry without the stores made the header wait vmcnt(0) on
     // every trip (draining the previous tile's stores)
 #pragma unroll
     for (int jj = 0; jj < ITEMS; ++jj) {
         const uint64_t o = a.trash + (uint64_t)(jj * THREADS + tid);   // distinct: not merged by the compiler
-        if constexpr (NW == 2) reinterpret_cast<uint3*>(a.b_key)[o] = make_uint3(0u, 0u, 0u);
-        else a.b_key[o] = 0ull;
-        if constexpr (NW != 2) a.b_rel[o] = 0;
+        a.b_key[o] = 0ull;
+        a.b_rel[o] = 0;
         if constexpr (PRE) a.b_n[o] = 0;
         if (NV > 0 && !NW) a.b_val0[o] = 0ull;
         if (NV > 1) a.b_val1[o] = 0ull;
@@ -990,8 +721,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 }
             }
             if constexpr (NW) {
-                if (code == kCodeAccept && ((int64_t)(int32_t)key != key ||
-                                            (NW != 3 && (int64_t)(int32_t)R.v0[j] != (int64_t)R.v0[j]))) {
+                if (code == kCodeAccept && ((int64_t)(int32_t)key != key || (int64_t)(int32_t)R.v0[j] != (int64_t)R.v0[j])) {
                     code = kCodeSlow;
                     ++wide;
                 }
@@ -1017,7 +747,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 const int x = xof(j);
                 x_key[x] = R.key[j];
                 x_rel[x] = (uint16_t)rel;
-                if constexpr (NW == 1) x_key[x] = (R.key[j] & 0xffffffffull) | (R.v0[j] << 32);
+                if constexpr (NW) x_key[x] = (R.key[j] & 0xffffffffull) | (R.v0[j] << 32);
                 else if (NV > 0) x_val[0][x] = R.v0[j];
                 if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = R.v1[j];
                 if constexpr (PRE) {
@@ -1026,21 +756,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                                         : (0x80000000u | p);                        // bucketed after the merge
                 }
                 else r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
-            } else if (!PRE && flat && i < a.n && !(W16 && i == a.n - 1 && (a.n & 1))) {
-                // flat layout: every record the histogram counted takes its slot; one not accepted leaves a hole
-                // (rel 0xFFFF, skipped by Phase A)
-                const uint64_t h = jm::mix64((uint64_t)key);
-                const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
-                const int x = xof(j);
-                x_key[x] = R.key[j];
-                x_rel[x] = 0xFFFF;
-                if (NV > 0) x_val[0][x] = 0ull;
-                if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = 0ull;
-                r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
             }
-            // EARLY: pair j/2 of this tile is staged; its registers take the next tile's pair now, so loads are in
-            // flight through the classify and the scan (the reservation below then waits for these loads)
-            if constexpr (EARLY > 0) if ((j & 1) && (j >> 1) < EARLY) load_pairs(R, nx < tend ? nx : tile, j >> 1, (j >> 1) + 1);
         }
         if constexpr (PRE) {
             __syncthreads();                        // the tile's staged (key, rel) visible to every lane
@@ -1075,17 +791,11 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         __syncthreads();
         QMARK(1);
         // the run reservations (returning atomics) are issued BEFORE the next tile's loads: vmcnt retires
-        // in order, so waiting for the reservations no longer drains the prefetch (partition2 waited
-        // vmcnt(0) right after its reservation, leaving no load in flight during scatter and store)
+        // in order, so waiting for the reservations does not drain the prefetch
         const int p = tid;
         const uint32_t h = p < a.np ? hist[p] : 0u;
-        uint32_t g = 0;
-        if (flat) { if (p < a.np) { g = sbase[p]; sbase[p] = g + h; } }   // the block's own cursor
-        else if (a.abl & 1) g = 0;                      // timing ablation only (FWA_PABL=1: wrong results)
-        else if (h) g = atomicAdd(&a.b_cnt[p * kSub + sub], h);
-        // the next tile in flight from here on (unconditional); EARLY: its first pairs were issued while classifying
-        if constexpr (EARLY) load_pairs(R, nx < tend ? nx : tile, EARLY, ITEMS / 2);
-        else load(R, nx < tend ? nx : tile);
+        const uint32_t g = h ? atomicAdd(&a.b_cnt[p * kSub + sub], h) : 0u;
+        load(R, nx < ntiles ? nx : tile);               // the next tile in flight from here on (unconditional)
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {               // the LDS scatter does not need the reservation: the
             if (r_pos[j] == ~0u) continue;              // reservation's latency overlaps this loop
@@ -1100,7 +810,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             // per (tile, overflowing partition) -- a per-wave reservation on the single spill counter
             // serialised ~100 K same-address device atomics per push under Zipf(1.1)
             const uint64_t end = (uint64_t)g + h;
-            if (!flat && end > (uint64_t)a.capb) {
+            if (end > (uint64_t)a.capb) {
                 const uint32_t ov = (uint32_t)(end - std::max<uint64_t>(g, (uint64_t)a.capb));
                 atomicAdd(&a.st->ovf_n, (int32_t)ov);
                 if constexpr (!PRE) sbase[p] = (uint32_t)atomicAdd(&a.st->spill_n, (int32_t)ov);
@@ -1118,9 +828,8 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
             const uint32_t p = valid ? s_part[sidx] : 0u;
             const uint32_t x = valid ? s_src[sidx] : 0u;
             const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
-            const bool inb = valid && dst < (uint64_t)(flat ? a.flat_cap : a.capb);
-            if (flat && valid && !inb) raise_error(a.st, FWA_E_STATE);   // cannot happen: sized by the histogram
-            else if (valid && !inb) {           // sub-bucket full (skewed keys)
+            const bool inb = valid && dst < (uint64_t)a.capb;
+            if (valid && !inb) {                // sub-bucket full (skewed keys)
                 if constexpr (PRE) {            // a merged entry has no record index to replay: apply it now
                     const int32_t slot = a.rel2slot[x_rel[x]];
                     if (slot >= 0)
@@ -1132,13 +841,9 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                 }
             }
             const uint64_t o = !inb ? a.trash + (uint64_t)(jj * THREADS + tid)
-                             : flat ? dst : ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
-            if constexpr (NW == 2)                       // 12-byte entry {key, value, slice}: one store
-                reinterpret_cast<uint3*>(a.b_key)[o] = make_uint3((uint32_t)x_key[x], (uint32_t)x_val[0][x], x_rel[x]);
-            else if constexpr (NW == 1) a.b_key[o] = x_key[x];    // packed at staging
-            else if constexpr (NW) a.b_key[o] = (x_key[x] & 0xffffffffull) | (x_val[0][x] << 32);
-            else a.b_key[o] = x_key[x];
-            if constexpr (NW != 2) a.b_rel[o] = x_rel[x];
+                                    : ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
+            a.b_key[o] = x_key[x];              // NW: packed at staging
+            a.b_rel[o] = x_rel[x];
             if constexpr (PRE) a.b_n[o] = (uint16_t)x_n[x];
             if (NV > 0 && !NW) a.b_val0[o] = x_val[0][x];
             if (NV > 1) a.b_val1[o] = x_val[NV > 1 ? 1 : 0][x];
@@ -1147,7 +852,7 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         __syncthreads();
         QMARK(4);
     };
-    for (; tile < tend; tile += tstep) step(ra, tile, tile + tstep);
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) step(ra, tile, tile + G);
     if (a.prof && tid == 0) for (int q = 0; q < 6; ++q) a.prof[(int64_t)blockIdx.x * 8 + q] = pacc[q];
 #undef QMARK
     for (int sh = 32; sh >= 1; sh >>= 1) {
@@ -1171,7 +876,6 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         }
 }
 
-
 struct CombineArgs {
     const unsigned long long* b_key;
     const unsigned long long* b_val0;
@@ -1185,11 +889,8 @@ struct CombineArgs {
     unsigned long long* key_table;
     unsigned long long* const* slot_base;
     int64_t stride;
-    int32_t abl;                       // ablation bits (timing experiments only)
     DevStatus* st;
-    long long* prof;                   // optional per-block phase cycle counters (FWA_APROF)
-    const uint32_t* flat_off;          // flat layout: partition p = [flat_off[p * G], flat_off[(p + 1) * G]), or nullptr
-    int32_t flat_g, pad_f;
+    long long* prof;                   // optional per-block phase cycle counters (FWA_OPT_PROFILE)
 };
 
 __device__ __forceinline__ unsigned long long ident_of(int acc_kind) { return acc_kind == ACC_MIN_ORD ? ~0ull : 0ull; }
@@ -1302,16 +1003,11 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         for (int i = tid; i < SL * seg; i += TH) lacc[(size_t)(cc - 1) * SL * seg + i] = id;
     }
     constexpr int64_t kChunk = (int64_t)IT * LPS;
-    const bool flat = a.flat_off != nullptr;
-    // sub-buckets: this wave's own list; flat layout: the partition's contiguous range, each chunk of
-    // kSub * kChunk entries split across the waves (all waves stay in the same stretch of event time)
-    const int64_t flo = flat ? (int64_t)a.flat_off[(int64_t)p * a.flat_g] : 0;
-    const int64_t flen = flat ? (int64_t)a.flat_off[(int64_t)(p + 1) * a.flat_g] - flo : 0;
-    const int64_t my_cnt = flat ? flen : min((int64_t)a.b_cnt[p * kSub + sub], a.capb);
-    const int64_t boff = flat ? flo : ((int64_t)p * kSub + sub) * a.capb;
+    // sub-buckets: this wave's own list
+    const int64_t my_cnt = min((int64_t)a.b_cnt[p * kSub + sub], a.capb);
+    const int64_t boff = ((int64_t)p * kSub + sub) * a.capb;
     int64_t cnt = 0;
-    if (flat) cnt = (flen + kSub * kChunk - 1) / (kSub * kChunk) * kChunk;
-    else for (int s2 = 0; s2 < kSub; ++s2) cnt = max(cnt, min((int64_t)a.b_cnt[p * kSub + s2], a.capb));
+    for (int s2 = 0; s2 < kSub; ++s2) cnt = max(cnt, min((int64_t)a.b_cnt[p * kSub + s2], a.capb));
     const gc_u64_ptr bk = (const gc_u64_ptr)(a.b_key + boff);
     const gc_u64_ptr bv0 = a.b_val0 ? (const gc_u64_ptr)(a.b_val0 + boff) : nullptr;
     const gc_u64_ptr bv1 = a.b_val1 ? (const gc_u64_ptr)(a.b_val1 + boff) : nullptr;
@@ -1378,22 +1074,12 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
     int nrel[IT];
     uint32_t nnn[IT];                   // PRE: records per entry
     auto load_chunk = [&](int64_t cb) {
-        const int64_t cbase = flat ? (cb / kChunk) * (kSub * kChunk) + sub * kChunk : cb;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
-            const int64_t i = cbase + (int64_t)j * LPS + li;
+            const int64_t i = cb + (int64_t)j * LPS + li;
             const bool ok = i < my_cnt;
             int r;
-            if constexpr (NW == 2) {                        // 12-byte entry {key, value, slice}: one load
-                uint3 q = make_uint3(0u, 0u, 0u);
-                if (ok) {
-                    const __attribute__((address_space(1))) uint32_t* qp =
-                        (const __attribute__((address_space(1))) uint32_t*)a.b_key + 3 * (boff + i);   // 12-byte entries
-                    q = make_uint3(qp[0], qp[1], qp[2]);
-                }
-                nkey[j] = (unsigned long long)q.x | ((unsigned long long)q.y << 32);
-                r = ok ? (int)q.z : -1;
-            } else if constexpr (NW) {                      // narrow entry (key | value << 32), unpacked at use
+            if constexpr (NW) {                             // narrow entry (key | value << 32), unpacked at use
                 nkey[j] = ok ? bk[i] : 0ull;
                 r = ok ? (int)br[i] : -1;
             } else {
@@ -1402,7 +1088,7 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
                 r = ok ? (int)br[i] : -1;
             }
             nx1[j] = (NV > 1 && ok) ? bv1[i] : 0ull;
-            nrel[j] = r == 0xFFFF ? -1 : r;                 // flat layout: a hole (record not accepted)
+            nrel[j] = r;
             nnn[j] = PRE ? (ok ? (uint32_t)bn[i] : 0u) : 1u;
         }
     };
@@ -1416,10 +1102,7 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         int rmin = 0x7fffffff, rmax = -1;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
-            if constexpr (NW == 3) {                        // 4-byte first column: raw bits, zero-extended
-                key[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)nkey[j];
-                x0[j] = nkey[j] >> 32;
-            } else if constexpr (NW) {
+            if constexpr (NW) {
                 key[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)nkey[j];
                 x0[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)(nkey[j] >> 32);
             } else {
@@ -1449,13 +1132,13 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         if (lo == 0x7fffffff) lo = cmin;
         if constexpr (MP) {
             if (cmin >= lo + SL) {          // the whole chunk is past the window: merge it out, jump to cmin
-                for (int r = lo; r < lo + SL; ++r) if (!(a.abl & 4)) flush(r);
+                for (int r = lo; r < lo + SL; ++r) flush(r);
                 if (a.prof) pacc[7] += 1000;
                 lo = cmin;
                 __syncthreads();
             }
         } else if (cmax >= lo + SL) {       // slide the window up to the chunk's newest slice
-            while (cmax >= lo + SL) { if (!(a.abl & 4)) flush(lo); ++lo; if (a.prof) pacc[7] += 1000; }
+            while (cmax >= lo + SL) { flush(lo); ++lo; if (a.prof) pacc[7] += 1000; }
             __syncthreads();
         }
         const int lo_c = lo;                // entries older than this are stragglers
@@ -1468,7 +1151,6 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
         for (int j = 0; j < IT; ++j) {
             loc[j] = -2;
             if (rel[j] < 0) continue;
-            if (a.abl & 1) { loc[j] = (int32_t)pos[j]; continue; }
             const unsigned long long kk = key[j];
             uint32_t b = pos[j] & ~(uint32_t)(kBucket - 1);
             int32_t found = -1;
@@ -1515,7 +1197,6 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
                     continue;
                 }
                 const int w = rel[j] & (SL - 1);
-                if (a.abl & 2) { if (x0[j] == 0x123456789ull) lcnt[0] = 1; continue; }
                 atomicAdd(&lcnt[w * seg + local], PRE ? nr[j] : 1u);
                 if constexpr (LAYOUT == 1) {
                     atomicAdd(&lacc[(size_t)w * seg + local], x0[j]);
@@ -1540,7 +1221,7 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
             __syncthreads();                // the window's adds done before it is merged out
             from = lo + SL;
             const int nl = min(lo + SL, cmax - SL + 1);
-            while (lo < nl) { if (!(a.abl & 4)) flush(lo); ++lo; if (a.prof) pacc[7] += 1000; }
+            while (lo < nl) { flush(lo); ++lo; if (a.prof) pacc[7] += 1000; }
             __syncthreads();                // merged and cleared before the next pass adds
         }
         PMARK(5);
@@ -1785,8 +1466,6 @@ struct FireSlideArgs {
     void* o_agg[FWA_MAX_AGGS];
     int64_t out_cap;                         // rows past it are counted, not written (host grows, relaunches)
     DevStatus* st;
-    int32_t abl;                             // timing ablation bits (0 in production)
-    unsigned long long* abl_ctr;             // ablation: 64 scratch counters (the push's want-set buffer)
 };
 
 // NA = the handle's accumulator count (compile time: the running sums and the next window's slice values stay in
@@ -1891,9 +1570,7 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
             uint32_t run = 0;
             for (int j = 0; j < kSlideJ; ++j)
                 for (int v = 0; v < kWaves; ++v) { const uint32_t t = woff[j][v]; woff[j][v] = run; run += t; }
-            // timing ablation only (FWA_FSABL=1: the reservation spread over 64 scratch counters -- wrong rows)
-            unsigned long long* ctr = f.abl ? f.abl_ctr + 16 * (blockIdx.x & 63) : &f.st->rows;
-            s_base = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
+            s_base = run ? atomicAdd(&f.st->rows, (unsigned long long)run) : 0ull;
         }
         __syncthreads();
         const int64_t ws = f.start0 + (int64_t)w * f.slide;
@@ -2440,28 +2117,6 @@ __global__ void __launch_bounds__(kBlock) sess3_min_kernel(Sess2Args a) {
     }
 }
 
-// Row buckets: a record's packed row goes to the region of its key's hash bucket (the top `bb` bits of mix64(key), i.e.
-// the top bits of its kid: kid = segment << seg_log | offset, segment = top part_bits of the hash), so that the segment
-// walk, which visits the rows in kid order, gathers from a few MB of rows at a time instead of the whole batch.
-constexpr int kRowBucketBits = 6;
-__device__ __forceinline__ uint32_t row_bucket(int64_t key, int bb) {
-    if ((uint64_t)key == kEmptyKey) return 1u << bb;               // the side slot (kid = capacity) sorts last
-    return bb ? (uint32_t)(jm::mix64((uint64_t)key) >> (64 - bb)) : 0u;
-}
-
-// Per block (a contiguous chunk of `chunk` records): row count per bucket, stored bucket-major (hist[bucket * G + b]).
-__global__ void __launch_bounds__(kBlock) sess3_hist_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t chunk,
-                                                           int bb, uint32_t* hist) {
-    __shared__ uint32_t h[(1 << kRowBucketBits) + 1];
-    const int nbk = (1 << bb) + 1;
-    for (int i = threadIdx.x; i < nbk; i += blockDim.x) h[i] = 0u;
-    __syncthreads();
-    const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(n, r0 + chunk);
-    for (int64_t t = r0 + threadIdx.x; t < r1; t += blockDim.x) atomicAdd(&h[row_bucket(keys[t], bb)], 1u);
-    __syncthreads();
-    for (int i = threadIdx.x; i < nbk; i += blockDim.x) hist[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
-}
-
 // Probe of the key's first 8-slot bucket (one 64-byte read); -1 when the key is not there (then key_slot, which also
 // inserts). Loads only: the caller issues several before using any.
 __device__ __forceinline__ int64_t key_probe8(const unsigned long long* table, int seg_log, int part_bits, int64_t key,
@@ -2485,17 +2140,13 @@ __device__ __forceinline__ int64_t key_probe8_find(const ulonglong2 (&bk)[4], ui
     return r;
 }
 
-// Records: block b routes its chunk [b * chunk, (b + 1) * chunk) (the chunks of sess3_hist_kernel): key-group check,
-// kid (U records' bucket probes in flight at once), 32-bit cell key and payload (the row position) at the record's
-// input position, and the packed row [ts, acc_1 .. acc_{nacc-1}] (COUNT is 1 for a record) in its bucket's region.
+// Records: block b routes its chunk [b * chunk, (b + 1) * chunk): key-group check, kid (U records' bucket probes in
+// flight at once), 32-bit cell key and payload (the row position) at the record's input position, and the packed row
+// [ts, acc_1 .. acc_{nacc-1}] (COUNT is 1 for a record) at the same position.
 template <int U>
-__global__ void __launch_bounds__(kBlock) sess3_route_kernel(Sess2Args a, const EngineConst* __restrict__ cp,
-                                                            const uint32_t* __restrict__ off, int64_t chunk, int bb) {
-    __shared__ uint32_t cur[(1 << kRowBucketBits) + 1];
+__global__ void __launch_bounds__(kBlock) sess3_route_kernel(Sess2Args a, const EngineConst* __restrict__ cp, int64_t chunk) {
     __shared__ uint32_t s_c[2];
     const EngineConst& c = *cp;
-    const int nbk = (1 << bb) + 1;
-    if (off) for (int i = threadIdx.x; i < nbk; i += blockDim.x) cur[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
     if (threadIdx.x == 0) { s_c[0] = 0u; s_c[1] = 0u; }
     __syncthreads();
     const int cb = a.tb;
@@ -2542,7 +2193,7 @@ __global__ void __launch_bounds__(kBlock) sess3_route_kernel(Sess2Args a, const 
             }
             uint32_t pos = 0u;
             if (k32 != kCellSent) {
-                pos = off ? atomicAdd(&cur[row_bucket(key[u], bb)], 1u) : (uint32_t)t;
+                pos = (uint32_t)t;
                 unsigned long long* row = a.pk + (int64_t)pos * a.pkw;
                 const int64_t tsu = ts[u];
                 auto word = [&](int cc) -> unsigned long long {
@@ -3391,13 +3042,9 @@ struct fwa_engine {
     int64_t* d_send2 = nullptr;
     unsigned long long* d_spk = nullptr;   // session bulk rows (Sess2Args::pk)
     void* d_sg = nullptr;                  // segment kernel staging (Sess2Args::sg_*)
-    uint32_t* d_flat = nullptr;            // flat Phase P layout: (partition, block) counts | their exclusive sum
-    int64_t flat_cap = 0;
     int64_t sg_cap = 0, sgw_cap = 0;
     int32_t cell_skip = 0;
     bool narrow = true, narrow_used = false;   // Phase P / A narrow bucket entries (sticky off after a wide push)
-    uint32_t* d_rh = nullptr;       // sessions cell path: per-block row-bucket counts and their exclusive sum
-    int64_t rh_cap = 0;          // sessions: pushes left before the cell path is tried again after a redo
     int64_t* d_spe = nullptr;
     int64_t* d_smax = nullptr;
     uint32_t* d_scid = nullptr;
@@ -3417,6 +3064,12 @@ struct fwa_engine {
     // FWA_CFG_RECORD_LISTS: TUMBLE window state as hash-partitioned record lists, aggregated at fire (sparse.inc)
     bool sparse = false;
     SpState* sp = nullptr;
+    // per-handle options (fwa_set_option; the defaults are the production behaviour)
+    int32_t opt_pre = -1, opt_mp = -1, opt_narrow = -1, opt_cells = -1;   // -1 adaptive, 0 never, 1 always
+    int64_t opt_out_min = 0;
+    bool opt_partials_v1 = false;
+    int32_t opt_profile = 0;
+    long long* d_prof = nullptr;          // FWA_OPT_PROFILE: per-block phase cycle counters of Phase P / A
 };
 
 namespace {
@@ -3841,7 +3494,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_flat, e->d_rh};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -3913,7 +3566,7 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         int share = -1;   // same accumulator kind over the same input column and input type: one column
         for (int i = 0; i < j && share < 0; ++i)
             if (c.agg[i].acc > 0 && !c.agg[i].alias && c.agg[i].acc_kind == d.acc_kind && c.agg[i].col == d.col &&
-                input_class(c.agg[i].kind) == input_class(d.kind) && !getenv("FWA_NO_ACC_SHARE"))
+                input_class(c.agg[i].kind) == input_class(d.kind))
                 share = i;
         if (share >= 0) { d.acc = c.agg[share].acc; d.alias = 1; continue; }
         d.acc = c.nacc;
@@ -3950,9 +3603,7 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         const int64_t kc0 = cfg->key_capacity > 0 ? cfg->key_capacity : (1 << 20);
         int cap_log = 10;
         while (((int64_t)1 << cap_log) < 2 * kc0) ++cap_log;
-        int seg_log = 12;
-        if (const char* sv = getenv("FWA_SEG_LOG")) seg_log = atoi(sv);
-        seg_log = std::max(6, std::min(seg_log, cap_log));
+        int seg_log = std::max(6, std::min(12, cap_log));
         e->seg_log = seg_log;
         e->part_bits = cap_log - seg_log;
         int cols[2] = {-1, -1}, sizes[2] = {8, 8}, nv = 0;
@@ -3980,7 +3631,7 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
             return sgz * 8 + 2 * sgz * 4 + (int64_t)(c.nacc - 1) * 2 * sgz * 8 + 4 * 4 * kSub + 16 +
                    (int64_t)sizeof(StragL) * kStragL + 256;   // + static LDS (straggler list, descriptors)
         };
-        while (!getenv("FWA_SEG_LOG") && seg_log > 9 && lds_need(seg_log) > 160 * 1024 &&
+        while (seg_log > 9 && lds_need(seg_log) > 160 * 1024 &&
                ((int64_t)1 << (cap_log - seg_log + 1)) <= kMaxPart)
             --seg_log;
         e->seg_log = seg_log;
@@ -3989,15 +3640,12 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         const int64_t bps = 4 + 8 * (int64_t)(c.nacc - 1);
         const int64_t avail = 160 * 1024 - 512 - (int64_t)sizeof(StragL) * kStragL - seg * 8;
         int sl = (int)std::min<int64_t>(8, avail > 0 ? avail / (bps * seg) : 0);
-        if (const char* sv = getenv("FWA_SL")) sl = std::min(sl, atoi(sv));
         if (lds_need(seg_log) > 160 * 1024) sl = 0;
         const int64_t np = (int64_t)1 << e->part_bits;
-        const char* force = getenv("FWA_INGEST");
-        // record lists (sparse.inc): asked for, or a key space of >= 2^25 keys (FWA_SPARSE=0 / 1 overrides)
-        bool want_sp = (cfg->flags & FWA_CFG_RECORD_LISTS) || kc0 >= ((int64_t)1 << 25);
-        if (const char* fs = getenv("FWA_SPARSE")) want_sp = atoi(fs) != 0;
+        // record lists (sparse.inc): asked for, or a key space of >= 2^25 keys
+        const bool want_sp = (cfg->flags & FWA_CFG_RECORD_LISTS) || kc0 >= ((int64_t)1 << 25);
         e->sparse = want_sp && sp_eligible(cfg);
-        ok = ok && np <= kMaxPart && sl >= 2 && !(force && !strcmp(force, "v1")) && e->kind != FWA_SESSION && !e->sparse;
+        ok = ok && np <= kMaxPart && sl >= 2 && e->kind != FWA_SESSION && !e->sparse;
         e->v2 = ok;
         if (ok) {
             e->np = (int32_t)np;
@@ -4165,6 +3813,30 @@ static int ensure_v2_buffers(fwa_engine* e, int64_t n, bool need_bn) {
     return FWA_OK;
 }
 
+// FWA_OPT_PROFILE: wait for a profiled kernel (events a, b) and print its per-block phase cycle counters (average
+// over the nb blocks and the slowest block): Phase P marks 6 phases, Phase A 8.
+static int print_phase_profile(fwa_engine* e, const char* tag, hipEvent_t a, hipEvent_t b, int nb, int nph) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, a, b));
+    std::vector<long long> hp(8 * (size_t)nb);
+    HIPCHK(e, hipMemcpy(hp.data(), e->d_prof, sizeof(long long) * 8 * nb, hipMemcpyDeviceToHost));
+    double tot[8] = {0};
+    int bmax = 0;
+    long long bsum_max = -1;
+    for (int blk = 0; blk < nb; ++blk) {
+        long long bs = 0;
+        for (int k = 0; k < nph; ++k) { tot[k] += (double)hp[blk * 8 + k] / nb; bs += hp[blk * 8 + k]; }
+        if (bs > bsum_max) { bsum_max = bs; bmax = blk; }
+    }
+    fprintf(stderr, "[%s] kernel %.3f ms; per-block avg cycles:", tag, ms);
+    for (int k = 0; k < nph; ++k) fprintf(stderr, " %.0f", tot[k]);
+    fprintf(stderr, " | slowest block %d:", bmax);
+    for (int k = 0; k < nph; ++k) fprintf(stderr, " %lld", hp[bmax * 8 + k]);
+    fprintf(stderr, "\n");
+    return FWA_OK;
+}
+
 // Two-phase ingest. Sets *ran = false (and leaves no state change besides key insertions) when the
 // batch must take the v1 path instead (bucket overflow on skewed keys).
 static int ensure_sort_tmp(fwa_engine* e, size_t bytes);
@@ -4177,13 +3849,11 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         for (int j = 0; j < e->cfg.num_aggs; ++j)
             if (e->ec.agg[j].acc == 1 && e->ec.agg[j].vslot == 0) layout = 1;
     }
-    static const int pre_env = getenv("FWA_PRE") ? atoi(getenv("FWA_PRE")) : -1;   // A/B: 0 never, 1 always
     const bool pre_ok = (layout == 2 && e->nv == 0) || (layout == 1 && e->nv == 1 && e->vsize[0] == 8);
     // partial accumulators (fwa_push_partials): the PRE buckets carry each row's record count, the value
     // column is the partial BIGINT sum; other aggregate lists keep the v1 path
-    if (a.pcount && (!pre_ok || e->cfg.nullable_cols || getenv("FWA_P2") != nullptr || getenv("FWA_PARTIALS_V1") != nullptr))
-        return FWA_OK;
-    const bool pre = a.pcount || (pre_ok && pre_env != 0 && (pre_env == 1 || e->pre) && getenv("FWA_P2") == nullptr);
+    if (a.pcount && (!pre_ok || e->cfg.nullable_cols || e->opt_partials_v1)) return FWA_OK;
+    const bool pre = a.pcount || (pre_ok && e->opt_pre != 0 && (e->opt_pre == 1 || e->pre));
     int rc = ensure_v2_buffers(e, a.n, pre);
     if (rc) return rc;
     const int64_t q_base = e->live.empty() ? 0 : e->live.begin()->first;
@@ -4263,76 +3933,29 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.dropidx = a.pcount ? nullptr : a.dropidx;   // partial rows: no record indices (as in v1)
     for (int c = 0; c < FWA_MAX_COLS; ++c) { pa.nulls[c] = a.nulls[c]; pa.any_null |= a.nulls[c] != nullptr; }
     pa.st = e->d_st;
-    static const int pabl = getenv("FWA_PABL") ? atoi(getenv("FWA_PABL")) : 0;
-    pa.abl = pabl;
-    static const int pprof = getenv("FWA_PPROF") ? atoi(getenv("FWA_PPROF")) : 0;
-    static long long* d_pprof = nullptr;
-    if (pprof && !d_pprof) HIPCHK(e, hipMalloc(&d_pprof, sizeof(long long) * 8 * 1024));
-    pa.prof = pprof ? d_pprof : nullptr;
+    if (e->opt_profile && !e->d_prof) HIPCHK(e, hipMalloc(&e->d_prof, sizeof(long long) * 8 * kMaxPart));
+    pa.prof = e->opt_profile ? e->d_prof : nullptr;
     HIPCHK(e, hipEventRecord(e->ev[4], e->stream));
-    int threads = 1024;
+    const int threads = 1024;
     const int items = e->nv == 2 ? 4 : (e->nv == 1 ? 6 : 8);
     const int64_t tile = (int64_t)items * threads;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256));
     const int vw = (e->vsize[0] == 8 ? 1 : 0) | (e->vsize[1] == 8 ? 2 : 0);
-    static const bool p2 = getenv("FWA_P2") != nullptr;   // A/B switch: the r01 Phase P kernel
-    const bool kg_all = e->cfg.kg_start == 0 && e->cfg.kg_end == e->cfg.max_parallelism - 1;
+    // ownership is checked per record unless the handle owns every key group; dictionary ids always (their key group
+    // may be past max_parallelism: key group -1, rejected with FWA_E_KEYGROUP)
+    const bool kg_all = e->cfg.kg_start == 0 && e->cfg.kg_end == e->cfg.max_parallelism - 1 &&
+                        e->cfg.key_kind != FWA_KEY_GROUP_PREFIXED;
     const int kgm = kg_all ? 0 : (e->cfg.key_kind == FWA_KEY_PREHASHED ? 2 : 1);
-    static const bool now16 = getenv("FWA_NOW16") != nullptr;  // A/B switch: 8-byte Phase P loads
-    static const int pdb = getenv("FWA_PDB") ? atoi(getenv("FWA_PDB")) : 0;   // A/B: next-tile pairs issued in classify
     auto al16 = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; };
-    const bool w16 = !now16 && !p2 && kgm == 0 && al16(pa.keys) && al16(pa.ts) &&
+    const bool w16 = kgm == 0 && al16(pa.keys) && al16(pa.ts) &&
                      (e->nv == 0 || ((uintptr_t)pa.cols[pa.vcol[0]] & ((e->vsize[0] == 8) ? 15 : 7)) == 0);
-    // flat bucket layout (part_hist_kernel, then reservation-free Phase P): an A/B option, off by default -- measured
-    // slower on C2 (Phase P 1.30 vs 0.81 ms: 512 open runs per block leave partial lines in L2)
-    static const int flat_env = getenv("FWA_FLAT") ? atoi(getenv("FWA_FLAT")) : 0;     // A/B: 1 = flat layout
-    const bool flat = flat_env != 0 && !pre && !p2;
     // narrow bucket entries (partition3 / combine3 NW): COUNT + one BIGINT SUM over an 8-byte column, the paired-load
     // kernel; on by default until a push finds more than 1/64 of its records needing 64-bit keys or values
-    const char* narrow_s = getenv("FWA_NARROW");                  // A/B: 0 never, 1 always (read per push)
-    const int narrow_env = narrow_s ? atoi(narrow_s) : -1;
-    const bool narrow = narrow_env != 0 && (narrow_env == 1 || e->narrow) && layout == 1 && e->nv == 1 && (vw & 1) &&
-                        w16 && !pre && !flat && !p2 && pdb == 0 && !a.pcount;
-    // NW 3: a 4-byte first value column (C5's FLOAT) packed with the 32-bit key, generic accumulator layout
-    // (opt-in, FWA_NARROW3=1: measured 2-6 % slower on C5, whose Phase P is bound by 4-record partition runs)
-    const char* n3_s = getenv("FWA_NARROW3");
-    const bool narrow3 = n3_s && atoi(n3_s) != 0 && narrow_env != 0 && (narrow_env == 1 || e->narrow) && e->nv == 2 &&
-                         vw == 2 && layout == 0 && kgm == 0 && !pre && !flat && !p2 && !a.pcount;
-    e->narrow_used = narrow || narrow3;
-    static const bool nitems8 = getenv("FWA_NITEMS8") && atoi(getenv("FWA_NITEMS8")) != 0;   // A/B: 8192-record tiles
-    const int grid8 = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + 8191) / 8192, 256));
-    const char* n12_s = getenv("FWA_NARROW12");                   // A/B: 12-byte AoS entries (one store / load each)
-    const bool n12 = n12_s && atoi(n12_s) != 0;
-    if (flat) {
-        const int64_t ntiles = (a.n + tile - 1) / tile;
-        const int64_t tpb = (ntiles + grid - 1) / grid;
-        const int64_t ncnt = (int64_t)e->np * grid + 1;
-        if (ncnt > e->flat_cap) {
-            if (e->d_flat) HIPCHK(e, hipFree(e->d_flat));
-            e->d_flat = nullptr;
-            e->flat_cap = std::max<int64_t>(ncnt, (int64_t)kMaxPart * 256 + 1);
-            HIPCHK(e, hipMalloc(&e->d_flat, 2 * sizeof(uint32_t) * (size_t)e->flat_cap));
-        }
-        uint32_t* cnts = e->d_flat;
-        uint32_t* offs = e->d_flat + e->flat_cap;
-        const bool w16k = w16 && e->nv == 1;          // the paired-load kernel below (it leaves an odd n's last record
-        part_hist_kernel<<<grid, 1024, 0, e->stream>>>(pa.keys, a.n, tile, tpb, e->part_bits, e->np,   // to the replay)
-                                                       (w16k && (a.n & 1)) ? 1 : 0, cnts);
-        HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipMemsetAsync(cnts + ncnt - 1, 0, 4, e->stream));
-        size_t bytes = 0;
-        HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnts, offs, (int)ncnt, e->stream));
-        if (int rc2 = ensure_sort_tmp(e, bytes)) return rc2;
-        bytes = e->sort_tmp_bytes;
-        HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(e->d_sort_tmp, bytes, cnts, offs, (int)ncnt, e->stream));
-        flat_skew_kernel<<<1, 1024, 0, e->stream>>>(offs, e->np, grid, e->capb * kSub, e->d_st);
-        HIPCHK(e, hipGetLastError());
-        pa.flat_off = offs;
-        pa.tpb = tpb;
-        pa.flat_cap = e->capb * e->np * kSub;
-    }
-#define P2LAUNCH(NV, IT, VW) do { if (p2) partition2_kernel<NV, IT, 1024, 1, VW><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
-        else if (kgm == 0) partition3_kernel<NV, IT, 1024, VW, 0><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
+    const bool narrow = e->opt_narrow != 0 && (e->opt_narrow == 1 || e->narrow) && layout == 1 && e->nv == 1 &&
+                        (vw & 1) && w16 && !pre && !a.pcount;
+    e->narrow_used = narrow;
+#define P3LAUNCH(NV, IT, VW) do { \
+        if (kgm == 0) partition3_kernel<NV, IT, 1024, VW, 0><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else if (kgm == 1) partition3_kernel<NV, IT, 1024, VW, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else partition3_kernel<NV, IT, 1024, VW, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
 #define PRELAUNCH(NV) do { const int gp = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + 4095) / 4096, 256)); \
@@ -4340,33 +3963,20 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else if (kgm == 1) partition3_kernel<NV, 4, 1024, 3, 1, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else partition3_kernel<NV, 4, 1024, 3, 2, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
     if (pre) { if (e->nv == 0) PRELAUNCH(0); else PRELAUNCH(1); }
-    else if (e->nv == 0) P2LAUNCH(0, 8, 3);
-    else if (e->nv == 1 && w16 && (vw & 1) && pdb == 1) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
-    else if (e->nv == 1 && w16 && (vw & 1) && pdb == 2) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
-    else if (e->nv == 1 && w16 && (vw & 1) && pdb == 3) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 3><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
-    else if (e->nv == 1 && w16 && (vw & 1) && narrow && n12) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 0, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
-    else if (e->nv == 1 && w16 && (vw & 1) && narrow && nitems8) partition3_kernel<1, 8, 1024, 3, 0, 0, 1, 0, 1><<<grid8, 1024, 0, e->stream>>>(pa, e->d_ec);
-    else if (e->nv == 1 && w16 && (vw & 1) && narrow) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
+    else if (e->nv == 0) P3LAUNCH(0, 8, 3);
+    else if (narrow) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
-    else if (e->nv == 1) { if (vw & 1) P2LAUNCH(1, 6, 3); else P2LAUNCH(1, 6, 2); }
-    else if (narrow3) partition3_kernel<2, 4, 1024, 2, 0, 0, 0, 0, 3><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
-    else if (vw == 3) P2LAUNCH(2, 4, 3); else if (vw == 2) P2LAUNCH(2, 4, 2);
-    else if (vw == 1) P2LAUNCH(2, 4, 1); else P2LAUNCH(2, 4, 0);
-#undef P2LAUNCH
+    else if (e->nv == 1) { if (vw & 1) P3LAUNCH(1, 6, 3); else P3LAUNCH(1, 6, 2); }
+    else if (vw == 3) P3LAUNCH(2, 4, 3); else if (vw == 2) P3LAUNCH(2, 4, 2);
+    else if (vw == 1) P3LAUNCH(2, 4, 1); else P3LAUNCH(2, 4, 0);
+#undef P3LAUNCH
 #undef PRELAUNCH
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[5], e->stream));
-    if (pprof) {
-        HIPCHK(e, hipStreamSynchronize(e->stream));
-        float ms = 0.f;
-        HIPCHK(e, hipEventElapsedTime(&ms, e->ev[4], e->ev[5]));
-        std::vector<long long> hp(8 * grid);
-        HIPCHK(e, hipMemcpy(hp.data(), d_pprof, sizeof(long long) * 8 * grid, hipMemcpyDeviceToHost));
-        double tot[6] = {0};
-        for (int b = 0; b < grid; ++b) for (int k = 0; k < 6; ++k) tot[k] += (double)hp[b * 8 + k] / grid;
-        fprintf(stderr, "[pprof] kernel %.3f ms; per-block avg cycles: classify %.0f scan %.0f scatter %.0f store %.0f endbar %.0f topbar %.0f\n",
-                ms, tot[0], tot[1], tot[2], tot[3], tot[4], tot[5]);
+    if (e->opt_profile) {
+        int rc2 = print_phase_profile(e, "pprof", e->ev[4], e->ev[5], grid, 6);
+        if (rc2) return rc2;
     }
     // no host round trip between the phases: Phase P marks touched slots itself, spills bucket
     // overflow to the v1 replay list, and the combiner applies stragglers in place
@@ -4387,19 +3997,11 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.slot_base = e->d_slot_base;
     ca.stride = e->stride;
     ca.st = e->d_st;
-    ca.flat_off = pa.flat_off;
-    ca.flat_g = grid;
-    static const int aabl = getenv("FWA_AABL") ? atoi(getenv("FWA_AABL")) : 0;
-    ca.abl = aabl;
-    static const int aprof = getenv("FWA_APROF") ? atoi(getenv("FWA_APROF")) : 0;
-    static long long* d_prof = nullptr;
-    if (aprof && !d_prof) HIPCHK(e, hipMalloc(&d_prof, sizeof(long long) * 8 * kMaxPart));
-    ca.prof = aprof ? d_prof : nullptr;
+    ca.prof = pa.prof;
     HIPCHK(e, hipEventRecord(e->ev[6], e->stream));
     const size_t seg3 = (size_t)1 << e->seg_log;
     const size_t lds3 = seg3 * 8 + 2 * seg3 * 4 + (size_t)(e->nacc - 1) * 2 * seg3 * 8 + 4 * 4 * kSub + 16;
-    static const int mp_env = getenv("FWA_MP") ? atoi(getenv("FWA_MP")) : -1;      // A/B: 0 never, 1 always
-    const bool mp = mp_env == 1 || (mp_env != 0 && e->mp);
+    const bool mp = e->opt_mp == 1 || (e->opt_mp != 0 && e->mp);
 #define C3M(IT, TH, NV, LY, PR) do { if (mp) combine3_kernel<IT, 2, NV, TH, LY, PR, 1><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); \
         else combine3_kernel<IT, 2, NV, TH, LY, PR, 0><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); } while (0)
 #define C3L(IT, TH, NV) do { \
@@ -4408,46 +4010,20 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else if (layout == 1) C3M(IT, TH, NV, 1, 0); \
         else if (layout == 2) C3M(IT, TH, NV, 2, 0); \
         else C3M(IT, TH, NV, 0, 0); } while (0)
-    static const int nit_env = getenv("FWA_NIT") ? atoi(getenv("FWA_NIT")) : 8;   // A/B: entries per lane and chunk (8: measured best)
-    if (narrow) {
-        if (mp && n12) combine3_kernel<4, 2, 1, 1024, 1, 0, 1, 2><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-        else if (mp) combine3_kernel<4, 2, 1, 1024, 1, 0, 1, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-        else if (n12) combine3_kernel<8, 2, 1, 1024, 1, 0, 0, 2><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-        else if (nit_env == 8) combine3_kernel<8, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-        else if (nit_env == 6) combine3_kernel<6, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-        else combine3_kernel<4, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-    } else if (narrow3) {
-        static const int nit3 = getenv("FWA_NIT3") ? atoi(getenv("FWA_NIT3")) : 4;   // A/B: entries per lane and chunk
-        if (mp) combine3_kernel<4, 2, 2, 1024, 0, 0, 1, 3><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-        else if (nit3 == 8) combine3_kernel<8, 2, 2, 1024, 0, 0, 0, 3><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-        else combine3_kernel<4, 2, 2, 1024, 0, 0, 0, 3><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+    if (narrow) {   // packed entries free the prefetch registers: 8 entries per lane and chunk (4 with window passes)
+        if (mp) combine3_kernel<4, 2, 1, 1024, 1, 0, 1, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        else combine3_kernel<8, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
     } else if (e->nv == 0) C3L(4, 1024, 0);
     else if (e->nv == 1) C3L(4, 1024, 1);
     else C3L(4, 1024, 2);
 #undef C3L
 #undef C3M
-
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[7], e->stream));
     e->v2_timing_pending = true;
-    if (aprof) {
-        HIPCHK(e, hipStreamSynchronize(e->stream));
-        float ms = 0.f;
-        HIPCHK(e, hipEventElapsedTime(&ms, e->ev[6], e->ev[7]));
-        std::vector<long long> hp(8 * e->np);
-        HIPCHK(e, hipMemcpy(hp.data(), d_prof, sizeof(long long) * 8 * e->np, hipMemcpyDeviceToHost));
-        double tot[8] = {0}, mx[8] = {0};
-        int bmax = 0;
-        long long bsum_max = 0;
-        for (int b = 0; b < e->np; ++b) {
-            long long bs = 0;
-            for (int k = 0; k < 8; ++k) { tot[k] += (double)hp[b * 8 + k] / e->np; if (k < 6) bs += hp[b * 8 + k]; }
-            if (bs > bsum_max) { bsum_max = bs; bmax = b; }
-        }
-        for (int k = 0; k < 8; ++k) mx[k] = (double)hp[bmax * 8 + k];
-        fprintf(stderr, "[aprof] kernel %.3f ms; per-block avg cycles: %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f | slowest block %d: %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n",
-                ms, tot[0], tot[1], tot[2], tot[3], tot[4], tot[5], tot[6], tot[7], bmax,
-                mx[0], mx[1], mx[2], mx[3], mx[4], mx[5], mx[6], mx[7]);
+    if (e->opt_profile) {
+        int rc2 = print_phase_profile(e, "aprof", e->ev[6], e->ev[7], e->np, 8);
+        if (rc2) return rc2;
     }
     e->ingest_launches++;
     e->ingest_records += a.n;
@@ -4622,13 +4198,10 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     s.ctr = e->d_sctr;
     s.dropidx = a.dropidx;
     s.st = e->d_st;
-    static const bool scan_path = getenv("FWA_SESS_SCAN") != nullptr;   // A/B: the r02 multi-pass bulk path
     // cell path (sess3_*): fixed gap, 32-bit cell keys; redone on the general path below when a record is not
     // order-free or a start falls outside the cell range (then not tried again for 8 pushes)
-    const char* cell_s = getenv("FWA_SESS_CELL");         // A/B switch, read per push (tests toggle it)
-    const int cell_env = cell_s ? atoi(cell_s) : 1;
     const int cb = 32 - e->kid_bits;
-    if (cell_env != 0 && !s.gapc && cb >= 1 && e->nacc <= 5 && !scan_path && n > 0 && e->cell_skip <= 0 &&
+    if (e->opt_cells != 0 && !s.gapc && cb >= 1 && e->nacc <= 5 && n > 0 && e->cell_skip <= 0 &&
         n + n_in < ((int64_t)1 << 31)) {
         Sess2Args t = s;
         t.tb = cb;
@@ -4641,34 +4214,12 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
         t.seg_out = 1;
         HIPCHK(e, hipEventRecord(e->ev[0], e->stream));
         sess3_min_kernel<<<grid_for(n + n_in, 1024), kBlock, 0, e->stream>>>(t);
-        const int bb = std::min<int>(e->part_bits, kRowBucketBits);
-        const int nbk = (1 << bb) + 1;
         const int G = (int)std::max<int64_t>(1, std::min<int64_t>(8192, (n + 2047) / 2048));   // >= 32 waves per CU (latency-bound probes)
         const int64_t chunk = ((n + G - 1) / G + 255) / 256 * 256;
-        const int64_t nh = (int64_t)nbk * G;
-        if (nh + 1 > e->rh_cap) {
-            HIPCHK(e, hipStreamSynchronize(e->stream));
-            if (e->d_rh) HIPCHK(e, hipFree(e->d_rh));
-            e->d_rh = nullptr;
-            e->rh_cap = nh + 1;
-            HIPCHK(e, hipMalloc(&e->d_rh, 2 * sizeof(uint32_t) * (size_t)e->rh_cap));
-        }
-        uint32_t* rh = e->d_rh;
-        uint32_t* roff = nullptr;                         // rows at the input position unless bucketed (A/B: FWA_ROWB=1)
-        size_t bytes = 0;
-        if (getenv("FWA_ROWB") && atoi(getenv("FWA_ROWB")) != 0) {
-            roff = e->d_rh + e->rh_cap;
-            sess3_hist_kernel<<<G, kBlock, 0, e->stream>>>(t.keys, n, chunk, bb, rh);
-            HIPCHK(e, hipGetLastError());
-            HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, rh, roff, (int)nh, e->stream));
-            if ((rc = ensure_sort_tmp(e, bytes))) return rc;
-            bytes = e->sort_tmp_bytes;
-            HIPCHK(e, hipcub::DeviceScan::ExclusiveSum(e->d_sort_tmp, bytes, rh, roff, (int)nh, e->stream));
-        }
-        sess3_route_kernel<2><<<G, kBlock, 0, e->stream>>>(t, e->d_ec, roff, chunk, bb);
+        sess3_route_kernel<2><<<G, kBlock, 0, e->stream>>>(t, e->d_ec, chunk);
         if (n_in > 0) sess3_route_sessions_kernel<<<grid_for(n_in, 256 * 16), kBlock, 0, e->stream>>>(t);
         HIPCHK(e, hipGetLastError());
-        bytes = 0;
+        size_t bytes = 0;
         const uint32_t* k0 = (const uint32_t*)e->d_skey[0];
         uint32_t* k1 = (uint32_t*)e->d_skey[1];
         HIPCHK(e, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k0, k1, (const uint32_t*)e->d_sval[0], e->d_sval[1],
@@ -4683,10 +4234,6 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
         HIPCHK(e, hipEventRecord(e->ev[1], e->stream));
         if ((rc = read_sess_ctr(e))) return rc;
         if (e->h_st->error) return FWA_OK;                // reported by the caller
-        if (getenv("FWA_DEBUG_CELL"))
-            fprintf(stderr, "[cell] n %lld n_in %lld kid_bits %d cb %d base %lld special %llu redo %llu out %llu\n",
-                    (long long)n, (long long)n_in, e->kid_bits, cb, (long long)jm::unord_i64(e->h_sctr->ts_min),
-                    e->h_sctr->n_special, e->h_sctr->n_redo, e->h_sctr->n_out_sp);
         if (e->h_sctr->n_special == 0 && e->h_sctr->n_redo == 0) {
             if ((rc = account_ingest(e))) return rc;
             e->ingest_launches++;
@@ -4753,7 +4300,7 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
         s.bkey = e->d_skey[1];
         s.bval = e->d_sval[1];
     }
-    s.seg_out = (!scan_path && e->nacc <= 5) ? 1 : 0;
+    s.seg_out = e->nacc <= 5 ? 1 : 0;
     if (nb > 0 && s.seg_out) {
         if ((rc = launch_segments(e, s, nb, false))) return rc;
     } else if (nb > 0) {
@@ -4905,8 +4452,7 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     // window holds far fewer rows. Start from min(bound, max(current capacity, 4M rows)); the kernel
     // counts rows past the capacity without writing them, and the host grows once and relaunches.
     const int64_t bound = (int64_t)hw.size() * nkeys + row0;
-    const char* om = getenv("FWA_OUT_MIN");   // first-sizing floor in rows (tests force the relaunch)
-    const int64_t floor_rows = om ? std::max<int64_t>(1, atoll(om)) : ((int64_t)1 << 22);
+    const int64_t floor_rows = e->opt_out_min > 0 ? e->opt_out_min : ((int64_t)1 << 22);   // tests force the relaunch
     rc = ensure_out(e, std::min<int64_t>(bound, std::max<int64_t>(e->out_cap, floor_rows + row0)));
     if (rc) return rc;
   relaunch:
@@ -5483,6 +5029,7 @@ static int snapshot_sessions(fwa_engine* e, fwa_blob* out) {
     for (int64_t i = 0; i < n; ++i) {
         key[i] = (int64_t)kid[i] < e->capacity ? (int64_t)table[kid[i]] : LONG_MIN_J;
         kg[i] = jm::key_group_of(key[i], e->cfg.key_kind, 0, maxp);
+        if (kg[i] < 0) return fail(e, FWA_E_STATE, "state holds a key outside every key group");
         off[kg[i] + 1]++;
     }
     for (int g = 0; g < maxp; ++g) off[g + 1] += off[g];
@@ -5637,6 +5184,7 @@ int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
     std::vector<int64_t> off((size_t)maxp + 1, 0);
     for (int64_t i = 0; i < n; ++i) {
         kg[i] = jm::key_group_of(cols[i], e->cfg.key_kind, 0, maxp);
+        if (kg[i] < 0) return fail(e, FWA_E_STATE, "state holds a key outside every key group");
         off[kg[i] + 1]++;
     }
     for (int g = 0; g < maxp; ++g) off[g + 1] += off[g];
@@ -5771,9 +5319,6 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
     f.out_cap = e->out_cap;
     f.st = e->d_st;
-    static const int fsabl = getenv("FWA_FSABL") ? atoi(getenv("FWA_FSABL")) : 0;   // timing ablation (wrong rows)
-    f.abl = fsabl && e->d_want && kWantCap >= 1024 ? fsabl : 0;
-    f.abl_ctr = e->d_want;
     const int64_t grid = (e->capacity + 1 + (int64_t)kBlock * kSlideJ - 1) / ((int64_t)kBlock * kSlideJ);
     HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
     switch (e->nacc) {
@@ -5840,8 +5385,7 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
     HIPCHK(e, hipSetDevice(e->cfg.device));
     int64_t nrows = 0;
     bool spec_done = false;
-    static const bool nospec = getenv("FWA_NOSPEC") != nullptr;   // A/B switch
-    if (e->pend && !nospec && e->kind == FWA_TUMBLE && wm > e->wm && e->late_rows == 0) {
+    if (e->pend && e->kind == FWA_TUMBLE && wm > e->wm && e->late_rows == 0) {
         int rc = speculative_fire(e, wm, &nrows, &spec_done);
         if (rc) return rc;
         if (!spec_done) nrows = 0;
@@ -5871,8 +5415,7 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
             }
         }
         bool slid = false;
-        static const bool noslide = getenv("FWA_NOSLIDE") != nullptr;   // A/B switch (timing experiments)
-        if (e->kind == FWA_SLIDE && wins.size() >= 2 && !noslide && e->late_rows == 0) {
+        if (e->kind == FWA_SLIDE && wins.size() >= 2 && e->late_rows == 0) {
             int rc = fire_slide(e, wins, &nrows, &slid);
             if (rc) return rc;
         }
@@ -5989,6 +5532,43 @@ int fwa_reset_timers(fwa_engine* e) {
     e->ingest_launches = e->ingest_records = e->replay_records = e->fire_launches = e->fire_rows = 0;
     e->ingest_ms = e->fire_ms = e->partition_ms = e->combine_ms = 0;
     return FWA_OK;
+}
+
+int fwa_set_option(fwa_engine* e, int32_t option, int64_t value) {
+    if (!e) return FWA_E_ARG;
+    if (int rc0 = settle_pending(e)) return rc0;
+    const int32_t tri = value < 0 ? -1 : (value > 0 ? 1 : 0);
+    switch (option) {
+        case FWA_OPT_SKEW_MERGE: e->opt_pre = tri; return FWA_OK;
+        case FWA_OPT_WINDOW_PASSES: e->opt_mp = tri; return FWA_OK;
+        case FWA_OPT_NARROW_ENTRIES: e->opt_narrow = tri; return FWA_OK;
+        case FWA_OPT_SESSION_CELLS: e->opt_cells = tri; return FWA_OK;
+        case FWA_OPT_OUT_MIN_ROWS: e->opt_out_min = std::max<int64_t>(0, value); return FWA_OK;
+        case FWA_OPT_PARTIALS_ONE_PASS: e->opt_partials_v1 = value > 0; return FWA_OK;
+        case FWA_OPT_SP_TABLE: case FWA_OPT_SP_FMAX: case FWA_OPT_SP_BUDGET: return sp_set_option(e, option, value);
+        case FWA_OPT_PROFILE: e->opt_profile = value > 0 ? 1 : 0; return FWA_OK;
+        default: return fail(e, FWA_E_ARG, "unknown option");
+    }
+}
+
+int fwa_get_option(const fwa_engine* e, int32_t option, int64_t* value) {
+    if (!e || !value) return FWA_E_ARG;
+    auto eff = [](int32_t opt, bool adaptive_on) -> int64_t { return opt == 1 || (opt != 0 && adaptive_on) ? 1 : 0; };
+    switch (option) {
+        case FWA_OPT_SKEW_MERGE: *value = eff(e->opt_pre, e->pre); return FWA_OK;
+        case FWA_OPT_WINDOW_PASSES: *value = eff(e->opt_mp, e->mp); return FWA_OK;
+        case FWA_OPT_NARROW_ENTRIES: *value = eff(e->opt_narrow, e->narrow); return FWA_OK;
+        case FWA_OPT_SESSION_CELLS: *value = eff(e->opt_cells, e->cell_skip <= 0); return FWA_OK;
+        case FWA_OPT_OUT_MIN_ROWS: *value = e->opt_out_min > 0 ? e->opt_out_min : ((int64_t)1 << 22); return FWA_OK;
+        case FWA_OPT_PARTIALS_ONE_PASS: *value = e->opt_partials_v1 ? 1 : 0; return FWA_OK;
+        case FWA_OPT_SP_TABLE: case FWA_OPT_SP_FMAX: case FWA_OPT_SP_BUDGET:
+            if (!e->sp) return FWA_E_UNSUPPORTED;
+            *value = option == FWA_OPT_SP_TABLE ? e->sp->T : option == FWA_OPT_SP_FMAX ? (e->sp->fmax ? e->sp->fmax : kSpMaxF)
+                                                                                    : (int64_t)e->sp->budget;
+            return FWA_OK;
+        case FWA_OPT_PROFILE: *value = e->opt_profile; return FWA_OK;
+        default: return FWA_E_ARG;
+    }
 }
 
 int fwa_set_input_stream(fwa_engine* e, void* stream) {

@@ -95,16 +95,20 @@ JM_HD int32_t binrow_hash(const uint64_t* slots, int arity, uint64_t nullbits) {
 }
 
 // key_kind: 0 JAVA_LONG, 1 BINROW_BIGINT, 2 PREHASHED (hash supplied), 3 GROUP_PREFIXED (key ids of a key
-// dictionary, fwa_keydict: the key group in the top 16 bits)
+// dictionary, fwa_keydict: the key group in the top 16 bits; an id whose key group is >= max_par -- a dictionary
+// created with another max parallelism, or not a dictionary id at all -- has key group -1, which no subtask owns)
 JM_HD int32_t key_hash(int64_t key, int key_kind, int32_t supplied) {
     return key_kind == 0 ? long_hash(key) : (key_kind == 1 ? binrow_bigint_hash(key) : supplied);
 }
 JM_HD int32_t key_group(int32_t hash, int32_t max_par) { return murmur_hash(hash) % max_par; }
 JM_HD int32_t key_group_of(int64_t key, int key_kind, int32_t supplied, int32_t max_par) {
-    if (key_kind == 3) return (int32_t)((uint64_t)key >> 48);
+    if (key_kind == 3) {
+        const int32_t kg = (int32_t)((uint64_t)key >> 48);
+        return kg < max_par ? kg : -1;
+    }
     return key_group(key_hash(key, key_kind, supplied), max_par);
 }
-JM_HD int32_t operator_index(int32_t max_par, int32_t par, int32_t kg) { return kg * par / max_par; }
+JM_HD int32_t operator_index(int32_t max_par, int32_t par, int32_t kg) { return kg < 0 ? -1 : kg * par / max_par; }
 
 // ---- 64-bit unsigned division by a runtime constant -------------------------------------------
 

@@ -132,6 +132,7 @@ __global__ void __launch_bounds__(kBlockKd) kd_lookup_kernel(KdCols k, KdDev d, 
         const uint32_t ps = d.pos[i];
         if (ps == 0xffffffffu) continue;
         const int64_t id = d.ht_id[ps & 0x7fffffffu];
+        if (id < 0) { atomicCAS(d.status, 0, FWA_E_OOM); ids[i] = -1; continue; }   // claimed when the dictionary was full
         const uint64_t seq = (uint64_t)id & kSeqMask;
         uint64_t slots[FWA_KEYDICT_MAX_ARITY], nb;
         row_of(k, i, slots, &nb);
@@ -209,7 +210,7 @@ extern "C" {
 int fwa_keydict_create(int32_t arity, const int32_t* field_types, int32_t max_parallelism, int64_t capacity,
                        int32_t device, fwa_keydict** out) {
     if (!out || arity < 1 || arity > FWA_KEYDICT_MAX_ARITY || !field_types || max_parallelism <= 0 ||
-        max_parallelism > 32768 || capacity <= 0 || capacity > ((int64_t)1 << 31))
+        max_parallelism > 32768 || capacity <= 0 || capacity > ((int64_t)1 << 29))   // slot index: 31 bits < sentinel
         return FWA_E_ARG;
     for (int c = 0; c < arity; ++c)
         if (field_types[c] < FWA_KEY_FIELD_BIGINT || field_types[c] > FWA_KEY_FIELD_DOUBLE) return FWA_E_ARG;
@@ -233,7 +234,9 @@ int fwa_keydict_create(int32_t arity, const int32_t* field_types, int32_t max_pa
             hipMalloc(&d->d.status, 4) != hipSuccess || hipMalloc(&d->d_colptr, 2 * sizeof(void*) * FWA_KEYDICT_MAX_ARITY) != hipSuccess) {
             rc = FWA_E_OOM; break;
         }
-        if (hipMemsetAsync(d->d.ht_key, 0, 8 * cap, d->stream) != hipSuccess || hipMemsetAsync(d->d.nrows, 0, 8, d->stream) != hipSuccess ||
+        // ht_id -1: a slot whose row was claimed but never given an id (the dictionary filled up) reads as "no id"
+        if (hipMemsetAsync(d->d.ht_key, 0, 8 * cap, d->stream) != hipSuccess || hipMemsetAsync(d->d.ht_id, 0xff, 8 * cap, d->stream) != hipSuccess ||
+            hipMemsetAsync(d->d.nrows, 0, 8, d->stream) != hipSuccess ||
             hipMemsetAsync(d->d.status, 0, 4, d->stream) != hipSuccess || hipStreamSynchronize(d->stream) != hipSuccess) {
             rc = FWA_E_DEVICE; break;
         }

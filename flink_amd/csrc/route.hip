@@ -43,7 +43,8 @@ struct RouteArgs {
 
 __device__ __forceinline__ int32_t dest_of(const RouteArgs& a, int64_t i) {
     const int32_t kg = jm::key_group_of(a.keys[i], a.key_kind, a.key_hash ? a.key_hash[i] : 0, a.maxp);
-    return jm::operator_index(a.maxp, a.par, kg);
+    // an id no subtask owns (key group -1, java_math.h) goes to subtask 0, whose ingest rejects it (FWA_E_KEYGROUP)
+    return kg < 0 ? 0 : jm::operator_index(a.maxp, a.par, kg);
 }
 
 __global__ void __launch_bounds__(kRouteBlock) route_count_kernel(RouteArgs a) {

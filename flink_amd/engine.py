@@ -87,6 +87,10 @@ def lib():
     L.fwa_generate.argtypes = [C.POINTER(A.GenParams), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                                C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     L.fwa_generate.restype = C.c_int
+    L.fwa_set_option.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
+    L.fwa_set_option.restype = C.c_int
+    L.fwa_get_option.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]
+    L.fwa_get_option.restype = C.c_int
     _LIB = L
     return L
 
@@ -120,10 +124,18 @@ def _check(rc, h=None, what=""):
         raise EngineError(rc, msg or what)
 
 
+# fwa_set_option (include/flink_amd.h enum fwa_option): per-handle tuning / test options
+OPTIONS = {"skew_merge": 1, "window_passes": 2, "narrow_entries": 3, "session_cells": 4, "out_min_rows": 5,
+           "partials_one_pass": 6, "sp_table": 7, "sp_fmax": 8, "sp_budget": 9, "profile": 10}
+# options applied to every new handle of this process before its own (test tooling sets these, e.g.
+# tests/forced_modes_check.py); empty in production
+DEFAULT_OPTIONS = {}
+
+
 class WindowAggregator:
     """One engine handle = one Flink subtask's window operator state (single-threaded)."""
 
-    def __init__(self, cfg):
+    def __init__(self, cfg, options=None):
         self.cfg = cfg
         self.names = A.agg_names(cfg)
         self.h = C.c_void_p()
@@ -132,6 +144,20 @@ class WindowAggregator:
         rc = lib().fwa_create(C.byref(cfg), C.byref(self.h))
         if rc:
             raise EngineError(rc, "fwa_create")
+        for name, value in DEFAULT_OPTIONS.items():    # where they apply to this handle's state layout
+            opt = OPTIONS[name] if isinstance(name, str) else int(name)
+            rc = lib().fwa_set_option(self.h, opt, int(value))
+            if rc and rc != -7:                        # FWA_E_UNSUPPORTED: not this layout
+                _check(rc, self.h)
+        for name, value in (options or {}).items():
+            self.set_option(name, value)
+
+    def set_option(self, name, value):
+        """fwa_set_option: name from OPTIONS (or the enum value), value -1 adaptive / 0 never / 1 always, or a size."""
+        opt = OPTIONS[name] if isinstance(name, str) else int(name)
+        rc = lib().fwa_set_option(self.h, opt, int(value))
+        self._settled()
+        _check(rc, self.h)
 
     def _order_after_producer(self, x):
         """Device inputs come from torch's current stream: make the engine's stream wait for it."""
@@ -144,6 +170,13 @@ class WindowAggregator:
     def _settled(self):
         """Called after every entry point that settles a pending async push."""
         self._inflight = None
+
+    def get_option(self, name):
+        """fwa_get_option: the option's effective value (tri-states: 1 if the handle currently takes that path)."""
+        opt = OPTIONS[name] if isinstance(name, str) else int(name)
+        v = C.c_int64(0)
+        _check(lib().fwa_get_option(self.h, opt, C.byref(v)), self.h)
+        return v.value
 
     # -- processElement (batched) --
     def push(self, keys, ts, cols=(), key_hash=None, sync=True, nulls=None):

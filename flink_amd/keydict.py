@@ -42,9 +42,17 @@ def _bind():
 
 
 def _dev(x, dtype):
+    """A contiguous CUDA tensor of exactly `dtype`: the kernels read sizeof(dtype) bytes per row, so a narrower tensor
+    would be read past its end and a host tensor would hand the GPU a host pointer."""
     import torch
     if type(x).__module__.startswith("torch"):
-        return x.contiguous()
+        if not x.is_cuda:
+            raise TypeError("key columns must be CUDA tensors or numpy arrays (got a host tensor)")
+        want = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32, np.dtype(np.float64): torch.float64,
+                np.dtype(np.uint8): torch.uint8}[np.dtype(dtype)]
+        if x.dtype != want and not (want == torch.uint8 and x.dtype == torch.bool):
+            raise TypeError("key column of dtype %s where %s is expected" % (x.dtype, want))
+        return x.contiguous().view(want) if x.dtype == torch.bool else x.contiguous()
     return torch.from_numpy(np.ascontiguousarray(x, dtype)).cuda()
 
 

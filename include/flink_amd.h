@@ -363,8 +363,31 @@ int fwa_late_records(fwa_engine* e, const int32_t** idx, int64_t* n);
 /* Reset the kernel timing counters of fwa_stats (bench warm-up). */
 int fwa_reset_timers(fwa_engine* e);
 
+/* Per-handle tuning / test options (no reference counterpart: the engine's own adaptive choices, which the defaults
+ * make). The library reads no environment variables; a TaskManager sets these per operator instance if at all.
+ * value -1 = adaptive (default), 0 = never, 1 = always for the tri-state options. FWA_E_ARG for an unknown option,
+ * FWA_E_UNSUPPORTED for an option that does not apply to the handle's state layout, FWA_E_STATE when the option can
+ * no longer change (FWA_OPT_SP_TABLE after the first push). */
+enum fwa_option {
+    FWA_OPT_SKEW_MERGE = 1,      /* Phase P tile pre-aggregation of equal (key, slice) records (skewed keys) */
+    FWA_OPT_WINDOW_PASSES = 2,   /* combiner window passes (chunks spanning more slices than the LDS window) */
+    FWA_OPT_NARROW_ENTRIES = 3,  /* 10-byte bucket entries for COUNT + SUM(BIGINT) while keys / values fit 32 bits */
+    FWA_OPT_SESSION_CELLS = 4,   /* sessions: the cell path for order-free pushes with a fixed gap (0 / -1) */
+    FWA_OPT_OUT_MIN_ROWS = 5,    /* first sizing of the fire's output columns in rows (0: 4M); tests force regrowth */
+    FWA_OPT_PARTIALS_ONE_PASS = 6, /* 1: fwa_push_partials merges through the one-pass atomic ingest */
+    FWA_OPT_SP_TABLE = 7,        /* record lists: LDS aggregation table slots (power of two >= 64, before any push) */
+    FWA_OPT_SP_FMAX = 8,         /* record lists: max fine buckets per (window, partition) at fire */
+    FWA_OPT_SP_BUDGET = 9,       /* record lists: live list bytes above which windows are compacted */
+    FWA_OPT_PROFILE = 10         /* 1: per-phase clock profile of Phase P / A, printed to stderr (diagnostic) */
+};
+int fwa_set_option(fwa_engine* e, int32_t option, int64_t value);
+/* The option's effective value: for the tri-state options 1 if the handle currently takes that path (forced, or
+ * switched on by the adaptive rule after a push), else 0; the sizes as set (or the default in use). */
+int fwa_get_option(const fwa_engine* e, int32_t option, int64_t* value);
+
 /* Stateless key-group assignment of n keys (device or host pointers per flags):
- * kg_out[i] = murmurHash(hash(key_i)) % max_parallelism; op_out[i] = kg*parallelism/max_parallelism.
+ * kg_out[i] = murmurHash(hash(key_i)) % max_parallelism; op_out[i] = kg*parallelism/max_parallelism
+ * (FWA_KEY_GROUP_PREFIXED: kg = the id's top 16 bits; both -1 for an id whose key group is >= max_parallelism).
  * op_out may be NULL. */
 int fwa_key_groups(const int64_t* keys, const int32_t* key_hash, int64_t n, int32_t key_kind,
                    int32_t max_parallelism, int32_t parallelism, int32_t* kg_out, int32_t* op_out,

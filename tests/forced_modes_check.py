@@ -1,6 +1,7 @@
-"""Child-process parity check with the adaptive combiner modes forced on from the first push (FWA_PRE=1:
-Phase P tile pre-aggregation, FWA_MP=1: window passes), so random streams exercise them at small sizes.
-Run by tests/test_skew_gpu.py::test_forced_pre_and_window_passes; exits non-zero on a mismatch."""
+"""Child-process parity check with the adaptive combiner modes forced on from the first push (fwa_set_option
+FWA_OPT_SKEW_MERGE = 1: Phase P tile pre-aggregation, FWA_OPT_WINDOW_PASSES = 1: window passes), so random streams
+exercise them at small sizes. Run by tests/test_skew_gpu.py::test_forced_pre_and_window_passes; exits non-zero on a
+mismatch."""
 import os
 import sys
 
@@ -24,7 +25,7 @@ AGGS = [[("COUNT", 0), ("SUM_I64", 0)], [("COUNT", 0)], [("COUNT", 0), ("SUM_F64
 
 
 def main():
-    assert os.environ.get("FWA_PRE") == "1" and os.environ.get("FWA_MP") == "1"
+    engine.DEFAULT_OPTIONS.update(skew_merge=1, window_passes=1)   # every handle of this process
     for ci, kw in enumerate(CONFIGS):
         for ai, aggs in enumerate(AGGS):
             rng = np.random.default_rng(100 * ci + ai)

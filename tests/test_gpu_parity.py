@@ -566,9 +566,8 @@ def test_late_record_indices_vs_oracle(eng_mod, ci):
 @pytest.mark.parametrize("ci", [0, 3])
 def test_partials_large_counts_and_late(eng_mod, ci):
     """Partial rows through the owner's two-phase path (COUNT + SUM(BIGINT): PRE buckets carry each row's record
-    count) against the per-row v1 path (FWA_PARTIALS_V1) on the same rows: counts above a bucket's u16 take the v1
+    count) against the per-row v1 path (FWA_OPT_PARTIALS_ONE_PASS) on the same rows: counts above a bucket's u16 take the v1
     path, late partials add their counts to the drops, rows are identical."""
-    import os
     cfg = A.make_config(aggs=C2_AGGS, key_capacity=4096, **CONFIGS[ci])
     names = A.agg_names(cfg)
     rng = np.random.default_rng(17)
@@ -582,18 +581,13 @@ def test_partials_large_counts_and_late(eng_mod, ci):
     acc = rng.integers(-2**40, 2**40, n).astype(np.int64)
     handles = {}
     for mode in ("v2", "v1"):
-        if mode == "v1":
-            os.environ["FWA_PARTIALS_V1"] = "1"
-        try:
-            g = eng_mod.WindowAggregator(cfg)
-            out, drops = [], 0
-            for sl, wm in ((slice(0, n // 2), 30_000), (slice(n // 2, n), A.LONG_MAX)):
-                drops += g.push_partials(keys[sl], sts[sl], cnt[sl], [cnt[sl], acc[sl]])
-                out.append(g.advance_watermark(wm))
-            handles[mode] = (out, drops, g.stats().ingest_launches)
-            g.close()
-        finally:
-            os.environ.pop("FWA_PARTIALS_V1", None)
+        g = eng_mod.WindowAggregator(cfg, options={"partials_one_pass": 1} if mode == "v1" else None)
+        out, drops = [], 0
+        for sl, wm in ((slice(0, n // 2), 30_000), (slice(n // 2, n), A.LONG_MAX)):
+            drops += g.push_partials(keys[sl], sts[sl], cnt[sl], [cnt[sl], acc[sl]])
+            out.append(g.advance_watermark(wm))
+        handles[mode] = (out, drops, g.stats().ingest_launches)
+        g.close()
     (o2, d2, _), (o1, d1, _) = handles["v2"], handles["v1"]
     assert d2 == d1 and d1 > 0
     for a_, b_ in zip(o2, o1):

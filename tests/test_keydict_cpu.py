@@ -112,3 +112,12 @@ def test_key_group_prefixed_ids():
     """FWA_KEY_GROUP_PREFIXED: the key group is the id's top 16 bits (a key dictionary's ids)."""
     for kg in (0, 5, 127):
         assert O.lib().or_key_group((kg << 48) | 12345, 3, 0, 128) == kg
+
+
+def test_torch_key_columns_are_type_checked():
+    """a torch key column must be a CUDA tensor of the field's exact dtype (the kernels read that many bytes
+    per row); a host tensor is refused before anything reaches the GPU."""
+    import torch
+    from flink_amd import keydict
+    with pytest.raises(TypeError):
+        keydict._dev(torch.zeros(4, dtype=torch.int64), np.int64)

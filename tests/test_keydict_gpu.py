@@ -151,6 +151,64 @@ def test_capacity_exhaustion_is_an_error():
     with pytest.raises(engine.EngineError) as ei:
         d.encode([np.arange(1000, dtype=np.int64)])
     assert A.STATUS[ei.value.code] == "E_OOM"
+    # after the failed batch: rows that got an id keep it, rows that were claimed without one still fail as E_OOM (not
+    # a garbage id), and a batch of rows that all got ids encodes fine
+    ok = None
+    for lo in range(0, 1000, 10):
+        try:
+            ok = d.encode([np.arange(lo, lo + 10, dtype=np.int64)]).cpu().numpy()
+            break
+        except engine.EngineError as e2:
+            assert A.STATUS[e2.code] == "E_OOM"
+    assert ok is not None and len(set(ok.tolist())) == 10 and (ok >= 0).all()
+    assert d.size() == 100
+    with pytest.raises(engine.EngineError) as ei:
+        d.encode([np.arange(1000, dtype=np.int64)])
+    assert A.STATUS[ei.value.code] == "E_OOM"
+    d.close()
+
+
+def test_torch_key_columns_of_the_wrong_dtype_are_refused():
+    import torch
+    from flink_amd.keydict import KeyDictionary
+    d = KeyDictionary(["BIGINT", "DOUBLE"], capacity=64)
+    with pytest.raises(TypeError):
+        d.encode([torch.zeros(8, dtype=torch.int32, device="cuda"), torch.zeros(8, dtype=torch.float64, device="cuda")])
+    ids = d.encode([torch.zeros(8, dtype=torch.int64, device="cuda"), torch.zeros(8, dtype=torch.float64, device="cuda")])
+    assert len(set(ids.cpu().numpy().tolist())) == 1
+    d.close()
+
+
+def test_ids_of_a_dictionary_with_a_larger_max_parallelism_are_rejected():
+    """an id whose key group (top 16 bits) is past the engine's max parallelism belongs to no subtask:
+    FWA_E_KEYGROUP on every ingest path, also when the engine owns every key group; fwa_key_groups reports -1."""
+    import torch
+    from flink_amd import engine
+    from flink_amd.keydict import KeyDictionary
+    d = KeyDictionary(["BIGINT"], max_parallelism=32768, capacity=50_000)
+    ids = d.encode([np.arange(50_000, dtype=np.int64)]).cpu().numpy()
+    bad = ids[(ids >> 48) >= 128][:64]
+    assert len(bad) == 64
+    kg, op = engine.key_groups(bad, max_parallelism=128, parallelism=4, key_kind=A.KEY_GROUP_PREFIXED)
+    assert (kg == -1).all() and (op == -1).all()
+    ts = np.arange(64, dtype=np.int64) * 10
+    for kw in (dict(), dict(window_kind="SLIDE", semantics="TABLE", size_ms=4000, slide_ms=1000),
+               dict(record_lists=True), dict(window_kind="SESSION", gap_ms=100)):
+        cfg = A.make_config(aggs=[("COUNT", 0), ("SUM_I64", 0)], key_kind=A.KEY_GROUP_PREFIXED, key_capacity=4096,
+                            **kw)
+        g = engine.WindowAggregator(cfg)
+        with pytest.raises(engine.EngineError) as ei:
+            g.push(bad, ts, [ts])
+        assert A.STATUS[ei.value.code] == "E_KEYGROUP", kw
+        with pytest.raises(engine.EngineError) as ei:   # device inputs (the two-phase path)
+            dk = torch.from_numpy(np.resize(bad, 1 << 16)).cuda()
+            dt = torch.arange(1 << 16, dtype=torch.int64, device="cuda")
+            g2 = engine.WindowAggregator(cfg)
+            g2.push(dk, dt, [dt])
+            g2.advance_watermark(A.LONG_MAX)
+        assert A.STATUS[ei.value.code] == "E_KEYGROUP", kw
+        g.close()
+        g2.close()
     d.close()
 
 

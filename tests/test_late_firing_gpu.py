@@ -85,12 +85,11 @@ def test_repeated_late_elements_same_window(eng_mod):
 
 @pytest.mark.parametrize("ci", [0, 2])
 def test_fire_output_regrow_relaunch(eng_mod, ci):
-    """Output capacity smaller than one watermark's rows (FWA_OUT_MIN forces a 1024-row first sizing):
+    """Output capacity smaller than one watermark's rows (FWA_OPT_OUT_MIN_ROWS forces a 16-row first sizing):
     the fire counts past the capacity, the host grows the output and relaunches, late-firing rows at the
     head included. Rows must still equal the oracle's."""
-    import os
-    os.environ["FWA_OUT_MIN"] = "16"
+    eng_mod.DEFAULT_OPTIONS["out_min_rows"] = 16
     try:
         test_late_firings_vs_oracle(eng_mod, ci, I64_AGGS)
     finally:
-        del os.environ["FWA_OUT_MIN"]
+        del eng_mod.DEFAULT_OPTIONS["out_min_rows"]

@@ -4,7 +4,8 @@ CPU oracle -- the layout the engine selects for key spaces where keys barely rep
 Same contract as the dense layout: rows equal the oracle's (WindowOperator / SlicingWindowOperator restatement) for
 DataStream and Table TUMBLE with offsets, late drops and their indices, key-group ownership and Long.MIN_VALUE
 errors, the Long.MIN_VALUE key, a push spanning many windows, partial accumulators and snapshot / restore with
-rescaling; the fire's fine-bucket and split-pass paths are forced with small LDS tables (FWA_SP_T / FWA_SP_FMAX).
+rescaling; the fire's fine-bucket and split-pass paths are forced with small LDS tables (FWA_OPT_SP_TABLE /
+FWA_OPT_SP_FMAX).
 """
 import os
 import subprocess
@@ -66,17 +67,14 @@ def test_record_lists_one_big_window_fine_buckets():
              [(keys, ts, [vi, vf, vd])], [A.LONG_MAX])
 
 
-@pytest.mark.parametrize("env", [{"FWA_SP_T": "128"}, {"FWA_SP_T": "256", "FWA_SP_FMAX": "1"}])
-def test_record_lists_split_passes(env):
+@pytest.mark.parametrize("opts", [{"sp_table": 128}, {"sp_table": 256, "sp_fmax": 1}])
+def test_record_lists_split_passes(monkeypatch, opts):
     """Tables far smaller than a partition's distinct keys: overflowing passes are redone as half passes."""
-    code = ("import sys; sys.path[:0] = [%r, %r]\n"
-            "from test_record_lists_gpu import test_record_lists_vs_oracle, test_record_lists_hot_keys\n"
-            "test_record_lists_vs_oracle('TABLE', 0)\n"
-            "test_record_lists_hot_keys()\n"
-            "print('ok')\n") % (ROOT, os.path.join(ROOT, "tests"))
-    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env}, capture_output=True, text=True,
-                       timeout=300)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+    from flink_amd import engine
+    for k, v in opts.items():
+        monkeypatch.setitem(engine.DEFAULT_OPTIONS, k, v)
+    test_record_lists_vs_oracle('TABLE', 0)
+    test_record_lists_hot_keys()
 
 
 def test_record_lists_hot_keys():
@@ -201,7 +199,7 @@ def test_record_lists_snapshot_restore_rescale():
 
 
 def record_lists_compaction_check():
-    """Few distinct keys, many records per window, a small FWA_SP_BUDGET (set by the caller): the growing windows'
+    """Few distinct keys, many records per window, a small FWA_OPT_SP_BUDGET (set by the caller): the growing windows'
     lists are folded into pre-aggregated runs, results still equal the oracle's, device memory stays bounded."""
     import torch
     rng = np.random.default_rng(29)
@@ -238,9 +236,10 @@ def record_lists_compaction_check():
 
 def test_record_lists_compaction_bounds_memory():
     code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "from flink_amd import engine\n"
+            "engine.DEFAULT_OPTIONS['sp_budget'] = 4 << 20\n"
             "from test_record_lists_gpu import record_lists_compaction_check\n"
             "record_lists_compaction_check()\n"
             "print('ok')\n") % (ROOT, os.path.join(ROOT, "tests"))
-    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "FWA_SP_BUDGET": str(4 << 20)},
-                       capture_output=True, text=True, timeout=300)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

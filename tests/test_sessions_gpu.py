@@ -140,7 +140,7 @@ def test_session_late_firings_mixed_with_bulk(eng_mod):
 
 # ---- cell path (sess3_*: fixed gap, every record of the push order-free) ---------------------------
 # A stream without late records batched as _batches does is order-free in every push (each record's window ends after
-# the previous watermark), so these pushes run on the cell path; FWA_SESS_CELL=0 forces the general path on the same
+# the previous watermark), so these pushes run on the cell path; FWA_OPT_SESSION_CELLS = 0 forces the general path on the same
 # stream. replay_records counts the records of pushes the cell path had to hand back to the general path.
 CELL_AGGS = {
     1: [("COUNT", 0)],
@@ -154,7 +154,7 @@ CELL_AGGS = {
 @pytest.mark.parametrize("cell", ["1", "0"])
 @pytest.mark.parametrize("nacc", [1, 2, 3, 4, 5])
 def test_cell_path_order_free_vs_oracle(eng_mod, monkeypatch, nacc, cell):
-    monkeypatch.setenv("FWA_SESS_CELL", cell)
+    monkeypatch.setitem(eng_mod.DEFAULT_OPTIONS, "session_cells", -1 if cell == "1" else 0)
     keys, ts, vi, vd = _stream(100 + nacc, 200_000, 3000, 400_000, 300, 0.0)
     cfg = A.make_config(window_kind="SESSION", gap_ms=700, aggs=CELL_AGGS[nacc], key_capacity=8192)
     dropped, st = _run(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 12, 300))

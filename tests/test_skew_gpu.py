@@ -30,7 +30,7 @@ def _mix64(z):
     return z ^ (z >> np.uint64(31))
 
 
-def _run(eng_mod, cfg, k, t, v, nb, delay, ctx):
+def _run(eng_mod, cfg, k, t, v, nb, delay, ctx, modes=None):
     from oracle.oracle import Oracle
     names = A.agg_names(cfg)
     g, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
@@ -46,6 +46,8 @@ def _run(eng_mod, cfg, k, t, v, nb, delay, ctx):
             wm = A.LONG_MAX
         assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), names, ctx="%s wm=%d" % (ctx, wm))
         replays.append(g.stats().replay_records)
+        if modes is not None and b < nb:              # the handle's pre-aggregation mode after push b
+            modes.append(g.get_option("skew_merge"))
     g.close()
     o.close()
     return replays
@@ -55,8 +57,7 @@ def _run(eng_mod, cfg, k, t, v, nb, delay, ctx):
 def test_zipf_head_key_switches_to_pre_aggregation(eng_mod, shape):
     """Zipf(1.1) over 1M keys (head key ~12 % of the records): the first push misses every slice (replayed); the
     second overflows the head key's partition's sub-buckets (those records take the v1 replay) and signals the skew;
-    the following pushes pre-aggregate and replay (almost) nothing. Every watermark's rows equal the oracle's. (With
-    the flat layout, FWA_FLAT=1, the second push cannot overflow and only signals the skew.)"""
+    the following pushes pre-aggregate and replay (almost) nothing. Every watermark's rows equal the oracle's."""
     import torch
     nkeys, n = 1_000_000, 1 << 21
     w = 1.0 / np.arange(1, nkeys + 1, dtype=np.float64) ** 1.1
@@ -76,10 +77,14 @@ def test_zipf_head_key_switches_to_pre_aggregation(eng_mod, shape):
     else:
         cfg = A.make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000,
                             aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=nkeys)
-    rep = _run(eng_mod, cfg, k, t, v, 4, 1000, shape)
-    # push 1 misses every slice (empty directory: all replayed); push 2 overflows on the head key's partition (v1
-    # replay, or nothing with the flat layout); pushes 3-4 pre-aggregate and replay (almost) nothing
-    assert rep[0] > 0 and rep[3] - rep[1] < (n // 4) // 100, rep
+    modes = []
+    rep = _run(eng_mod, cfg, k, t, v, 4, 1000, shape, modes)
+    # push 1 misses every slice (empty directory: all replayed) and does not see the skew; push 2 overflows on the
+    # head key's partition (those records take the v1 replay) and switches the handle to pre-aggregation, which
+    # pushes 3-4 then use and replay (almost) nothing
+    assert modes[0] == 0 and modes[1] == 1 and modes[3] == 1, modes
+    assert rep[0] > 0 and rep[1] - rep[0] > 0, rep
+    assert rep[3] - rep[1] < (n // 4) // 100, rep
 
 
 @pytest.mark.parametrize("aggs", [[("COUNT", 0), ("SUM_I64", 0)], [("COUNT", 0)]], ids=["count_sum", "count"])
@@ -100,13 +105,12 @@ def test_pre_entries_past_bucket_end_applied_with_atomics(eng_mod, aggs):
 
 
 def test_forced_pre_and_window_passes():
-    """FWA_PRE=1 / FWA_MP=1 (process-wide switches) in a child process: the pre-aggregating Phase P and the
+    """FWA_OPT_SKEW_MERGE / FWA_OPT_WINDOW_PASSES forced on for every handle of a child process: the pre-aggregating Phase P and the
     combiner's window passes from the first push, over Zipf keys, small HOP/CUMULATE slices and late records."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, FWA_PRE="1", FWA_MP="1")
-    r = subprocess.run([sys.executable, os.path.join(here, "forced_modes_check.py")], env=env, timeout=300,
+    r = subprocess.run([sys.executable, os.path.join(here, "forced_modes_check.py")], timeout=300,
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
