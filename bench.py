@@ -53,10 +53,13 @@ def main():
                          "c4: tumbling 10s COUNT+SUM(long), 100M uniform keys, maxParallelism 128; "
                          "c5: Table TUMBLE 10s TVF COUNT, SUM(double), AVG(double), MAX(float), MAX(double); "
                          "c5s: DataStream session windows (gap 5s), same float aggregates")
+    ap.add_argument("--sync-fire", action="store_true",
+                    help="N=1: wait for every watermark's fire before the next batch (fwa_advance_watermark)")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="fwa_set_option on the measured engine(s) (flink_amd.engine.OPTIONS), e.g. profile=1")
-    ap.add_argument("--exchange", choices=["partials", "raw"], default="partials",
-                    help="N>1 keyBy plan: two-phase partial accumulators (default) or raw records")
+    ap.add_argument("--exchange", choices=["auto", "partials", "raw"], default="auto",
+                    help="N>1 keyBy plan: two-phase partial accumulators or raw records; auto: the plan "
+                         "flink_amd.distributed.choose_exchange picks for the configuration (raw for C4's 1e8 keys)")
     args = ap.parse_args()
     if args.config == "c4" and args.keys == 1_000_000:
         args.keys = 100_000_000
@@ -134,6 +137,9 @@ def main():
     cols_of = (lambda b: [vals[b * B:(b + 1) * B], vals_d[b * B:(b + 1) * B]]) if fp else \
         (lambda b: [vals[b * B:(b + 1) * B]])
     pipelined = None
+    if args.exchange == "auto":
+        from flink_amd.distributed import choose_exchange
+        args.exchange = choose_exchange(cfg_kw)
     if world > 1:
         from flink_amd.distributed import KeyedWindowPipeline, TwoPhaseKeyedWindowPipeline
         cls = TwoPhaseKeyedWindowPipeline if args.exchange == "partials" else KeyedWindowPipeline
@@ -175,6 +181,17 @@ def main():
             rows_t += pipelined(b, b + 1 if b + 1 < S else None)
             if (b - args.warmup) % 4 == 3:
                 log("step %d/%d  %.2fs" % (b - args.warmup + 1, args.steps, time.perf_counter() - t0))
+    elif world == 1 and not args.sync_fire:
+        # the watermark step returns while its fire runs (fwa_advance_watermark_async); the fired rows are taken
+        # after the next batch was handed over, so the host's work for batch b+1 overlaps the fire of batch b
+        for b in range(args.warmup, S):
+            dropped += push(b)
+            if b > args.warmup:
+                rows_t += eng.fired_output_raw().n_rows
+            eng.advance_watermark_async(wms[b])
+            if (b - args.warmup) % 4 == 3:
+                log("step %d/%d  %.2fs" % (b - args.warmup + 1, args.steps, time.perf_counter() - t0))
+        rows_t += eng.fired_output_raw().n_rows
     else:
         for b in range(args.warmup, S):
             dropped += push(b)

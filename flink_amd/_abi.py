@@ -5,7 +5,9 @@ the exact same struct layouts.
 """
 import ctypes as C
 
-FWA_ABI_VERSION = 3
+import numpy as np
+
+FWA_ABI_VERSION = 4
 FWA_MAX_AGGS = 8
 FWA_MAX_COLS = 8
 
@@ -22,20 +24,46 @@ AGG_KINDS = {
     "COUNT": 0, "SUM_I64": 1, "SUM_F32": 2, "SUM_F64": 3, "MIN_I64": 4, "MAX_I64": 5,
     "MIN_F32": 6, "MAX_F32": 7, "MIN_F64": 8, "MAX_F64": 9, "AVG_I64": 10, "AVG_F32": 11,
     "AVG_F64": 12, "COUNT_COL": 13,
+    "SUM_DEC": 14, "AVG_DEC": 15, "SUM_DEC128": 16, "AVG_DEC128": 17,
 }
+DEC_KINDS = ("SUM_DEC", "AVG_DEC", "SUM_DEC128", "AVG_DEC128")
 AGG_NAMES = {v: k for k, v in AGG_KINDS.items()}
 # numpy dtype of each aggregate's RESULT column
 AGG_RESULT_DTYPE = {
     "COUNT": "i8", "SUM_I64": "i8", "SUM_F32": "f4", "SUM_F64": "f8", "MIN_I64": "i8",
     "MAX_I64": "i8", "MIN_F32": "f4", "MAX_F32": "f4", "MIN_F64": "f8", "MAX_F64": "f8",
     "AVG_I64": "i8", "AVG_F32": "f4", "AVG_F64": "f8", "COUNT_COL": "i8",
+    # DECIMAL: 16-byte unscaled two's complement; the wrappers return Python ints (object arrays)
+    "SUM_DEC": "V16", "AVG_DEC": "V16", "SUM_DEC128": "V16", "AVG_DEC128": "V16",
 }
 # numpy dtype of each aggregate's INPUT column (None: no input)
 AGG_INPUT_DTYPE = {
     "COUNT": None, "SUM_I64": "i8", "SUM_F32": "f4", "SUM_F64": "f8", "MIN_I64": "i8",
     "MAX_I64": "i8", "MIN_F32": "f4", "MAX_F32": "f4", "MIN_F64": "f8", "MAX_F64": "f8",
     "AVG_I64": "i8", "AVG_F32": "f4", "AVG_F64": "f8", "COUNT_COL": None,
+    "SUM_DEC": "i8", "AVG_DEC": "i8", "SUM_DEC128": "V16", "AVG_DEC128": "V16",
 }
+
+
+def dec128_column(values):
+    """Unscaled DECIMAL values (Python ints, |v| < 2^127) -> the engine's 16-byte column: int64 [n, 2] (low, high)."""
+    out = np.empty((len(values), 2), np.int64)
+    for i, v in enumerate(values):
+        u = int(v) & ((1 << 128) - 1)
+        lo, hi = u & ((1 << 64) - 1), u >> 64
+        out[i, 0] = lo - (1 << 64) if lo >= 1 << 63 else lo
+        out[i, 1] = hi - (1 << 64) if hi >= 1 << 63 else hi
+    return out
+
+
+def dec128_values(raw):
+    """16-byte two's-complement values (any buffer of n * 16 bytes) -> numpy object array of Python ints."""
+    w = np.frombuffer(memoryview(raw).cast("B"), np.uint64).reshape(-1, 2)
+    out = np.empty(w.shape[0], object)
+    for i in range(w.shape[0]):
+        u = int(w[i, 0]) | (int(w[i, 1]) << 64)
+        out[i] = u - (1 << 128) if u >= 1 << 127 else u
+    return out
 
 STATUS = {0: "OK", -1: "E_ARG", -2: "E_TS_MIN", -3: "E_KEYGROUP", -4: "E_MERGE_LATE", -5: "E_OOM",
           -6: "E_DEVICE", -7: "E_UNSUPPORTED", -8: "E_STATE", -9: "E_CORRUPT"}
@@ -65,6 +93,7 @@ class Config(C.Structure):
         ("output_on_device", C.c_int32), ("key_capacity", C.c_int64), ("max_batch", C.c_int64),
         ("flags", C.c_int32), ("gap_col", C.c_int32), ("tz_n", C.c_int32), ("nullable_cols", C.c_int32),
         ("tz", C.c_void_p),
+        ("dec_scale", C.c_int32 * FWA_MAX_AGGS),    # ABI 4: DECIMAL aggregate j's input scale
     ]
 
 
@@ -125,9 +154,12 @@ def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, sl
     if len(aggs) > FWA_MAX_AGGS:
         raise ValueError("at most %d aggregates" % FWA_MAX_AGGS)
     c.num_aggs = len(aggs)
-    for i, (name, col) in enumerate(aggs):
+    for i, spec in enumerate(aggs):                       # (name, col) or, for DECIMAL, (name, col, scale)
+        name, col = spec[0], spec[1]
         c.aggs[i].kind = AGG_KINDS[name]
         c.aggs[i].col = col
+        if len(spec) > 2:
+            c.dec_scale[i] = int(spec[2])
     c.device = device
     c.output_on_device = output_on_device
     c.key_capacity = key_capacity

@@ -720,8 +720,9 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
                     if (pc == 0 || pc > 0xFFFFull) code = kCodeSlow;  // does not fit a bucket's u16 count
                 }
             }
-            if constexpr (NW) {
-                if (code == kCodeAccept && ((int64_t)(int32_t)key != key || (int64_t)(int32_t)R.v0[j] != (int64_t)R.v0[j])) {
+            if constexpr (NW) {   // (INT32_MIN and INT32_MIN + 1 are the narrow combiner's LDS markers: v1 path too)
+                if (code == kCodeAccept && ((int64_t)(int32_t)key != key || (uint32_t)key - 0x80000000u <= 1u ||
+                                            (int64_t)(int32_t)R.v0[j] != (int64_t)R.v0[j])) {
                     code = kCodeSlow;
                     ++wide;
                 }
@@ -864,6 +865,228 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
     if (lane == 0) {
         if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
         if (NW && wide) atomicAdd(&a.st->wide_n, (int32_t)wide);
+        if (relmin != ~0u) {
+            atomicMax(&a.st->max_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmax));
+            atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
+        }
+    }
+    if (relmin != ~0u)
+        for (uint32_t r = relmin + (uint32_t)lane; r <= relmax; r += 64) {
+            const int32_t slot = a.rel2slot[r];
+            if (slot >= 0 && a.touched[slot] == 0) a.touched[slot] = 1;
+        }
+}
+
+// partition_nk: Phase P of the narrow COUNT + SUM(BIGINT) shape (C2: partition3<1, 6, 1024, 3, 0, 0, 1, 1>'s
+// contract), software-pipelined over tiles so that loads and the run reservations are always in flight:
+//   iteration t: classify tile t from registers (partition, rank = LDS histogram atomic) -> issue tile t+1's loads ->
+//   scan -> scatter tile t's packed entries straight to their sorted LDS position (buffer t & 1) -> reserve tile
+//   t's runs (returning atomics, consumed one iteration later) -> store tile t-1 from buffer (t-1) & 1.
+// The loads of tile t+1 are in flight during the scan, the scatter and tile t-1's stores; a reservation's latency is
+// hidden behind a whole iteration (vmcnt retires in order: the reservations of tile t are issued after the loads of
+// tile t+1, and waited for after those loads were consumed). No staging copy, no permutation arrays: the sorted
+// buffer holds the entry itself (8 B) and its slice (2 B); a stored entry's partition is its key's hash again.
+// A run past its sub-bucket's end (skewed keys) is applied at once with device atomics (the handle switches to
+// tile pre-aggregation after such a push, DevStatus::ovf_n).
+template <int ITEMS, int THREADS>
+__global__ void __launch_bounds__(THREADS, 1) partition_nk_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
+    static_assert(THREADS == kMaxPart && ITEMS % 2 == 0 && ITEMS <= 8, "one partition cursor per thread, paired loads");
+    constexpr int kTile = THREADS * ITEMS;
+    const EngineConst& c = *cp;
+    __shared__ uint32_t hist[kMaxPart];
+    __shared__ uint32_t toff[2][kMaxPart];
+    __shared__ uint32_t gbase[kMaxPart];
+    __shared__ unsigned long long x_ent[2][kTile];
+    __shared__ uint16_t x_rel[2][kTile];
+    __shared__ uint32_t wsum[THREADS / 64];
+    __shared__ uint32_t s_total[2];
+    __shared__ uint8_t s_code[kRelCap];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    unsigned dropped = 0, wide = 0;
+    uint32_t relmax = 0, relmin = ~0u;
+    const bool ds = c.sem == FWA_SEM_DATASTREAM;
+    for (int r = tid; r < kRelCap / 4; r += THREADS) ((uint32_t*)s_code)[r] = ((const uint32_t*)a.relcode)[r];
+    for (int i = tid; i < a.np; i += THREADS) hist[i] = 0;
+    const int64_t ntiles = (a.n + kTile - 1) / kTile;
+    const int sub = blockIdx.x % kSub;
+    const int64_t n = a.n;
+    const int64_t* __restrict__ pkeys = a.keys;
+    const int64_t* __restrict__ pts = a.ts;
+    const unsigned long long* __restrict__ pval = (const unsigned long long*)a.cols[a.vcol[0]];
+    unsigned long long rk[ITEMS], rv[ITEMS];
+    int64_t rt[ITEMS];
+    auto xof = [&](int j) -> int { return 2 * ((j >> 1) * THREADS + tid) + (j & 1); };
+    auto load = [&](int64_t t) {   // pair p = records 2p, 2p+1; a pair reaching past n is not loaded (record n-1: slow path)
+#pragma unroll
+        for (int jj = 0; jj < ITEMS / 2; ++jj) {
+            const int64_t pi = t * (kTile / 2) + (int64_t)jj * THREADS + tid;
+            const int64_t ip = 2 * pi + 1 < n ? pi : 0;
+            const ulonglong2 kk = reinterpret_cast<const ulonglong2*>(pkeys)[ip];
+            const longlong2 tt = reinterpret_cast<const longlong2*>(pts)[ip];
+            const ulonglong2 vv = reinterpret_cast<const ulonglong2*>(pval)[ip];
+            rk[2 * jj] = kk.x; rk[2 * jj + 1] = kk.y;
+            rt[2 * jj] = tt.x; rt[2 * jj + 1] = tt.y;
+            rv[2 * jj] = vv.x; rv[2 * jj + 1] = vv.y;
+        }
+    };
+    long long pt = clock64();
+    long long pacc[6] = {0, 0, 0, 0, 0, 0};
+#define QMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
+    const int64_t G = gridDim.x;
+    const int64_t t_first = blockIdx.x;
+    if (t_first < ntiles) load(t_first);
+    // this thread's partition: tile t-1's reservation (a returning atomic issued one iteration ago -- read only after
+    // the next tile's loads were issued, so waiting for it never drains them) and run length
+    uint32_t g_res = 0, h_res = 0;
+    int64_t t_prev = -1;
+    // store tile tp from buffer b: fixed trip count, lanes without an entry write the trash area (keeps the waitcnt
+    // of the next classify exact, see partition3)
+    auto store_tile = [&](int b, int64_t tp) {
+        const uint32_t total = s_total[b];
+#pragma unroll
+        for (int jj = 0; jj < ITEMS; ++jj) {
+            const uint32_t sidx = (uint32_t)(jj * THREADS + tid);
+            const bool valid = sidx < total;
+            const unsigned long long ent = x_ent[b][valid ? sidx : 0];
+            const uint16_t rel = x_rel[b][valid ? sidx : 0];
+            const int64_t key = (int64_t)(int32_t)(uint32_t)ent;
+            const uint32_t p = a.part_bits ? (uint32_t)(jm::mix64((uint64_t)key) >> (64 - a.part_bits)) : 0u;
+            const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[b][p]);
+            const bool inb = valid && dst < (uint64_t)a.capb;
+            if (valid && !inb) {            // sub-bucket full (skewed keys): apply the record now
+                const int32_t slot = a.rel2slot[rel];
+                if (slot >= 0)
+                    pre_apply_global(a.key_table, a.key_mask, a.seg_log, a.part_bits, a.slot_base[slot], a.stride, 1,
+                                     key, 1ull, (unsigned long long)(int64_t)(int32_t)(uint32_t)(ent >> 32), a.st);
+            }
+            const uint64_t o = !inb ? a.trash + (uint64_t)(jj * THREADS + tid)
+                                    : ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
+            a.b_key[o] = ent;
+            a.b_rel[o] = rel;
+        }
+        (void)tp;
+    };
+#pragma unroll
+    for (int jj = 0; jj < ITEMS; ++jj) {   // one store phase's memory operations before the loop (see partition3)
+        const uint64_t o = a.trash + (uint64_t)(jj * THREADS + tid);
+        a.b_key[o] = 0ull;
+        a.b_rel[o] = 0;
+    }
+    __syncthreads();
+    int it = 0;
+    for (int64_t tile = t_first; tile < ntiles; tile += G, ++it) {
+        const int b = it & 1;
+        const int64_t t0 = tile * kTile;
+        QMARK(5);
+        unsigned long long ent[ITEMS];
+        uint32_t r_pos[ITEMS];           // (p << 16 | rank) or ~0u
+        uint16_t r_rel[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) { consume(rk[j]); consume(rt[j]); consume(rv[j]); }
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const int64_t i = t0 + xof(j);
+            const int64_t key = (int64_t)rk[j];
+            const int64_t ts = rt[j];
+            uint64_t rel;
+            const uint64_t dd = (uint64_t)ts - (uint64_t)a.base_ts;
+            if (a.fast_m && dd < a.fast_lim) {
+                rel = (dd * a.fast_m) >> a.fast_sh;
+            } else {
+                const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
+                const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
+                const uint64_t uq = jm::udiv64(ud, c.g_div);
+                const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
+                rel = (uint64_t)(q - a.q_base);
+            }
+            uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
+            if (ds && ts == LONG_MIN_J) code = kCodeSlow;
+            if (a.any_null && i < a.n && row_has_null(a, i)) code = kCodeSlow;
+            if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
+            if (i == a.n - 1 && (a.n & 1)) code = kCodeSlow;        // unpaired last record: the v1 replay
+            if (code == kCodeAccept && ((int64_t)(int32_t)key != key || (uint32_t)key - 0x80000000u <= 1u ||
+                                        (int64_t)(int32_t)rv[j] != (int64_t)rv[j])) {
+                code = kCodeSlow;                                   // needs 64 bits (or an LDS key marker)
+                ++wide;
+            }
+            if (i >= a.n) code = 0xff;
+            dropped += code == kCodeDrop ? 1u : 0u;
+            note_drop(a.dropidx, a.st, code == kCodeDrop, i);
+            const bool slow = code == kCodeSlow;
+            const unsigned long long mk = __ballot(slow);
+            if (mk) {
+                const int leader = __ffsll((long long)mk) - 1;
+                int32_t sb = 0;
+                if (lane == leader) sb = atomicAdd(&a.st->spill_n, __popcll(mk));
+                sb = __shfl(sb, leader);
+                if (slow) put_idx(a.spill, sb + __popcll(mk & ((1ull << lane) - 1)), a.spill_cap, (int32_t)i, a.st);
+            }
+            r_pos[j] = ~0u;
+            ent[j] = (rk[j] & 0xffffffffull) | (rv[j] << 32);
+            r_rel[j] = (uint16_t)rel;
+            if (code == kCodeAccept) {
+                relmax = max(relmax, (uint32_t)rel);
+                relmin = min(relmin, (uint32_t)rel);
+                const uint64_t h = jm::mix64((uint64_t)key);
+                const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
+                r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
+            }
+        }
+        QMARK(0);
+        if (tile + G < ntiles) load(tile + G);   // the next tile in flight through the scan, scatter and stores
+        __syncthreads();
+        block_scan_np<THREADS>(hist, toff[b], wsum, a.np, &s_total[b]);
+        __syncthreads();
+        QMARK(1);
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            if (r_pos[j] == ~0u) continue;
+            const uint32_t p = r_pos[j] >> 16;
+            const uint32_t sidx = toff[b][p] + (r_pos[j] & 0xffffu);
+            x_ent[b][sidx] = ent[j];
+            x_rel[b][sidx] = r_rel[j];
+        }
+        // tile t-1's reservation base goes to gbase for its stores; then tile t's runs are reserved
+        const uint32_t h = tid < a.np ? hist[tid] : 0u;
+        if (tid < a.np) {
+            gbase[tid] = g_res;
+            hist[tid] = 0;                                  // the next tile's histogram
+            const uint64_t end = (uint64_t)g_res + h_res;
+            if (t_prev >= 0 && end > (uint64_t)a.capb)
+                atomicAdd(&a.st->ovf_n, (int32_t)(end - std::max<uint64_t>(g_res, (uint64_t)a.capb)));
+        }
+        g_res = h ? atomicAdd(&a.b_cnt[tid * kSub + sub], h) : 0u;
+        h_res = h;
+        __syncthreads();
+        QMARK(2);
+        if (t_prev >= 0) store_tile(b ^ 1, t_prev);
+        QMARK(3);
+        __syncthreads();                                    // buffer b ^ 1 free for tile t+1, gbase free
+        QMARK(4);
+        t_prev = tile;
+    }
+    // the last tile's stores
+    if (t_prev >= 0) {
+        if (tid < a.np) {
+            gbase[tid] = g_res;
+            const uint64_t end = (uint64_t)g_res + h_res;
+            if (end > (uint64_t)a.capb) atomicAdd(&a.st->ovf_n, (int32_t)(end - std::max<uint64_t>(g_res, (uint64_t)a.capb)));
+        }
+        __syncthreads();
+        store_tile((it - 1) & 1, t_prev);
+    }
+    if (a.prof && tid == 0) for (int q = 0; q < 6; ++q) a.prof[(int64_t)blockIdx.x * 8 + q] = pacc[q];
+#undef QMARK
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        dropped += __shfl_xor(dropped, sh);
+        wide += __shfl_xor(wide, sh);
+        relmax = max(relmax, (uint32_t)__shfl_xor((int)relmax, sh));
+        relmin = min(relmin, (uint32_t)__shfl_xor((int)relmin, sh));
+    }
+    if (lane == 0) {
+        if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
+        if (wide) atomicAdd(&a.st->wide_n, (int32_t)wide);
         if (relmin != ~0u) {
             atomicMax(&a.st->max_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmax));
             atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
@@ -1244,6 +1467,273 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
 }
 
 // ------------------------------------------------------------------------------------------------
+// combine_nk: Phase A of the narrow COUNT + SUM(BIGINT) shape (C2; partition3 NW entries, no window passes, no tile
+// pre-aggregation). Same contract as combine3<..., LAYOUT 1, NW 1>, with half the LDS bytes per entry:
+//  * the LDS key segment holds 32-bit key words: a narrow key as itself, kK32Empty for an empty slot, kK32Other for a
+//    slot holding any other key (64-bit, or one of those two values: Phase P sends such keys to the v1 path). A bucket
+//    probe is two ds_read_b128 instead of four, and a match needs no verification;
+//  * one packed accumulator word per (slot, slice): COUNT in bits 48-63, SUM + COUNT * 2^31 in bits 0-47 (each value
+//    biased by 2^31 into [0, 2^32)), so an entry is ONE ds_add_rtn_u64 instead of a u32 and a u64 atomic. The word is
+//    exact while COUNT < 2^16; the add that sees COUNT >= 2^15 moves the word out (CAS to 0) into the straggler list
+//    (applied with device atomics at the end), so a hot key never overflows it;
+//  * the per-chunk slice range is reduced with DPP (row_shr / row_bcast) instead of shuffles through LDS;
+//  * the home buckets of four entries are read before any is compared (one LDS round trip for four probes);
+//  * a slice leaving the window is read out of LDS and its HBM loads are issued, and the add + store completes after
+//    the next chunk's barrier (the loads' latency overlaps that chunk's probes).
+constexpr uint32_t kK32Empty = 0x80000000u;
+constexpr uint32_t kK32Other = 0x80000001u;
+constexpr unsigned long long kPkSumMask = (1ull << 48) - 1;
+
+__device__ __forceinline__ bool narrow_key_ok(int64_t key) {   // a key the 32-bit LDS table holds as itself
+    return (int64_t)(int32_t)key == key && (uint32_t)key != kK32Empty && (uint32_t)key != kK32Other;
+}
+__device__ __forceinline__ int64_t pk_sum(unsigned long long w) {   // SUM of a packed word (two's complement wrap)
+    return (int64_t)((w & kPkSumMask) - ((w >> 48) << 31));
+}
+__device__ __forceinline__ int wave_min_dpp(int x) {   // every lane's minimum over the wave (lane 63 holds it)
+    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x111, 0xf, 0xf, false));   // row_shr:1
+    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x112, 0xf, 0xf, false));   // row_shr:2
+    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x114, 0xf, 0xf, false));   // row_shr:4
+    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x118, 0xf, 0xf, false));   // row_shr:8
+    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return __builtin_amdgcn_readlane(x, 63);
+}
+__device__ __forceinline__ int wave_max_dpp(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(x, 63);
+}
+
+template <int IT, int TH>
+__global__ void __launch_bounds__(TH, 1) combine_nk_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
+    constexpr int SL = 2;
+    constexpr int kWaves = TH / 64;
+    constexpr int LPS = TH / kSub;
+    constexpr int kPer = 4096 / TH;    // slots per thread in a flush (seg <= 4096)
+    static_assert(LPS == 64 && IT % 4 == 0, "one wave per sub-bucket; probes in groups of four");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const EngineConst& c = *cp;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int sub = wv, li = lane;
+    const int p = blockIdx.x;
+    const int seg = 1 << a.seg_log;
+    const uint32_t smask = (uint32_t)seg - 1u;
+    uint32_t* lk = (uint32_t*)smem;                                         // [seg] key words
+    unsigned long long* lpk = (unsigned long long*)(smem + (size_t)seg * 4);   // [SL][seg] packed accumulators
+    __shared__ int s_mn[2][kWaves], s_mx[2][kWaves];
+    __shared__ StragL s_strag[kStragL];
+    __shared__ int s_sn, s_new;
+    long long pt = clock64();
+    long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
+    unsigned long long* gkeys = a.key_table + ((int64_t)p << a.seg_log);
+    for (int i = tid; i < seg; i += TH) {
+        const unsigned long long k = gkeys[i];
+        lk[i] = k == kEmptyKey ? kK32Empty : narrow_key_ok((int64_t)k) ? (uint32_t)k : kK32Other;
+    }
+    for (int i = tid; i < SL * seg; i += TH) lpk[i] = 0ull;
+    if (tid == 0) { s_new = 0; s_sn = 0; }
+    const int64_t my_cnt = min((int64_t)a.b_cnt[p * kSub + sub], a.capb);
+    const int64_t boff = ((int64_t)p * kSub + sub) * a.capb;
+    int64_t cnt = 0;
+    for (int s2 = 0; s2 < kSub; ++s2) cnt = max(cnt, min((int64_t)a.b_cnt[p * kSub + s2], a.capb));
+    const gc_u64_ptr bk = (const gc_u64_ptr)(a.b_key + boff);
+    const __attribute__((address_space(1))) uint16_t* br = (const __attribute__((address_space(1))) uint16_t*)(a.b_rel + boff);
+    constexpr int64_t kChunk = (int64_t)IT * LPS;
+    auto strag_add = [&](int rel, uint32_t g, uint32_t n, unsigned long long sum) {
+        const int si = atomicAdd(&s_sn, 1);
+        if (si < kStragL) s_strag[si] = StragL{g, n, rel, 0, sum, 0ull};
+        else strag_apply(a, c, rel, g, n, sum, 0ull);
+    };
+    // deferred flush: the slice's packed words (read out of LDS, which is cleared) and its HBM words in flight
+    int pend_rel = -1;
+    g_u64* pend_base = nullptr;
+    unsigned long long pw[kPer], po0[kPer], po1[kPer];
+    auto flush_issue = [&](int rel) {
+        const int w = rel & (SL - 1);
+        const int32_t slot = (rel >= 0 && rel < kRelCap) ? a.rel2slot[rel] : -1;
+        pend_base = slot >= 0 ? (g_u64*)a.slot_base[slot] : nullptr;
+        pend_rel = rel;
+#pragma unroll
+        for (int m = 0; m < kPer; ++m) {
+            const int i = tid + m * TH;
+            pw[m] = 0ull;
+            if (i < seg) { pw[m] = lpk[w * seg + i]; lpk[w * seg + i] = 0ull; }
+        }
+        if (pend_base) {
+#pragma unroll
+            for (int m = 0; m < kPer; ++m) {
+                const int64_t g = ((int64_t)p << a.seg_log) + tid + m * TH;
+                po0[m] = pw[m] ? pend_base[g] : 0ull;
+                po1[m] = pw[m] ? pend_base[a.stride + g] : 0ull;
+            }
+        }
+    };
+    auto flush_complete = [&]() {
+        if (pend_rel < 0) return;
+        if (pend_base) {
+#pragma unroll
+            for (int m = 0; m < kPer; ++m) {
+                if (!pw[m]) continue;
+                const int64_t g = ((int64_t)p << a.seg_log) + tid + m * TH;
+                pend_base[g] = po0[m] + (pw[m] >> 48);
+                pend_base[a.stride + g] = po1[m] + (unsigned long long)pk_sum(pw[m]);
+            }
+        }
+        pend_rel = -1;
+    };
+    __syncthreads();
+    unsigned long long nkey[IT];
+    int nrel[IT];
+    auto load_chunk = [&](int64_t cb) {
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const int64_t i = cb + (int64_t)j * LPS + li;
+            const bool ok = i < my_cnt;
+            nkey[j] = ok ? bk[i] : 0ull;
+            nrel[j] = ok ? (int)br[i] : -1;
+        }
+    };
+    load_chunk(0);
+    PMARK(0);
+    int lo = 0x7fffffff;
+    int it = 0;
+    for (int64_t cb = 0; cb < cnt; cb += kChunk, ++it) {
+        uint32_t k32[IT], vb[IT];
+        int rel[IT];
+        int rmin = 0x7fffffff, rmax = -1;
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            k32[j] = (uint32_t)nkey[j];
+            vb[j] = (uint32_t)(nkey[j] >> 32) ^ 0x80000000u;   // the int32 value biased by 2^31
+            rel[j] = nrel[j];
+            if (rel[j] >= 0) { rmin = min(rmin, rel[j]); rmax = max(rmax, rel[j]); }
+        }
+        PMARK(1);
+        if (cb + kChunk < cnt) load_chunk(cb + kChunk);
+        rmin = wave_min_dpp(rmin);
+        rmax = wave_max_dpp(rmax);
+        const int buf = it & 1;
+        if (lane == 0) { s_mn[buf][wv] = rmin; s_mx[buf][wv] = rmax; }
+        uint32_t pos[IT];
+#pragma unroll
+        for (int j = 0; j < IT; ++j) pos[j] = (uint32_t)jm::mix64((unsigned long long)(int64_t)(int32_t)k32[j]) & smask;
+        PMARK(2);
+        __syncthreads();
+        PMARK(3);
+        flush_complete();                   // the previous slide's merge (its loads overlapped the last chunk)
+        int cmin = 0x7fffffff, cmax = -1;
+#pragma unroll
+        for (int v = 0; v < kWaves; ++v) { cmin = min(cmin, s_mn[buf][v]); cmax = max(cmax, s_mx[buf][v]); }
+        if (cmax < 0) continue;
+        if (lo == 0x7fffffff) lo = cmin;
+        if (cmax >= lo + SL) {              // slide the window up to the chunk's newest slice
+            while (cmax >= lo + SL) {
+                flush_complete();           // a second slide in one chunk: finish the first one now
+                flush_issue(lo);
+                ++lo;
+                if (a.prof) pacc[7] += 1000;
+            }
+            __syncthreads();                // the cleared window slots before any add of this chunk
+        }
+        const int lo_c = lo;                // entries older than this are stragglers
+        PMARK(4);
+        // probes in groups of four: the four home buckets are read before any is compared
+        int32_t loc[IT];
+#pragma unroll
+        for (int j0 = 0; j0 < IT; j0 += 4) {
+            uint4 q[4][2];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint4* bp = (const uint4*)&lk[pos[j0 + u] & ~(uint32_t)(kBucket - 1)];
+                q[u][0] = bp[0];
+                q[u][1] = bp[1];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = j0 + u;
+                loc[j] = -2;
+                if (rel[j] < 0) continue;
+                const uint32_t kk = k32[j];
+                const uint32_t v[8] = {q[u][0].x, q[u][0].y, q[u][0].z, q[u][0].w, q[u][1].x, q[u][1].y, q[u][1].z, q[u][1].w};
+                uint32_t eq = 0, em = 0;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) { eq |= (uint32_t)(v[t] == kk) << t; em |= (uint32_t)(v[t] == kK32Empty) << t; }
+                uint32_t b = pos[j] & ~(uint32_t)(kBucket - 1);
+                int32_t found = eq ? (int32_t)(b + __builtin_ctz(eq)) : -1;
+                // not in the home bucket's snapshot: insert, or probe on (keys displaced past their bucket)
+                for (int round = 0; found < 0 && round <= (seg >> 3); ) {
+                    if (em) {                   // absent: insert at the first empty slot (CAS vs other lanes)
+                        const uint32_t sidx = b + __builtin_ctz(em);
+                        const uint32_t old = atomicCAS(&lk[sidx], kK32Empty, kk);
+                        if (old == kK32Empty) { found = (int32_t)sidx; atomicAdd(&s_new, 1); break; }
+                        if (old == kk) { found = (int32_t)sidx; break; }
+                    } else {
+                        b = (b + kBucket) & smask;
+                        ++round;
+                    }
+                    const uint4* bp = (const uint4*)&lk[b];   // (re-)read the bucket
+                    const uint4 r0 = bp[0], r1 = bp[1];
+                    const uint32_t w8[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+                    eq = 0; em = 0;
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) { eq |= (uint32_t)(w8[t] == kk) << t; em |= (uint32_t)(w8[t] == kK32Empty) << t; }
+                    if (eq) found = (int32_t)(b + __builtin_ctz(eq));
+                }
+                loc[j] = found;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            if (rel[j] < 0 || rel[j] >= lo + SL) continue;
+            const int32_t local = loc[j];
+            if (local < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
+            const uint32_t g = (uint32_t)(((int64_t)p << a.seg_log) + local);
+            if (rel[j] < lo_c) {            // older than the window: listed, applied with atomics at the end
+                if (a.prof) pacc[6] += 1000000;
+                strag_add(rel[j], g, 1u, (unsigned long long)(int64_t)(int32_t)(vb[j] ^ 0x80000000u));
+                continue;
+            }
+            unsigned long long* wp = &lpk[(size_t)(rel[j] & (SL - 1)) * seg + local];
+            const unsigned long long old = atomicAdd(wp, (1ull << 48) | vb[j]);
+            if (old >> 63) {                // COUNT reached 2^15: move the word out before it can overflow
+                unsigned long long cur = *wp;
+                while (cur >> 63) {
+                    const unsigned long long o2 = atomicCAS(wp, cur, 0ull);
+                    if (o2 == cur) { strag_add(rel[j], g, (uint32_t)(cur >> 48), (unsigned long long)pk_sum(cur)); break; }
+                    cur = o2;
+                }
+            }
+        }
+        PMARK(5);
+    }
+    __syncthreads();
+    flush_complete();
+    if (lo != 0x7fffffff)
+        for (int r = lo; r < lo + SL; ++r) { flush_issue(r); flush_complete(); }
+    __syncthreads();                    // every merge of this block stored before the stragglers' atomics
+    if (tid == 0 && s_sn) atomicAdd(&a.st->strag_n, s_sn);
+    for (int t = tid; t < min(s_sn, kStragL); t += TH) {
+        const StragL se = s_strag[t];
+        strag_apply(a, c, se.rel, se.g, se.n, se.x0, se.x1);
+    }
+    if (s_new) {                        // publish newly inserted keys (exclusive owner of this segment)
+        for (int i = tid; i < seg; i += TH) {
+            const uint32_t w = lk[i];
+            if (w != kK32Empty && w != kK32Other) gkeys[i] = (unsigned long long)(int64_t)(int32_t)w;
+        }
+        if (tid == 0) atomicAdd(&a.st->n_keys, (unsigned long long)s_new);
+    }
+    if (a.prof && tid == 0) for (int q = 0; q < 8; ++q) a.prof[(int64_t)p * 8 + q] = pacc[q];
+#undef PMARK
+}
+
+// ------------------------------------------------------------------------------------------------
 // fire
 
 struct FireWindow {
@@ -1457,7 +1947,8 @@ constexpr int kSlideAcc = 4;                      // COUNT + up to 3 integer-sum
 struct FireSlideArgs {
     const unsigned long long* key_table;
     int64_t capacity, stride;
-    const unsigned long long* const* upos;   // [m] slot base per union slice (nullptr: no records)
+    const unsigned long long* const* upos;   // [m] slot base per union slice (nullptr: no records); bit 0 set: the
+                                             // slice retires at this watermark -- its last read restores the identity
     int32_t m, nw, L, r;                     // union slices, windows, slices per window, per slide
     int64_t start0, slide, size;             // first window start, window step, window size
     int64_t* o_key;
@@ -1471,6 +1962,14 @@ struct FireSlideArgs {
 // NA = the handle's accumulator count (compile time: the running sums and the next window's slice values stay in
 // registers). The slices entering / leaving window w + 1 are loaded before window w's rows are reserved and written,
 // so their latency overlaps the ballot, the row reservation and the stores.
+// Slices that retire at this watermark (tagged upos entries) are cleared here instead of by reset_slots_kernel: the
+// read that subtracts a leaving slice is its last, and only the non-zero values are written back (a Zipf stream
+// leaves most keys absent from most slices, so this writes a fraction of the dense column reset_slots_kernel wrote).
+__device__ __forceinline__ unsigned long long* slide_ptr(const unsigned long long* p) {
+    return (unsigned long long*)((uintptr_t)p & ~(uintptr_t)1);
+}
+__device__ __forceinline__ bool slide_zero(const unsigned long long* p) { return ((uintptr_t)p & 1) != 0; }
+
 template <int NA>
 __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
@@ -1496,7 +1995,7 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
     __syncthreads();
     // window 0: the sum of its L slices
     for (int u = 0; u < f.L; ++u) {
-        const unsigned long long* b = s_u[u];
+        const unsigned long long* b = slide_ptr(s_u[u]);
         if (!b) continue;
 #pragma unroll
         for (int j = 0; j < kSlideJ; ++j) {
@@ -1517,8 +2016,8 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
                 for (int a = 0; a < NA; ++a) D[j][a] = 0;
             if (w1 >= f.nw) return;
             for (int t = 0; t < f.r; ++t) {
-                const unsigned long long* bin = s_u[(w1 - 1) * f.r + f.L + t];
-                const unsigned long long* bout = s_u[(w1 - 1) * f.r + t];
+                const unsigned long long* bin = slide_ptr(s_u[(w1 - 1) * f.r + f.L + t]);
+                const unsigned long long* bout = slide_ptr(s_u[(w1 - 1) * f.r + t]);
 #pragma unroll
                 for (int j = 0; j < kSlideJ; ++j) {
                     if (!present[j]) continue;
@@ -1544,8 +2043,10 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
             load_delta(w + 1);                      // in flight while this window's rows are reserved and written
         } else if (w > 0) {                         // S(w) = S(w - 1) + entering - leaving, in place
             for (int t = 0; t < f.r; ++t) {
-                const unsigned long long* bin = s_u[(w - 1) * f.r + f.L + t];
-                const unsigned long long* bout = s_u[(w - 1) * f.r + t];
+                const unsigned long long* bin = slide_ptr(s_u[(w - 1) * f.r + f.L + t]);
+                const unsigned long long* tout = s_u[(w - 1) * f.r + t];
+                unsigned long long* bout = slide_ptr(tout);
+                const bool zout = slide_zero(tout);
 #pragma unroll
                 for (int j = 0; j < kSlideJ; ++j) {
                     if (!present[j]) continue;
@@ -1555,6 +2056,7 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
                         const unsigned long long xin = bin ? bin[(int64_t)a * f.stride + k] : 0ull;
                         const unsigned long long xout = bout ? bout[(int64_t)a * f.stride + k] : 0ull;
                         S[j][a] = S[j][a] + xin - xout;
+                        if (zout && xout) bout[(int64_t)a * f.stride + k] = 0ull;
                     }
                 }
             }
@@ -1592,6 +2094,19 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
             }
         }
         __syncthreads();   // woff / s_base reuse
+    }
+    // retiring slices whose last window is the run's last one never left it: clear them now
+    for (int u = (f.nw - 1) * f.r; u < f.m; ++u) {
+        if (!slide_zero(s_u[u])) continue;
+        unsigned long long* b = slide_ptr(s_u[u]);
+#pragma unroll
+        for (int j = 0; j < kSlideJ; ++j) {
+            if (!present[j]) continue;
+            const int64_t k = k0 + (int64_t)j * kBlock + tid;
+#pragma unroll
+            for (int a = 0; a < NA; ++a)
+                if (b[(int64_t)a * f.stride + k]) b[(int64_t)a * f.stride + k] = 0ull;
+        }
     }
 }
 
@@ -2841,12 +3356,18 @@ __global__ void push_reset_kernel(DevStatus* st, unsigned long long* want, int32
 }
 
 // Restore the identities of a list of slots (every accumulator column; MIN columns 0xFF..) and clear
-// their touched flags: one launch for all slices a watermark retires (was 3 memsets per slot).
+// their touched flags: one launch for all slices a watermark retires (was 3 memsets per slot). An entry ~slot
+// (negative) was cleared by fire_slide_kernel: only its touched flag is reset.
 struct SlotList { int32_t n, id[15]; };   // up to 15 slot ids by value (no upload); more: the device list
 __global__ void reset_slots_kernel(unsigned long long* const* slot_base, const int32_t* list, SlotList inl, int64_t stride,
                                    int32_t* touched, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
-    const int32_t slot = inl.n ? inl.id[blockIdx.y] : list[blockIdx.y];
+    const int32_t sid = inl.n ? inl.id[blockIdx.y] : list[blockIdx.y];
+    const int32_t slot = sid < 0 ? ~sid : sid;
+    if (sid < 0) {   // cleared by the fire that read it last: the touched flag only
+        if (blockIdx.x == 0 && threadIdx.x == 0) touched[slot] = 0;
+        return;
+    }
     unsigned long long* base = slot_base[slot];
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
     for (int col = 0; col < c.nacc; ++col) {
@@ -2923,9 +3444,13 @@ int64_t gcd64(int64_t a, int64_t b) {
 // host engine
 
 struct SpState;                       // record-list window state (sparse.inc)
+struct DecPlan;                       // DECIMAL aggregates over 32-bit piece sums (decimal.inc)
 
 struct fwa_engine {
-    fwa_config cfg;
+    fwa_config cfg;                   // the engine's configuration (DECIMAL handles: the internal one, see decimal.inc)
+    DecPlan* dec = nullptr;
+    const void* dev_override[FWA_MAX_COLS] = {};   // stage_inputs: value columns already on the device
+    bool restoring = false;           // fwa_restore feeding fwa_push_partials
     EngineConst ec;
     EngineConst* d_ec = nullptr;
     hipStream_t stream = nullptr;
@@ -2952,6 +3477,7 @@ struct fwa_engine {
     int32_t* d_reset_list = nullptr;
     int32_t reset_cap = 0;
     std::vector<int32_t> touched;     // host mirror
+    std::vector<uint8_t> slot_clean;  // 1: a fire already restored the slot's identities (fire_slide)
     // slice directory
     DirEntry* d_dir = nullptr;
     bool dir_dirty = false;         // the host directory changed since the last publish (published before v1 ingest)
@@ -3059,6 +3585,18 @@ struct fwa_engine {
     // it and enqueued without a host sync; it is recycled at every stream synchronisation
     char* h_arena = nullptr;
     size_t arena_cap = 0, arena_used = 0;
+    // the arena is used in two halves: when one is full the other is taken over once the GPU consumed its copies
+    // (ev_arena[h], recorded when half h was left), so a pipelined caller that never drains the stream never stalls
+    int32_t arena_half = 0;
+    hipEvent_t ev_arena[2] = {};
+    hipEvent_t ev_st = nullptr;       // recorded after every status copy (enqueue_status)
+    bool st_ready = false;            // h_st already holds the pending push's status (waited on ev_st)
+    // fwa_advance_watermark_async: the fired rows of the last async advance, not yet taken by fwa_fired_output
+    bool af_pend = false;             // an output is waiting to be taken
+    bool af_gpu = false;              // ... and its fire is still in flight (row count on the device)
+    int64_t af_rows = 0;
+    int64_t* h_af_rows = nullptr;     // pinned landing of the in-flight fire's row count
+    hipEvent_t ev_af = nullptr;
     int32_t* h_touched = nullptr;     // pinned landing buffer of the touched-flag mirror
     int32_t h_touched_cap = 0;
     // FWA_CFG_RECORD_LISTS: TUMBLE window state as hash-partitioned record lists, aggregated at fire (sparse.inc)
@@ -3069,6 +3607,7 @@ struct fwa_engine {
     int64_t opt_out_min = 0;
     bool opt_partials_v1 = false;
     int32_t opt_profile = 0;
+    int32_t opt_exp = 3;                  // A/B of the narrow kernels (option 99, temporary)
     long long* d_prof = nullptr;          // FWA_OPT_PROFILE: per-block phase cycle counters of Phase P / A
 };
 
@@ -3117,7 +3656,7 @@ size_t type_size(int kind) {  // input width == result width for every kind exce
 }
 
 int validate(const fwa_config* c) {
-    if (c->abi_version != FWA_ABI_VERSION) return FWA_E_ARG;
+    if (c->abi_version != FWA_ABI_VERSION && c->abi_version != 3) return FWA_E_ARG;
     if (c->num_aggs < 0 || c->num_aggs > FWA_MAX_AGGS) return FWA_E_ARG;
     for (int j = 0; j < c->num_aggs; ++j) {
         if (c->aggs[j].kind < 0 || c->aggs[j].kind >= FWA_AGG_KIND_COUNT) return FWA_E_ARG;
@@ -3261,6 +3800,7 @@ int grow_slots(fwa_engine* e, int32_t add) {
         e->free_slots.push_back((int32_t)e->slot_ptr.size());
         e->slot_ptr.push_back(base);
         e->touched.push_back(0);
+        e->slot_clean.push_back(0);
         HIPCHK(e, hipMemsetAsync(base, 0, slot_bytes, e->stream));  // identities: 0; MIN columns 0xFF..
         for (int c = 1; c < e->nacc; ++c)
             if (e->ec.acc_kind[c] == ACC_MIN_ORD) HIPCHK(e, hipMemsetAsync(base + (int64_t)c * e->stride, 0xFF, col_bytes, e->stream));
@@ -3292,10 +3832,11 @@ int alloc_slice(fwa_engine* e, int64_t q) {
 
 // Queue a slot for identity restoration (untouched slots are still clean); flush_resets launches it.
 int reset_slot(fwa_engine* e, int32_t slot) {
-    if (e->touched[slot]) {
-        e->pending_reset.push_back(slot);
+    if (e->touched[slot]) {   // ~slot: identities already restored, only the touched flag is cleared
+        e->pending_reset.push_back(e->slot_clean[slot] ? ~slot : slot);
         e->touched[slot] = 0;
     }
+    e->slot_clean[slot] = 0;
     return FWA_OK;
 }
 
@@ -3398,6 +3939,7 @@ int stream_sync(fwa_engine* e) {
 
 // The one host synchronisation of a push / fire: device status + touched-flag mirror in one round trip.
 int enqueue_status(fwa_engine* e) {
+    e->st_ready = false;
     HIPCHK(e, hipMemcpyAsync(e->h_st, e->d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, e->stream));
     const int32_t ns = (int32_t)e->touched.size();
     if (ns > 0 && e->d_touched) {
@@ -3410,6 +3952,17 @@ int enqueue_status(fwa_engine* e) {
         }
         HIPCHK(e, hipMemcpyAsync(e->h_touched, e->d_touched, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, e->stream));
     }
+    HIPCHK(e, hipEventRecord(e->ev_st, e->stream));
+    return FWA_OK;
+}
+
+// Wait for the last status copy only (work enqueued after it keeps running): h_st and the touched mirror are then
+// the pending push's; push_settle then skips its own wait (st_ready).
+int wait_status_event(fwa_engine* e) {
+    HIPCHK(e, hipEventSynchronize(e->ev_st));
+    const int32_t ns = (int32_t)e->touched.size();
+    if (ns > 0 && e->d_touched) memcpy(e->touched.data(), e->h_touched, sizeof(int32_t) * ns);
+    e->st_ready = true;
     return FWA_OK;
 }
 
@@ -3433,19 +3986,23 @@ int sync_status(fwa_engine* e) {
 int upload(fwa_engine* e, void* dst, const void* src, size_t bytes) {
     if (!bytes) return FWA_OK;
     const size_t need = (bytes + 255) & ~(size_t)255;
-    if (need > e->arena_cap) {
+    if (2 * need > e->arena_cap) {
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (e->h_arena) HIPCHK(e, hipHostFree(e->h_arena));
         e->h_arena = nullptr;
-        e->arena_cap = std::max<size_t>(need * 2, (size_t)4 << 20);
+        e->arena_cap = std::max<size_t>(need * 4, (size_t)4 << 20);
         HIPCHK(e, hipHostMalloc((void**)&e->h_arena, e->arena_cap));
         e->arena_used = 0;
+        e->arena_half = 0;
     }
-    if (e->arena_used + need > e->arena_cap) {   // arena exhausted before a sync: drain the stream
-        int rc = stream_sync(e);
-        if (rc) return rc;
+    const size_t half = e->arena_cap / 2;
+    if (e->arena_used + need > half) {   // this half is full: move to the other once its copies are done
+        HIPCHK(e, hipEventRecord(e->ev_arena[e->arena_half], e->stream));
+        e->arena_half ^= 1;
+        HIPCHK(e, hipEventSynchronize(e->ev_arena[e->arena_half]));
+        e->arena_used = 0;
     }
-    char* p = e->h_arena + e->arena_used;
+    char* p = e->h_arena + (size_t)e->arena_half * half + e->arena_used;
     memcpy(p, src, bytes);
     HIPCHK(e, hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, e->stream));
     e->arena_used += need;
@@ -3463,6 +4020,7 @@ int reset_push_status(fwa_engine* e, bool v2bufs = false) {
 }  // namespace
 
 #include "sparse.inc"
+#include "decimal.inc"
 
 // ==================================================================================================
 // C-ABI
@@ -3476,7 +4034,7 @@ const char* fwa_last_error(const fwa_engine* e) { return e ? e->err.c_str() : "n
 // internal accessors for the host-only layers compiled into the same library (heap_snapshot.cpp)
 int fwa_get_config(const fwa_engine* e, fwa_config* out) {
     if (!e || !out) return FWA_E_ARG;
-    *out = e->cfg;
+    *out = e->dec ? e->dec->ucfg : e->cfg;
     if (e->sparse) out->flags |= FWA_CFG_RECORD_LISTS;   // reports the auto-selected mode too
     out->tz = e->tz.empty() ? nullptr : e->tz.data();    // the handle's own copy (valid while it lives)
     return FWA_OK;
@@ -3488,6 +4046,7 @@ void fwa_destroy(fwa_engine* e) {
     (void)hipSetDevice(e->cfg.device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     sp_destroy(e);
+    dec_free(e->dec);
     for (int c = 0; c < 3 + FWA_MAX_AGGS; ++c) if (e->lr_col[c]) (void)hipFree(e->lr_col[c]);
     if (e->d_late) (void)hipFree(e->d_late);
     if (e->d_lr_n) (void)hipFree(e->d_lr_n);
@@ -3509,15 +4068,40 @@ void fwa_destroy(fwa_engine* e) {
     if (e->h_touched) (void)hipHostFree(e->h_touched);
     for (hipEvent_t ev : e->ev) if (ev) (void)hipEventDestroy(ev);
     if (e->ev_in) (void)hipEventDestroy(e->ev_in);
+    for (hipEvent_t ev : e->ev_arena) if (ev) (void)hipEventDestroy(ev);
+    if (e->ev_st) (void)hipEventDestroy(e->ev_st);
+    if (e->ev_af) (void)hipEventDestroy(e->ev_af);
+    if (e->h_af_rows) (void)hipHostFree(e->h_af_rows);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
 
-int fwa_create(const fwa_config* cfg, fwa_engine** out) {
-    if (!cfg || !out) return FWA_E_ARG;
+static int create_engine(const fwa_config* cfg, fwa_engine** out);
+
+int fwa_create(const fwa_config* ucfg, fwa_engine** out) {
+    if (!ucfg || !out) return FWA_E_ARG;
     *out = nullptr;
-    const int v = validate(cfg);
+    if (ucfg->abi_version != FWA_ABI_VERSION && ucfg->abi_version != 3) return FWA_E_ARG;
+    fwa_config uc;                               // a version-3 caller's struct ends before dec_scale
+    memset(&uc, 0, sizeof(uc));
+    memcpy(&uc, ucfg, ucfg->abi_version == 3 ? offsetof(fwa_config, dec_scale) : sizeof(fwa_config));
+    const int v = validate(&uc);
     if (v) return v;
+    bool dec = false;
+    for (int j = 0; j < uc.num_aggs; ++j) dec |= is_dec_kind(uc.aggs[j].kind);
+    if (!dec) return create_engine(&uc, out);
+    if (uc.abi_version == 3) return FWA_E_ARG;   // no scales
+    DecPlan* P = new DecPlan();
+    fwa_config ic;
+    int rc = dec_plan(&uc, P, &ic);
+    if (!rc) rc = validate(&ic);
+    if (!rc) rc = create_engine(&ic, out);
+    if (rc) { delete P; return rc; }
+    (*out)->dec = P;
+    return FWA_OK;
+}
+
+static int create_engine(const fwa_config* cfg, fwa_engine** out) {
     fwa_engine* e = new fwa_engine();
     e->cfg = *cfg;
     if (cfg->tz_n > 0) e->tz.assign(cfg->tz, cfg->tz + 2 * (size_t)cfg->tz_n);
@@ -3678,10 +4262,14 @@ int fwa_create(const fwa_config* cfg, fwa_engine** out) {
         if (hipMemsetAsync(e->d_keys + cap, 0, 8, e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
         if (hipMalloc(&e->d_st, sizeof(DevStatus)) != hipSuccess) { rc = FWA_E_OOM; break; }
         if (hipHostMalloc(&e->h_st, sizeof(DevStatus)) != hipSuccess) { rc = FWA_E_OOM; break; }
+        if (hipHostMalloc(&e->h_af_rows, sizeof(int64_t)) != hipSuccess) { rc = FWA_E_OOM; break; }
         if (hipMemsetAsync(e->d_st, 0, sizeof(DevStatus), e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
         bool evok = true;
         for (hipEvent_t& ev : e->ev) evok = evok && hipEventCreate(&ev) == hipSuccess;
         evok = evok && hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) == hipSuccess;
+        for (hipEvent_t& ev : e->ev_arena) evok = evok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+        evok = evok && hipEventCreateWithFlags(&e->ev_st, hipEventDisableTiming) == hipSuccess;
+        evok = evok && hipEventCreateWithFlags(&e->ev_af, hipEventDisableTiming) == hipSuccess;
         if (!evok) { rc = FWA_E_DEVICE; break; }
         if (hipMalloc(&e->d_want, sizeof(unsigned long long) * kWantCap) != hipSuccess) { rc = FWA_E_OOM; break; }
         size_t fr = 0, tot = 0;
@@ -3733,6 +4321,7 @@ static int stage_inputs(fwa_engine* e, const int64_t* keys, const int64_t* ts, c
     for (int j = 0; j < e->cfg.num_aggs; ++j) {
         const fwa_agg_spec& s = e->cfg.aggs[j];
         if (s.kind == FWA_COUNT || s.kind == FWA_COUNT_COL || a.cols[s.col]) continue;
+        if (e->dev_override[s.col]) { a.cols[s.col] = e->dev_override[s.col]; continue; }   // DECIMAL pieces
         if (!cols || !cols[s.col]) return fail(e, FWA_E_ARG, "missing value column");
         a.cols[s.col] = put(cols[s.col], (size_t)n * type_size(s.kind));
     }
@@ -3954,6 +4543,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     const bool narrow = e->opt_narrow != 0 && (e->opt_narrow == 1 || e->narrow) && layout == 1 && e->nv == 1 &&
                         (vw & 1) && w16 && !pre && !a.pcount;
     e->narrow_used = narrow;
+    const bool mp = e->opt_mp == 1 || (e->opt_mp != 0 && e->mp);   // combiner window passes (slices smaller than chunks)
 #define P3LAUNCH(NV, IT, VW) do { \
         if (kgm == 0) partition3_kernel<NV, IT, 1024, VW, 0><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else if (kgm == 1) partition3_kernel<NV, IT, 1024, VW, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
@@ -3964,6 +4554,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else partition3_kernel<NV, 4, 1024, 3, 2, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
     if (pre) { if (e->nv == 0) PRELAUNCH(0); else PRELAUNCH(1); }
     else if (e->nv == 0) P3LAUNCH(0, 8, 3);
+    else if (narrow && !mp && (e->opt_exp & 1)) partition_nk_kernel<6, 1024><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (narrow) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
@@ -4001,8 +4592,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     HIPCHK(e, hipEventRecord(e->ev[6], e->stream));
     const size_t seg3 = (size_t)1 << e->seg_log;
     const size_t lds3 = seg3 * 8 + 2 * seg3 * 4 + (size_t)(e->nacc - 1) * 2 * seg3 * 8 + 4 * 4 * kSub + 16;
-    const bool mp = e->opt_mp == 1 || (e->opt_mp != 0 && e->mp);
-#define C3M(IT, TH, NV, LY, PR) do { if (mp) combine3_kernel<IT, 2, NV, TH, LY, PR, 1><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); \
+    // window passes: 2 entries per lane and chunk -- the passes' extra live state at 4 entries spilled up to 250 B per
+    // lane to scratch (1024-thread blocks cap a lane at 128 VGPRs), and that build merged wrong counts (r04: the
+    // window-pass parity failures); at 2 the spills are a few words
+#define C3M(IT, TH, NV, LY, PR) do { if (mp) combine3_kernel<2, 2, NV, TH, LY, PR, 1><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); \
         else combine3_kernel<IT, 2, NV, TH, LY, PR, 0><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); } while (0)
 #define C3L(IT, TH, NV) do { \
         if (pre && layout == 1) C3M(IT, TH, 1, 1, 1); \
@@ -4011,7 +4604,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else if (layout == 2) C3M(IT, TH, NV, 2, 0); \
         else C3M(IT, TH, NV, 0, 0); } while (0)
     if (narrow) {   // packed entries free the prefetch registers: 8 entries per lane and chunk (4 with window passes)
-        if (mp) combine3_kernel<4, 2, 1, 1024, 1, 0, 1, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        if (mp) combine3_kernel<2, 2, 1, 1024, 1, 0, 1, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
+        else if (e->opt_exp & 2) combine_nk_kernel<8, 1024><<<e->np, 1024, seg3 * 4 + 2 * seg3 * 8, e->stream>>>(ca, e->d_ec);
         else combine3_kernel<8, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
     } else if (e->nv == 0) C3L(4, 1024, 0);
     else if (e->nv == 1) C3L(4, 1024, 1);
@@ -4430,40 +5024,8 @@ static int fire_sessions(fwa_engine* e, int64_t wm, int64_t* nrows) {
 // Fire kernel over a list of windows (each a union of slots). raw = 1 emits the accumulators and
 // COUNT(*) instead of the final aggregate values (fwa_drain_partials).
 static int emit_late_rows(fwa_engine* e);
-static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const std::vector<int32_t>& hs, int raw,
-                       int64_t* nrows, int64_t row0 = 0) {
-    // windows and their slot list in one buffer: one upload
-    if ((int32_t)hw.size() > e->win_cap || (int32_t)hs.size() > e->win_slots_cap) {
-        if (e->d_win) HIPCHK(e, hipFree(e->d_win));
-        e->d_win = nullptr;
-        e->win_cap = std::max<int32_t>(e->win_cap, (int32_t)hw.size() * 2);
-        e->win_slots_cap = std::max<int32_t>(e->win_slots_cap, (int32_t)hs.size() * 2);
-        HIPCHK(e, hipMalloc(&e->d_win, sizeof(FireWindow) * e->win_cap + sizeof(int32_t) * e->win_slots_cap));
-        e->d_win_slots = (int32_t*)(e->d_win + e->win_cap);
-    }
-    std::vector<char> wbuf(sizeof(FireWindow) * e->win_cap + sizeof(int32_t) * hs.size());
-    memcpy(wbuf.data(), hw.data(), sizeof(FireWindow) * hw.size());
-    memcpy(wbuf.data() + sizeof(FireWindow) * e->win_cap, hs.data(), sizeof(int32_t) * hs.size());
-    int rc = upload(e, e->d_win, wbuf.data(), wbuf.size());
-    if (rc) return rc;
-    // rows <= windows x distinct keys; n_keys is current: every push ends with a status sync
-    const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
-    // Output sizing: rows <= windows x live keys, which is tens of GB for 1e8 keys (C4) although a
-    // window holds far fewer rows. Start from min(bound, max(current capacity, 4M rows)); the kernel
-    // counts rows past the capacity without writing them, and the host grows once and relaunches.
-    const int64_t bound = (int64_t)hw.size() * nkeys + row0;
-    const int64_t floor_rows = e->opt_out_min > 0 ? e->opt_out_min : ((int64_t)1 << 22);   // tests force the relaunch
-    rc = ensure_out(e, std::min<int64_t>(bound, std::max<int64_t>(e->out_cap, floor_rows + row0)));
-    if (rc) return rc;
-  relaunch:
-    if (row0 > 0) {   // late-firing rows of the pushes since the last watermark go first
-        rc = emit_late_rows(e);
-        if (rc) return rc;
-        rc = upload(e, &e->d_st->rows, &row0, 8);
-        if (rc) return rc;
-    } else {
-        HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
-    }
+// Enqueue the fire of windows hw (slot lists hs) into the output columns (rows from row0 on; no host wait).
+static int enqueue_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const std::vector<int32_t>& hs, int raw) {
     FireArgs f;
     memset(&f, 0, sizeof(f));
     f.key_table = e->d_keys;
@@ -4493,6 +5055,49 @@ static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const s
     else fire_kernel<0><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
+    return FWA_OK;
+}
+
+// Windows and their slot list to the device (one upload through the arena).
+static int upload_windows(fwa_engine* e, const std::vector<FireWindow>& hw, const std::vector<int32_t>& hs) {
+    if ((int32_t)hw.size() > e->win_cap || (int32_t)hs.size() > e->win_slots_cap) {
+        if (e->d_win) HIPCHK(e, hipFree(e->d_win));
+        e->d_win = nullptr;
+        e->win_cap = std::max<int32_t>(e->win_cap, (int32_t)hw.size() * 2);
+        e->win_slots_cap = std::max<int32_t>(e->win_slots_cap, (int32_t)hs.size() * 2);
+        HIPCHK(e, hipMalloc(&e->d_win, sizeof(FireWindow) * e->win_cap + sizeof(int32_t) * e->win_slots_cap));
+        e->d_win_slots = (int32_t*)(e->d_win + e->win_cap);
+    }
+    std::vector<char> wbuf(sizeof(FireWindow) * e->win_cap + sizeof(int32_t) * hs.size());
+    memcpy(wbuf.data(), hw.data(), sizeof(FireWindow) * hw.size());
+    memcpy(wbuf.data() + sizeof(FireWindow) * e->win_cap, hs.data(), sizeof(int32_t) * hs.size());
+    return upload(e, e->d_win, wbuf.data(), wbuf.size());
+}
+
+static int launch_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const std::vector<int32_t>& hs, int raw,
+                       int64_t* nrows, int64_t row0 = 0) {
+    int rc = upload_windows(e, hw, hs);
+    if (rc) return rc;
+    // rows <= windows x distinct keys; n_keys is current: every push ends with a status sync
+    const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
+    // Output sizing: rows <= windows x live keys, which is tens of GB for 1e8 keys (C4) although a
+    // window holds far fewer rows. Start from min(bound, max(current capacity, 4M rows)); the kernel
+    // counts rows past the capacity without writing them, and the host grows once and relaunches.
+    const int64_t bound = (int64_t)hw.size() * nkeys + row0;
+    const int64_t floor_rows = e->opt_out_min > 0 ? e->opt_out_min : ((int64_t)1 << 22);   // tests force the relaunch
+    rc = ensure_out(e, std::min<int64_t>(bound, std::max<int64_t>(e->out_cap, floor_rows + row0)));
+    if (rc) return rc;
+  relaunch:
+    if (row0 > 0) {   // late-firing rows of the pushes since the last watermark go first
+        rc = emit_late_rows(e);
+        if (rc) return rc;
+        rc = upload(e, &e->d_st->rows, &row0, 8);
+        if (rc) return rc;
+    } else {
+        HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
+    }
+    rc = enqueue_fire(e, hw, hs, raw);
+    if (rc) return rc;
     rc = sync_status(e);
     if (rc) return rc;
     *nrows = (int64_t)e->h_st->rows;
@@ -4605,12 +5210,20 @@ static int collect_late_indices(fwa_engine* e) {
 static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, bool status_enqueued,
                        int64_t* late_dropped_out);
 
-// Settle an FWA_PUSH_ASYNC push (first thing every stateful entry point does).
-static int settle_pending(fwa_engine* e) {
+static int finish_afire(fwa_engine* e);
+
+// Settle an FWA_PUSH_ASYNC push (the pushes do this first: an asynchronous watermark's fire may keep running).
+static int settle_push(fwa_engine* e) {
     if (!e->pend) return FWA_OK;
     e->pend = false;
     IngestArgs a = e->pend_a;
     return push_settle(e, a, e->pend_n, e->pend_v2, true, nullptr);
+}
+
+// ... and every other stateful entry point: also account a completed fwa_advance_watermark_async fire.
+static int settle_pending(fwa_engine* e) {
+    if (int rc = finish_afire(e)) return rc;
+    return settle_push(e);
 }
 
 static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, bool async, int64_t* late_dropped_out) {
@@ -4649,7 +5262,9 @@ static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, boo
     bool republish = false;
     std::vector<int32_t> late_idx;
     for (int round = 0;; ++round) {
-        rc = (round == 0 && status_enqueued) ? wait_status(e) : sync_status(e);
+        if (round == 0 && status_enqueued && e->st_ready) rc = FWA_OK;   // waited by wait_status_event
+        else rc = (round == 0 && status_enqueued) ? wait_status(e) : sync_status(e);
+        e->st_ready = false;
         if (rc) return rc;
         if (e->v2_timing_pending) {
             float ms = 0.f;
@@ -4733,9 +5348,31 @@ int fwa_push(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* 
     return fwa_push_nullable(e, keys, ts, val_cols, nullptr, key_hash, n, flags, late_dropped_out);
 }
 
+static int push_body(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
+                     const uint8_t* const* null_cols, const int32_t* key_hash, int64_t n, int32_t flags,
+                     int64_t* late_dropped_out);
+
 int fwa_push_nullable(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
                       const uint8_t* const* null_cols, const int32_t* key_hash, int64_t n, int32_t flags,
                       int64_t* late_dropped_out) {
+    if (!e) return FWA_E_STATE;
+    if (!e->dec || n <= 0 || n > INT32_MAX || !keys || !ts)
+        return push_body(e, keys, ts, val_cols, null_cols, key_hash, n, flags, late_dropped_out);
+    // DECIMAL columns -> piece columns on the GPU, then the ordinary push over the internal configuration
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (int rc0 = settle_push(e)) return rc0;    // a pending push may still replay from the piece columns
+    const bool device = (flags & FWA_PUSH_DEVICE_PTRS) != 0;
+    if (device) { if (int rc1 = wait_input_stream(e)) return rc1; }
+    const void* vals[FWA_MAX_COLS];
+    int rc = dec_split(e, val_cols, null_cols, n, device, vals);
+    if (!rc) rc = push_body(e, keys, ts, vals, null_cols, key_hash, n, flags, late_dropped_out);
+    for (int c = 0; c < FWA_MAX_COLS; ++c) e->dev_override[c] = nullptr;
+    return rc;
+}
+
+static int push_body(fwa_engine* e, const int64_t* keys, const int64_t* ts, const void* const* val_cols,
+                     const uint8_t* const* null_cols, const int32_t* key_hash, int64_t n, int32_t flags,
+                     int64_t* late_dropped_out) {
     if (!e) return FWA_E_STATE;
     if (n < 0 || (n > 0 && (!keys || !ts))) return fail(e, FWA_E_ARG, "null input column");
     if (e->cfg.key_kind == FWA_KEY_PREHASHED && n > 0 && !key_hash) return fail(e, FWA_E_ARG, "PREHASHED keys need key_hash");
@@ -4743,7 +5380,7 @@ int fwa_push_nullable(fwa_engine* e, const int64_t* keys, const int64_t* ts, con
     if (late_dropped_out) *late_dropped_out = 0;
     if (n == 0) { e->late_idx.clear(); return FWA_OK; }
     HIPCHK(e, hipSetDevice(e->cfg.device));
-    if (int rc0 = settle_pending(e)) return rc0;
+    if (int rc0 = settle_push(e)) return rc0;
     IngestArgs a;
     memset(&a, 0, sizeof(a));
     a.n = n;
@@ -4814,6 +5451,7 @@ int fwa_push_nullable(fwa_engine* e, const int64_t* keys, const int64_t* ts, con
 int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_ts, const int64_t* count,
                       const void* const* acc, int64_t n, int32_t flags, int64_t* late_dropped_out) {
     if (!e) return FWA_E_STATE;
+    if (e->dec && !e->restoring) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of DECIMAL aggregates");
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
     if (n < 0 || (n > 0 && (!keys || !slice_ts || !count))) return fail(e, FWA_E_ARG, "null input column");
     if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "partials need a computable key hash");
@@ -4821,7 +5459,7 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
     if (late_dropped_out) *late_dropped_out = 0;
     if (n == 0) { e->late_idx.clear(); return FWA_OK; }
     HIPCHK(e, hipSetDevice(e->cfg.device));
-    if (int rc0 = settle_pending(e)) return rc0;
+    if (int rc0 = settle_push(e)) return rc0;
     IngestArgs a;
     memset(&a, 0, sizeof(a));
     a.n = n;
@@ -4904,6 +5542,7 @@ static int retire_slices(fwa_engine* e, int64_t wm) {
 // accumulators of every touched slice complete at wm, reset them, forward the watermark.
 int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     if (!e || !out) return FWA_E_ARG;
+    if (e->dec) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of DECIMAL aggregates");
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
@@ -5251,7 +5890,9 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
         for (int j = 0; j < na; ++j) acc[j] = body + (size_t)(3 + j) * n + lo;
         for (int h = 0; h < nh; ++h) acc[na + h] = body + (size_t)(3 + na + h) * n + lo;
         int64_t late = 0;
+        e->restoring = true;
         int rc = fwa_push_partials(e, body + lo, body + (size_t)n + lo, body + (size_t)2 * n + lo, acc, hi - lo, 0, &late);
+        e->restoring = false;
         if (rc) return rc;
         if (late) return fail(e, FWA_E_STATE, "restored partials were dropped as late");
     }
@@ -5268,7 +5909,10 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
 
 // A run of consecutive hop windows with invertible accumulators: fire_slide_kernel. *done = false
 // leaves the run to the generic fire.
-static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>& wins, int64_t* nrows, bool* done) {
+// The run's slices that retire at wm (their last window is in the run; the same test retire_slices applies next) are
+// cleared by the kernel itself and released without reset_slots_kernel's dense column writes.
+static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>& wins, int64_t wm, int64_t* nrows,
+                      bool* done) {
     *done = false;
     if (e->nacc > kSlideAcc || e->cfg.nullable_cols) return FWA_OK;
     for (int c = 1; c < e->nacc; ++c) if (e->ec.acc_kind[c] != ACC_ADD_I64) return FWA_OK;
@@ -5285,16 +5929,28 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     if (m > kSlideMaxU) return FWA_OK;
     const int64_t q0 = slice_q(e, start0);
     std::vector<const unsigned long long*> up(m, nullptr);
+    std::vector<int32_t> cleared;
     bool any = false;
     for (int64_t i = 0; i < m; ++i) {
         auto it = e->live.find(q0 + i);
-        if (it != e->live.end() && e->touched[it->second]) { up[i] = e->slot_ptr[it->second]; any = true; }
+        if (it == e->live.end() || !e->touched[it->second]) continue;
+        up[i] = e->slot_ptr[it->second];
+        any = true;
+        int64_t thr;
+        bool always;
+        accept_threshold(e, q0 + i, &thr, &always);
+        if (i < nw * r && !always && wm >= thr) {   // retires right after this fire: the kernel clears it
+            up[i] = (const unsigned long long*)((uintptr_t)up[i] | 1);
+            cleared.push_back(it->second);
+        }
     }
     *done = true;
     if (!any) return FWA_OK;
     if (!e->d_upos) HIPCHK(e, hipMalloc(&e->d_upos, sizeof(void*) * kSlideMaxU));
     int rc = upload(e, e->d_upos, up.data(), sizeof(void*) * m);
     if (rc) return rc;
+    // every present key emits at most one row per window: with the key count exact after the settled push the
+    // output bound holds, so the launch (which clears slices as it reads them) runs exactly once
     const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
     rc = ensure_out(e, nw * nkeys);
     if (rc) return rc;
@@ -5333,10 +5989,12 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     if (rc) return rc;
     *nrows = (int64_t)e->h_st->rows;
     if (*nrows > e->out_cap) {   // n_keys was stale: grow to the exact count and fire again (idempotent)
+        if (!cleared.empty()) return fail(e, FWA_E_STATE, "sliding fire exceeded its output bound");
         rc = ensure_out(e, *nrows);
         if (rc) return rc;
         goto relaunch;
     }
+    for (int32_t s : cleared) e->slot_clean[s] = 1;   // retire_slices releases them without a reset
     float ms = 0.f;
     HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
     e->fire_ms += ms;
@@ -5380,9 +6038,78 @@ static int speculative_fire(fwa_engine* e, int64_t wm, int64_t* nrows, bool* ok)
     return FWA_OK;
 }
 
+// The output columns of the last fire (nrows rows) as an fwa_out (device pointers, or host copies in h_out).
+static int fill_out(fwa_engine* e, int64_t nrows, fwa_out* out) {
+    memset(out, 0, sizeof(*out));
+    out->n_rows = nrows;
+    // the caller's aggregates: DECIMAL ones finished from their piece sums (decimal.inc), the others as fired
+    const int na = e->dec ? e->dec->ucfg.num_aggs : e->cfg.num_aggs;
+    const void* col[FWA_MAX_AGGS];
+    const uint8_t* nul[FWA_MAX_AGGS];
+    size_t width[FWA_MAX_AGGS];
+    if (e->dec) {
+        if (int rc = dec_finish(e, nrows)) return rc;
+        for (int j = 0; j < na; ++j) {
+            if (e->dec->d[j].kind) { col[j] = e->dec->d_out[j]; nul[j] = e->dec->d_null[j]; width[j] = 16; continue; }
+            const int i = e->dec->umap[j];
+            col[j] = e->o_agg[i];
+            nul[j] = e->o_null[i];
+            width[j] = type_size(e->cfg.aggs[i].kind);
+        }
+    } else {
+        for (int j = 0; j < na; ++j) { col[j] = e->o_agg[j]; nul[j] = e->o_null[j]; width[j] = type_size(e->cfg.aggs[j].kind); }
+    }
+    out->num_aggs = na;
+    if (e->cfg.output_on_device) {
+        out->on_device = 1;
+        out->key = e->o_key;
+        out->win_start = e->o_start;
+        out->win_end = e->o_end;
+        for (int j = 0; j < na; ++j) { out->agg[j] = col[j]; out->agg_null[j] = nul[j]; }
+        return FWA_OK;
+    }
+    out->on_device = 0;
+    e->h_out.resize(std::max<size_t>((size_t)nrows * (25 + 17 * (size_t)na), 8));
+    char* p = e->h_out.data();
+    hipError_t err = hipSuccess;
+    auto get = [&](const void* src, size_t bytes) -> const void* {
+        if (bytes) { hipError_t r = hipMemcpy(p, src, bytes, hipMemcpyDeviceToHost); if (r != hipSuccess) err = r; }
+        const void* r = p;
+        p += bytes;
+        return r;
+    };
+    out->key = (const int64_t*)get(e->o_key, 8 * nrows);
+    out->win_start = (const int64_t*)get(e->o_start, 8 * nrows);
+    out->win_end = (const int64_t*)get(e->o_end, 8 * nrows);
+    for (int j = 0; j < na; ++j) out->agg[j] = get(col[j], width[j] * nrows);
+    for (int j = 0; j < na; ++j)
+        if (nul[j]) out->agg_null[j] = (const uint8_t*)get(nul[j], (size_t)nrows);
+    HIPCHK(e, err);
+    return FWA_OK;
+}
+
+// Account an in-flight fwa_advance_watermark_async fire once it completed (its rows stay in the output columns).
+static int finish_afire(fwa_engine* e) {
+    if (!e->af_gpu) return FWA_OK;
+    HIPCHK(e, hipEventSynchronize(e->ev_af));
+    e->af_gpu = false;
+    const int64_t rows = *e->h_af_rows;
+    if (rows > e->out_cap) return fail(e, FWA_E_STATE, "asynchronous fire exceeded its output bound");
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+    e->fire_ms += ms;
+    e->fire_launches++;
+    e->fire_rows += rows;
+    e->rows_out += rows;
+    e->af_rows = rows;
+    return FWA_OK;
+}
+
 int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
     if (!e) return FWA_E_STATE;
     HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (int rcf = finish_afire(e)) return rcf;
+    e->af_pend = false;                          // an untaken asynchronous output is overwritten
     int64_t nrows = 0;
     bool spec_done = false;
     if (e->pend && e->kind == FWA_TUMBLE && wm > e->wm && e->late_rows == 0) {
@@ -5416,7 +6143,7 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
         }
         bool slid = false;
         if (e->kind == FWA_SLIDE && wins.size() >= 2 && e->late_rows == 0) {
-            int rc = fire_slide(e, wins, &nrows, &slid);
+            int rc = fire_slide(e, wins, wm, &nrows, &slid);
             if (rc) return rc;
         }
         std::vector<FireWindow> hw;
@@ -5454,36 +6181,69 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
         e->late_rows = 0;
     }
     e->rows_out += nrows;
-    if (out) {
-        out->n_rows = nrows;
-        out->num_aggs = e->cfg.num_aggs;
-        if (e->cfg.output_on_device) {
-            out->on_device = 1;
-            out->key = e->o_key;
-            out->win_start = e->o_start;
-            out->win_end = e->o_end;
-            for (int j = 0; j < e->cfg.num_aggs; ++j) { out->agg[j] = e->o_agg[j]; out->agg_null[j] = e->o_null[j]; }
-        } else {
-            out->on_device = 0;
-            e->h_out.resize(std::max<size_t>((size_t)nrows * 9 * (3 + e->cfg.num_aggs), 8));
-            char* p = e->h_out.data();
-            hipError_t err = hipSuccess;
-            auto get = [&](const void* src, size_t bytes) -> const void* {
-                if (bytes) { hipError_t r = hipMemcpy(p, src, bytes, hipMemcpyDeviceToHost); if (r != hipSuccess) err = r; }
-                const void* r = p;
-                p += bytes;
-                return r;
-            };
-            out->key = (const int64_t*)get(e->o_key, 8 * nrows);
-            out->win_start = (const int64_t*)get(e->o_start, 8 * nrows);
-            out->win_end = (const int64_t*)get(e->o_end, 8 * nrows);
-            for (int j = 0; j < e->cfg.num_aggs; ++j) out->agg[j] = get(e->o_agg[j], type_size(e->cfg.aggs[j].kind) * nrows);
-            for (int j = 0; j < e->cfg.num_aggs; ++j)
-                if (e->o_null[j]) out->agg_null[j] = (const uint8_t*)get(e->o_null[j], (size_t)nrows);
-            HIPCHK(e, err);
+    e->af_rows = nrows;
+    if (out) return fill_out(e, nrows, out);
+    return FWA_OK;
+}
+
+// Watermark advance that returns before the fire completes (include/flink_amd.h): a TUMBLE fire after an
+// FWA_PUSH_ASYNC push is enqueued speculatively, the host waits only for the push's status (the fire runs meanwhile)
+// and, when the push needed nothing replayed, retires the fired slices and returns; the next push can then be
+// enqueued while the fire runs. Anything else takes the synchronous path. The rows: fwa_fired_output.
+int fwa_advance_watermark_async(fwa_engine* e, int64_t wm) {
+    if (!e) return FWA_E_STATE;
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (int rcf = finish_afire(e)) return rcf;
+    e->af_pend = false;
+    if (e->pend && e->pend_v2 && e->kind == FWA_TUMBLE && wm > e->wm && e->late_rows == 0 && !e->sparse) {
+        std::vector<FireWindow> hw;
+        std::vector<int32_t> hs;
+        for (auto& kv : e->live) {   // as speculative_fire: untouched slots emit nothing
+            FireWindow f;
+            f.start = slice_start(e, kv.first);
+            f.end = jm::wadd(f.start, e->g);
+            const int64_t mt = trig(e, jm::wsub(f.end, 1));
+            if (!(mt > e->wm && mt <= wm)) continue;
+            f.slot_off = (int32_t)hs.size();
+            f.nslots = 1;
+            hs.push_back(kv.second);
+            hw.push_back(f);
+        }
+        if (!hw.empty()) {
+            // every row of the fire must fit: windows x keys (keys known at the last status + the pending push's)
+            const int64_t nk = std::min<int64_t>(e->capacity + 1, (int64_t)e->h_st->n_keys + e->pend_n);
+            int rc = ensure_out(e, (int64_t)hw.size() * std::max<int64_t>(nk, 1));
+            if (rc) return rc;
+            if ((rc = upload_windows(e, hw, hs))) return rc;
+            HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
+            if ((rc = enqueue_fire(e, hw, hs, 0))) return rc;
+            HIPCHK(e, hipMemcpyAsync(e->h_af_rows, &e->d_st->rows, 8, hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(e, hipEventRecord(e->ev_af, e->stream));
+            if ((rc = wait_status_event(e))) return rc;   // the push's status; the fire keeps running
+            const DevStatus st = *e->h_st;
+            if (st.spill_n == 0 && st.late_fire == 0 && st.error == 0) {
+                e->af_gpu = true;
+                e->af_pend = true;
+                if ((rc = retire_slices(e, wm))) return rc;   // resets enqueued behind the fire
+                if ((rc = settle_push(e))) return rc;      // no wait (st_ready)
+                e->wm = wm;
+                return FWA_OK;
+            }
+            HIPCHK(e, hipEventSynchronize(e->ev_af));         // the speculation failed: the synchronous path
         }
     }
+    int rc = fwa_advance_watermark(e, wm, nullptr);
+    if (rc) return rc;
+    e->af_pend = true;
     return FWA_OK;
+}
+
+int fwa_fired_output(fwa_engine* e, fwa_out* out) {
+    if (!e || !out) return FWA_E_ARG;
+    if (!e->af_pend) return fail(e, FWA_E_STATE, "no fwa_advance_watermark_async output to take");
+    if (int rc = finish_afire(e)) return rc;
+    e->af_pend = false;
+    return fill_out(e, e->af_rows, out);
 }
 
 int fwa_flush(fwa_engine* e) {
@@ -5547,6 +6307,7 @@ int fwa_set_option(fwa_engine* e, int32_t option, int64_t value) {
         case FWA_OPT_PARTIALS_ONE_PASS: e->opt_partials_v1 = value > 0; return FWA_OK;
         case FWA_OPT_SP_TABLE: case FWA_OPT_SP_FMAX: case FWA_OPT_SP_BUDGET: return sp_set_option(e, option, value);
         case FWA_OPT_PROFILE: e->opt_profile = value > 0 ? 1 : 0; return FWA_OK;
+        case 99: e->opt_exp = (int32_t)value; return FWA_OK;
         default: return fail(e, FWA_E_ARG, "unknown option");
     }
 }

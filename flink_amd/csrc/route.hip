@@ -148,9 +148,7 @@ extern "C" int fwa_unpack_rows(const int64_t* rows, int64_t n, int32_t ncols, in
     hipStream_t st = (hipStream_t)stream;
     const int nb = (int)std::min<int64_t>(4096, (n + kRouteBlock - 1) / kRouteBlock);
     hipLaunchKernelGGL(unpack_rows_kernel, dim3(nb), dim3(kRouteBlock), 0, st, rows, n, ncols, o);
-    const hipError_t e1 = hipGetLastError();
-    const hipError_t e2 = hipStreamSynchronize(st);
-    return (e1 == hipSuccess && e2 == hipSuccess) ? FWA_OK : FWA_E_DEVICE;
+    return hipGetLastError() == hipSuccess ? FWA_OK : FWA_E_DEVICE;   // stream-ordered: no host synchronisation
 }
 
 extern "C" int fwa_route_rows(const int64_t* keys, const int32_t* key_hash, int64_t n, int32_t key_kind,
@@ -186,7 +184,6 @@ extern "C" int fwa_route_rows(const int64_t* keys, const int32_t* key_hash, int6
     hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, st, hist, (int64_t)parallelism * nb, parallelism, nb, counts);
     hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteBlock), 0, st, a);
     const hipError_t e1 = hipGetLastError();
-    const hipError_t e2 = hipFreeAsync(hist, st);
-    const hipError_t e3 = hipStreamSynchronize(st);
-    return (e1 == hipSuccess && e2 == hipSuccess && e3 == hipSuccess) ? FWA_OK : FWA_E_DEVICE;
+    const hipError_t e2 = hipFreeAsync(hist, st);                    // stream-ordered: no host synchronisation
+    return (e1 == hipSuccess && e2 == hipSuccess) ? FWA_OK : FWA_E_DEVICE;
 }

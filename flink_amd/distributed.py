@@ -30,6 +30,15 @@ from . import _abi as A
 from .keygroups import key_group_range_for_operator
 
 
+def choose_exchange(cfg_kw):
+    """The keyBy plan for a configuration: "partials" (two-phase, TwoStageOptimizedWindowAggregateRule) unless the key
+    space is so large that a step's (key, slice) partials barely outnumber its records -- the engine's record-list
+    regime (key_capacity >= 2^25, FWA_CFG_RECORD_LISTS; C4's 1e8 keys: ~1 record per key and window) -- where shipping
+    partial rows (32-40 B) instead of records (24 B) would grow the exchange: "raw"."""
+    kc = int(cfg_kw.get("key_capacity", 0) or 0)
+    return "raw" if kc >= 1 << 25 or cfg_kw.get("record_lists") else "partials"
+
+
 def _gpu_router(max_parallelism, world, key_kind):
     from . import engine
 
@@ -55,6 +64,12 @@ class KeyedWindowPipeline:
         self.route_on_gpu = router is None          # a custom router (tests) keeps the torch grouping
         self.names = A.agg_names(self.cfg)
         self.exchanged = 0
+        # the watermark valve is a host value: under RCCL its MIN-allreduce runs on a gloo group over the same ranks,
+        # so no device synchronisation (a .item() would wait for every kernel queued on the stream)
+        self.wm_group = group
+        if dist.get_backend(group) == "nccl":
+            ranks = None if group is None else dist.get_process_group_ranks(group)
+            self.wm_group = dist.new_group(ranks=ranks, backend="gloo")
 
     def _a2a(self, x, send_splits, recv_splits):
         out = torch.empty(sum(recv_splits), dtype=x.dtype, device=x.device)
@@ -72,10 +87,10 @@ class KeyedWindowPipeline:
         return self.engine.push(k.numpy(), t.numpy(), [x.numpy() for x in c])
 
     def global_watermark(self, local_wm):
-        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
-        w = torch.tensor([int(local_wm)], dtype=torch.int64, device=dev)
-        dist.all_reduce(w, op=dist.ReduceOp.MIN, group=self.group)
-        return int(w.item())
+        """StatusWatermarkValve (StatusWatermarkValve.java:192): the MIN over ranks, on the host (gloo)."""
+        w = torch.tensor([int(local_wm)], dtype=torch.int64)
+        dist.all_reduce(w, op=dist.ReduceOp.MIN, group=self.wm_group)
+        return int(w[0])
 
     def advance_watermark(self, local_wm, device_output=False):
         wm = self.global_watermark(local_wm)

@@ -91,6 +91,10 @@ def lib():
     L.fwa_set_option.restype = C.c_int
     L.fwa_get_option.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]
     L.fwa_get_option.restype = C.c_int
+    L.fwa_advance_watermark_async.argtypes = [C.c_void_p, C.c_int64]
+    L.fwa_advance_watermark_async.restype = C.c_int
+    L.fwa_fired_output.argtypes = [C.c_void_p, C.POINTER(A.Out)]
+    L.fwa_fired_output.restype = C.c_int
     _LIB = L
     return L
 
@@ -145,7 +149,7 @@ class WindowAggregator:
         if rc:
             raise EngineError(rc, "fwa_create")
         for name, value in DEFAULT_OPTIONS.items():    # where they apply to this handle's state layout
-            opt = OPTIONS[name] if isinstance(name, str) else int(name)
+            opt = OPTIONS[name] if name in OPTIONS else int(name)
             rc = lib().fwa_set_option(self.h, opt, int(value))
             if rc and rc != -7:                        # FWA_E_UNSUPPORTED: not this layout
                 _check(rc, self.h)
@@ -154,7 +158,7 @@ class WindowAggregator:
 
     def set_option(self, name, value):
         """fwa_set_option: name from OPTIONS (or the enum value), value -1 adaptive / 0 never / 1 always, or a size."""
-        opt = OPTIONS[name] if isinstance(name, str) else int(name)
+        opt = OPTIONS[name] if name in OPTIONS else int(name)
         rc = lib().fwa_set_option(self.h, opt, int(value))
         self._settled()
         _check(rc, self.h)
@@ -173,7 +177,7 @@ class WindowAggregator:
 
     def get_option(self, name):
         """fwa_get_option: the option's effective value (tri-states: 1 if the handle currently takes that path)."""
-        opt = OPTIONS[name] if isinstance(name, str) else int(name)
+        opt = OPTIONS[name] if name in OPTIONS else int(name)
         v = C.c_int64(0)
         _check(lib().fwa_get_option(self.h, opt, C.byref(v)), self.h)
         return v.value
@@ -222,14 +226,34 @@ class WindowAggregator:
         _check(rc, self.h)
         return out
 
+    def advance_watermark_async(self, wm):
+        """fwa_advance_watermark_async: the watermark step without waiting for the fire (rows: fired_output*)."""
+        rc = lib().fwa_advance_watermark_async(self.h, int(wm))
+        self._settled()
+        _check(rc, self.h)
+
+    def fired_output_raw(self):
+        """fwa_fired_output: the rows of the last advance_watermark_async (waits for its fire)."""
+        out = A.Out()
+        _check(lib().fwa_fired_output(self.h, C.byref(out)), self.h)
+        return out
+
+    def fired_output(self):
+        return self._rows(self.fired_output_raw())
+
     def advance_watermark(self, wm):
         """Fire every window with maxTimestamp <= wm; returns the fired rows as numpy columns."""
-        out = self.advance_watermark_raw(wm)
+        return self._rows(self.advance_watermark_raw(wm))
+
+    def _rows(self, out):
         n = out.n_rows
         conv = _dev_to_np if out.on_device else _host_to_np
         res = {f: conv(getattr(out, f), n, np.dtype("i8")) for f in ("key", "win_start", "win_end")}
         for j, name in enumerate(self.names):
-            res["agg%d" % j] = conv(out.agg[j], n, np.dtype(A.AGG_RESULT_DTYPE[name]))
+            if name in A.DEC_KINDS:                    # 16-byte unscaled DECIMAL -> Python ints
+                res["agg%d" % j] = A.dec128_values(conv(out.agg[j], 2 * n, np.dtype("i8")))
+            else:
+                res["agg%d" % j] = conv(out.agg[j], n, np.dtype(A.AGG_RESULT_DTYPE[name]))
             if out.agg_null[j]:
                 res["null%d" % j] = conv(out.agg_null[j], n, np.dtype("u1"))
         return res
@@ -241,7 +265,10 @@ class WindowAggregator:
         n = out.n_rows
         res = {f: dev_view(getattr(out, f), n, np.dtype("i8")) for f in ("key", "win_start", "win_end")}
         for j, name in enumerate(self.names):
-            res["agg%d" % j] = dev_view(out.agg[j], n, np.dtype(A.AGG_RESULT_DTYPE[name]))
+            if name in A.DEC_KINDS:                    # int64 [n, 2] (low, high) per row
+                res["agg%d" % j] = dev_view(out.agg[j], 2 * n, np.dtype("i8")).view(-1, 2)
+            else:
+                res["agg%d" % j] = dev_view(out.agg[j], n, np.dtype(A.AGG_RESULT_DTYPE[name]))
         return res
 
     # -- two-phase aggregation (LocalSlicingWindowAggOperator -> GlobalAggCombiner) --

@@ -14,7 +14,7 @@ unspecified in the reference too (TimerHeapInternalTimer orders by timestamp onl
 import numpy as np
 
 from . import _abi as A
-from .assigners import WindowSpec
+from .assigners import WindowSpec, is_window_fired, to_utc_timestamp_mills
 
 
 class _Batcher:
@@ -131,15 +131,22 @@ class SlicingWindowProcessor(_Base):
 
     def __init__(self, spec, aggs, **kw):
         kw.setdefault("track_late", True)
+        self.spec = spec
+        self.tz = kw.get("tz")
         super().__init__(spec, aggs, **kw)
 
     def process_element(self, key, row_values, rowtime):
-        """The reference returns true for a dropped late record and SlicingWindowOperator marks
-        lateRecordsDroppedRate (SlicingWindowOperator.java:222-226). Records are applied in batches, so the
-        GPU processor owns that metric instead: num_late_records_dropped counts them and late_records lists
-        them (per-push indices from fwa_late_records) once the batch is pushed; this returns False."""
+        """True when the record is dropped as late, which SlicingWindowOperator turns into lateRecordsDroppedRate
+        (SlicingWindowOperator.java:222-226): its slice fired and so did the last window containing that slice,
+        under the current progress (AbstractWindowAggProcessor.processElement :142-182, TimeWindowUtil.isWindowFired
+        :175-183, a shift time zone's local time and timer instants included). The record is buffered either way: the
+        engine drops the same records when the batch is pushed (num_late_records_dropped, late_records)."""
         self._add(key, rowtime, row_values)
-        return False
+        if self.current_watermark == A.LONG_MIN:
+            return False
+        slice_end = self.spec.assign_slice_end(to_utc_timestamp_mills(rowtime, self.tz))
+        return (is_window_fired(slice_end, self.current_watermark, self.tz) and
+                is_window_fired(self.spec.last_window_end(slice_end), self.current_watermark, self.tz))
 
     def advance_progress(self, progress):
         self._push()

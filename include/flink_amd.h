@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FWA_ABI_VERSION 3
+#define FWA_ABI_VERSION 4   /* 4: fwa_config.dec_scale (DECIMAL aggregates); version-3 configurations are still accepted */
 #define FWA_MAX_AGGS 8
 #define FWA_MAX_COLS 8
 
@@ -90,8 +90,28 @@ enum fwa_agg_kind {
     FWA_AVG_F64 = 12,/* AVG(DOUBLE)                                 [f64] */
     FWA_COUNT_COL = 13,/* COUNT(col): non-NULL values of col (Count aggregate over a nullable column;
                           COUNT(*) when col is not nullable)       [i64] */
-    FWA_AGG_KIND_COUNT = 14
+    FWA_SUM_DEC = 14,  /* SUM(DECIMAL(p, s)), p <= 18: int64 unscaled input (DecimalData's compact form);
+                          result DECIMAL(38, s)                      [i128] */
+    FWA_AVG_DEC = 15,  /* AVG(DECIMAL(p, s)), p <= 18: result DECIMAL(38, max(6, s))  [i128] */
+    FWA_SUM_DEC128 = 16,/* SUM(DECIMAL(p, s)), p <= 38: 16-byte unscaled input        [i128] */
+    FWA_AVG_DEC128 = 17,/* AVG(DECIMAL(p, s)), p <= 38                               [i128] */
+    FWA_AGG_KIND_COUNT = 18
 };
+/* DECIMAL aggregates (Table semantics; the input column's scale s in fwa_config.dec_scale[j]). Values are unscaled
+ * integers in 16-byte little-endian two's complement ([i128]: low 8 bytes, then high 8 bytes).
+ *  SUM: DecimalSumAggFunction (SumAggFunction.java:150-168): the exact sum at the result type of
+ *       LogicalTypeMerging.findSumAggType (:280-294), DECIMAL(38, s); NULL when it has more than 38 digits
+ *       (DecimalDataUtils.add -> DecimalData.fromBigDecimal, DecimalData.java:184-195), or no non-NULL input.
+ *  AVG: DecimalAvgAggFunction (AvgAggFunction.java:213-251): that sum over the non-NULL count, divided as
+ *       DecimalDataUtils.divide (DecimalDataUtils.java:40,145-148) into findAvgAggType's DECIMAL(38, max(6, s))
+ *       (LogicalTypeMerging.java:261-277): the quotient rounded HALF_UP to 38 significant digits, then HALF_UP to the
+ *       result scale; NULL past 38 digits or with no non-NULL input.
+ * Overflow is decided on the window's exact total. The reference decides it on each running sum in arrival order (a
+ * SUM whose running sum overflowed restarts from the next value): results differ only for windows in which a
+ * running sum passes 38 digits. A (key, window) may hold up to 2^32 - 1 records (FWA_E_UNSUPPORTED at the fire
+ * beyond). Internally each DECIMAL source column is summed as 2 (int64 input) or 4 (16-byte) 32-bit pieces, each one of
+ * the handle's FWA_MAX_AGGS aggregates, plus a count; a list past that budget is FWA_E_UNSUPPORTED at fwa_create. Not
+ * available for fwa_drain_partials / fwa_push_partials / fwa_snapshot_heap (FWA_E_UNSUPPORTED). */
 /* SQL NULL semantics (fwa_config.nullable_cols, Table semantics): SUM/MIN/MAX/AVG skip NULL inputs and are
  * NULL when a window holds no non-NULL input (SumAggFunction.java:54-110, MaxAggFunction.java:63-73,
  * MinAggFunction.java:63-, AvgAggFunction.java:65-106: AVG = sum / count of non-NULL inputs); COUNT(*) counts
@@ -152,6 +172,8 @@ typedef struct fwa_config {
     int32_t nullable_cols;       /* Table: bit c set = value column c may hold SQL NULLs (fwa_push_nullable) */
     const int64_t* tz;           /* [2 * tz_n]: from UTC instant tz[2i] (ms, ascending) on, the zone's offset is
                                     tz[2i+1] ms (java.time ZoneRules transitions); copied by fwa_create */
+    /* ABI 4 */
+    int32_t dec_scale[FWA_MAX_AGGS];   /* DECIMAL aggregate j: the scale s of its input column (0..38) */
 } fwa_config;
 
 /* fwa_config.flags */
@@ -240,6 +262,17 @@ int fwa_set_input_stream(fwa_engine* e, void* stream);
  * does not advance).
  * Output rows (fired (key, window) results) stay valid until the next call on this handle. */
 int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out);
+
+/* fwa_advance_watermark split in two so the caller can hand the next batch to the engine while the fire runs (the
+ * mailbox thread emitting the fired rows downstream while the next network buffer is processed, StreamTask
+ * processInput -> WindowOperator.processWatermark -> output.collect). fwa_advance_watermark_async takes the same
+ * watermark step and returns without waiting for the fire when it can (a TUMBLE handle after an FWA_PUSH_ASYNC push:
+ * the fire is enqueued and the host waits only for the push's status); the rows are taken with fwa_fired_output,
+ * which waits for them. Between the two, fwa_push / fwa_push_partials may be called (their ingest runs behind the
+ * fire); any other call completes the fire first. The output stays valid until the next watermark call. Results are
+ * those of fwa_advance_watermark at the same point. */
+int fwa_advance_watermark_async(fwa_engine* e, int64_t wm);
+int fwa_fired_output(fwa_engine* e, fwa_out* out);
 
 /* Make every pushed record visible in state (checkpoint barrier, SlicingWindowOperator.java:267-269). */
 int fwa_flush(fwa_engine* e);
@@ -398,12 +431,14 @@ int fwa_key_groups(const int64_t* keys, const int32_t* key_hash, int64_t n, int3
  * max_parallelism, parallelism, assignToKeyGroup(key_i)); the ncols columns (cols[c]: col_bytes[c] = 4 or 8 bytes
  * per row, 4-byte columns zero-extended) are packed into out[n][ncols] int64 rows grouped by destination, in arrival
  * order within a destination, and counts[d] receives the rows for destination d (parallelism <= 64, ncols <= 16).
- * All pointers are device pointers; work is enqueued on `stream` (NULL: the default stream) and complete on return. */
+ * All pointers are device pointers; work is enqueued on `stream` (NULL: the default stream) without a host
+ * synchronisation: outputs are complete once that stream's work is (a consumer on another stream waits on it). */
 int fwa_route_rows(const int64_t* keys, const int32_t* key_hash, int64_t n, int32_t key_kind, int32_t max_parallelism,
                    int32_t parallelism, const void* const* cols, const int32_t* col_bytes, int32_t ncols, int64_t* out,
                    int64_t* counts, int32_t device, void* stream);
 
-/* The receive side of that exchange: rows[n][ncols] (int64 cells) -> cols[c][n], device pointers, on `stream`. */
+/* The receive side of that exchange: rows[n][ncols] (int64 cells) -> cols[c][n], device pointers, enqueued on `stream`
+ * (no host synchronisation). */
 int fwa_unpack_rows(const int64_t* rows, int64_t n, int32_t ncols, int64_t* const* cols, int32_t device, void* stream);
 
 /* ---- key dictionary: multi-column Table keys ----

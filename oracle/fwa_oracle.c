@@ -314,7 +314,56 @@ static int th_pop_due(theap* t, int64_t wm, timer_t_* out) {
 
 /* ------------------------------------------------------------------ accumulators */
 
-typedef union { int64_t i; double d; float f; } aval;
+typedef union { int64_t i; double d; float f; __int128 q; } aval;   /* q: DECIMAL unscaled value */
+
+/* ---- DECIMAL (DecimalSumAggFunction / DecimalAvgAggFunction, SumAggFunction.java:150-168, AvgAggFunction.java:213-251):
+   DecimalDataUtils.add (:106-121) -> DecimalData.fromBigDecimal (DecimalData.java:184-195): NULL past 38 digits */
+static int is_dec(int k) { return k >= FWA_SUM_DEC && k <= FWA_AVG_DEC128; }
+static int is_dec_avg(int k) { return k == FWA_AVG_DEC || k == FWA_AVG_DEC128; }
+static const unsigned __int128 DEC_LIM = (unsigned __int128)10000000000000000000ull * 10000000000000000000ull; /* 10^38 */
+static int dec_fits(__int128 v) { unsigned __int128 a = v < 0 ? -(unsigned __int128)v : (unsigned __int128)v; return a < DEC_LIM; }
+static __int128 dec_input(const void* col, int64_t i, int kind) {
+    if (kind == FWA_SUM_DEC || kind == FWA_AVG_DEC) return (__int128)((const int64_t*)col)[i];
+    const uint64_t* p = (const uint64_t*)col + 2 * i;            /* 16-byte little-endian two's complement */
+    return (__int128)(((unsigned __int128)p[1] << 64) | p[0]);
+}
+/* AVG's value (AvgAggFunction.getValueExpression :100-106): DecimalDataUtils.divide(sum, count) (:145-148): the exact
+   quotient |sum| * 10^-s / cnt rounded HALF_UP to 38 significant digits (MathContext MC_DIVIDE :40), then
+   fromBigDecimal at the result type DECIMAL(38, t): setScale(t, HALF_UP), NULL past 38 digits. Written as a decimal
+   digit expansion of the quotient. Returns 0 for NULL. */
+static int dec_divide(__int128 sum, int64_t cnt, int s, int t, __int128* out) {
+    const int neg = sum < 0;
+    unsigned __int128 a = neg ? -(unsigned __int128)sum : (unsigned __int128)sum;
+    if (a == 0) { *out = 0; return 1; }
+    enum { ND = 200 };
+    signed char d[ND];                                     /* digits of a / cnt; the point sits after ni digits */
+    int ni = 0;
+    unsigned __int128 ip = a / (uint64_t)cnt;
+    uint64_t r = (uint64_t)(a % (uint64_t)cnt);
+    char tmp[48]; int k = 0;
+    while (ip) { tmp[k++] = (char)(ip % 10); ip /= 10; }
+    for (int i = k - 1; i >= 0; i--) d[ni++] = tmp[i];
+    for (int i = ni; i < ND; i++) { unsigned __int128 x = (unsigned __int128)r * 10u; d[i] = (signed char)(x / (uint64_t)cnt); r = (uint64_t)(x % (uint64_t)cnt); }
+    int p0 = 0;
+    while (d[p0] == 0) p0++;                               /* first significant digit */
+    unsigned __int128 q1 = 0;
+    for (int i = p0; i < p0 + 38; i++) q1 = q1 * 10u + (unsigned)d[i];
+    if (d[p0 + 38] >= 5) q1 += 1u;                         /* HALF_UP at 38 significant digits */
+    const int u = s + (p0 + 38 - ni);                      /* scale of q1 */
+    unsigned __int128 res;
+    if (u > t) {                                           /* setScale(t, HALF_UP) */
+        int drop = u - t; unsigned last = 0;
+        res = q1;
+        for (int i = 0; i < drop; i++) { last = (unsigned)(res % 10u); res /= 10u; }
+        if (last >= 5) res += 1u;
+    } else {
+        res = q1;
+        for (int i = 0; i < t - u; i++) { if (res >= DEC_LIM / 10u) return 0; res *= 10u; }
+    }
+    if (res >= DEC_LIM) return 0;
+    *out = neg ? -(__int128)res : (__int128)res;
+    return 1;
+}
 
 typedef struct or_engine {
     fwa_config c;
@@ -344,8 +393,7 @@ static int64_t acc_new(or_engine* e) {
         id = e->pool_n++;
     }
     aval* a = &e->pool[id * e->nacc];
-    a[0].i = 0;
-    for (int j = 0; j < e->c.num_aggs; j++) a[1 + e->c.num_aggs + j].i = 0;
+    memset(a, 0, sizeof(aval) * e->nacc);
     for (int j = 0; j < e->c.num_aggs; j++) {           /* createAccumulators */
         switch (e->c.aggs[j].kind) {
         case FWA_SUM_F32: a[1 + j].i = 0; a[1 + j].f = 0.0f; break;
@@ -373,6 +421,19 @@ static void acc_add(or_engine* e, aval* a, const void* const* cols, int64_t i) {
         if ((e->c.nullable_cols >> cj & 1) && e->nulls && e->nulls[cj] && e->nulls[cj][i]) continue;
         int first = (a[1 + na + j].i == 0);               /* buffer still NULL */
         a[1 + na + j].i++;
+        if (is_dec(e->c.aggs[j].kind)) {
+            const __int128 v = dec_input(col, i, e->c.aggs[j].kind);
+            int64_t* ovf = &a[1 + 2 * na + j].i;
+            if (is_dec_avg(e->c.aggs[j].kind)) {          /* sum starts at 0; plus(NULL, v) stays NULL */
+                if (!*ovf) { x->q += v; if (!dec_fits(x->q)) *ovf = 1; }
+            } else if (first || *ovf) {                   /* SUM: ifThenElse(isNull(sum), operand, ...) */
+                x->q = v; *ovf = 0;
+            } else {
+                x->q += v;
+                if (!dec_fits(x->q)) *ovf = 1;
+            }
+            continue;
+        }
         switch (e->c.aggs[j].kind) {
         case FWA_COUNT: case FWA_COUNT_COL: break;
         case FWA_SUM_I64: case FWA_AVG_I64: x->i = jladd(x->i, ((const int64_t*)col)[i]); break;
@@ -397,6 +458,24 @@ static void acc_merge(or_engine* e, aval* a, const aval* b) {
     a[0].i = jladd(a[0].i, b[0].i);
     for (int j = 0; j < na; j++) {
         aval* x = &a[1 + j]; const aval* y = &b[1 + j];
+        if (is_dec(e->c.aggs[j].kind)) {                  /* mergeExpressions */
+            const int kind = e->c.aggs[j].kind;
+            int64_t* ovf = &a[1 + 2 * na + j].i;
+            const int64_t ovb = b[1 + 2 * na + j].i;
+            const int anull = a[1 + na + j].i == 0 || *ovf, bnull = b[1 + na + j].i == 0 || ovb;
+            a[1 + na + j].i += b[1 + na + j].i;
+            if (is_dec_avg(kind)) {                       /* sum + other.sum: NULL if either is */
+                if (*ovf || ovb) *ovf = 1;
+                else { x->q += y->q; if (!dec_fits(x->q)) *ovf = 1; }
+            } else if (bnull) {
+            } else if (anull) {
+                x->q = y->q; *ovf = 0;
+            } else {
+                x->q += y->q;
+                if (!dec_fits(x->q)) *ovf = 1;
+            }
+            continue;
+        }
         if (b[1 + na + j].i == 0) continue;               /* merging a NULL buffer changes nothing */
         int first = (a[1 + na + j].i == 0);
         a[1 + na + j].i += b[1 + na + j].i;
@@ -421,7 +500,7 @@ static void emit(or_engine* e, int64_t key, int64_t ws, int64_t we, const aval* 
         e->o_key = (int64_t*)realloc(e->o_key, 8 * e->out_cap);
         e->o_start = (int64_t*)realloc(e->o_start, 8 * e->out_cap);
         e->o_end = (int64_t*)realloc(e->o_end, 8 * e->out_cap);
-        for (int j = 0; j < e->c.num_aggs; j++) e->o_agg[j] = (aval*)realloc(e->o_agg[j], 8 * e->out_cap);
+        for (int j = 0; j < e->c.num_aggs; j++) e->o_agg[j] = (aval*)realloc(e->o_agg[j], sizeof(aval) * e->out_cap);
         for (int j = 0; j < e->c.num_aggs; j++) e->o_null[j] = (uint8_t*)realloc(e->o_null[j], e->out_cap);
     }
     int64_t r = e->out_n++;
@@ -434,6 +513,14 @@ static void emit(or_engine* e, int64_t key, int64_t ws, int64_t we, const aval* 
         const int kind = e->c.aggs[j].kind;
         e->o_null[j][r] = (kind != FWA_COUNT && kind != FWA_COUNT_COL && nn == 0);   /* SQL NULL result */
         if (e->o_null[j][r]) continue;
+        if (is_dec(kind)) {
+            o->q = 0;
+            if (a[1 + 2 * na + j].i) { e->o_null[j][r] = 1; continue; }   /* the sum overflowed */
+            if (!is_dec_avg(kind)) { o->q = x->q; continue; }
+            const int s = e->c.dec_scale[j];
+            if (!dec_divide(x->q, nn, s, s > 6 ? s : 6, &o->q)) { e->o_null[j][r] = 1; o->q = 0; }
+            continue;
+        }
         if (kind == FWA_AVG_I64 || kind == FWA_AVG_F32 || kind == FWA_AVG_F64) cnt = nn;   /* AVG: non-NULL count */
         else cnt = a[0].i;
         switch (kind) {
@@ -477,7 +564,7 @@ int or_create(const fwa_config* c, or_engine** out) {
     }
     if (e->c.max_parallelism <= 0) e->c.max_parallelism = 128;
     e->wm = J_LONG_MIN;
-    e->nacc = 1 + 2 * c->num_aggs;
+    e->nacc = 1 + 3 * c->num_aggs;            /* count, values, non-NULL counts, DECIMAL overflow flags */
     hm_init(&e->state, 1024);
     th_init(&e->timers);
     hm_init(&e->wl_head, 64);
@@ -851,8 +938,8 @@ int or_advance_watermark(or_engine* e, int64_t wm, fwa_out* out) {
         for (int j = 0; j < e->c.num_aggs; j++) {
             out->agg[j] = e->o_agg[j];
             const int kind = e->c.aggs[j].kind;
-            if ((e->c.nullable_cols >> e->c.aggs[j].col & 1) && kind != FWA_COUNT && kind != FWA_COUNT_COL)
-                out->agg_null[j] = e->o_null[j];
+            if (((e->c.nullable_cols >> e->c.aggs[j].col & 1) && kind != FWA_COUNT && kind != FWA_COUNT_COL) || is_dec(kind))
+                out->agg_null[j] = e->o_null[j];                 /* DECIMAL: NULL on overflow too */
         }
     }
     e->out_ret = 1;

@@ -92,10 +92,17 @@ def rows_from_out(out, names):
     for j, name in enumerate(names):
         dt = np.dtype(A.AGG_RESULT_DTYPE[name])
         if n == 0:
-            res["agg%d" % j] = np.zeros(0, dt)
+            res["agg%d" % j] = np.zeros(0, object if name in A.DEC_KINDS else dt)
             continue
-        # oracle stores each result in an 8-byte slot (union); f32 results sit in the low 4 bytes
-        raw = np.ctypeslib.as_array(C.cast(out.agg[j], C.POINTER(C.c_uint64)), (n,)).copy()
+        # oracle stores each result in a 16-byte slot (union); i64/f64 results in the low 8 bytes, f32 in the low 4,
+        # DECIMAL ones fill it
+        raw16 = np.ctypeslib.as_array(C.cast(out.agg[j], C.POINTER(C.c_uint64)), (2 * n,)).copy()
+        if name in A.DEC_KINDS:
+            res["agg%d" % j] = A.dec128_values(raw16)
+            if out.agg_null[j]:
+                res["null%d" % j] = np.ctypeslib.as_array(C.cast(out.agg_null[j], C.POINTER(C.c_uint8)), (n,)).copy()
+            continue
+        raw = raw16[0::2].copy()
         if dt.itemsize == 4:
             res["agg%d" % j] = (raw & 0xffffffff).astype(np.uint32).view(dt)
         else:

@@ -7,7 +7,8 @@ Data only, transcribed by hand from the reference's own test:
          flink-table/flink-table-planner/src/test/scala/org/apache/flink/table/planner/runtime/stream/sql/WindowAggregateITCase.scala:174-207, 492-530, 696-741
 The ITCase's columns this engine computes: COUNT(*), SUM(bigdec), MAX(double), MIN(float) (COUNT(DISTINCT) and
 the UDAF are not on this path). Mapping: name "a" -> key 1, "b" -> 2, NULL -> 3 (a NULL grouping key is a key
-like any other); bigdec DECIMAL(.., 2) -> its unscaled long (SUM over the unscaled values, exact, x100);
+like any other); bigdec DECIMAL(10, 2) -> its unscaled long, summed by SUM_DEC (scale 2: the DECIMAL(38, 2) result
+as its unscaled value, x100);
 rowtime TIMESTAMP(3) -> epoch millis of the local time read as UTC (the non-LTZ parameterisation). Watermark:
 `rowtime - INTERVAL '1' SECOND` after every record (the ITCase's per-record watermark assigner), then MAX at
 the end of input. The ITCase asserts the multiset of all emitted rows; so does the replay.
@@ -109,7 +110,7 @@ def events():
 def case(name, lines, lo, kind, size, slide):
     return {"name": "WindowAggregateITCase.%s" % name, "src": "%s:%s (input TestData.scala:729-742)" % (SRC_IT, lo),
             "window_kind": kind, "size_ms": size, "slide_ms": slide, "offset_ms": 0,
-            "aggs": [["COUNT", 0], ["SUM_I64", 0], ["MAX_F64", 1], ["MIN_F32", 2]],
+            "aggs": [["COUNT", 0], ["SUM_DEC", 0, 2], ["MAX_F64", 1], ["MIN_F32", 2]],
             "col_types": ["i8", "f8", "f4"], "nullable_cols": [0, 1, 2],
             "events": events(), "expected": parse(lines), "late_dropped": 1 if kind == "TUMBLE" else 0}
 

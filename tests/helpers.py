@@ -146,7 +146,8 @@ def replay_sql_kat(case, make_engine):
             r = [rows["key"][i].item(), rows["win_start"][i].item(), rows["win_end"][i].item()]
             for j in range(naggs):
                 nul = rows.get("null%d" % j)
-                r.append(None if nul is not None and nul[i] else rows["agg%d" % j][i].item())
+                v = rows["agg%d" % j][i]
+                r.append(None if nul is not None and nul[i] else (v.item() if hasattr(v, "item") else v))
             got.append(r)
     flush()
     key = lambda r: tuple((x is None, x) for x in r)
@@ -155,11 +156,42 @@ def replay_sql_kat(case, make_engine):
     eng.close()
 
 
+def load_decimal_kats():
+    """DECIMAL SUM / AVG KATs (tests/golden/gen_decimal_kats.py)."""
+    with open(os.path.join(GOLDEN, "decimal_kats.json")) as f:
+        return json.load(f)["cases"]
+
+
+def dec_input(kind, values):
+    """The engine's input column for unscaled DECIMAL values: int64 (SUM_DEC / AVG_DEC) or 16-byte (the *128 kinds)."""
+    if kind.endswith("128"):
+        return A.dec128_column(values)
+    return np.array(values, np.int64)
+
+
+def replay_decimal_kat(case, make_engine):
+    """One key, one Table tumbling window holding the case's inputs; the fired value must be the expected one."""
+    cfg = A.make_config(window_kind="TUMBLE", semantics="TABLE", size_ms=1000,
+                        aggs=[("COUNT", 0), (case["agg"], 0, case["scale"])])
+    eng = make_engine(cfg)
+    n = len(case["inputs"])
+    eng.push(np.full(n, 7, np.int64), np.arange(n, dtype=np.int64), [dec_input(case["agg"], case["inputs"])])
+    rows = eng.advance_watermark(A.LONG_MAX)
+    assert len(rows["key"]) == 1 and int(rows["agg0"][0]) == n, case["name"]
+    assert rows.get("null1") is None or not rows["null1"][0], case["name"]
+    assert int(rows["agg1"][0]) == case["expected"], "%s: %s != %s" % (case["name"], rows["agg1"][0], case["expected"])
+    eng.close()
+
+
 def assert_rows_equal(a, b, names, rtol=None, ctx=""):
     """Multiset equality of two fired-row dicts. Integer columns bit-exact; float columns within rtol
     (relative, with the same absolute floor) when rtol is given, else exact."""
     n = len(a["key"])
-    assert n == len(b["key"]), "%s row count %d != %d" % (ctx, n, len(b["key"]))
+    if n != len(b["key"]):                                 # name the (key, window) pairs only one side has
+        ka = {(int(k), int(s), int(e)) for k, s, e in zip(a["key"], a["win_start"], a["win_end"])}
+        kb = {(int(k), int(s), int(e)) for k, s, e in zip(b["key"], b["win_start"], b["win_end"])}
+        raise AssertionError("%s row count %d != %d; only first: %s; only second: %s" %
+                             (ctx, n, len(b["key"]), sorted(ka - kb)[:8], sorted(kb - ka)[:8]))
     if n == 0:
         return
     oa = np.lexsort((a["win_end"], a["win_start"], a["key"]))

@@ -163,3 +163,12 @@ def test_two_rank_keyby_pipeline_matches_single_operator(tmp_path, two_phase, pi
     # every key's rows live on exactly the rank owning its key group
     ranks = [np.load(tmp_path / ("rank%d.npy" % r)) for r in range(world)]
     assert not (set(ranks[0][:, 0].tolist()) & set(ranks[1][:, 0].tolist()))
+
+
+def test_choose_exchange_plan():
+    """Two-phase partials unless the key space puts the engine in its record-list regime (C4), where a step's partial
+    rows would outnumber and outweigh its records."""
+    from flink_amd.distributed import choose_exchange
+    assert choose_exchange(dict(key_capacity=1_000_000)) == "partials"
+    assert choose_exchange(dict(key_capacity=100_000_000)) == "raw"
+    assert choose_exchange(dict(key_capacity=4096, record_lists=True)) == "raw"

@@ -63,7 +63,7 @@ def test_narrow_entries_with_a_few_wide_records(eng_mod, monkeypatch):
     keys, ts, vals = _stream(2, 1 << 20, 50_000, 40_000, 300)
     rng = np.random.default_rng(3)
     k = rng.random(len(keys)) < 0.004
-    keys[k] = rng.choice(np.array([2**31, -2**31 - 1, 2**40 + 7, -2**62, 2**31 - 1, -2**31], np.int64), k.sum())
+    keys[k] = rng.choice(np.array([2**31, -2**31 - 1, 2**40 + 7, -2**62, 2**31 - 1, -2**31, -2**31 + 1], np.int64), k.sum())
     v = rng.random(len(keys)) < 0.004
     vals[v] = rng.choice(np.array([2**31, -2**31 - 1, 2**62 + 5, -2**63, 2**31 - 1, -2**31], np.int64), v.sum())
     monkeypatch.setitem(eng_mod.DEFAULT_OPTIONS, "narrow_entries", 0)

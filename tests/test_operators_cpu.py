@@ -41,20 +41,44 @@ def test_window_operator_facade_tumbling_kat(batch):
     op.close()
 
 
-def test_slicing_processor_facade_hopping_kat():
-    case = KATS["SlicingWindowAggOperatorTest.testEventTimeHoppingWindows"]
-    proc = SlicingWindowProcessor(SliceAssigners.hopping(3000, 1000), [("SUM_I64", 0), ("COUNT", 0)],
-                                  batch_size=2, engine_factory=Oracle).open()
+TABLE_SPECS = {"SLIDE": lambda: SliceAssigners.hopping(3000, 1000), "CUMULATE": lambda: SliceAssigners.cumulative(3000, 1000),
+               "TUMBLE": lambda: SliceAssigners.tumbling(3000)}
+
+
+@pytest.mark.parametrize("kind", ["SLIDE", "CUMULATE", "TUMBLE"])
+def test_slicing_processor_facade_kats(kind):
+    """SlicingWindowAggOperatorTest sequences through the facade: rows per watermark, and processElement returns true
+    exactly for the records the reference drops (SlicingWindowOperator.java:222-226 lateRecordsDroppedRate)."""
+    name = {"SLIDE": "Hopping", "CUMULATE": "Cumulative", "TUMBLE": "Tumbling"}[kind]
+    case = KATS["SlicingWindowAggOperatorTest.testEventTime%sWindows" % name]
+    proc = SlicingWindowProcessor(TABLE_SPECS[kind](), [("SUM_I64", 0), ("COUNT", 0)], batch_size=2,
+                                  engine_factory=Oracle).open()
+    flagged = []
     for ev in case["events"]:
         if ev[0] == "e":
-            assert proc.process_element(ev[1], [ev[2]], ev[3]) is False
+            if proc.process_element(ev[1], [ev[2]], ev[3]):
+                flagged.append((ev[1], ev[3]))
         else:
             got = sorted(proc.advance_progress(ev[1]))
             exp = sorted((k, s, c, ws, we) for k, ws, we, s, c in ev[2])
             assert got == exp
-    assert proc.num_late_records_dropped == case["late_dropped"]
     proc.prepare_checkpoint()
+    assert proc.num_late_records_dropped == case["late_dropped"] == len(flagged)
+    assert sorted(flagged) == sorted((k, ts) for k, _, ts in proc.late_records)
     proc.close()
+
+
+def test_window_fired_and_slice_helpers():
+    """TimeWindowUtil.isWindowFired / SliceAssigners geometry restated for the facade (UTC and a shift zone)."""
+    from flink_amd.assigners import is_window_fired, to_epoch_mills_for_timer, window_start_with_offset
+    assert window_start_with_offset(-1, 0, 1000) == -1000 and window_start_with_offset(1999, 300, 1000) == 1300
+    hop = SliceAssigners.hopping(3000, 1000)
+    assert hop.assign_slice_end(2999) == 3000 and hop.last_window_end(3000) == 5000
+    cum = SliceAssigners.cumulative(3000, 1000)
+    assert cum.assign_slice_end(4500) == 5000 and cum.last_window_end(5000) == 6000
+    assert not is_window_fired(3000, 2998) and is_window_fired(3000, 2999) and not is_window_fired(A.LONG_MAX, A.LONG_MAX)
+    shanghai = [(-2**63, 8 * 3600_000)]                # fixed +08:00
+    assert to_epoch_mills_for_timer(10 * 3600_000, shanghai) == 2 * 3600_000
 
 
 def test_window_operator_side_output_of_late_records():
@@ -84,4 +108,50 @@ def test_slicing_processor_lists_dropped_records():
         else:
             proc.advance_progress(ev[1])
     assert [(k, ts) for k, _, ts in proc.late_records] == [(1, 2999)]   # "late for all assigned windows"
+    proc.close()
+
+
+def test_timer_and_local_time_against_reference_kats():
+    """The facade's toEpochMillsForTimer / toUtcTimestampMills restatement against TimeWindowUtilTest's cases
+    (Asia/Shanghai, America/Los_Angeles DST), and the slice assigners against the *SliceAssignerTest cases."""
+    from flink_amd.assigners import to_epoch_mills_for_timer, to_utc_timestamp_mills
+    from helpers import load_tz_kats
+    tzk = load_tz_kats()
+    n = 0
+    for c in tzk["timer"]:
+        tz = [tuple(p) for p in c["tz"]]
+        for local, inst in c["timer"]:
+            assert to_epoch_mills_for_timer(local, tz) == inst, (c["zone"], local)
+            n += 1
+        for inst, local in c.get("to_local", []):
+            assert to_utc_timestamp_mills(inst, tz) == local, (c["zone"], inst)
+    for c in tzk["slice_ends"]:
+        tz = [tuple(p) for p in c["tz"]]
+        spec = {"TUMBLE": lambda: SliceAssigners.tumbling(c["size"], c["offset"]),
+                "SLIDE": lambda: SliceAssigners.hopping(c["size"], c["slide"], c["offset"]),
+                "CUMULATE": lambda: SliceAssigners.cumulative(c["size"], c["slide"], c["offset"])}[c["kind"]]()
+        for ts, end in c["cases"]:
+            assert spec.assign_slice_end(to_utc_timestamp_mills(ts, tz)) == end, (c["src"], ts)
+            n += 1
+    assert n > 20
+
+
+@pytest.mark.parametrize("kind", ["SLIDE", "CUMULATE", "TUMBLE"])
+def test_slicing_processor_late_flags_shanghai(kind):
+    """The Asia/Shanghai parameterisation of SlicingWindowAggOperatorTest through the facade (oracle engine): rows and
+    the per-record late flag under a shift time zone."""
+    from helpers import load_tz_kats
+    case = [c for c in load_tz_kats()["operators"] if c["window_kind"] == kind and c["semantics"] == "TABLE"][0]
+    tz = [tuple(p) for p in case["tz"]]
+    proc = SlicingWindowProcessor(TABLE_SPECS[kind](), [("SUM_I64", 0), ("COUNT", 0)], batch_size=3,
+                                  engine_factory=Oracle, tz=tz).open()
+    flagged = 0
+    for ev in case["events"]:
+        if ev[0] == "e":
+            flagged += bool(proc.process_element(ev[1], [ev[2]], ev[3]))
+        else:
+            got = sorted(proc.advance_progress(ev[1]))
+            assert got == sorted((k, s, c, ws, we) for k, ws, we, s, c in ev[2])
+    proc.prepare_checkpoint()
+    assert flagged == proc.num_late_records_dropped == case["late_dropped"]
     proc.close()

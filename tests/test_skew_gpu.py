@@ -82,8 +82,9 @@ def test_zipf_head_key_switches_to_pre_aggregation(eng_mod, shape):
     # push 1 misses every slice (empty directory: all replayed) and does not see the skew; push 2 overflows on the
     # head key's partition (those records take the v1 replay) and switches the handle to pre-aggregation, which
     # pushes 3-4 then use and replay (almost) nothing
+    # (the narrow Phase P, partition_nk, applies a full sub-bucket's records in place instead of replaying them)
     assert modes[0] == 0 and modes[1] == 1 and modes[3] == 1, modes
-    assert rep[0] > 0 and rep[1] - rep[0] > 0, rep
+    assert rep[0] > 0 and rep[1] - rep[0] >= 0, rep
     assert rep[3] - rep[1] < (n // 4) // 100, rep
 
 
