@@ -53,8 +53,9 @@ def main():
                          "c4: tumbling 10s COUNT+SUM(long), 100M uniform keys, maxParallelism 128; "
                          "c5: Table TUMBLE 10s TVF COUNT, SUM(double), AVG(double), MAX(float), MAX(double); "
                          "c5s: DataStream session windows (gap 5s), same float aggregates")
-    ap.add_argument("--sync-fire", action="store_true",
-                    help="N=1: wait for every watermark's fire before the next batch (fwa_advance_watermark)")
+    ap.add_argument("--async-fire", action="store_true",
+                    help="N=1: take each watermark's rows after the next batch was handed over "
+                         "(fwa_advance_watermark_async; r04: 41.8 vs 47.8 G rec/s on C2, so not the default)")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="fwa_set_option on the measured engine(s) (flink_amd.engine.OPTIONS), e.g. profile=1")
     ap.add_argument("--exchange", choices=["auto", "partials", "raw"], default="auto",
@@ -181,7 +182,7 @@ def main():
             rows_t += pipelined(b, b + 1 if b + 1 < S else None)
             if (b - args.warmup) % 4 == 3:
                 log("step %d/%d  %.2fs" % (b - args.warmup + 1, args.steps, time.perf_counter() - t0))
-    elif world == 1 and not args.sync_fire:
+    elif world == 1 and args.async_fire:
         # the watermark step returns while its fire runs (fwa_advance_watermark_async); the fired rows are taken
         # after the next batch was handed over, so the host's work for batch b+1 overlaps the fire of batch b
         for b in range(args.warmup, S):
@@ -327,7 +328,8 @@ def main():
 def ingest_kernels(args, eng):
     """Names of the kernels whose device time `roofline.achieved` divides by (HIP events around them)."""
     if args.config == "c5s":
-        return "sess2_classify+sess2_route+radix sort+scan-by-key+sess2_reduce (+sess2_ordered)"
+        return ("s4_range+s4_route+s4_hist+s4_colscan+scan+s4_scatter+s4_sess_count/scatter+s4_group "
+                "(cell pre-aggregation; sess3_* sort-based cells or sess2_* when a push leaves its range)")
     if eng.record_lists:
         return "sp_range_kernel+sp_hist_kernel+sp_scan_kernel+sp_scatter_kernel (record lists)"
     return "partition3_kernel+combine3_kernel" if eng.stats().partition_ms > 0 else "ingest_kernel"

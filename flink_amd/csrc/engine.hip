@@ -877,228 +877,6 @@ __global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, cons
         }
 }
 
-// partition_nk: Phase P of the narrow COUNT + SUM(BIGINT) shape (C2: partition3<1, 6, 1024, 3, 0, 0, 1, 1>'s
-// contract), software-pipelined over tiles so that loads and the run reservations are always in flight:
-//   iteration t: classify tile t from registers (partition, rank = LDS histogram atomic) -> issue tile t+1's loads ->
-//   scan -> scatter tile t's packed entries straight to their sorted LDS position (buffer t & 1) -> reserve tile
-//   t's runs (returning atomics, consumed one iteration later) -> store tile t-1 from buffer (t-1) & 1.
-// The loads of tile t+1 are in flight during the scan, the scatter and tile t-1's stores; a reservation's latency is
-// hidden behind a whole iteration (vmcnt retires in order: the reservations of tile t are issued after the loads of
-// tile t+1, and waited for after those loads were consumed). No staging copy, no permutation arrays: the sorted
-// buffer holds the entry itself (8 B) and its slice (2 B); a stored entry's partition is its key's hash again.
-// A run past its sub-bucket's end (skewed keys) is applied at once with device atomics (the handle switches to
-// tile pre-aggregation after such a push, DevStatus::ovf_n).
-template <int ITEMS, int THREADS>
-__global__ void __launch_bounds__(THREADS, 1) partition_nk_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
-    static_assert(THREADS == kMaxPart && ITEMS % 2 == 0 && ITEMS <= 8, "one partition cursor per thread, paired loads");
-    constexpr int kTile = THREADS * ITEMS;
-    const EngineConst& c = *cp;
-    __shared__ uint32_t hist[kMaxPart];
-    __shared__ uint32_t toff[2][kMaxPart];
-    __shared__ uint32_t gbase[kMaxPart];
-    __shared__ unsigned long long x_ent[2][kTile];
-    __shared__ uint16_t x_rel[2][kTile];
-    __shared__ uint32_t wsum[THREADS / 64];
-    __shared__ uint32_t s_total[2];
-    __shared__ uint8_t s_code[kRelCap];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    unsigned dropped = 0, wide = 0;
-    uint32_t relmax = 0, relmin = ~0u;
-    const bool ds = c.sem == FWA_SEM_DATASTREAM;
-    for (int r = tid; r < kRelCap / 4; r += THREADS) ((uint32_t*)s_code)[r] = ((const uint32_t*)a.relcode)[r];
-    for (int i = tid; i < a.np; i += THREADS) hist[i] = 0;
-    const int64_t ntiles = (a.n + kTile - 1) / kTile;
-    const int sub = blockIdx.x % kSub;
-    const int64_t n = a.n;
-    const int64_t* __restrict__ pkeys = a.keys;
-    const int64_t* __restrict__ pts = a.ts;
-    const unsigned long long* __restrict__ pval = (const unsigned long long*)a.cols[a.vcol[0]];
-    unsigned long long rk[ITEMS], rv[ITEMS];
-    int64_t rt[ITEMS];
-    auto xof = [&](int j) -> int { return 2 * ((j >> 1) * THREADS + tid) + (j & 1); };
-    auto load = [&](int64_t t) {   // pair p = records 2p, 2p+1; a pair reaching past n is not loaded (record n-1: slow path)
-#pragma unroll
-        for (int jj = 0; jj < ITEMS / 2; ++jj) {
-            const int64_t pi = t * (kTile / 2) + (int64_t)jj * THREADS + tid;
-            const int64_t ip = 2 * pi + 1 < n ? pi : 0;
-            const ulonglong2 kk = reinterpret_cast<const ulonglong2*>(pkeys)[ip];
-            const longlong2 tt = reinterpret_cast<const longlong2*>(pts)[ip];
-            const ulonglong2 vv = reinterpret_cast<const ulonglong2*>(pval)[ip];
-            rk[2 * jj] = kk.x; rk[2 * jj + 1] = kk.y;
-            rt[2 * jj] = tt.x; rt[2 * jj + 1] = tt.y;
-            rv[2 * jj] = vv.x; rv[2 * jj + 1] = vv.y;
-        }
-    };
-    long long pt = clock64();
-    long long pacc[6] = {0, 0, 0, 0, 0, 0};
-#define QMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
-    const int64_t G = gridDim.x;
-    const int64_t t_first = blockIdx.x;
-    if (t_first < ntiles) load(t_first);
-    // this thread's partition: tile t-1's reservation (a returning atomic issued one iteration ago -- read only after
-    // the next tile's loads were issued, so waiting for it never drains them) and run length
-    uint32_t g_res = 0, h_res = 0;
-    int64_t t_prev = -1;
-    // store tile tp from buffer b: fixed trip count, lanes without an entry write the trash area (keeps the waitcnt
-    // of the next classify exact, see partition3)
-    auto store_tile = [&](int b, int64_t tp) {
-        const uint32_t total = s_total[b];
-#pragma unroll
-        for (int jj = 0; jj < ITEMS; ++jj) {
-            const uint32_t sidx = (uint32_t)(jj * THREADS + tid);
-            const bool valid = sidx < total;
-            const unsigned long long ent = x_ent[b][valid ? sidx : 0];
-            const uint16_t rel = x_rel[b][valid ? sidx : 0];
-            const int64_t key = (int64_t)(int32_t)(uint32_t)ent;
-            const uint32_t p = a.part_bits ? (uint32_t)(jm::mix64((uint64_t)key) >> (64 - a.part_bits)) : 0u;
-            const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[b][p]);
-            const bool inb = valid && dst < (uint64_t)a.capb;
-            if (valid && !inb) {            // sub-bucket full (skewed keys): apply the record now
-                const int32_t slot = a.rel2slot[rel];
-                if (slot >= 0)
-                    pre_apply_global(a.key_table, a.key_mask, a.seg_log, a.part_bits, a.slot_base[slot], a.stride, 1,
-                                     key, 1ull, (unsigned long long)(int64_t)(int32_t)(uint32_t)(ent >> 32), a.st);
-            }
-            const uint64_t o = !inb ? a.trash + (uint64_t)(jj * THREADS + tid)
-                                    : ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
-            a.b_key[o] = ent;
-            a.b_rel[o] = rel;
-        }
-        (void)tp;
-    };
-#pragma unroll
-    for (int jj = 0; jj < ITEMS; ++jj) {   // one store phase's memory operations before the loop (see partition3)
-        const uint64_t o = a.trash + (uint64_t)(jj * THREADS + tid);
-        a.b_key[o] = 0ull;
-        a.b_rel[o] = 0;
-    }
-    __syncthreads();
-    int it = 0;
-    for (int64_t tile = t_first; tile < ntiles; tile += G, ++it) {
-        const int b = it & 1;
-        const int64_t t0 = tile * kTile;
-        QMARK(5);
-        unsigned long long ent[ITEMS];
-        uint32_t r_pos[ITEMS];           // (p << 16 | rank) or ~0u
-        uint16_t r_rel[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) { consume(rk[j]); consume(rt[j]); consume(rv[j]); }
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const int64_t i = t0 + xof(j);
-            const int64_t key = (int64_t)rk[j];
-            const int64_t ts = rt[j];
-            uint64_t rel;
-            const uint64_t dd = (uint64_t)ts - (uint64_t)a.base_ts;
-            if (a.fast_m && dd < a.fast_lim) {
-                rel = (dd * a.fast_m) >> a.fast_sh;
-            } else {
-                const int64_t d = jm::wsub(assign_ts(c, ts), c.off);
-                const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
-                const uint64_t uq = jm::udiv64(ud, c.g_div);
-                const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
-                rel = (uint64_t)(q - a.q_base);
-            }
-            uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
-            if (ds && ts == LONG_MIN_J) code = kCodeSlow;
-            if (a.any_null && i < a.n && row_has_null(a, i)) code = kCodeSlow;
-            if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
-            if (i == a.n - 1 && (a.n & 1)) code = kCodeSlow;        // unpaired last record: the v1 replay
-            if (code == kCodeAccept && ((int64_t)(int32_t)key != key || (uint32_t)key - 0x80000000u <= 1u ||
-                                        (int64_t)(int32_t)rv[j] != (int64_t)rv[j])) {
-                code = kCodeSlow;                                   // needs 64 bits (or an LDS key marker)
-                ++wide;
-            }
-            if (i >= a.n) code = 0xff;
-            dropped += code == kCodeDrop ? 1u : 0u;
-            note_drop(a.dropidx, a.st, code == kCodeDrop, i);
-            const bool slow = code == kCodeSlow;
-            const unsigned long long mk = __ballot(slow);
-            if (mk) {
-                const int leader = __ffsll((long long)mk) - 1;
-                int32_t sb = 0;
-                if (lane == leader) sb = atomicAdd(&a.st->spill_n, __popcll(mk));
-                sb = __shfl(sb, leader);
-                if (slow) put_idx(a.spill, sb + __popcll(mk & ((1ull << lane) - 1)), a.spill_cap, (int32_t)i, a.st);
-            }
-            r_pos[j] = ~0u;
-            ent[j] = (rk[j] & 0xffffffffull) | (rv[j] << 32);
-            r_rel[j] = (uint16_t)rel;
-            if (code == kCodeAccept) {
-                relmax = max(relmax, (uint32_t)rel);
-                relmin = min(relmin, (uint32_t)rel);
-                const uint64_t h = jm::mix64((uint64_t)key);
-                const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
-                r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
-            }
-        }
-        QMARK(0);
-        if (tile + G < ntiles) load(tile + G);   // the next tile in flight through the scan, scatter and stores
-        __syncthreads();
-        block_scan_np<THREADS>(hist, toff[b], wsum, a.np, &s_total[b]);
-        __syncthreads();
-        QMARK(1);
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            if (r_pos[j] == ~0u) continue;
-            const uint32_t p = r_pos[j] >> 16;
-            const uint32_t sidx = toff[b][p] + (r_pos[j] & 0xffffu);
-            x_ent[b][sidx] = ent[j];
-            x_rel[b][sidx] = r_rel[j];
-        }
-        // tile t-1's reservation base goes to gbase for its stores; then tile t's runs are reserved
-        const uint32_t h = tid < a.np ? hist[tid] : 0u;
-        if (tid < a.np) {
-            gbase[tid] = g_res;
-            hist[tid] = 0;                                  // the next tile's histogram
-            const uint64_t end = (uint64_t)g_res + h_res;
-            if (t_prev >= 0 && end > (uint64_t)a.capb)
-                atomicAdd(&a.st->ovf_n, (int32_t)(end - std::max<uint64_t>(g_res, (uint64_t)a.capb)));
-        }
-        g_res = h ? atomicAdd(&a.b_cnt[tid * kSub + sub], h) : 0u;
-        h_res = h;
-        __syncthreads();
-        QMARK(2);
-        if (t_prev >= 0) store_tile(b ^ 1, t_prev);
-        QMARK(3);
-        __syncthreads();                                    // buffer b ^ 1 free for tile t+1, gbase free
-        QMARK(4);
-        t_prev = tile;
-    }
-    // the last tile's stores
-    if (t_prev >= 0) {
-        if (tid < a.np) {
-            gbase[tid] = g_res;
-            const uint64_t end = (uint64_t)g_res + h_res;
-            if (end > (uint64_t)a.capb) atomicAdd(&a.st->ovf_n, (int32_t)(end - std::max<uint64_t>(g_res, (uint64_t)a.capb)));
-        }
-        __syncthreads();
-        store_tile((it - 1) & 1, t_prev);
-    }
-    if (a.prof && tid == 0) for (int q = 0; q < 6; ++q) a.prof[(int64_t)blockIdx.x * 8 + q] = pacc[q];
-#undef QMARK
-    for (int sh = 32; sh >= 1; sh >>= 1) {
-        dropped += __shfl_xor(dropped, sh);
-        wide += __shfl_xor(wide, sh);
-        relmax = max(relmax, (uint32_t)__shfl_xor((int)relmax, sh));
-        relmin = min(relmin, (uint32_t)__shfl_xor((int)relmin, sh));
-    }
-    if (lane == 0) {
-        if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
-        if (wide) atomicAdd(&a.st->wide_n, (int32_t)wide);
-        if (relmin != ~0u) {
-            atomicMax(&a.st->max_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmax));
-            atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
-        }
-    }
-    if (relmin != ~0u)
-        for (uint32_t r = relmin + (uint32_t)lane; r <= relmax; r += 64) {
-            const int32_t slot = a.rel2slot[r];
-            if (slot >= 0 && a.touched[slot] == 0) a.touched[slot] = 1;
-        }
-}
-
 struct CombineArgs {
     const unsigned long long* b_key;
     const unsigned long long* b_val0;
@@ -1466,272 +1244,6 @@ __global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const En
 #undef PMARK
 }
 
-// ------------------------------------------------------------------------------------------------
-// combine_nk: Phase A of the narrow COUNT + SUM(BIGINT) shape (C2; partition3 NW entries, no window passes, no tile
-// pre-aggregation). Same contract as combine3<..., LAYOUT 1, NW 1>, with half the LDS bytes per entry:
-//  * the LDS key segment holds 32-bit key words: a narrow key as itself, kK32Empty for an empty slot, kK32Other for a
-//    slot holding any other key (64-bit, or one of those two values: Phase P sends such keys to the v1 path). A bucket
-//    probe is two ds_read_b128 instead of four, and a match needs no verification;
-//  * one packed accumulator word per (slot, slice): COUNT in bits 48-63, SUM + COUNT * 2^31 in bits 0-47 (each value
-//    biased by 2^31 into [0, 2^32)), so an entry is ONE ds_add_rtn_u64 instead of a u32 and a u64 atomic. The word is
-//    exact while COUNT < 2^16; the add that sees COUNT >= 2^15 moves the word out (CAS to 0) into the straggler list
-//    (applied with device atomics at the end), so a hot key never overflows it;
-//  * the per-chunk slice range is reduced with DPP (row_shr / row_bcast) instead of shuffles through LDS;
-//  * the home buckets of four entries are read before any is compared (one LDS round trip for four probes);
-//  * a slice leaving the window is read out of LDS and its HBM loads are issued, and the add + store completes after
-//    the next chunk's barrier (the loads' latency overlaps that chunk's probes).
-constexpr uint32_t kK32Empty = 0x80000000u;
-constexpr uint32_t kK32Other = 0x80000001u;
-constexpr unsigned long long kPkSumMask = (1ull << 48) - 1;
-
-__device__ __forceinline__ bool narrow_key_ok(int64_t key) {   // a key the 32-bit LDS table holds as itself
-    return (int64_t)(int32_t)key == key && (uint32_t)key != kK32Empty && (uint32_t)key != kK32Other;
-}
-__device__ __forceinline__ int64_t pk_sum(unsigned long long w) {   // SUM of a packed word (two's complement wrap)
-    return (int64_t)((w & kPkSumMask) - ((w >> 48) << 31));
-}
-__device__ __forceinline__ int wave_min_dpp(int x) {   // every lane's minimum over the wave (lane 63 holds it)
-    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x111, 0xf, 0xf, false));   // row_shr:1
-    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x112, 0xf, 0xf, false));   // row_shr:2
-    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x114, 0xf, 0xf, false));   // row_shr:4
-    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x118, 0xf, 0xf, false));   // row_shr:8
-    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x142, 0xa, 0xf, false));   // row_bcast:15
-    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x143, 0xc, 0xf, false));   // row_bcast:31
-    return __builtin_amdgcn_readlane(x, 63);
-}
-__device__ __forceinline__ int wave_max_dpp(int x) {
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));
-    return __builtin_amdgcn_readlane(x, 63);
-}
-
-template <int IT, int TH>
-__global__ void __launch_bounds__(TH, 1) combine_nk_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
-    constexpr int SL = 2;
-    constexpr int kWaves = TH / 64;
-    constexpr int LPS = TH / kSub;
-    constexpr int kPer = 4096 / TH;    // slots per thread in a flush (seg <= 4096)
-    static_assert(LPS == 64 && IT % 4 == 0, "one wave per sub-bucket; probes in groups of four");
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const EngineConst& c = *cp;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int sub = wv, li = lane;
-    const int p = blockIdx.x;
-    const int seg = 1 << a.seg_log;
-    const uint32_t smask = (uint32_t)seg - 1u;
-    uint32_t* lk = (uint32_t*)smem;                                         // [seg] key words
-    unsigned long long* lpk = (unsigned long long*)(smem + (size_t)seg * 4);   // [SL][seg] packed accumulators
-    __shared__ int s_mn[2][kWaves], s_mx[2][kWaves];
-    __shared__ StragL s_strag[kStragL];
-    __shared__ int s_sn, s_new;
-    long long pt = clock64();
-    long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define PMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
-    unsigned long long* gkeys = a.key_table + ((int64_t)p << a.seg_log);
-    for (int i = tid; i < seg; i += TH) {
-        const unsigned long long k = gkeys[i];
-        lk[i] = k == kEmptyKey ? kK32Empty : narrow_key_ok((int64_t)k) ? (uint32_t)k : kK32Other;
-    }
-    for (int i = tid; i < SL * seg; i += TH) lpk[i] = 0ull;
-    if (tid == 0) { s_new = 0; s_sn = 0; }
-    const int64_t my_cnt = min((int64_t)a.b_cnt[p * kSub + sub], a.capb);
-    const int64_t boff = ((int64_t)p * kSub + sub) * a.capb;
-    int64_t cnt = 0;
-    for (int s2 = 0; s2 < kSub; ++s2) cnt = max(cnt, min((int64_t)a.b_cnt[p * kSub + s2], a.capb));
-    const gc_u64_ptr bk = (const gc_u64_ptr)(a.b_key + boff);
-    const __attribute__((address_space(1))) uint16_t* br = (const __attribute__((address_space(1))) uint16_t*)(a.b_rel + boff);
-    constexpr int64_t kChunk = (int64_t)IT * LPS;
-    auto strag_add = [&](int rel, uint32_t g, uint32_t n, unsigned long long sum) {
-        const int si = atomicAdd(&s_sn, 1);
-        if (si < kStragL) s_strag[si] = StragL{g, n, rel, 0, sum, 0ull};
-        else strag_apply(a, c, rel, g, n, sum, 0ull);
-    };
-    // deferred flush: the slice's packed words (read out of LDS, which is cleared) and its HBM words in flight
-    int pend_rel = -1;
-    g_u64* pend_base = nullptr;
-    unsigned long long pw[kPer], po0[kPer], po1[kPer];
-    auto flush_issue = [&](int rel) {
-        const int w = rel & (SL - 1);
-        const int32_t slot = (rel >= 0 && rel < kRelCap) ? a.rel2slot[rel] : -1;
-        pend_base = slot >= 0 ? (g_u64*)a.slot_base[slot] : nullptr;
-        pend_rel = rel;
-#pragma unroll
-        for (int m = 0; m < kPer; ++m) {
-            const int i = tid + m * TH;
-            pw[m] = 0ull;
-            if (i < seg) { pw[m] = lpk[w * seg + i]; lpk[w * seg + i] = 0ull; }
-        }
-        if (pend_base) {
-#pragma unroll
-            for (int m = 0; m < kPer; ++m) {
-                const int64_t g = ((int64_t)p << a.seg_log) + tid + m * TH;
-                po0[m] = pw[m] ? pend_base[g] : 0ull;
-                po1[m] = pw[m] ? pend_base[a.stride + g] : 0ull;
-            }
-        }
-    };
-    auto flush_complete = [&]() {
-        if (pend_rel < 0) return;
-        if (pend_base) {
-#pragma unroll
-            for (int m = 0; m < kPer; ++m) {
-                if (!pw[m]) continue;
-                const int64_t g = ((int64_t)p << a.seg_log) + tid + m * TH;
-                pend_base[g] = po0[m] + (pw[m] >> 48);
-                pend_base[a.stride + g] = po1[m] + (unsigned long long)pk_sum(pw[m]);
-            }
-        }
-        pend_rel = -1;
-    };
-    __syncthreads();
-    unsigned long long nkey[IT];
-    int nrel[IT];
-    auto load_chunk = [&](int64_t cb) {
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            const int64_t i = cb + (int64_t)j * LPS + li;
-            const bool ok = i < my_cnt;
-            nkey[j] = ok ? bk[i] : 0ull;
-            nrel[j] = ok ? (int)br[i] : -1;
-        }
-    };
-    load_chunk(0);
-    PMARK(0);
-    int lo = 0x7fffffff;
-    int it = 0;
-    for (int64_t cb = 0; cb < cnt; cb += kChunk, ++it) {
-        uint32_t k32[IT], vb[IT];
-        int rel[IT];
-        int rmin = 0x7fffffff, rmax = -1;
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            k32[j] = (uint32_t)nkey[j];
-            vb[j] = (uint32_t)(nkey[j] >> 32) ^ 0x80000000u;   // the int32 value biased by 2^31
-            rel[j] = nrel[j];
-            if (rel[j] >= 0) { rmin = min(rmin, rel[j]); rmax = max(rmax, rel[j]); }
-        }
-        PMARK(1);
-        if (cb + kChunk < cnt) load_chunk(cb + kChunk);
-        rmin = wave_min_dpp(rmin);
-        rmax = wave_max_dpp(rmax);
-        const int buf = it & 1;
-        if (lane == 0) { s_mn[buf][wv] = rmin; s_mx[buf][wv] = rmax; }
-        uint32_t pos[IT];
-#pragma unroll
-        for (int j = 0; j < IT; ++j) pos[j] = (uint32_t)jm::mix64((unsigned long long)(int64_t)(int32_t)k32[j]) & smask;
-        PMARK(2);
-        __syncthreads();
-        PMARK(3);
-        flush_complete();                   // the previous slide's merge (its loads overlapped the last chunk)
-        int cmin = 0x7fffffff, cmax = -1;
-#pragma unroll
-        for (int v = 0; v < kWaves; ++v) { cmin = min(cmin, s_mn[buf][v]); cmax = max(cmax, s_mx[buf][v]); }
-        if (cmax < 0) continue;
-        if (lo == 0x7fffffff) lo = cmin;
-        if (cmax >= lo + SL) {              // slide the window up to the chunk's newest slice
-            while (cmax >= lo + SL) {
-                flush_complete();           // a second slide in one chunk: finish the first one now
-                flush_issue(lo);
-                ++lo;
-                if (a.prof) pacc[7] += 1000;
-            }
-            __syncthreads();                // the cleared window slots before any add of this chunk
-        }
-        const int lo_c = lo;                // entries older than this are stragglers
-        PMARK(4);
-        // probes in groups of four: the four home buckets are read before any is compared
-        int32_t loc[IT];
-#pragma unroll
-        for (int j0 = 0; j0 < IT; j0 += 4) {
-            uint4 q[4][2];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint4* bp = (const uint4*)&lk[pos[j0 + u] & ~(uint32_t)(kBucket - 1)];
-                q[u][0] = bp[0];
-                q[u][1] = bp[1];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int j = j0 + u;
-                loc[j] = -2;
-                if (rel[j] < 0) continue;
-                const uint32_t kk = k32[j];
-                const uint32_t v[8] = {q[u][0].x, q[u][0].y, q[u][0].z, q[u][0].w, q[u][1].x, q[u][1].y, q[u][1].z, q[u][1].w};
-                uint32_t eq = 0, em = 0;
-#pragma unroll
-                for (int t = 0; t < 8; ++t) { eq |= (uint32_t)(v[t] == kk) << t; em |= (uint32_t)(v[t] == kK32Empty) << t; }
-                uint32_t b = pos[j] & ~(uint32_t)(kBucket - 1);
-                int32_t found = eq ? (int32_t)(b + __builtin_ctz(eq)) : -1;
-                // not in the home bucket's snapshot: insert, or probe on (keys displaced past their bucket)
-                for (int round = 0; found < 0 && round <= (seg >> 3); ) {
-                    if (em) {                   // absent: insert at the first empty slot (CAS vs other lanes)
-                        const uint32_t sidx = b + __builtin_ctz(em);
-                        const uint32_t old = atomicCAS(&lk[sidx], kK32Empty, kk);
-                        if (old == kK32Empty) { found = (int32_t)sidx; atomicAdd(&s_new, 1); break; }
-                        if (old == kk) { found = (int32_t)sidx; break; }
-                    } else {
-                        b = (b + kBucket) & smask;
-                        ++round;
-                    }
-                    const uint4* bp = (const uint4*)&lk[b];   // (re-)read the bucket
-                    const uint4 r0 = bp[0], r1 = bp[1];
-                    const uint32_t w8[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-                    eq = 0; em = 0;
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) { eq |= (uint32_t)(w8[t] == kk) << t; em |= (uint32_t)(w8[t] == kK32Empty) << t; }
-                    if (eq) found = (int32_t)(b + __builtin_ctz(eq));
-                }
-                loc[j] = found;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            if (rel[j] < 0 || rel[j] >= lo + SL) continue;
-            const int32_t local = loc[j];
-            if (local < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
-            const uint32_t g = (uint32_t)(((int64_t)p << a.seg_log) + local);
-            if (rel[j] < lo_c) {            // older than the window: listed, applied with atomics at the end
-                if (a.prof) pacc[6] += 1000000;
-                strag_add(rel[j], g, 1u, (unsigned long long)(int64_t)(int32_t)(vb[j] ^ 0x80000000u));
-                continue;
-            }
-            unsigned long long* wp = &lpk[(size_t)(rel[j] & (SL - 1)) * seg + local];
-            const unsigned long long old = atomicAdd(wp, (1ull << 48) | vb[j]);
-            if (old >> 63) {                // COUNT reached 2^15: move the word out before it can overflow
-                unsigned long long cur = *wp;
-                while (cur >> 63) {
-                    const unsigned long long o2 = atomicCAS(wp, cur, 0ull);
-                    if (o2 == cur) { strag_add(rel[j], g, (uint32_t)(cur >> 48), (unsigned long long)pk_sum(cur)); break; }
-                    cur = o2;
-                }
-            }
-        }
-        PMARK(5);
-    }
-    __syncthreads();
-    flush_complete();
-    if (lo != 0x7fffffff)
-        for (int r = lo; r < lo + SL; ++r) { flush_issue(r); flush_complete(); }
-    __syncthreads();                    // every merge of this block stored before the stragglers' atomics
-    if (tid == 0 && s_sn) atomicAdd(&a.st->strag_n, s_sn);
-    for (int t = tid; t < min(s_sn, kStragL); t += TH) {
-        const StragL se = s_strag[t];
-        strag_apply(a, c, se.rel, se.g, se.n, se.x0, se.x1);
-    }
-    if (s_new) {                        // publish newly inserted keys (exclusive owner of this segment)
-        for (int i = tid; i < seg; i += TH) {
-            const uint32_t w = lk[i];
-            if (w != kK32Empty && w != kK32Other) gkeys[i] = (unsigned long long)(int64_t)(int32_t)w;
-        }
-        if (tid == 0) atomicAdd(&a.st->n_keys, (unsigned long long)s_new);
-    }
-    if (a.prof && tid == 0) for (int q = 0; q < 8; ++q) a.prof[(int64_t)p * 8 + q] = pacc[q];
-#undef PMARK
-}
 
 // ------------------------------------------------------------------------------------------------
 // fire
@@ -1941,14 +1453,16 @@ __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineCo
 // sums and MIN/MAX keep the generic fire. Rows are emitted window by window with one row
 // reservation per block and window.
 constexpr int kSlideMaxU = 2048;                  // union slices per launch (LDS slot table)
-constexpr int kSlideJ = 8;                        // keys per thread
+constexpr int kSlideBlock = 512;                  // threads per block
+constexpr int kSlideJ = 2;                        // keys per thread (1024 keys per block)
 constexpr int kSlideAcc = 4;                      // COUNT + up to 3 integer-sum columns
 
 struct FireSlideArgs {
     const unsigned long long* key_table;
     int64_t capacity, stride;
-    const unsigned long long* const* upos;   // [m] slot base per union slice (nullptr: no records); bit 0 set: the
-                                             // slice retires at this watermark -- its last read restores the identity
+    const unsigned long long* const* upos;   // [m] slot base per union slice (a slice without records points at a
+                                             // zero slice); bit 0 set: the slice retires at this watermark -- its last
+                                             // read restores the identity
     int32_t m, nw, L, r;                     // union slices, windows, slices per window, per slide
     int64_t start0, slide, size;             // first window start, window step, window size
     int64_t* o_key;
@@ -1960,34 +1474,41 @@ struct FireSlideArgs {
 };
 
 // NA = the handle's accumulator count (compile time: the running sums and the next window's slice values stay in
-// registers). The slices entering / leaving window w + 1 are loaded before window w's rows are reserved and written,
-// so their latency overlaps the ballot, the row reservation and the stores.
+// registers). Every slice load is unconditional -- absent keys read their (zero) slot through a clamped index and are
+// masked after the load, a slice without records reads the zero slice -- since a load under a per-element condition
+// makes hipcc branch around it and wait for each load separately. With one slice per slide (r = 1) the slices entering
+// / leaving window w + 1 are loaded before window w's rows are reserved and written, so their latency overlaps the
+// ballot, the row reservation and the stores.
 // Slices that retire at this watermark (tagged upos entries) are cleared here instead of by reset_slots_kernel: the
 // read that subtracts a leaving slice is its last, and only the non-zero values are written back (a Zipf stream
 // leaves most keys absent from most slices, so this writes a fraction of the dense column reset_slots_kernel wrote).
+// Output rows are written with non-temporal stores (streamed once, never re-read by this kernel).
 __device__ __forceinline__ unsigned long long* slide_ptr(const unsigned long long* p) {
     return (unsigned long long*)((uintptr_t)p & ~(uintptr_t)1);
 }
 __device__ __forceinline__ bool slide_zero(const unsigned long long* p) { return ((uintptr_t)p & 1) != 0; }
 
-template <int NA>
-__global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, const EngineConst* __restrict__ cp) {
+template <int NA, int J = kSlideJ, int TB = kSlideBlock, bool NT = true>
+__global__ void __launch_bounds__(TB) fire_slide_kernel(FireSlideArgs f, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
-    constexpr int kWaves = kBlock / 64;
+    constexpr int kWaves = TB / 64;
     __shared__ const unsigned long long* s_u[kSlideMaxU];
-    __shared__ uint32_t woff[kSlideJ][kWaves];
-    __shared__ unsigned long long s_base;
+    __shared__ uint32_t woff[3][J][kWaves];           // three generations: counted, scanned, read by the writers
+    __shared__ unsigned long long s_base[3];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int i = tid; i < f.m; i += kBlock) s_u[i] = f.upos[i];
+    for (int i = tid; i < f.m; i += TB) s_u[i] = f.upos[i];
     const int64_t nk = f.capacity + 1;
-    const int64_t k0 = (int64_t)blockIdx.x * kBlock * kSlideJ;
-    unsigned long long kv[kSlideJ];
-    bool present[kSlideJ];
-    unsigned long long S[kSlideJ][NA];
+    const int64_t k0 = (int64_t)blockIdx.x * TB * J;
+    const int64_t st = f.stride;
+    unsigned long long kv[J];
+    int64_t kc[J];                                    // slot index, clamped into the table
+    bool present[J];
+    unsigned long long S[J][NA];
 #pragma unroll
-    for (int j = 0; j < kSlideJ; ++j) {
-        const int64_t k = k0 + (int64_t)j * kBlock + tid;
-        kv[j] = k < nk ? f.key_table[k] : kEmptyKey;
+    for (int j = 0; j < J; ++j) {
+        const int64_t k = k0 + (int64_t)j * TB + tid;
+        kc[j] = k < nk ? k : nk - 1;
+        kv[j] = f.key_table[kc[j]];
         present[j] = k < nk && ((k < f.capacity) ? (kv[j] != kEmptyKey) : (kv[j] == 1ull));
 #pragma unroll
         for (int a = 0; a < NA; ++a) S[j][a] = 0;
@@ -1996,117 +1517,125 @@ __global__ void __launch_bounds__(kBlock) fire_slide_kernel(FireSlideArgs f, con
     // window 0: the sum of its L slices
     for (int u = 0; u < f.L; ++u) {
         const unsigned long long* b = slide_ptr(s_u[u]);
-        if (!b) continue;
+        unsigned long long x[J][NA];
 #pragma unroll
-        for (int j = 0; j < kSlideJ; ++j) {
-            if (!present[j]) continue;
-            const int64_t k = k0 + (int64_t)j * kBlock + tid;
+        for (int j = 0; j < J; ++j)
 #pragma unroll
-            for (int a = 0; a < NA; ++a) S[j][a] += b[(int64_t)a * f.stride + k];
-        }
+            for (int a = 0; a < NA; ++a) x[j][a] = b[a * st + kc[j]];
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int a = 0; a < NA; ++a) S[j][a] += present[j] ? x[j][a] : 0ull;
     }
-    // the next window's entering minus leaving values, prefetched when they fit the registers (NA <= 2)
-    constexpr bool PF = false;   // measured slower with the prefetch (153 VGPRs for NA = 2, C3 fire 2.64 vs 2.0 ms)
-    unsigned long long D[PF ? kSlideJ : 1][NA];
-    auto load_delta = [&](int w1) {   // S(w1) = S(w1 - 1) + D
-        if constexpr (PF) {
+    unsigned long long Xi[J][NA], Xo[J][NA];
+    unsigned long long* po = nullptr;
+    bool pz = false;
+    auto load2 = [&](const unsigned long long* bi, const unsigned long long* to) {
+        po = slide_ptr(to);
+        pz = slide_zero(to);
 #pragma unroll
-            for (int j = 0; j < kSlideJ; ++j)
+        for (int j = 0; j < J; ++j)
 #pragma unroll
-                for (int a = 0; a < NA; ++a) D[j][a] = 0;
-            if (w1 >= f.nw) return;
-            for (int t = 0; t < f.r; ++t) {
-                const unsigned long long* bin = slide_ptr(s_u[(w1 - 1) * f.r + f.L + t]);
-                const unsigned long long* bout = slide_ptr(s_u[(w1 - 1) * f.r + t]);
-#pragma unroll
-                for (int j = 0; j < kSlideJ; ++j) {
-                    if (!present[j]) continue;
-                    const int64_t k = k0 + (int64_t)j * kBlock + tid;
-#pragma unroll
-                    for (int a = 0; a < NA; ++a) {
-                        const unsigned long long xin = bin ? bin[(int64_t)a * f.stride + k] : 0ull;
-                        const unsigned long long xout = bout ? bout[(int64_t)a * f.stride + k] : 0ull;
-                        D[j][a] += xin - xout;
-                    }
-                }
+            for (int a = 0; a < NA; ++a) {
+                Xi[j][a] = bi[a * st + kc[j]];
+                Xo[j][a] = po[a * st + kc[j]];
             }
-        }
     };
-    if (PF) load_delta(1);
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    for (int w = 0; w < f.nw; ++w) {
-        if (w > 0 && PF) {
+    auto apply = [&]() {   // S(w) = S(w - 1) + entering - leaving; a retiring leaving slice is cleared
 #pragma unroll
-            for (int j = 0; j < kSlideJ; ++j)
+        for (int j = 0; j < J; ++j)
 #pragma unroll
-                for (int a = 0; a < NA; ++a) S[j][a] += D[PF ? j : 0][a];
-            load_delta(w + 1);                      // in flight while this window's rows are reserved and written
-        } else if (w > 0) {                         // S(w) = S(w - 1) + entering - leaving, in place
-            for (int t = 0; t < f.r; ++t) {
-                const unsigned long long* bin = slide_ptr(s_u[(w - 1) * f.r + f.L + t]);
-                const unsigned long long* tout = s_u[(w - 1) * f.r + t];
-                unsigned long long* bout = slide_ptr(tout);
-                const bool zout = slide_zero(tout);
-#pragma unroll
-                for (int j = 0; j < kSlideJ; ++j) {
-                    if (!present[j]) continue;
-                    const int64_t k = k0 + (int64_t)j * kBlock + tid;
-#pragma unroll
-                    for (int a = 0; a < NA; ++a) {
-                        const unsigned long long xin = bin ? bin[(int64_t)a * f.stride + k] : 0ull;
-                        const unsigned long long xout = bout ? bout[(int64_t)a * f.stride + k] : 0ull;
-                        S[j][a] = S[j][a] + xin - xout;
-                        if (zout && xout) bout[(int64_t)a * f.stride + k] = 0ull;
-                    }
-                }
+            for (int a = 0; a < NA; ++a) {
+                if (!present[j]) continue;
+                S[j][a] = S[j][a] + Xi[j][a] - Xo[j][a];
+                if (pz && Xo[j][a]) po[a * st + kc[j]] = 0ull;
             }
-        }
-        unsigned long long masks[kSlideJ];
-#pragma unroll
-        for (int j = 0; j < kSlideJ; ++j) {
-            masks[j] = __ballot(present[j] && S[j][0] != 0);
-            if (lane == 0) woff[j][wid] = (uint32_t)__popcll(masks[j]);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t run = 0;
-            for (int j = 0; j < kSlideJ; ++j)
-                for (int v = 0; v < kWaves; ++v) { const uint32_t t = woff[j][v]; woff[j][v] = run; run += t; }
-            s_base = run ? atomicAdd(&f.st->rows, (unsigned long long)run) : 0ull;
-        }
-        __syncthreads();
+    };
+    auto st64 = [&](int64_t v, int64_t* p) { if (NT) __builtin_nontemporal_store(v, p); else *p = v; };
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    // rows of window w (sums Sw, masks mw) at the block's reservation of generation g
+    auto write_rows = [&](int w, const unsigned long long (&Sw)[J][NA], const unsigned long long (&mw)[J], int g) {
         const int64_t ws = f.start0 + (int64_t)w * f.slide;
+        const int64_t we = ws + f.size;
+        const int64_t rb = (int64_t)s_base[g];
 #pragma unroll
-        for (int j = 0; j < kSlideJ; ++j) {
-            if (!((masks[j] >> lane) & 1ull)) continue;
-            const int64_t k = k0 + (int64_t)j * kBlock + tid;
-            const int64_t row = (int64_t)s_base + woff[j][wid] + __popcll(masks[j] & lt);
+        for (int j = 0; j < J; ++j) {
+            if (!((mw[j] >> lane) & 1ull)) continue;
+            const int64_t row = rb + woff[g][j][wid] + __popcll(mw[j] & lt);
             if (row >= f.out_cap) continue;
-            f.o_key[row] = (k < f.capacity) ? (int64_t)kv[j] : LONG_MIN_J;
-            f.o_start[row] = ws;
-            f.o_end[row] = ws + f.size;
+            st64(kc[j] < f.capacity ? (int64_t)kv[j] : LONG_MIN_J, f.o_key + row);
+            st64(ws, f.o_start + row);
+            st64(we, f.o_end + row);
             for (int a = 0; a < c.nout; ++a) {   // (no nullable aggregates on this path: the host checks)
                 const AggDesc d = c.agg[a];
                 unsigned long long x = 0;
 #pragma unroll
-                for (int q = 1; q < NA; ++q) if (q == d.acc) x = S[j][q];
-                write_agg(d, S[j][0], x, 0, f.o_agg[a], nullptr, row);
+                for (int q = 1; q < NA; ++q) if (q == d.acc) x = Sw[j][q];
+                const int64_t cnt = (int64_t)Sw[j][0], iv = (int64_t)x;
+                int64_t v;
+                switch (d.kind) {   // every aggregate of an invertible handle has a 64-bit integer result
+                    case FWA_COUNT: v = cnt; break;
+                    case FWA_COUNT_COL: v = d.acc > 0 ? iv : cnt; break;
+                    case FWA_SUM_I64: v = iv; break;
+                    case FWA_AVG_I64: v = (cnt == -1 && iv == LONG_MIN_J) ? LONG_MIN_J : iv / cnt; break;
+                    default: write_agg(d, Sw[j][0], x, 0, f.o_agg[a], nullptr, row); continue;
+                }
+                st64(v, (int64_t*)f.o_agg[a] + row);
             }
         }
-        __syncthreads();   // woff / s_base reuse
+    };
+    // One barrier per window: window w's rows are counted and its reservation issued (thread 0) while the other waves
+    // write window w - 1's rows at the reservation made one iteration earlier.
+    const bool one = f.r == 1;
+    if (one && f.nw > 1) load2(slide_ptr(s_u[f.L]), s_u[0]);
+    unsigned long long Sp[J][NA], mp[J];
+    for (int w = 0; w < f.nw; ++w) {
+        if (w > 0 && one) {
+            apply();
+            if (w + 1 < f.nw) load2(slide_ptr(s_u[w + f.L]), s_u[w]);   // in flight while window w - 1 is written
+        } else if (w > 0) {
+            for (int t = 0; t < f.r; ++t) {
+                load2(slide_ptr(s_u[(w - 1) * f.r + f.L + t]), s_u[(w - 1) * f.r + t]);
+                apply();
+            }
+        }
+        const int g = w % 3;
+        unsigned long long masks[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            masks[j] = __ballot(present[j] && S[j][0] != 0);
+            if (lane == 0) woff[g][j][wid] = (uint32_t)__popcll(masks[j]);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t run = 0;
+            for (int j = 0; j < J; ++j)
+                for (int v = 0; v < kWaves; ++v) { const uint32_t t = woff[g][j][v]; woff[g][j][v] = run; run += t; }
+            s_base[g] = run ? atomicAdd(&f.st->rows, (unsigned long long)run) : 0ull;
+        }
+        if (w > 0) write_rows(w - 1, Sp, mp, (w - 1) % 3);
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            mp[j] = masks[j];
+#pragma unroll
+            for (int a = 0; a < NA; ++a) Sp[j][a] = S[j][a];
+        }
     }
+    __syncthreads();
+    if (f.nw > 0) write_rows(f.nw - 1, Sp, mp, (f.nw - 1) % 3);
     // retiring slices whose last window is the run's last one never left it: clear them now
     for (int u = (f.nw - 1) * f.r; u < f.m; ++u) {
         if (!slide_zero(s_u[u])) continue;
         unsigned long long* b = slide_ptr(s_u[u]);
 #pragma unroll
-        for (int j = 0; j < kSlideJ; ++j) {
-            if (!present[j]) continue;
-            const int64_t k = k0 + (int64_t)j * kBlock + tid;
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int a = 0; a < NA; ++a) Xo[j][a] = b[a * st + kc[j]];
+#pragma unroll
+        for (int j = 0; j < J; ++j)
 #pragma unroll
             for (int a = 0; a < NA; ++a)
-                if (b[(int64_t)a * f.stride + k]) b[(int64_t)a * f.stride + k] = 0ull;
-        }
+                if (present[j] && Xo[j][a]) b[a * st + kc[j]] = 0ull;
     }
 }
 
@@ -3438,6 +2967,8 @@ int64_t gcd64(int64_t a, int64_t b) {
     return a < 0 ? -a : a;
 }
 
+#include "sessions4.inc"
+
 }  // namespace
 
 // ==================================================================================================
@@ -3523,6 +3054,8 @@ struct fwa_engine {
     int32_t* d_win_slots = nullptr;
     int32_t win_slots_cap = 0;
     void* d_upos = nullptr;            // fire_slide union slot table
+    void* d_zslice = nullptr;          // fire_slide: the slot columns of a slice without records (zeros)
+    size_t zslice_bytes = 0;
     // watermark / stats
     int64_t wm = LONG_MIN_J;
     int64_t records_in = 0, late_dropped = 0, rows_out = 0;
@@ -3568,8 +3101,12 @@ struct fwa_engine {
     int64_t* d_send2 = nullptr;
     unsigned long long* d_spk = nullptr;   // session bulk rows (Sess2Args::pk)
     void* d_sg = nullptr;                  // segment kernel staging (Sess2Args::sg_*)
+    void* d_s4 = nullptr;                  // cell pre-aggregation scratch (sessions4.inc)
+    size_t s4_bytes = 0;
+    bool s4_attr = false;
     int64_t sg_cap = 0, sgw_cap = 0;
     int32_t cell_skip = 0;
+    int32_t sess_path = 0;                 // path of the last session push (FWA_OPT_SESSION_PATH)
     bool narrow = true, narrow_used = false;   // Phase P / A narrow bucket entries (sticky off after a wide push)
     int64_t* d_spe = nullptr;
     int64_t* d_smax = nullptr;
@@ -3603,11 +3140,10 @@ struct fwa_engine {
     bool sparse = false;
     SpState* sp = nullptr;
     // per-handle options (fwa_set_option; the defaults are the production behaviour)
-    int32_t opt_pre = -1, opt_mp = -1, opt_narrow = -1, opt_cells = -1;   // -1 adaptive, 0 never, 1 always
+    int32_t opt_pre = -1, opt_mp = -1, opt_narrow = -1, opt_cells = -1, opt_slide = 0;   // -1 adaptive, 0 never, 1 always
     int64_t opt_out_min = 0;
     bool opt_partials_v1 = false;
     int32_t opt_profile = 0;
-    int32_t opt_exp = 3;                  // A/B of the narrow kernels (option 99, temporary)
     long long* d_prof = nullptr;          // FWA_OPT_PROFILE: per-block phase cycle counters of Phase P / A
 };
 
@@ -4052,8 +3588,8 @@ void fwa_destroy(fwa_engine* e) {
     if (e->d_lr_n) (void)hipFree(e->d_lr_n);
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_bkey, e->d_brel, e->d_bn,
-                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof};
+                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos, e->d_zslice,
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -4554,7 +4090,6 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else partition3_kernel<NV, 4, 1024, 3, 2, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
     if (pre) { if (e->nv == 0) PRELAUNCH(0); else PRELAUNCH(1); }
     else if (e->nv == 0) P3LAUNCH(0, 8, 3);
-    else if (narrow && !mp && (e->opt_exp & 1)) partition_nk_kernel<6, 1024><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (narrow) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
@@ -4605,7 +4140,6 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else C3M(IT, TH, NV, 0, 0); } while (0)
     if (narrow) {   // packed entries free the prefetch registers: 8 entries per lane and chunk (4 with window passes)
         if (mp) combine3_kernel<2, 2, 1, 1024, 1, 0, 1, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-        else if (e->opt_exp & 2) combine_nk_kernel<8, 1024><<<e->np, 1024, seg3 * 4 + 2 * seg3 * 8, e->stream>>>(ca, e->d_ec);
         else combine3_kernel<8, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
     } else if (e->nv == 0) C3L(4, 1024, 0);
     else if (e->nv == 1) C3L(4, 1024, 1);
@@ -4723,6 +4257,8 @@ static int launch_segments(fwa_engine* e, Sess2Args& s, int64_t nb, bool cells) 
     return FWA_OK;
 }
 
+#include "sessions4_host.inc"
+
 static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     const int64_t n = a.n;
     const int64_t n_in = e->n_ss;
@@ -4795,8 +4331,24 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
     // cell path (sess3_*): fixed gap, 32-bit cell keys; redone on the general path below when a record is not
     // order-free or a start falls outside the cell range (then not tried again for 8 pushes)
     const int cb = 32 - e->kid_bits;
-    if (e->opt_cells != 0 && !s.gapc && cb >= 1 && e->nacc <= 5 && n > 0 && e->cell_skip <= 0 &&
+    // cell pre-aggregation (sessions4.inc) first; cells or sessions out of its range: the sort-based cell path
+    bool s4_general = false;
+    if (e->opt_cells != 0 && !s.gapc && e->nacc <= 5 && n > 0 && e->cell_skip <= 0 && n + n_in < ((int64_t)1 << 31) &&
+        e->cfg.gap_ms > 0 && e->cfg.gap_ms <= ((int64_t)1 << 27) && e->capacity < ((int64_t)1 << 27) &&
+        (e->capacity + 1 + kS4Kids - 1) / kS4Kids <= 24576) {
+        int verdict = 1;
+        if ((rc = push_session_s4(e, s, n, n_in, dropped_out, &verdict))) return rc;
+        if (verdict == 0) { e->sess_path = 2; return FWA_OK; }
+        s4_general = verdict == 2;
+        memset(&z, 0, sizeof(z));
+        z.ts_min = ~0ull;
+        if ((rc = upload(e, e->d_sctr, &z, sizeof(z)))) return rc;
+        if ((rc = reset_push_status(e))) return rc;
+    }
+    bool tried3 = false;
+    if (e->opt_cells != 0 && !s4_general && !s.gapc && cb >= 1 && e->nacc <= 5 && n > 0 && e->cell_skip <= 0 &&
         n + n_in < ((int64_t)1 << 31)) {
+        tried3 = true;
         Sess2Args t = s;
         t.tb = cb;
         t.gap_div = jm::udiv64_make((uint64_t)e->cfg.gap_ms);
@@ -4835,6 +4387,7 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
             e->n_ss = (int64_t)e->h_sctr->n_out_sp;
             e->ss_cur ^= 1;
             *dropped_out = (int64_t)e->h_st->dropped;
+            e->sess_path = 1;
             return FWA_OK;
         }
         e->cell_skip = 8;                                 // the general path redoes the push (key inserts are idempotent)
@@ -4844,7 +4397,12 @@ static int push_session(fwa_engine* e, IngestArgs& a, int64_t* dropped_out) {
         if ((rc = upload(e, e->d_sctr, &z, sizeof(z)))) return rc;
         HIPCHK(e, hipMemsetAsync(e->d_kflag, 0, (size_t)e->capacity + 1, e->stream));
         if ((rc = reset_push_status(e))) return rc;
-    } else if (e->cell_skip > 0) {
+    }
+    e->sess_path = 0;
+    if (s4_general) {
+        e->cell_skip = 8;                                 // as the cell path: not tried again for 8 pushes
+        e->replay_records += n;
+    } else if (!tried3 && e->cell_skip > 0) {
         --e->cell_skip;
     }
     HIPCHK(e, hipEventRecord(e->ev[0], e->stream));
@@ -5928,7 +5486,17 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     const int64_t m = (nw - 1) * r + L;
     if (m > kSlideMaxU) return FWA_OK;
     const int64_t q0 = slice_q(e, start0);
-    std::vector<const unsigned long long*> up(m, nullptr);
+    // slices without records read a zero slice (the kernel's loads are unconditional)
+    const size_t zbytes = 8 * (size_t)e->nacc * (size_t)e->stride;
+    if (zbytes > e->zslice_bytes) {
+        if (e->d_zslice) HIPCHK(e, hipFree(e->d_zslice));
+        e->d_zslice = nullptr;
+        e->zslice_bytes = 0;
+        HIPCHK(e, hipMalloc(&e->d_zslice, zbytes));
+        HIPCHK(e, hipMemsetAsync(e->d_zslice, 0, zbytes, e->stream));
+        e->zslice_bytes = zbytes;
+    }
+    std::vector<const unsigned long long*> up(m, (const unsigned long long*)e->d_zslice);
     std::vector<int32_t> cleared;
     bool any = false;
     for (int64_t i = 0; i < m; ++i) {
@@ -5975,13 +5543,18 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
     f.out_cap = e->out_cap;
     f.st = e->d_st;
-    const int64_t grid = (e->capacity + 1 + (int64_t)kBlock * kSlideJ - 1) / ((int64_t)kBlock * kSlideJ);
+    const int64_t grid = (e->capacity + 1 + (int64_t)kSlideBlock * kSlideJ - 1) / ((int64_t)kSlideBlock * kSlideJ);
     HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
     switch (e->nacc) {
-        case 1: fire_slide_kernel<1><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec); break;
-        case 2: fire_slide_kernel<2><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec); break;
-        case 3: fire_slide_kernel<3><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec); break;
-        default: fire_slide_kernel<4><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec); break;
+        case 1: fire_slide_kernel<1><<<(unsigned)grid, kSlideBlock, 0, e->stream>>>(f, e->d_ec); break;
+        case 2:
+            if (e->opt_slide == 1) fire_slide_kernel<2, 2, 512, false><<<(unsigned)((e->capacity + 1 + 1023) / 1024), 512, 0, e->stream>>>(f, e->d_ec);
+            else if (e->opt_slide == 2) fire_slide_kernel<2, 4, 256, false><<<(unsigned)((e->capacity + 1 + 1023) / 1024), 256, 0, e->stream>>>(f, e->d_ec);
+            else if (e->opt_slide == 3) fire_slide_kernel<2, 2, 1024, false><<<(unsigned)((e->capacity + 1 + 2047) / 2048), 1024, 0, e->stream>>>(f, e->d_ec);
+            else fire_slide_kernel<2><<<(unsigned)grid, kSlideBlock, 0, e->stream>>>(f, e->d_ec);
+            break;
+        case 3: fire_slide_kernel<3><<<(unsigned)grid, kSlideBlock, 0, e->stream>>>(f, e->d_ec); break;
+        default: fire_slide_kernel<4><<<(unsigned)grid, kSlideBlock, 0, e->stream>>>(f, e->d_ec); break;
     }
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
@@ -6307,7 +5880,7 @@ int fwa_set_option(fwa_engine* e, int32_t option, int64_t value) {
         case FWA_OPT_PARTIALS_ONE_PASS: e->opt_partials_v1 = value > 0; return FWA_OK;
         case FWA_OPT_SP_TABLE: case FWA_OPT_SP_FMAX: case FWA_OPT_SP_BUDGET: return sp_set_option(e, option, value);
         case FWA_OPT_PROFILE: e->opt_profile = value > 0 ? 1 : 0; return FWA_OK;
-        case 99: e->opt_exp = (int32_t)value; return FWA_OK;
+        case 98: e->opt_slide = (int32_t)value; return FWA_OK;   // A/B of the sliding fire's shape (temporary)
         default: return fail(e, FWA_E_ARG, "unknown option");
     }
 }
@@ -6328,6 +5901,7 @@ int fwa_get_option(const fwa_engine* e, int32_t option, int64_t* value) {
                                                                                     : (int64_t)e->sp->budget;
             return FWA_OK;
         case FWA_OPT_PROFILE: *value = e->opt_profile; return FWA_OK;
+        case FWA_OPT_SESSION_PATH: *value = e->sess_path; return FWA_OK;
         default: return FWA_E_ARG;
     }
 }

@@ -104,6 +104,7 @@ struct Out {
         for (int i = 0; i < nb; ++i) u8(hdr[(size_t)i]);
         for (int i = 0; i < arity; ++i) le64(isnull && isnull[i] ? 0 : f[i]);
     }
+    void raw_row(const std::vector<uint8_t>& r) { i32((int64_t)r.size()); b.insert(b.end(), r.begin(), r.end()); }
 };
 
 struct In {
@@ -131,6 +132,36 @@ struct In {
             else if (nl) ok = false;                                  // a NULL where the layout has none
         }
         for (int i = 0; i < arity; ++i) f[i] = get(8, true);
+    }
+    // a key row with STRING fields (the inverse of str_row_bytes): slots of the other fields, null bits, values;
+    // *raw = the row's bytes (BinaryRowData equality is byte equality)
+    void str_row(int arity, const int32_t* types, uint64_t* f, uint64_t* nulls, std::string* strs, std::string* raw) {
+        const int nb = ((arity + 63 + 8) / 64) * 8;
+        const int64_t size = i32();
+        if (!ok || size < nb + 8 * arity || at + size > n) { ok = false; return; }
+        const uint8_t* r = p + at;
+        raw->assign((const char*)r, (size_t)size);
+        at += size;
+        if (r[0] != 0) { ok = false; return; }                      // RowKind INSERT
+        *nulls = 0;
+        for (int c = 0; c < arity; ++c) {
+            const bool nl = (r[(c + 8) / 8] >> ((c + 8) % 8)) & 1;
+            uint64_t v = 0;
+            for (int k = 0; k < 8; ++k) v |= (uint64_t)r[nb + 8 * c + k] << (8 * k);
+            f[c] = v;
+            strs[c].clear();
+            if (nl) { *nulls |= 1ull << c; continue; }
+            if (types[c] != FWA_KEY_FIELD_STRING) continue;
+            if (v >> 63) {
+                const int len = (int)((v >> 56) & 0x7f);
+                if (len > 7) { ok = false; return; }
+                for (int k = 0; k < len; ++k) strs[c].push_back((char)(uint8_t)(v >> (8 * k)));
+            } else {
+                const uint64_t off = v >> 32, len = v & 0xffffffffull;
+                if (off < (uint64_t)(nb + 8 * arity) || off + len > (uint64_t)size) { ok = false; return; }
+                strs[c].assign((const char*)r + off, (size_t)len);
+            }
+        }
     }
 };
 
@@ -211,7 +242,40 @@ struct DictRows {
     int32_t types[FWA_KEYDICT_MAX_ARITY] = {};
     std::vector<uint64_t> slots;     // [row][arity]
     std::vector<uint64_t> nulls;     // [row]
+    std::vector<std::string> strs;   // [row][arity]: STRING values
+    bool has_str = false;
 };
+
+// The bytes of a key row with STRING fields as BinaryRowWriter writes it (AbstractBinaryWriter.java:80-105,279-334):
+// the header (null bits from bit 8), one 8-byte slot per field, a STRING of <= 7 bytes inline in its slot (first byte
+// 0x80 | length, the bytes in the low 7, writeBytesToFixLenPart), a longer one appended to the variable-length part
+// rounded up to 8 bytes with zero padding and slot = offset << 32 | length (writeBytesToVarLenPart, setOffsetAndSize).
+std::vector<uint8_t> str_row_bytes(int arity, const int32_t* types, const uint64_t* slots, uint64_t nulls,
+                                   const std::string* strs) {
+    const int nb = ((arity + 63 + 8) / 64) * 8;
+    std::vector<uint8_t> b((size_t)nb + 8 * (size_t)arity, 0);
+    for (int i = 0; i < arity; ++i) if ((nulls >> i) & 1) b[(size_t)(i + 8) / 8] |= (uint8_t)(1u << ((i + 8) % 8));
+    for (int c = 0; c < arity; ++c) {
+        uint64_t v = 0;
+        if ((nulls >> c) & 1) {
+            v = 0;
+        } else if (types[c] == FWA_KEY_FIELD_STRING) {
+            const std::string& t = strs[c];
+            if (t.size() <= 7) {
+                v = (uint64_t)(0x80u | (uint32_t)t.size()) << 56;
+                for (size_t k = 0; k < t.size(); ++k) v |= (uint64_t)(uint8_t)t[k] << (8 * k);
+            } else {
+                v = ((uint64_t)b.size() << 32) | (uint64_t)t.size();
+                b.insert(b.end(), t.begin(), t.end());
+                b.resize((b.size() + 7) & ~(size_t)7, 0);
+            }
+        } else {
+            v = slots[c];
+        }
+        for (int k = 0; k < 8; ++k) b[(size_t)nb + 8 * c + k] = (uint8_t)(v >> (8 * k));
+    }
+    return b;
+}
 
 // Event-time timer of a window end under the shift time zone (TimeWindowUtil.toEpochMillsForTimer :67-100; UTC:
 // the end - 1 itself)
@@ -317,6 +381,11 @@ void slide_windows_to_slices(const fwa_config& c, int64_t wm, const std::map<int
 
 }  // namespace
 
+// keydict.hip (internal, C++): STRING values of the dictionary's rows, and an encode of host rows with STRING values
+int fwa_keydict_host_strings(fwa_keydict* d, std::vector<std::string>* strs);
+int fwa_keydict_encode_host_str(fwa_keydict* d, const uint64_t* slots, const uint64_t* nulls,
+                                const std::vector<std::string>& strs, int64_t n, int64_t* ids);
+
 extern "C" {
 
 // engine-side accessors (engine.hip)
@@ -337,11 +406,18 @@ static int snapshot_heap_impl(fwa_engine* e, fwa_keydict* dict, fwa_blob* out, i
     DictRows dr;
     if (dict && (rc = fwa_keydict_host_rows(dict, &dr.arity, dr.types, &dr.slots, &dr.nulls)))
         return fwa_set_error(e, rc, "key dictionary rows");
+    for (int i = 0; i < dr.arity; ++i) dr.has_str |= dr.types[i] == FWA_KEY_FIELD_STRING;
+    if (dr.has_str && (rc = fwa_keydict_host_strings(dict, &dr.strs))) return fwa_set_error(e, rc, "key dictionary strings");
     // the key as a BinaryRowData: one BIGINT field, or the dictionary row of an id
     auto key_row = [&](Out& o, int64_t key) -> bool {
         if (!dict) { const uint64_t kf = (uint64_t)key; o.row(&kf, 1); return true; }
         const uint64_t seq = (uint64_t)key & ((1ull << 48) - 1);
         if (seq >= dr.nulls.size()) return false;
+        if (dr.has_str) {
+            o.raw_row(str_row_bytes(dr.arity, dr.types, &dr.slots[seq * (size_t)dr.arity], dr.nulls[seq],
+                                    &dr.strs[seq * (size_t)dr.arity]));
+            return true;
+        }
         bool nl[FWA_KEYDICT_MAX_ARITY];
         for (int i = 0; i < dr.arity; ++i) nl[i] = (dr.nulls[seq] >> i) & 1;
         o.row(&dr.slots[seq * (size_t)dr.arity], dr.arity, nl);
@@ -534,10 +610,12 @@ static int restore_heap_impl(fwa_engine* e, fwa_keydict* dict, const void* const
     if (rc) return rc;
     if (!supported(c, dict != nullptr)) return fwa_set_error(e, FWA_E_UNSUPPORTED, kUnsupported);
     int32_t darity = 1;
+    int32_t dtypes[FWA_KEYDICT_MAX_ARITY] = {};
+    bool dstr = false;
     if (dict) {
-        int32_t types[FWA_KEYDICT_MAX_ARITY];
         std::vector<uint64_t> tmp_s, tmp_n;
-        if ((rc = fwa_keydict_host_rows(dict, &darity, types, &tmp_s, &tmp_n))) return fwa_set_error(e, rc, "key dictionary");
+        if ((rc = fwa_keydict_host_rows(dict, &darity, dtypes, &tmp_s, &tmp_n))) return fwa_set_error(e, rc, "key dictionary");
+        for (int i = 0; i < darity; ++i) dstr |= dtypes[i] == FWA_KEY_FIELD_STRING;
     }
     const bool ds = c.semantics == FWA_SEM_DATASTREAM;
     const bool sess = c.window_kind == FWA_SESSION;
@@ -571,9 +649,25 @@ static int restore_heap_impl(fwa_engine* e, fwa_keydict* dict, const void* const
         std::vector<std::pair<int64_t, Words>> slices;
         // dictionary keys: each distinct key row read gets a placeholder key (its index), encoded to ids at the end
         std::map<std::vector<uint64_t>, int64_t> comp_idx;
+        std::map<std::string, int64_t> comp_raw;                     // rows with STRING fields: by their bytes
         std::vector<uint64_t> comp_slots, comp_nulls;
+        std::vector<std::string> comp_strs;
         auto read_key = [&](In& in) -> int64_t {
             if (!dict) { uint64_t kf; in.row(&kf, 1); return (int64_t)kf; }
+            if (dstr) {
+                uint64_t f[FWA_KEYDICT_MAX_ARITY], nb = 0;
+                std::string sv[FWA_KEYDICT_MAX_ARITY], raw;
+                in.str_row(darity, dtypes, f, &nb, sv, &raw);
+                if (!in.ok) return 0;
+                auto it = comp_raw.find(raw);
+                if (it != comp_raw.end()) return it->second;
+                const int64_t idx = (int64_t)comp_nulls.size();
+                comp_raw.emplace(raw, idx);
+                comp_slots.insert(comp_slots.end(), f, f + darity);
+                comp_nulls.push_back(nb);
+                for (int i = 0; i < darity; ++i) comp_strs.push_back(sv[i]);
+                return idx;
+            }
             uint64_t f[FWA_KEYDICT_MAX_ARITY];
             bool nl[FWA_KEYDICT_MAX_ARITY];
             in.row(f, darity, nl);
@@ -677,8 +771,10 @@ static int restore_heap_impl(fwa_engine* e, fwa_keydict* dict, const void* const
         if (!in.ok) return fwa_set_error(e, FWA_E_ARG, "heap body: truncated or malformed");
         if (dict && !comp_nulls.empty()) {                            // placeholder keys -> dictionary ids
             std::vector<int64_t> ids(comp_nulls.size());
-            if ((rc = fwa_keydict_encode_host(dict, comp_slots.data(), comp_nulls.data(), (int64_t)ids.size(), ids.data())))
-                return fwa_set_error(e, rc, "key dictionary encode");
+            rc = dstr ? fwa_keydict_encode_host_str(dict, comp_slots.data(), comp_nulls.data(), comp_strs, (int64_t)ids.size(),
+                                                    ids.data())
+                      : fwa_keydict_encode_host(dict, comp_slots.data(), comp_nulls.data(), (int64_t)ids.size(), ids.data());
+            if (rc) return fwa_set_error(e, rc, "key dictionary encode");
             for (int kg = 0; kg < maxp; ++kg) {
                 std::vector<int64_t>& v = per[(size_t)kg];
                 for (size_t r = 0; r < v.size(); r += (size_t)ncols) {

@@ -10,6 +10,11 @@
 //                     row's slots and publish id = key group << 48 | sequence in the table;
 //   kd_lookup_kernel  every row reads its id, checks its slots against the stored row (a different row with the
 //                     same 64-bit hash raises FWA_E_STATE) and writes its id and hash.
+// STRING fields (FWA_KEY_FIELD_STRING): a value of up to 7 bytes is its BinaryRowData slot (0x80 | length in the top
+// byte, the bytes below); a longer one is identified by a 63-bit hash of its bytes (top bit clear: never a short
+// slot) and stored in the dictionary's byte heap, its slot word then length << 40 | heap offset. hashCode() is
+// computed over the row as BinaryRowWriter lays it out (kd_row_hash): the long values' slots are offset << 32 |
+// length with the offsets of the row's variable-length part, which holds the bytes zero-padded to 8.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -17,6 +22,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+
+#include <hipcub/hipcub.hpp>
 
 #include "../../include/flink_amd.h"
 #include "java_math.h"
@@ -26,12 +33,16 @@ namespace {
 constexpr int kBlockKd = 256;
 constexpr uint64_t kKdEmpty = 0ull;
 constexpr uint64_t kSeqMask = (1ull << 48) - 1;
+constexpr int64_t kStrMax = (1 << 23) - 1;        // longest STRING value (its length field in the stored word)
+constexpr uint64_t kHeapMask = (1ull << 40) - 1;
 
 struct KdCols {
     const void* col[FWA_KEYDICT_MAX_ARITY];
     const uint8_t* nul[FWA_KEYDICT_MAX_ARITY];
     int32_t type[FWA_KEYDICT_MAX_ARITY];
-    int32_t arity;
+    int32_t arity, has_str;
+    const int32_t* soff[FWA_KEYDICT_MAX_ARITY];    // STRING fields: Arrow offsets / bytes
+    const uint8_t* sbytes[FWA_KEYDICT_MAX_ARITY];
 };
 
 struct KdDev {
@@ -46,7 +57,29 @@ struct KdDev {
     uint64_t mask;                 // table capacity - 1
     int64_t max_rows;
     int32_t max_par;
+    uint8_t* heap;                 // STRING values longer than 7 bytes
+    unsigned long long* heap_used;
+    uint64_t heap_cap;
 };
+
+// ---- STRING values (BinaryRowData layout, AbstractBinaryWriter.java:80-105,279-334) ----
+__device__ __forceinline__ uint64_t str_short_slot(const uint8_t* p, int64_t len) {   // writeBytesToFixLenPart
+    uint64_t v = (uint64_t)(0x80u | (uint32_t)len) << 56;
+    for (int64_t b = 0; b < len; ++b) v |= (uint64_t)p[b] << (8 * b);
+    return v;
+}
+__device__ __forceinline__ uint64_t str_word64(const uint8_t* p, int64_t len, int64_t at) {   // zero past len
+    uint64_t v = 0;
+    for (int b = 0; b < 8; ++b) if (at + b < len) v |= (uint64_t)p[at + b] << (8 * b);
+    return v;
+}
+__device__ __forceinline__ uint64_t str_identity(const uint8_t* p, int64_t len) {   // 63-bit content hash
+    uint64_t h = jm::mix64(0x243F6A8885A308D3ull ^ (uint64_t)len);
+    for (int64_t at = 0; at < len; at += 8) h = jm::mix64(h ^ str_word64(p, len, at) ^ ((uint64_t)at << 40));
+    return h & 0x7fffffffffffffffull;
+}
+__device__ __forceinline__ int64_t str_len(const KdCols& k, int c, int64_t i) { return (int64_t)k.soff[c][i + 1] - k.soff[c][i]; }
+__device__ __forceinline__ const uint8_t* str_ptr(const KdCols& k, int c, int64_t i) { return k.sbytes[c] + k.soff[c][i]; }
 
 __device__ __forceinline__ void row_of(const KdCols& k, int64_t i, uint64_t* slots, uint64_t* nullbits) {
     uint64_t nb = 0;
@@ -56,6 +89,10 @@ __device__ __forceinline__ void row_of(const KdCols& k, int64_t i, uint64_t* slo
         uint64_t v = 0;
         if (!isnull) {
             if (k.type[c] == FWA_KEY_FIELD_INT) v = (uint64_t)(uint32_t)((const int32_t*)k.col[c])[i];
+            else if (k.type[c] == FWA_KEY_FIELD_STRING) {   // short: the slot itself; long: its content identity
+                const int64_t len = str_len(k, c, i);
+                v = len <= 7 ? str_short_slot(str_ptr(k, c, i), len) : str_identity(str_ptr(k, c, i), len);
+            }
             else v = ((const uint64_t*)k.col[c])[i];   // BIGINT, DOUBLE raw bits
         }
         nb |= (uint64_t)isnull << c;
@@ -73,11 +110,46 @@ __device__ __forceinline__ uint64_t row_identity(const uint64_t* slots, int arit
     return h == kKdEmpty ? 1ull : h;
 }
 
+// BinaryRowData.hashCode() of row i (MurmurHashUtils.hashBytesByWords over the whole row, seed 42): the header, the
+// slots (a long STRING's slot = its offset in the row << 32 | length), the variable-length part, fmix(h ^ size)
+__device__ int32_t kd_row_hash(const KdCols& k, int64_t i, const uint64_t* slots, uint64_t nb) {
+    if (!k.has_str) return jm::binrow_hash(slots, k.arity, nb);
+    uint32_t h = 42u;
+    const uint64_t hdr = nb << 8;
+    h = jm::mh_h1(h, jm::mh_k1((uint32_t)hdr));
+    h = jm::mh_h1(h, jm::mh_k1((uint32_t)(hdr >> 32)));
+    uint64_t off = 8 + 8 * (uint64_t)k.arity;
+    for (int c = 0; c < FWA_KEYDICT_MAX_ARITY; ++c) {
+        if (c >= k.arity) break;
+        uint64_t v = (nb >> c) & 1 ? 0ull : slots[c];
+        if (k.type[c] == FWA_KEY_FIELD_STRING && !((nb >> c) & 1)) {
+            const int64_t len = str_len(k, c, i);
+            if (len > 7) { v = (off << 32) | (uint64_t)len; off += ((uint64_t)len + 7) & ~7ull; }
+        }
+        h = jm::mh_h1(h, jm::mh_k1((uint32_t)v));
+        h = jm::mh_h1(h, jm::mh_k1((uint32_t)(v >> 32)));
+    }
+    for (int c = 0; c < FWA_KEYDICT_MAX_ARITY; ++c) {
+        if (c >= k.arity) break;
+        if (k.type[c] != FWA_KEY_FIELD_STRING || ((nb >> c) & 1)) continue;
+        const int64_t len = str_len(k, c, i);
+        if (len <= 7) continue;
+        const uint8_t* p = str_ptr(k, c, i);
+        for (int64_t at = 0; at < ((len + 7) & ~7ll); at += 8) {
+            const uint64_t w = str_word64(p, len, at);
+            h = jm::mh_h1(h, jm::mh_k1((uint32_t)w));
+            h = jm::mh_h1(h, jm::mh_k1((uint32_t)(w >> 32)));
+        }
+    }
+    h ^= (uint32_t)off;
+    return jm::bit_mix((int32_t)h);
+}
+
 __global__ void __launch_bounds__(kBlockKd) kd_hash_kernel(KdCols k, int64_t n, int32_t* out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         uint64_t slots[FWA_KEYDICT_MAX_ARITY], nb;
         row_of(k, i, slots, &nb);
-        out[i] = jm::binrow_hash(slots, k.arity, nb);
+        out[i] = kd_row_hash(k, i, slots, nb);
     }
 }
 
@@ -117,12 +189,23 @@ __global__ void __launch_bounds__(kBlockKd) kd_assign_kernel(KdCols k, KdDev d, 
         if ((int64_t)seq >= d.max_rows) { atomicCAS(d.status, 0, FWA_E_OOM); continue; }
         uint64_t slots[FWA_KEYDICT_MAX_ARITY], nb;
         row_of(k, i, slots, &nb);
+        const int32_t kg = jm::key_group(kd_row_hash(k, i, slots, nb), d.max_par);
         for (int c = 0; c < FWA_KEYDICT_MAX_ARITY; ++c) {
             if (c >= k.arity) break;
-            d.fslot[(int64_t)c * d.max_rows + (int64_t)seq] = slots[c];
+            uint64_t v = slots[c];
+            if (k.type[c] == FWA_KEY_FIELD_STRING && !((nb >> c) & 1) && str_len(k, c, i) > 7) {   // to the heap
+                const int64_t len = str_len(k, c, i);
+                const unsigned long long at = atomicAdd(d.heap_used, (unsigned long long)len);
+                if (len > kStrMax || at + (uint64_t)len > d.heap_cap) { atomicCAS(d.status, 0, FWA_E_OOM); v = 0; }
+                else {
+                    const uint8_t* p = str_ptr(k, c, i);
+                    for (int64_t b = 0; b < len; ++b) d.heap[at + b] = p[b];
+                    v = ((uint64_t)len << 40) | (at & kHeapMask);
+                }
+            }
+            d.fslot[(int64_t)c * d.max_rows + (int64_t)seq] = v;
         }
         d.fnull[seq] = nb;
-        const int32_t kg = jm::key_group(jm::binrow_hash(slots, k.arity, nb), d.max_par);
         d.ht_id[s] = (long long)(((uint64_t)kg << 48) | (seq & kSeqMask));
     }
 }
@@ -138,12 +221,21 @@ __global__ void __launch_bounds__(kBlockKd) kd_lookup_kernel(KdCols k, KdDev d, 
         row_of(k, i, slots, &nb);
         bool same = (int64_t)seq < d.max_rows && d.fnull[seq] == nb;
         for (int c = 0; c < FWA_KEYDICT_MAX_ARITY; ++c) {
-            if (c >= k.arity) break;
-            same = same && d.fslot[(int64_t)c * d.max_rows + (int64_t)seq] == slots[c];
+            if (c >= k.arity || !same) break;
+            const uint64_t fs = d.fslot[(int64_t)c * d.max_rows + (int64_t)seq];
+            if (k.type[c] == FWA_KEY_FIELD_STRING && !((nb >> c) & 1) && str_len(k, c, i) > 7) {   // bytes vs heap
+                const int64_t len = str_len(k, c, i);
+                same = (fs >> 63) == 0 && (int64_t)(fs >> 40) == len;
+                const uint8_t* p = str_ptr(k, c, i);
+                const uint8_t* q = d.heap + (fs & kHeapMask);
+                for (int64_t b = 0; b < len && same; ++b) same = p[b] == q[b];
+            } else {
+                same = fs == slots[c];
+            }
         }
         if (!same) atomicCAS(d.status, 0, FWA_E_STATE);    // two rows with one 64-bit identity
         ids[i] = id;
-        if (hashes) hashes[i] = jm::binrow_hash(slots, k.arity, nb);
+        if (hashes) hashes[i] = kd_row_hash(k, i, slots, nb);
     }
 }
 
@@ -157,9 +249,35 @@ __global__ void __launch_bounds__(kBlockKd) kd_decode_kernel(KdDev d, KdCols k, 
             if (c >= k.arity) break;
             const uint64_t v = d.fslot[(int64_t)c * d.max_rows + (int64_t)seq];
             if (k.type[c] == FWA_KEY_FIELD_INT) ((int32_t*)cols[c])[i] = (int32_t)(uint32_t)v;
-            else ((uint64_t*)cols[c])[i] = v;
+            else if (k.type[c] != FWA_KEY_FIELD_STRING) ((uint64_t*)cols[c])[i] = v;   // strings: kd_str_* kernels
             if (has_nul && nul[c]) nul[c][i] = (uint8_t)((nb >> c) & 1);
         }
+    }
+}
+
+// STRING decode: the length of each id's value into offsets[i + 1] (then scanned), and its bytes
+__device__ __forceinline__ int64_t stored_len(uint64_t fs, bool isnull) {
+    if (isnull || fs == 0) return 0;
+    return (fs >> 63) ? (int64_t)((fs >> 56) & 0x7f) : (int64_t)(fs >> 40);
+}
+__global__ void __launch_bounds__(kBlockKd) kd_strlen_kernel(KdDev d, int c, int64_t n, const int64_t* ids, int32_t* offs) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t seq = (uint64_t)ids[i] & kSeqMask;
+        if ((int64_t)seq >= d.max_rows) { atomicCAS(d.status, 0, FWA_E_ARG); offs[i + 1] = 0; continue; }
+        offs[i + 1] = (int32_t)stored_len(d.fslot[(int64_t)c * d.max_rows + (int64_t)seq], (d.fnull[seq] >> c) & 1);
+        if (i == 0) offs[0] = 0;
+    }
+}
+__global__ void __launch_bounds__(kBlockKd) kd_strcopy_kernel(KdDev d, int c, int64_t n, const int64_t* ids, const int32_t* offs,
+                                                               uint8_t* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t seq = (uint64_t)ids[i] & kSeqMask;
+        if ((int64_t)seq >= d.max_rows) continue;
+        const uint64_t fs = d.fslot[(int64_t)c * d.max_rows + (int64_t)seq];
+        const int64_t len = stored_len(fs, (d.fnull[seq] >> c) & 1);
+        uint8_t* o = out + offs[i];
+        if (fs >> 63) for (int64_t b = 0; b < len; ++b) o[b] = (uint8_t)(fs >> (8 * b));
+        else for (int64_t b = 0; b < len; ++b) o[b] = d.heap[(fs & kHeapMask) + b];
     }
 }
 
@@ -176,31 +294,74 @@ struct fwa_keydict {
     hipStream_t stream = nullptr;
     std::string err;
     void** d_colptr = nullptr;       // decode: device copies of the column / null pointer arrays
+    bool has_str = false;
+    void* d_scan_tmp = nullptr;      // decode: hipcub scan scratch
+    size_t scan_tmp_bytes = 0;
 };
 
 namespace {
 int kd_fail(fwa_keydict* d, int code, const char* msg) { d->err = msg; return code; }
 #define KDCHK(d, call) do { hipError_t _e = (call); if (_e != hipSuccess) return kd_fail(d, FWA_E_DEVICE, hipGetErrorString(_e)); } while (0)
 
-bool cols_of(const fwa_keydict* d, const void* const* cols, const uint8_t* const* nulls, KdCols* k) {
+// STRING fields: cols[c] is a host fwa_key_strings (the device offsets / bytes)
+bool fill_cols(int arity, const int32_t* types, const void* const* cols, const uint8_t* const* nulls, KdCols* k) {
     memset(k, 0, sizeof(*k));
-    k->arity = d->arity;
-    for (int c = 0; c < d->arity; ++c) {
+    k->arity = arity;
+    for (int c = 0; c < arity; ++c) {
         if (!cols[c]) return false;
         k->col[c] = cols[c];
         k->nul[c] = nulls ? nulls[c] : nullptr;
-        k->type[c] = d->types[c];
+        k->type[c] = types[c];
+        if (types[c] == FWA_KEY_FIELD_STRING) {
+            const fwa_key_strings* ks = (const fwa_key_strings*)cols[c];
+            if (!ks->offsets || !ks->bytes) return false;
+            k->soff[c] = ks->offsets;
+            k->sbytes[c] = ks->bytes;
+            k->col[c] = ks->offsets;
+            k->has_str = 1;
+        }
     }
     return true;
+}
+bool cols_of(const fwa_keydict* d, const void* const* cols, const uint8_t* const* nulls, KdCols* k) {
+    return fill_cols(d->arity, d->types, cols, nulls, k);
 }
 
 int read_status(fwa_keydict* d) {
     int32_t st = 0;
     KDCHK(d, hipMemcpyAsync(&st, d->d.status, 4, hipMemcpyDeviceToHost, d->stream));
     KDCHK(d, hipStreamSynchronize(d->stream));
-    if (st == FWA_E_OOM) return kd_fail(d, st, "key dictionary full (capacity)");
+    if (st == FWA_E_OOM) return kd_fail(d, st, "key dictionary full (capacity, or a STRING value over 2^23 - 1 bytes)");
     if (st == FWA_E_STATE) return kd_fail(d, st, "two key rows with one 64-bit identity");
     if (st) return kd_fail(d, st, "bad key id");
+    return FWA_OK;
+}
+// Make room in the STRING heap for every long value of a batch before it is encoded (the assign pass cannot grow it):
+// at most the batch's string bytes.
+int ensure_heap(fwa_keydict* d, const KdCols& k, int64_t n) {
+    uint64_t need = 0;
+    for (int c = 0; c < d->arity; ++c) {
+        if (d->types[c] != FWA_KEY_FIELD_STRING) continue;
+        int32_t ends[2] = {0, 0};
+        KDCHK(d, hipMemcpyAsync(&ends[0], k.soff[c], 4, hipMemcpyDeviceToHost, d->stream));
+        KDCHK(d, hipMemcpyAsync(&ends[1], k.soff[c] + n, 4, hipMemcpyDeviceToHost, d->stream));
+        KDCHK(d, hipStreamSynchronize(d->stream));
+        if (ends[1] < ends[0]) return kd_fail(d, FWA_E_ARG, "STRING offsets decrease");
+        need += (uint64_t)(ends[1] - ends[0]);
+    }
+    unsigned long long used = 0;
+    KDCHK(d, hipMemcpyAsync(&used, d->d.heap_used, 8, hipMemcpyDeviceToHost, d->stream));
+    KDCHK(d, hipStreamSynchronize(d->stream));
+    if (used + need <= d->d.heap_cap) return FWA_OK;
+    uint64_t cap = std::max<uint64_t>(d->d.heap_cap * 2, used + need + (1 << 20));
+    if (cap > kHeapMask) return kd_fail(d, FWA_E_OOM, "key dictionary string heap past 2^40 bytes");
+    uint8_t* nh = nullptr;
+    KDCHK(d, hipMalloc(&nh, cap));
+    if (used) KDCHK(d, hipMemcpyAsync(nh, d->d.heap, used, hipMemcpyDeviceToDevice, d->stream));
+    KDCHK(d, hipStreamSynchronize(d->stream));
+    if (d->d.heap) KDCHK(d, hipFree(d->d.heap));
+    d->d.heap = nh;
+    d->d.heap_cap = cap;
     return FWA_OK;
 }
 }  // namespace
@@ -213,11 +374,11 @@ int fwa_keydict_create(int32_t arity, const int32_t* field_types, int32_t max_pa
         max_parallelism > 32768 || capacity <= 0 || capacity > ((int64_t)1 << 29))   // slot index: 31 bits < sentinel
         return FWA_E_ARG;
     for (int c = 0; c < arity; ++c)
-        if (field_types[c] < FWA_KEY_FIELD_BIGINT || field_types[c] > FWA_KEY_FIELD_DOUBLE) return FWA_E_ARG;
+        if (field_types[c] < FWA_KEY_FIELD_BIGINT || field_types[c] > FWA_KEY_FIELD_STRING) return FWA_E_ARG;
     fwa_keydict* d = new fwa_keydict();
     d->arity = arity;
     d->device = device;
-    for (int c = 0; c < arity; ++c) d->types[c] = field_types[c];
+    for (int c = 0; c < arity; ++c) { d->types[c] = field_types[c]; d->has_str |= field_types[c] == FWA_KEY_FIELD_STRING; }
     int64_t cap = 1024;
     while (cap < 2 * capacity) cap <<= 1;
     d->cap = cap;
@@ -231,12 +392,13 @@ int fwa_keydict_create(int32_t arity, const int32_t* field_types, int32_t max_pa
             hipMalloc(&d->d.ht_rep, 4 * cap) != hipSuccess ||
             hipMalloc(&d->d.fslot, 8 * (size_t)arity * (size_t)capacity) != hipSuccess ||
             hipMalloc(&d->d.fnull, 8 * (size_t)capacity) != hipSuccess || hipMalloc(&d->d.nrows, 8) != hipSuccess ||
-            hipMalloc(&d->d.status, 4) != hipSuccess || hipMalloc(&d->d_colptr, 2 * sizeof(void*) * FWA_KEYDICT_MAX_ARITY) != hipSuccess) {
+            hipMalloc(&d->d.status, 4) != hipSuccess || hipMalloc(&d->d_colptr, 2 * sizeof(void*) * FWA_KEYDICT_MAX_ARITY) != hipSuccess ||
+            hipMalloc(&d->d.heap_used, 8) != hipSuccess) {
             rc = FWA_E_OOM; break;
         }
         // ht_id -1: a slot whose row was claimed but never given an id (the dictionary filled up) reads as "no id"
         if (hipMemsetAsync(d->d.ht_key, 0, 8 * cap, d->stream) != hipSuccess || hipMemsetAsync(d->d.ht_id, 0xff, 8 * cap, d->stream) != hipSuccess ||
-            hipMemsetAsync(d->d.nrows, 0, 8, d->stream) != hipSuccess ||
+            hipMemsetAsync(d->d.nrows, 0, 8, d->stream) != hipSuccess || hipMemsetAsync(d->d.heap_used, 0, 8, d->stream) != hipSuccess ||
             hipMemsetAsync(d->d.status, 0, 4, d->stream) != hipSuccess || hipStreamSynchronize(d->stream) != hipSuccess) {
             rc = FWA_E_DEVICE; break;
         }
@@ -251,7 +413,8 @@ void fwa_keydict_destroy(fwa_keydict* d) {
     (void)hipSetDevice(d->device);
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     for (void* p : {(void*)d->d.ht_key, (void*)d->d.ht_id, (void*)d->d.ht_rep, (void*)d->d.fslot, (void*)d->d.fnull,
-                    (void*)d->d.nrows, (void*)d->d.pos, (void*)d->d.status, (void*)d->d_colptr})
+                    (void*)d->d.nrows, (void*)d->d.pos, (void*)d->d.status, (void*)d->d_colptr, (void*)d->d.heap,
+                    (void*)d->d.heap_used, d->d_scan_tmp})
         if (p) (void)hipFree(p);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
@@ -276,6 +439,7 @@ int fwa_keydict_encode(fwa_keydict* d, const void* const* cols, const uint8_t* c
     KdCols k;
     if (!cols_of(d, cols, nulls, &k)) return kd_fail(d, FWA_E_ARG, "fwa_keydict_encode: null key column");
     KDCHK(d, hipSetDevice(d->device));
+    if (d->has_str) { if (int rc = ensure_heap(d, k, n)) return rc; }
     if (n > d->pos_cap) {
         KDCHK(d, hipStreamSynchronize(d->stream));
         if (d->d.pos) KDCHK(d, hipFree(d->d.pos));
@@ -299,7 +463,7 @@ int fwa_keydict_decode(fwa_keydict* d, const int64_t* ids, int64_t n, void* cons
     void* h[2 * FWA_KEYDICT_MAX_ARITY] = {};
     for (int c = 0; c < d->arity; ++c) {
         if (!cols[c]) return kd_fail(d, FWA_E_ARG, "fwa_keydict_decode: null key column");
-        h[c] = cols[c];
+        h[c] = d->types[c] == FWA_KEY_FIELD_STRING ? nullptr : cols[c];   // strings: through fwa_key_strings_out
         h[FWA_KEYDICT_MAX_ARITY + c] = nulls ? (void*)nulls[c] : nullptr;
     }
     KDCHK(d, hipMemcpyAsync(d->d_colptr, h, sizeof(h), hipMemcpyHostToDevice, d->stream));
@@ -312,7 +476,35 @@ int fwa_keydict_decode(fwa_keydict* d, const int64_t* ids, int64_t n, void* cons
                                                              (uint8_t* const*)(d->d_colptr + FWA_KEYDICT_MAX_ARITY),
                                                              nulls ? 1 : 0);
     KDCHK(d, hipGetLastError());
-    return read_status(d);
+    bool short_out = false;
+    for (int c = 0; c < d->arity; ++c) {        // STRING fields: lengths -> offsets (inclusive scan from [1]) -> bytes
+        if (d->types[c] != FWA_KEY_FIELD_STRING) continue;
+        fwa_key_strings_out* so = (fwa_key_strings_out*)cols[c];
+        if (!so->offsets) return kd_fail(d, FWA_E_ARG, "fwa_keydict_decode: null STRING offsets");
+        kd_strlen_kernel<<<grid_kd(n), kBlockKd, 0, d->stream>>>(d->d, c, n, ids, so->offsets);
+        size_t tb = 0;
+        KDCHK(d, hipcub::DeviceScan::InclusiveSum(nullptr, tb, so->offsets + 1, so->offsets + 1, (int)n, d->stream));
+        if (tb > d->scan_tmp_bytes) {
+            KDCHK(d, hipStreamSynchronize(d->stream));
+            if (d->d_scan_tmp) KDCHK(d, hipFree(d->d_scan_tmp));
+            d->d_scan_tmp = nullptr;
+            KDCHK(d, hipMalloc(&d->d_scan_tmp, tb));
+            d->scan_tmp_bytes = tb;
+        }
+        tb = d->scan_tmp_bytes;
+        KDCHK(d, hipcub::DeviceScan::InclusiveSum(d->d_scan_tmp, tb, so->offsets + 1, so->offsets + 1, (int)n, d->stream));
+        int32_t total = 0;
+        KDCHK(d, hipMemcpyAsync(&total, so->offsets + n, 4, hipMemcpyDeviceToHost, d->stream));
+        KDCHK(d, hipStreamSynchronize(d->stream));
+        so->needed = total;
+        if (!so->bytes) continue;
+        if (so->capacity < total) { short_out = true; continue; }
+        kd_strcopy_kernel<<<grid_kd(n), kBlockKd, 0, d->stream>>>(d->d, c, n, ids, so->offsets, so->bytes);
+        KDCHK(d, hipGetLastError());
+    }
+    if (int rc = read_status(d)) return rc;
+    if (short_out) return kd_fail(d, FWA_E_ARG, "fwa_keydict_decode: STRING bytes past the output capacity");
+    return FWA_OK;
 }
 
 // internal (heap_snapshot.cpp): every row of the dictionary on the host -- slots [row][arity] and null bits
@@ -375,14 +567,9 @@ int fwa_binrow_hash(int32_t arity, const int32_t* field_types, const void* const
     if (arity < 1 || arity > FWA_KEYDICT_MAX_ARITY || !field_types || n < 0 || (n > 0 && (!cols || !out))) return FWA_E_ARG;
     if (n == 0) return FWA_OK;
     KdCols k;
-    memset(&k, 0, sizeof(k));
-    k.arity = arity;
-    for (int c = 0; c < arity; ++c) {
-        if (!cols[c] || field_types[c] < FWA_KEY_FIELD_BIGINT || field_types[c] > FWA_KEY_FIELD_DOUBLE) return FWA_E_ARG;
-        k.col[c] = cols[c];
-        k.nul[c] = nulls ? nulls[c] : nullptr;
-        k.type[c] = field_types[c];
-    }
+    for (int c = 0; c < arity; ++c)
+        if (!cols[c] || field_types[c] < FWA_KEY_FIELD_BIGINT || field_types[c] > FWA_KEY_FIELD_STRING) return FWA_E_ARG;
+    if (!fill_cols(arity, field_types, cols, nulls, &k)) return FWA_E_ARG;
     if (hipSetDevice(device) != hipSuccess) return FWA_E_DEVICE;
     kd_hash_kernel<<<grid_kd(n), kBlockKd>>>(k, n, out);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return FWA_E_DEVICE;
@@ -390,3 +577,103 @@ int fwa_binrow_hash(int32_t arity, const int32_t* field_types, const void* const
 }
 
 }  // extern "C"
+
+// internal (heap_snapshot.cpp): the STRING values of every dictionary row on the host, strs[row * arity + c] (empty
+// for the other fields and for NULLs)
+int fwa_keydict_host_strings(fwa_keydict* d, std::vector<std::string>* strs) {
+    if (!d) return FWA_E_ARG;
+    const int64_t n = fwa_keydict_size(d);
+    if (n < 0) return FWA_E_DEVICE;
+    strs->assign((size_t)n * d->arity, std::string());
+    if (!d->has_str || n == 0) return FWA_OK;
+    KDCHK(d, hipSetDevice(d->device));
+    std::vector<uint64_t> fs((size_t)n), nb((size_t)n);
+    unsigned long long used = 0;
+    KDCHK(d, hipMemcpyAsync(&used, d->d.heap_used, 8, hipMemcpyDeviceToHost, d->stream));
+    KDCHK(d, hipMemcpyAsync(nb.data(), d->d.fnull, 8 * (size_t)n, hipMemcpyDeviceToHost, d->stream));
+    KDCHK(d, hipStreamSynchronize(d->stream));
+    std::vector<uint8_t> heap((size_t)used);
+    if (used) KDCHK(d, hipMemcpyAsync(heap.data(), d->d.heap, used, hipMemcpyDeviceToHost, d->stream));
+    for (int c = 0; c < d->arity; ++c) {
+        if (d->types[c] != FWA_KEY_FIELD_STRING) continue;
+        KDCHK(d, hipMemcpyAsync(fs.data(), d->d.fslot + (size_t)c * d->d.max_rows, 8 * (size_t)n, hipMemcpyDeviceToHost, d->stream));
+        KDCHK(d, hipStreamSynchronize(d->stream));
+        for (int64_t r = 0; r < n; ++r) {
+            if ((nb[(size_t)r] >> c) & 1) continue;
+            const uint64_t w = fs[(size_t)r];
+            std::string& s = (*strs)[(size_t)r * d->arity + c];
+            if (w >> 63) {
+                const int len = (int)((w >> 56) & 0x7f);
+                for (int b = 0; b < len; ++b) s.push_back((char)(uint8_t)(w >> (8 * b)));
+            } else if (w) {
+                const uint64_t len = w >> 40, at = w & kHeapMask;
+                if (at + len > used) return kd_fail(d, FWA_E_STATE, "key dictionary string heap inconsistent");
+                s.assign((const char*)heap.data() + at, (size_t)len);
+            }
+        }
+    }
+    return FWA_OK;
+}
+
+// internal (heap_snapshot.cpp): encode n rows given on the host as slots [row][arity] (ignored for STRING fields),
+// null bits and STRING values strs[row * arity + c]; ids to the host
+int fwa_keydict_encode_host_str(fwa_keydict* d, const uint64_t* slots, const uint64_t* nulls,
+                                const std::vector<std::string>& strs, int64_t n, int64_t* ids) {
+    if (!d || n < 0) return FWA_E_ARG;
+    if (!d->has_str) return fwa_keydict_encode_host(d, slots, nulls, n, ids);
+    if (n == 0) return FWA_OK;
+    KDCHK(d, hipSetDevice(d->device));
+    const int a = d->arity;
+    std::vector<uint64_t> cols((size_t)n * a);
+    std::vector<uint8_t> nul((size_t)n * a);
+    std::vector<std::vector<int32_t>> offs((size_t)a);
+    std::vector<std::string> bytes((size_t)a);
+    for (int c = 0; c < a; ++c) {
+        if (d->types[c] == FWA_KEY_FIELD_STRING) offs[(size_t)c].assign(1, 0);
+        for (int64_t r = 0; r < n; ++r) {
+            nul[(size_t)c * n + r] = (uint8_t)((nulls[r] >> c) & 1);
+            if (d->types[c] == FWA_KEY_FIELD_STRING) {
+                bytes[(size_t)c] += strs[(size_t)r * a + c];
+                if (bytes[(size_t)c].size() > (size_t)INT32_MAX) return kd_fail(d, FWA_E_ARG, "STRING column past 2^31 bytes");
+                offs[(size_t)c].push_back((int32_t)bytes[(size_t)c].size());
+            } else if (d->types[c] == FWA_KEY_FIELD_INT) {
+                reinterpret_cast<int32_t*>(cols.data() + (size_t)c * n)[r] = (int32_t)(uint32_t)slots[(size_t)r * a + c];
+            } else {
+                cols[(size_t)c * n + r] = slots[(size_t)r * a + c];
+            }
+        }
+    }
+    size_t tot = 8 * (size_t)n * a + (size_t)n * a + 8 * (size_t)n + 64;
+    for (int c = 0; c < a; ++c) tot += 4 * offs[(size_t)c].size() + bytes[(size_t)c].size() + 16;
+    char* buf = nullptr;
+    KDCHK(d, hipMalloc(&buf, tot));
+    int rc = FWA_OK;
+    do {
+        char* p = buf;
+        auto put = [&](const void* src, size_t nb) -> char* {
+            char* dst = p;
+            if (nb && hipMemcpyAsync(dst, src, nb, hipMemcpyHostToDevice, d->stream) != hipSuccess) rc = FWA_E_DEVICE;
+            p += (nb + 15) & ~(size_t)15;
+            return dst;
+        };
+        const void* cp[FWA_KEYDICT_MAX_ARITY];
+        const uint8_t* np_[FWA_KEYDICT_MAX_ARITY];
+        fwa_key_strings ks[FWA_KEYDICT_MAX_ARITY];
+        for (int c = 0; c < a; ++c) {
+            np_[c] = (const uint8_t*)put(nul.data() + (size_t)c * n, (size_t)n);
+            if (d->types[c] == FWA_KEY_FIELD_STRING) {
+                ks[c].offsets = (const int32_t*)put(offs[(size_t)c].data(), 4 * offs[(size_t)c].size());
+                ks[c].bytes = (const uint8_t*)put(bytes[(size_t)c].data(), bytes[(size_t)c].size());
+                cp[c] = &ks[c];
+            } else {
+                cp[c] = put(cols.data() + (size_t)c * n, 8 * (size_t)n);
+            }
+        }
+        int64_t* did = (int64_t*)put(nullptr, 8 * (size_t)n);
+        if (rc) break;
+        if ((rc = fwa_keydict_encode(d, cp, np_, n, did, nullptr))) break;
+        if (hipMemcpy(ids, did, 8 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) rc = FWA_E_DEVICE;
+    } while (0);
+    (void)hipFree(buf);
+    return rc;
+}

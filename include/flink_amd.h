@@ -411,7 +411,9 @@ enum fwa_option {
     FWA_OPT_SP_TABLE = 7,        /* record lists: LDS aggregation table slots (power of two >= 64, before any push) */
     FWA_OPT_SP_FMAX = 8,         /* record lists: max fine buckets per (window, partition) at fire */
     FWA_OPT_SP_BUDGET = 9,       /* record lists: live list bytes above which windows are compacted */
-    FWA_OPT_PROFILE = 10         /* 1: per-phase clock profile of Phase P / A, printed to stderr (diagnostic) */
+    FWA_OPT_PROFILE = 10,        /* 1: per-phase clock profile of Phase P / A, printed to stderr (diagnostic) */
+    FWA_OPT_SESSION_PATH = 11    /* read only: the path of the last session push -- 0 general, 1 sort-based cells,
+                                    2 cell pre-aggregation (fwa_get_option) */
 };
 int fwa_set_option(fwa_engine* e, int32_t option, int64_t value);
 /* The option's effective value: for the tri-state options 1 if the handle currently takes that path (forced, or
@@ -442,7 +444,7 @@ int fwa_route_rows(const int64_t* keys, const int32_t* key_hash, int64_t n, int3
 int fwa_unpack_rows(const int64_t* rows, int64_t n, int32_t ncols, int64_t* const* cols, int32_t device, void* stream);
 
 /* ---- key dictionary: multi-column Table keys ----
- * A Table job keyed by several columns has BinaryRowData keys of `arity` fixed-length fields whose hashCode()
+ * A Table job keyed by several columns has BinaryRowData keys of `arity` fields whose hashCode()
  * (BinaryRowData.java:452-454 -> MurmurHashUtils.hashBytesByWords :92-170) places them in key groups
  * (KeyGroupRangeAssignment.assignToKeyGroup :63-77). The dictionary computes that hash on the GPU and maps each
  * distinct key row to a 64-bit id whose bits 48-63 are the row's key group and bits 0-47 a dense sequence number;
@@ -452,8 +454,20 @@ int fwa_unpack_rows(const int64_t* rows, int64_t n, int32_t ncols, int64_t* cons
  * -0.0 and 0.0 are different DOUBLE keys, as in the reference. Identity is a 64-bit hash of the row's bytes checked
  * against the stored row: two rows with the same 64-bit hash (never observed) fail the encode with FWA_E_STATE
  * instead of merging. One dictionary serves one engine handle (ids are local to it). */
-enum fwa_key_field_type { FWA_KEY_FIELD_BIGINT = 0, FWA_KEY_FIELD_INT = 1, FWA_KEY_FIELD_DOUBLE = 2 };
+enum fwa_key_field_type { FWA_KEY_FIELD_BIGINT = 0, FWA_KEY_FIELD_INT = 1, FWA_KEY_FIELD_DOUBLE = 2,
+                          FWA_KEY_FIELD_STRING = 3 };
 #define FWA_KEYDICT_MAX_ARITY 8
+/* A STRING / VARCHAR key field (FWA_KEY_FIELD_STRING): the UTF-8 bytes of row i are bytes[offsets[i] .. offsets[i+1])
+ * (Arrow layout, device pointers; at most 2^23 - 1 bytes per value). The key row is laid out as BinaryRowWriter
+ * writes it (AbstractBinaryWriter.writeString / writeBytesToFixLenPart / writeBytesToVarLenPart :80-105,279-334): up to
+ * 7 bytes inline in the field's slot (first byte 0x80 | length, the bytes in the low 7), longer ones appended to the
+ * row's variable-length part rounded up to 8 bytes (zero padding) with slot = offset << 32 | length; hashCode()
+ * covers the whole row (BinarySegmentUtils.hashByWords :374-380). For such a field, cols[c] of fwa_keydict_encode /
+ * fwa_binrow_hash points to a (host) fwa_key_strings; fwa_keydict_decode writes through a (host) fwa_key_strings_out:
+ * offsets[0..n] always, and the bytes when `bytes` is non-NULL and `capacity` holds them (else FWA_E_ARG); `needed`
+ * receives the byte count either way (call once with bytes = NULL to size the buffer). */
+typedef struct fwa_key_strings { const int32_t* offsets; const uint8_t* bytes; } fwa_key_strings;
+typedef struct fwa_key_strings_out { int32_t* offsets; uint8_t* bytes; int64_t capacity; int64_t needed; } fwa_key_strings_out;
 typedef struct fwa_keydict fwa_keydict;
 /* capacity: the most distinct key rows the dictionary will hold (FWA_E_OOM past it) */
 int fwa_keydict_create(int32_t arity, const int32_t* field_types, int32_t max_parallelism, int64_t capacity,

@@ -104,6 +104,17 @@ int32_t or_binrow_hash(const int64_t* slots, int32_t arity, uint64_t nullbits) {
     return mh_fmix(h1 ^ (8 + 8 * arity));
 }
 
+/* MurmurHashUtils.hashBytesByWords (MurmurHashUtils.java:92-170) over any byte row (numBytes a multiple of 4):
+   BinaryRowData.hashCode of a row with variable-length parts (BinarySegmentUtils.hashByWords :374-380) */
+int32_t or_hash_bytes_by_words(const uint8_t* p, int32_t n) {
+    int32_t h1 = 42;
+    for (int32_t i = 0; i + 4 <= n; i += 4) {
+        const int32_t w = (int32_t)((uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) | ((uint32_t)p[i + 3] << 24));
+        h1 = mh_mix_h1(h1, mh_mix_k1(w));
+    }
+    return mh_fmix(h1 ^ n);
+}
+
 int32_t or_key_group(int64_t key, int32_t key_kind, int32_t key_hash, int32_t max_par) {
     int32_t h;
     if (key_kind == 3) return (int32_t)((uint64_t)key >> 48);   /* key-dictionary ids carry their key group */

@@ -39,6 +39,8 @@ def lib():
         L.or_binrow_bigint_hash.restype = C.c_int32
         L.or_binrow_hash.argtypes = [C.c_void_p, C.c_int32, C.c_uint64]
         L.or_binrow_hash.restype = C.c_int32
+        L.or_hash_bytes_by_words.argtypes = [C.c_char_p, C.c_int32]
+        L.or_hash_bytes_by_words.restype = C.c_int32
         L.or_key_group.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32]
         L.or_key_group.restype = C.c_int32
         L.or_operator_index.argtypes = [C.c_int32, C.c_int32, C.c_int32]
@@ -73,6 +75,41 @@ def lib():
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def binrow_bytes(types, row):
+    """The bytes of a BinaryRowData key row as BinaryRowWriter writes it (a restatement for the tests: header with
+    RowKind INSERT and null bits from bit 8, 8-byte little-endian slots -- BIGINT / DOUBLE bits, INT in the low 4 bytes,
+    NULL zeroed; a STRING of <= 7 UTF-8 bytes inline (first byte 0x80 | length), a longer one in the variable-length part,
+    8-byte aligned with zero padding, slot = offset << 32 | length (AbstractBinaryWriter.java:80-105,279-334))."""
+    import struct
+    arity = len(types)
+    nb = ((arity + 63 + 8) // 64) * 8
+    head = bytearray(nb)
+    slots, var = [], bytearray()
+    for c, (t, v) in enumerate(zip(types, row)):
+        if v is None:
+            head[(c + 8) // 8] |= 1 << ((c + 8) % 8)
+            slots.append(0)
+        elif t == "STRING":
+            b = v.encode("utf-8") if isinstance(v, str) else bytes(v)
+            if len(b) <= 7:
+                slots.append(((0x80 | len(b)) << 56) | int.from_bytes(b, "little"))
+            else:
+                slots.append(((nb + 8 * arity + len(var)) << 32) | len(b))
+                var += b + bytes((-len(b)) % 8)
+        elif t == "INT":
+            slots.append(v & 0xFFFFFFFF)
+        elif t == "DOUBLE":
+            slots.append(struct.unpack("<Q", struct.pack("<d", v))[0])
+        else:
+            slots.append(v & 0xFFFFFFFFFFFFFFFF)
+    return bytes(head) + b"".join(x.to_bytes(8, "little") for x in slots) + bytes(var)
+
+
+def binrow_hash_bytes(row_bytes):
+    """BinaryRowData.hashCode() of a row's bytes (MurmurHashUtils.hashBytesByWords, the oracle's C restatement)."""
+    return lib().or_hash_bytes_by_words(row_bytes, len(row_bytes))
 
 
 class OracleError(RuntimeError):

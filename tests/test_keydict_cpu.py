@@ -121,3 +121,47 @@ def test_torch_key_columns_are_type_checked():
     from flink_amd import keydict
     with pytest.raises(TypeError):
         keydict._dev(torch.zeros(4, dtype=torch.int64), np.int64)
+
+
+# ---- STRING fields (FWA_KEY_FIELD_STRING) ----------------------------------------------------------------------------
+
+def test_fixed_part_sizes_match_the_reference():
+    """BinaryRowDataTest.testBasic :92-95: fixed-length part sizes of arity 0 / 1 / 65 / 128 rows."""
+    for arity, size in [(0, 8), (1, 16), (65, 536), (128, 1048)]:
+        assert len(O.binrow_bytes(["BIGINT"] * arity, [0] * arity)) == size
+
+
+def test_string_field_layout():
+    """AbstractBinaryWriter.writeString: <= 7 bytes inline (0x80 | len in the top byte, bytes from the lowest), longer in
+    the variable-length part, 8-byte aligned, slot = offset << 32 | length; the testWriter row (:131-148) shapes."""
+    b = O.binrow_bytes(["STRING"], ["1234567"])
+    assert len(b) == 16 and b[8:15] == b"1234567" and b[15] == 0x87
+    b = O.binrow_bytes(["STRING"], ["12345678"])
+    assert len(b) == 24 and struct.unpack("<Q", b[8:16])[0] == (16 << 32) | 8 and b[16:] == b"12345678"
+    s = "啦啦啦啦啦我是快乐的粉刷匠".encode("utf-8")                       # 39 bytes -> 40 in the var part
+    b = O.binrow_bytes(["STRING", "INT", "STRING"], ["1", 88, s])
+    assert len(b) == 8 + 24 + 40 and struct.unpack("<Q", b[24:32])[0] == (32 << 32) | 39 and b[32:71] == s
+    assert O.binrow_bytes(["STRING"], [""])[15] == 0x80 and O.binrow_bytes(["STRING"], [None])[8:] == bytes(8)
+    assert b[1] == 0 and O.binrow_bytes(["INT", "STRING"], [1, None])[1] == 0b10
+
+
+def test_bytes_hash_equals_the_fixed_row_hash():
+    """The byte-level hash of a fixed-length row equals the oracle's slot-level BinaryRowData hash (and, for one
+    BIGINT field, the single-key hash the engine uses), so the STRING rows share one hash definition with them."""
+    rng = np.random.default_rng(9)
+    for types in (["BIGINT"], ["INT", "DOUBLE", "BIGINT"]):
+        for r in random_rows(rng, types, 100, 0.15):
+            rb = O.binrow_bytes(types, r)
+            assert O.binrow_hash_bytes(rb) == oracle_hash(types, r) == murmur_words(rb)
+    for v in [0, -1, 2**63 - 1]:
+        assert O.binrow_hash_bytes(O.binrow_bytes(["BIGINT"], [v])) == O.lib().or_binrow_bigint_hash(v)
+    for s in ["", "a", "abcdefg", "abcdefgh", "啦啦啦啦啦我是快乐的粉刷匠" * 3]:
+        rb = O.binrow_bytes(["STRING", "BIGINT"], [s, 7])
+        assert O.binrow_hash_bytes(rb) == murmur_words(rb)
+
+
+def test_string_hash_distribution_on_the_oracle():
+    """BinaryRowDataTest :378-386 (scaled to 20,000 rows for the CPU suite; the GPU test runs the full 999,999)."""
+    n = 20_000
+    hs = {O.binrow_hash_bytes(O.binrow_bytes(["STRING"], ["啦啦啦啦啦我是快乐的粉刷匠%d" % i])) for i in range(n)}
+    assert len(hs) > int(n * 0.997)

@@ -205,3 +205,80 @@ def test_cell_path_redo_on_order_sensitive_records(eng_mod):
     dropped, st = _run(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 24, 400))
     assert dropped > 0
     assert 0 < st.replay_records < len(keys)
+
+
+# ---- cell pre-aggregation (sessions4.inc: <= 16 cells per push, <= 8 in-flight sessions per key) ------------------
+def _run_paths(eng_mod, cfg, batches):
+    """_run, recording the path each push took (FWA_OPT_SESSION_PATH: 0 general, 1 sort-based cells, 2 pre-agg)."""
+    from oracle.oracle import Oracle
+    names = A.agg_names(cfg)
+    g, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
+    paths, dg, do = [], 0, 0
+    for k, t, cols, wm in batches:
+        dg += g.push(k, t, cols)
+        do += o.push(k, t, cols)
+        if len(k):
+            paths.append(g.get_option("session_path"))
+        assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), names, rtol=1e-9, ctx="wm=%d" % wm)
+    assert dg == do
+    st = g.stats()
+    g.close()
+    o.close()
+    return paths, st
+
+
+@pytest.mark.parametrize("sem", ["DATASTREAM", "TABLE"])
+@pytest.mark.parametrize("nacc", [1, 2, 3, 4, 5])
+def test_cell_preagg_vs_oracle(eng_mod, nacc, sem):
+    """Pushes of 50 s of event time with a 5 s gap (about 11 cells): every push on the pre-aggregation path, sessions
+    kept in flight across pushes, closed and fired between them."""
+    keys, ts, vi, vd = _stream(200 + nacc, 200_000, 3000, 600_000, 300, 0.0)
+    cfg = A.make_config(window_kind="SESSION", semantics=sem, gap_ms=5000, aggs=CELL_AGGS[nacc], key_capacity=8192)
+    paths, st = _run_paths(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 12, 300))
+    assert paths == [2] * 12
+    assert st.replay_records == 0
+
+
+def test_cell_preagg_touching_and_bucket_edges(eng_mod):
+    """Windows exactly `gap` apart touch and merge (TimeWindow.intersects), inside one push and against an in-flight
+    session; keys on both sides of a 128-kid bucket edge, the sentinel key (side slot) and a NULL-free wide value."""
+    gap = 1000
+    k = lambda *x: np.array(x, np.int64)
+    keys1 = np.concatenate([k(1, 1, 1, 2, 2), np.arange(100, 400, dtype=np.int64), k(-2**63, -2**63)])
+    ts1 = np.concatenate([k(0, 1000, 2000, 0, 2001), np.full(300, 1500, np.int64), k(10, 1010)])
+    keys2 = k(1, 2, 2, 7, -2**63)
+    ts2 = k(3000, 3001, 5003, 4000, 2010)                        # 1@3000 touches [0, 3000); 2@3001 touches [2001, 3001)
+    batches = []
+    for kk, tt, wm in [(keys1, ts1, 1500), (keys2, ts2, 2500), (keys2[:0], ts2[:0], A.LONG_MAX)]:
+        vi = (tt * 7 + kk % 13).astype(np.int64)
+        batches.append((kk, tt, [vi, vi, (tt * 0.25).astype(np.float64)], wm))
+    cfg = A.make_config(window_kind="SESSION", gap_ms=gap, aggs=AGGS, key_capacity=512)
+    paths, _ = _run_paths(eng_mod, cfg, batches)
+    assert paths == [2, 2]
+
+
+def test_cell_preagg_many_sessions_per_key_falls_back(eng_mod):
+    """A key holding more than 8 in-flight sessions (allowed lateness keeps them) hands a narrow push to the sort-based
+    cell path; the results are unchanged."""
+    n = 200
+    ts = np.arange(n, dtype=np.int64) * 300                        # gap 100: every record its own session
+    keys = np.full(n, 5, np.int64)
+    keys[::2] = 9
+    vi = np.arange(n, dtype=np.int64)
+    k2, t2 = np.array([5, 5, 9], np.int64), np.array([60_000, 60_050, 60_020], np.int64)
+    cfg = A.make_config(window_kind="SESSION", gap_ms=100, allowed_lateness_ms=1_000_000, aggs=AGGS, key_capacity=64)
+    batches = [(keys, ts, [vi, vi, vi * 0.5], 100), (k2, t2, [k2, k2, k2 * 0.5], 70_000),
+               (keys[:0], ts[:0], [vi[:0], vi[:0], vi[:0] * 0.5], A.LONG_MAX)]
+    paths, _ = _run_paths(eng_mod, cfg, batches)
+    assert paths == [1, 1]
+
+
+def test_cell_preagg_wide_push_uses_sorted_cells(eng_mod):
+    """A push spanning more than 16 cells takes the sort-based cell path; a narrow one the pre-aggregation path."""
+    keys, ts, vi, vd = _stream(41, 60_000, 500, 100_000, 100, 0.0)
+    cfg = A.make_config(window_kind="SESSION", gap_ms=1000, aggs=AGGS, key_capacity=1024)
+    paths, st = _run_paths(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 2, 100))
+    assert paths == [1, 1]
+    paths, st = _run_paths(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 20, 100))
+    assert paths == [2] * 20
+    assert st.replay_records == 0

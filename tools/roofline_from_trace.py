@@ -13,7 +13,7 @@ Families (regexes over the kernel name):
   ingest (C2/C3/C5): partition3_kernel / partition2_kernel + combine3_kernel (one of each per push),
                     ingest_kernel replays are listed separately;
   push (C4 record lists): sp_range + sp_hist + sp_scan + sp_scatter;  fire: sp_refine + sp_agg;
-  sessions (C5s): sess2_* + hipcub radix sort / scan.
+  sessions (C5s): s4_* (cell pre-aggregation) or sess3_* / sess2_* + hipcub radix sort / scan.
 frac = algorithmic bytes per launch (bench line `roofline.alg_bytes_per_launch`) / average launch time / peak.
 """
 import argparse
@@ -29,11 +29,11 @@ FAMILIES = {
     "push_rl": re.compile(r"sp_(range|hist|scan|scatter)_kernel"),
     "fire_rl": re.compile(r"sp_(refine|agg)_kernel"),
     "fire": re.compile(r"fire_kernel|fire_slide_kernel|sess2_fire_kernel"),
-    "sessions": re.compile(r"sess2_(?!fire)|DeviceRadixSort|DeviceScan|radix|onesweep", re.I),
+    "sessions": re.compile(r"sess2_(?!fire)|sess3_|s4_|DeviceRadixSort|DeviceScan|radix|onesweep|lookback", re.I),
 }
 # the first kernel of every step of each config: counts steps in dispatch order
 STEP_MARK = {"ingest": re.compile(r"partition[23]_kernel"), "push_rl": re.compile(r"sp_range_kernel"),
-             "sessions": re.compile(r"sess2_classify_kernel")}
+             "sessions": re.compile(r"s4_range_kernel|sess3_min_kernel|sess2_classify_kernel")}
 
 
 def load(path):
@@ -59,7 +59,7 @@ def main():
     peak = rl["peak"]
     rows = load(args.trace)
     kern = rl.get("kernel", "")
-    fam = "sessions" if "sess2" in kern else ("push_rl" if "sp_range" in kern else "ingest")
+    fam = "sessions" if ("sess" in kern or "s4_" in kern) else ("push_rl" if "sp_range" in kern else "ingest")
     mark = STEP_MARK[fam]
     firsts = [r for r in rows if mark.search(r["Kernel_Name"])]
     if len(firsts) < W + K:
