@@ -1453,8 +1453,8 @@ __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineCo
 // sums and MIN/MAX keep the generic fire. Rows are emitted window by window with one row
 // reservation per block and window.
 constexpr int kSlideMaxU = 2048;                  // union slices per launch (LDS slot table)
-constexpr int kSlideBlock = 512;                  // threads per block
-constexpr int kSlideJ = 2;                        // keys per thread (1024 keys per block)
+constexpr int kSlideBlock = 1024;                 // threads per block
+constexpr int kSlideJ = 2;                        // keys per thread (2048 keys per block)
 constexpr int kSlideAcc = 4;                      // COUNT + up to 3 integer-sum columns
 
 struct FireSlideArgs {
@@ -1482,13 +1482,18 @@ struct FireSlideArgs {
 // Slices that retire at this watermark (tagged upos entries) are cleared here instead of by reset_slots_kernel: the
 // read that subtracts a leaving slice is its last, and only the non-zero values are written back (a Zipf stream
 // leaves most keys absent from most slices, so this writes a fraction of the dense column reset_slots_kernel wrote).
-// Output rows are written with non-temporal stores (streamed once, never re-read by this kernel).
+// Measured (r04, C3, ms per fire at 67 windows x ~1M keys): 2.24 the r03 kernel (8 keys per lane, conditional loads,
+// two barriers and one reservation per window); 2.19-2.33 this one over 256..1024-thread blocks and 2..8 keys per lane,
+// with or without non-temporal row stores -- the fire moves ~9 GB per launch (window 0's 60 slices, 2 slices x 2 columns
+// per window over the whole 2M-slot table, 40-byte rows) at ~4 TB/s, so it is bandwidth-bound on the dense slot layout.
+// Clearing: the conditional clear here 2.25 ms + no reset, an unconditional (full-line) clear 2.44, no clear 1.99 +
+// reset_slots_kernel -- 5.83 / 6.20 / 6.00 ms per C3 step.
 __device__ __forceinline__ unsigned long long* slide_ptr(const unsigned long long* p) {
     return (unsigned long long*)((uintptr_t)p & ~(uintptr_t)1);
 }
 __device__ __forceinline__ bool slide_zero(const unsigned long long* p) { return ((uintptr_t)p & 1) != 0; }
 
-template <int NA, int J = kSlideJ, int TB = kSlideBlock, bool NT = true>
+template <int NA, int J = kSlideJ, int TB = kSlideBlock>
 __global__ void __launch_bounds__(TB) fire_slide_kernel(FireSlideArgs f, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
     constexpr int kWaves = TB / 64;
@@ -1551,7 +1556,6 @@ __global__ void __launch_bounds__(TB) fire_slide_kernel(FireSlideArgs f, const E
                 if (pz && Xo[j][a]) po[a * st + kc[j]] = 0ull;
             }
     };
-    auto st64 = [&](int64_t v, int64_t* p) { if (NT) __builtin_nontemporal_store(v, p); else *p = v; };
     const unsigned long long lt = (1ull << lane) - 1ull;
     // rows of window w (sums Sw, masks mw) at the block's reservation of generation g
     auto write_rows = [&](int w, const unsigned long long (&Sw)[J][NA], const unsigned long long (&mw)[J], int g) {
@@ -1563,9 +1567,9 @@ __global__ void __launch_bounds__(TB) fire_slide_kernel(FireSlideArgs f, const E
             if (!((mw[j] >> lane) & 1ull)) continue;
             const int64_t row = rb + woff[g][j][wid] + __popcll(mw[j] & lt);
             if (row >= f.out_cap) continue;
-            st64(kc[j] < f.capacity ? (int64_t)kv[j] : LONG_MIN_J, f.o_key + row);
-            st64(ws, f.o_start + row);
-            st64(we, f.o_end + row);
+            f.o_key[row] = kc[j] < f.capacity ? (int64_t)kv[j] : LONG_MIN_J;
+            f.o_start[row] = ws;
+            f.o_end[row] = we;
             for (int a = 0; a < c.nout; ++a) {   // (no nullable aggregates on this path: the host checks)
                 const AggDesc d = c.agg[a];
                 unsigned long long x = 0;
@@ -1580,7 +1584,7 @@ __global__ void __launch_bounds__(TB) fire_slide_kernel(FireSlideArgs f, const E
                     case FWA_AVG_I64: v = (cnt == -1 && iv == LONG_MIN_J) ? LONG_MIN_J : iv / cnt; break;
                     default: write_agg(d, Sw[j][0], x, 0, f.o_agg[a], nullptr, row); continue;
                 }
-                st64(v, (int64_t*)f.o_agg[a] + row);
+                ((int64_t*)f.o_agg[a])[row] = v;
             }
         }
     };
@@ -3140,7 +3144,7 @@ struct fwa_engine {
     bool sparse = false;
     SpState* sp = nullptr;
     // per-handle options (fwa_set_option; the defaults are the production behaviour)
-    int32_t opt_pre = -1, opt_mp = -1, opt_narrow = -1, opt_cells = -1, opt_slide = 0;   // -1 adaptive, 0 never, 1 always
+    int32_t opt_pre = -1, opt_mp = -1, opt_narrow = -1, opt_cells = -1;   // -1 adaptive, 0 never, 1 always
     int64_t opt_out_min = 0;
     bool opt_partials_v1 = false;
     int32_t opt_profile = 0;
@@ -5547,14 +5551,12 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
     switch (e->nacc) {
         case 1: fire_slide_kernel<1><<<(unsigned)grid, kSlideBlock, 0, e->stream>>>(f, e->d_ec); break;
-        case 2:
-            if (e->opt_slide == 1) fire_slide_kernel<2, 2, 512, false><<<(unsigned)((e->capacity + 1 + 1023) / 1024), 512, 0, e->stream>>>(f, e->d_ec);
-            else if (e->opt_slide == 2) fire_slide_kernel<2, 4, 256, false><<<(unsigned)((e->capacity + 1 + 1023) / 1024), 256, 0, e->stream>>>(f, e->d_ec);
-            else if (e->opt_slide == 3) fire_slide_kernel<2, 2, 1024, false><<<(unsigned)((e->capacity + 1 + 2047) / 2048), 1024, 0, e->stream>>>(f, e->d_ec);
-            else fire_slide_kernel<2><<<(unsigned)grid, kSlideBlock, 0, e->stream>>>(f, e->d_ec);
-            break;
+        case 2: fire_slide_kernel<2><<<(unsigned)grid, kSlideBlock, 0, e->stream>>>(f, e->d_ec); break;
         case 3: fire_slide_kernel<3><<<(unsigned)grid, kSlideBlock, 0, e->stream>>>(f, e->d_ec); break;
-        default: fire_slide_kernel<4><<<(unsigned)grid, kSlideBlock, 0, e->stream>>>(f, e->d_ec); break;
+        default:   // 512 threads: the 4-accumulator running sums do not fit the 128 VGPRs of a 1024-thread block
+            fire_slide_kernel<4, kSlideJ, 512><<<(unsigned)((e->capacity + 1 + 512 * kSlideJ - 1) / (512 * kSlideJ)), 512, 0,
+                                                 e->stream>>>(f, e->d_ec);
+            break;
     }
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
@@ -5880,7 +5882,6 @@ int fwa_set_option(fwa_engine* e, int32_t option, int64_t value) {
         case FWA_OPT_PARTIALS_ONE_PASS: e->opt_partials_v1 = value > 0; return FWA_OK;
         case FWA_OPT_SP_TABLE: case FWA_OPT_SP_FMAX: case FWA_OPT_SP_BUDGET: return sp_set_option(e, option, value);
         case FWA_OPT_PROFILE: e->opt_profile = value > 0 ? 1 : 0; return FWA_OK;
-        case 98: e->opt_slide = (int32_t)value; return FWA_OK;   // A/B of the sliding fire's shape (temporary)
         default: return fail(e, FWA_E_ARG, "unknown option");
     }
 }

@@ -652,7 +652,7 @@ int fwa_keydict_encode_host_str(fwa_keydict* d, const uint64_t* slots, const uin
         char* p = buf;
         auto put = [&](const void* src, size_t nb) -> char* {
             char* dst = p;
-            if (nb && hipMemcpyAsync(dst, src, nb, hipMemcpyHostToDevice, d->stream) != hipSuccess) rc = FWA_E_DEVICE;
+            if (nb && src && hipMemcpyAsync(dst, src, nb, hipMemcpyHostToDevice, d->stream) != hipSuccess) rc = FWA_E_DEVICE;
             p += (nb + 15) & ~(size_t)15;
             return dst;
         };
@@ -669,7 +669,7 @@ int fwa_keydict_encode_host_str(fwa_keydict* d, const uint64_t* slots, const uin
                 cp[c] = put(cols.data() + (size_t)c * n, 8 * (size_t)n);
             }
         }
-        int64_t* did = (int64_t*)put(nullptr, 8 * (size_t)n);
+        int64_t* did = (int64_t*)put(nullptr, 8 * (size_t)n);   // output only: reserved, not copied
         if (rc) break;
         if ((rc = fwa_keydict_encode(d, cp, np_, n, did, nullptr))) break;
         if (hipMemcpy(ids, did, 8 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) rc = FWA_E_DEVICE;
