@@ -32,7 +32,7 @@ FAMILIES = {
     "sessions": re.compile(r"sess2_(?!fire)|sess3_|s4_|DeviceRadixSort|DeviceScan|radix|onesweep|lookback", re.I),
 }
 # the first kernel of every step of each config: counts steps in dispatch order
-STEP_MARK = {"ingest": re.compile(r"partition[23]_kernel"), "push_rl": re.compile(r"sp_range_kernel"),
+STEP_MARK = {"ingest": re.compile(r"partition[23]_kernel"), "push_rl": re.compile(r"sp_hist_kernel"),
              "sessions": re.compile(r"s4_range_kernel|sess3_min_kernel|sess2_classify_kernel")}
 
 
