@@ -328,7 +328,7 @@ def main():
 def ingest_kernels(args, eng):
     """Names of the kernels whose device time `roofline.achieved` divides by (HIP events around them)."""
     if args.config == "c5s":
-        return ("s4_range+s4_route+s4_hist+s4_colscan+scan+s4_scatter+s4_sess_count/scatter+s4_group "
+        return ("s4_route+s4_hist+s4_colscan+scan+s4_part<1>+s4_hist2+s4_part<2>+s4_sess_count/scatter+s4_group "
                 "(cell pre-aggregation; sess3_* sort-based cells or sess2_* when a push leaves its range)")
     if eng.record_lists:
         return "sp_range_kernel+sp_hist_kernel+sp_scan_kernel+sp_scatter_kernel (record lists)"

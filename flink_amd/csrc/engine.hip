@@ -1668,7 +1668,8 @@ __global__ void __launch_bounds__(TB) fire_slide_kernel(FireSlideArgs f, const E
 //    on an element); every session with cleanup = end - 1 + L <= wm is cleared (clearAllState).
 
 struct SessCtr {                 // per-push device counters (zeroed by the host before a push / fire)
-    unsigned long long ts_min, ts_max;   // ord-encoded, over records and in-flight session starts
+    unsigned long long ts_min, ts_max;   // ord-encoded, over records and in-flight session starts (cell pre-aggregation:
+                                         // the smallest / largest cell number of the push)
     unsigned long long n_special;        // records whose lone window ends at or before the watermark
     unsigned long long n_bulk, n_sp;     // elements routed to the bulk / the arrival-order path
     unsigned long long n_out_sp;         // sessions written by the arrival-order path

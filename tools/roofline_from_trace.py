@@ -33,7 +33,7 @@ FAMILIES = {
 }
 # the first kernel of every step of each config: counts steps in dispatch order
 STEP_MARK = {"ingest": re.compile(r"partition[23]_kernel"), "push_rl": re.compile(r"sp_hist_kernel"),
-             "sessions": re.compile(r"s4_range_kernel|sess3_min_kernel|sess2_classify_kernel")}
+             "sessions": re.compile(r"s4_route_kernel|sess3_min_kernel|sess2_classify_kernel")}
 
 
 def load(path):
