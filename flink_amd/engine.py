@@ -165,9 +165,16 @@ class WindowAggregator:
         _check(rc, self.h)
 
     def _order_after_producer(self, x):
-        """Device inputs come from torch's current stream: make the engine's stream wait for it."""
+        """Device inputs come from torch's current stream: make the engine's stream wait for it. torch's legacy
+        default stream has no handle the engine's (non-blocking) stream can wait on -- a NULL input stream means
+        "the inputs are complete" (fwa_set_input_stream) -- so work still pending there is waited for on the host:
+        without it a push read columns the keyBy exchange had not finished writing (the stream-ordered
+        fwa_route_rows / fwa_unpack_rows keep no host synchronisation of their own)."""
         import torch
-        s = torch.cuda.current_stream(x.device).cuda_stream
+        cs = torch.cuda.current_stream(x.device)
+        s = cs.cuda_stream
+        if s == 0:
+            cs.synchronize()
         if s != self._in_stream:
             _check(lib().fwa_set_input_stream(self.h, C.c_void_p(s)), self.h)
             self._in_stream = s

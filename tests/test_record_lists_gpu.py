@@ -243,3 +243,34 @@ def test_record_lists_compaction_bounds_memory():
             "print('ok')\n") % (ROOT, os.path.join(ROOT, "tests"))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_record_lists_owned_range_across_watermarks():
+    """A subtask owning half the key groups (N = 2 keyBy owner) on the record lists: pushes after a watermark take the
+    fused histogram pass (key-group check on the same loads); every push holds owned keys only."""
+    from flink_amd import engine
+    from oracle.oracle import Oracle
+    rng = np.random.default_rng(123)
+    n = 1 << 20
+    keys = rng.integers(0, 100_000_000, 4 * n).astype(np.int64)
+    kgs, _ = engine.key_groups(keys, 128, 1, A.KEY_JAVA_LONG)
+    keys = keys[kgs <= 63]
+    m = len(keys)
+    ts = np.sort(rng.integers(0, 40_000, m)).astype(np.int64) - rng.integers(0, 1000, m)
+    vi = rng.integers(0, 1000, m).astype(np.int64)
+    vf = rng.random(m).astype(np.float32)
+    vd = rng.random(m)
+    cfg = A.make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, aggs=AGGS, record_lists=True,
+                        kg_start=0, kg_end=63, key_capacity=1 << 26)
+    names = A.agg_names(cfg)
+    g, o = engine.WindowAggregator(cfg), Oracle(cfg)
+    mx = -2**63
+    for b in range(4):
+        sl = slice(b * m // 4, (b + 1) * m // 4)
+        cols = [vi[sl], vf[sl], vd[sl]]
+        assert g.push(keys[sl], ts[sl], cols) == o.push(keys[sl], ts[sl], cols)
+        mx = max(mx, int(ts[sl].max()))
+        wm = mx - 1001 if b < 3 else A.LONG_MAX
+        assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), names, rtol=1e-6, ctx="batch %d" % b)
+    g.close()
+    o.close()
