@@ -173,7 +173,7 @@ class WindowAggregator:
         import torch
         cs = torch.cuda.current_stream(x.device)
         s = cs.cuda_stream
-        if s == 0:
+        if s == 0 and not cs.query():
             cs.synchronize()
         if s != self._in_stream:
             _check(lib().fwa_set_input_stream(self.h, C.c_void_p(s)), self.h)
