@@ -40,1209 +40,7 @@
 
 namespace {
 
-constexpr int kBlock = 256;
-constexpr uint64_t kEmptyKey = 0x8000000000000000ull;  // key-table sentinel (INT64_MIN); that key uses a side slot
-constexpr int kBucket = 8;                              // key-table probe bucket: 8 slots = 64 B
-constexpr int32_t kWantCap = 1 << 14;                   // distinct missing slices reported per launch
-
-// ------------------------------------------------------------------------------------------------
-// device-side structures
-
-struct DirEntry {               // slice directory entry (32 B), read-only during a launch
-    int64_t q;                  // slice number
-    int32_t slot;               // accumulator slot, -1: not allocated
-    int32_t flags;              // bit0 occupied, bit1 always accepted (last window end == LONG_MAX)
-    int64_t thr;                // a record is accepted iff wm < thr (or bit1)
-    int64_t first_maxts;        // maxTimestamp of the earliest window containing the slice
-};
-
-struct DevStatus {
-    int32_t error;              // first fwa_status error code raised by a kernel (0 = none)
-    int32_t spill_n;            // records whose slice had no slot (replayed)
-    int32_t want_n;             // distinct slice numbers in want[]
-    int32_t key_full;
-    unsigned long long dropped;
-    unsigned long long n_keys;  // distinct keys in the key table (incl. side slot)
-    unsigned long long late_fire;
-    unsigned long long rows;    // fire kernel output counter
-    unsigned long long max_q;   // ord-encoded max / min slice number accepted this push
-    unsigned long long min_q;
-    int32_t pad;                // host-side scratch (straggler count copy)
-    int32_t pad2;
-    unsigned long long sess_live;  // sessions: in-flight sessions (rows a fire can emit at most)
-    unsigned long long drop_n;     // FWA_CFG_LATE_INDICES: entries in the dropped-record index list this push
-    int32_t ovf_n;                 // Phase P: bucket entries past their sub-bucket's end this push (skew signal)
-    int32_t strag_n;               // Phase A: entries older than their combiner's LDS window this push
-    int32_t wide_n;                // Phase P narrow entries: accepted records whose key or value needs 64 bits (replayed)
-    int32_t pad3;
-};
-
-// FWA_CFG_LATE_INDICES: record index of a late-dropped record (lateDataOutputTag / lateRecordsDroppedRate),
-// appended with one reservation per wave; list capacity = the push's record count.
-__device__ __forceinline__ void note_drop(int32_t* list, DevStatus* st, bool drop, int64_t i) {
-    if (!list) return;
-    const unsigned long long m = __ballot(drop);
-    if (!m) return;
-    const int lane = threadIdx.x & 63;
-    const int ld = __ffsll((long long)m) - 1;
-    unsigned long long b = 0;
-    if (lane == ld) b = atomicAdd(&st->drop_n, (unsigned long long)__popcll(m));
-    b = __shfl(b, ld);
-    if (drop) list[b + __popcll(m & ((1ull << lane) - 1))] = (int32_t)i;
-}
-
-enum AccKind : int32_t { ACC_NONE = 0, ACC_ADD_I64 = 1, ACC_ADD_F64 = 2, ACC_MIN_ORD = 3, ACC_MAX_ORD = 4 };
-
-struct AggDesc {
-    int32_t kind;               // fwa_agg_kind
-    int32_t col;                // input column
-    int32_t acc;                // accumulator column (>=1) or 0 for COUNT
-    int32_t acc_kind;
-    int32_t vslot;              // partitioned path: which carried value column feeds this aggregate
-    int32_t alias;              // 1: shares the accumulator column of an earlier aggregate (e.g. SUM(d) and
-                                // AVG(d) keep one double sum): read at fire, never updated through it
-    int32_t nn;                 // accumulator column counting the non-NULL inputs of a nullable column (0: none)
-};
-constexpr int kMaxAggsInt = FWA_MAX_AGGS + FWA_MAX_COLS;   // user aggregates + hidden non-NULL counters
-
-struct EngineConst {
-    jm::UDiv64 g_div;           // slice size
-    int64_t g, off;
-    int32_t sem, lateness_pos;  // lateness_pos: DataStream allowed lateness > 0
-    int32_t key_kind, max_par, kg_lo, kg_hi;
-    int32_t naggs, nacc;        // naggs: user + hidden aggregates; nacc = 1 (count) + stateful agg columns
-    int32_t nout, nullable;     // nout: user aggregates (output columns); nullable: fwa_config.nullable_cols
-    AggDesc agg[kMaxAggsInt];
-    int32_t acc_kind[1 + kMaxAggsInt];
-    const int64_t* tz;          // shift time zone table (device copy of fwa_config.tz), tz_n pairs
-    int32_t tz_n, pad_tz;
-};
-
-// Slice-assignment timestamp: the record's local wall-clock time under a Table shift time zone
-// (AbstractSliceAssigner.assignSliceEnd -> TimeWindowUtil.toUtcTimestampMills), else the timestamp.
-__device__ __forceinline__ int64_t assign_ts(const EngineConst& c, int64_t ts) {
-    return c.tz_n ? jm::tz_to_local(c.tz, c.tz_n, ts) : ts;
-}
-
-struct IngestArgs {
-    const int64_t* keys;
-    const int64_t* ts;
-    const void* cols[FWA_MAX_AGGS + FWA_MAX_COLS];   // value columns; partials: aggregate j's accumulator column
-                                                     // (hidden non-NULL counters after the user aggregates)
-    const int32_t* key_hash;
-    const int32_t* idx;         // optional index list (miss replay)
-    const unsigned long long* pcount;  // partial accumulators (fwa_push_partials): COUNT per row; cols[j] = acc of agg j
-    int64_t n;
-    int64_t wm;
-    unsigned long long* key_table;
-    uint64_t key_mask;          // capacity-1 (power of two); side slot at capacity
-    int32_t seg_log, part_bits; // key-table segmentation (see key_slot)
-    const DirEntry* dir;
-    uint32_t dir_mask;
-    unsigned long long* want;   // open-addressing set of ord(q), kWantCap entries, 0 = empty
-    int32_t* spill;
-    int32_t* late;              // DataStream late firings (window fired, within allowed lateness): deferred
-    int32_t* touched;           // per slot
-    unsigned long long* const* slot_base;
-    int64_t stride;             // elements per accumulator column
-    int64_t spill_cap;          // entries of spill[] and late[] (a store past it raises FWA_E_STATE instead)
-    int32_t* dropidx;           // FWA_CFG_LATE_INDICES: dropped-record indices (nullptr: not collected)
-    const uint8_t* nulls[FWA_MAX_COLS];   // SQL NULL flags per value column (nullptr: no NULLs)
-    DevStatus* st;
-};
-
-__device__ __forceinline__ void raise_error(DevStatus* st, int code) { atomicCAS(&st->error, 0, code); }
-
-// Bounds-checked scatter of a record index into a spill / late list: an index past the list's capacity
-// would be a logic error upstream; it is reported (FWA_E_STATE) instead of faulting the device.
-__device__ __forceinline__ void put_idx(int32_t* list, int64_t pos, int64_t cap, int32_t v, DevStatus* st) {
-    if (pos >= 0 && pos < cap) list[pos] = v;
-    else raise_error(st, FWA_E_STATE);
-}
-
-// Key table: SEGMENTED open addressing. h = mix64(key); segment p = top part_bits of h (the v2
-// combiner's partition), probe linearly inside the segment from the kBucket-aligned home
-// (h & (SEG-1)) & ~(kBucket-1); CAS insert. The aligned home lets the combiner read a key's whole
-// home bucket (64 B) with one LDS round instead of walking the probe sequence slot by slot: linear
-// probing's displacement tail (~20 slots at load 0.5 over a 4096-slot segment) made a wave's probe
-// loop run for the worst of its 256 records (r01 clock64 profile: 75 % of combine time).
-// A stale EMPTY read only sends us to the CAS, which returns the winner's key: no hand-off needed.
-__device__ __forceinline__ uint64_t seg_base(uint64_t h, int seg_log, int part_bits) {
-    return part_bits ? ((h >> (64 - part_bits)) << seg_log) : 0ull;
-}
-__device__ __forceinline__ int64_t key_slot(unsigned long long* table, uint64_t mask, int seg_log, int part_bits,
-                                            int64_t key, DevStatus* st) {
-    if ((uint64_t)key == kEmptyKey) {
-        const unsigned long long side = mask + 1;
-        if (table[side] != 1ull && atomicCAS(&table[side], 0ull, 1ull) == 0ull) atomicAdd(&st->n_keys, 1ull);
-        return (int64_t)side;
-    }
-    const uint64_t h = jm::mix64((uint64_t)key);
-    const uint64_t base = seg_base(h, seg_log, part_bits);
-    const uint64_t smask = ((uint64_t)1 << seg_log) - 1;
-    const uint64_t home = h & smask & ~(uint64_t)(kBucket - 1);   // probing starts at a bucket boundary
-    for (uint64_t probe = 0; probe <= smask; ++probe) {
-        const uint64_t i = base | ((home + probe) & smask);
-        const unsigned long long cur = table[i];
-        if (cur == (unsigned long long)key) return (int64_t)i;
-        if (cur == kEmptyKey) {
-            const unsigned long long old = atomicCAS(&table[i], kEmptyKey, (unsigned long long)key);
-            if (old == kEmptyKey) {
-                atomicAdd(&st->n_keys, 1ull);
-                return (int64_t)i;
-            }
-            if (old == (unsigned long long)key) return (int64_t)i;
-        }
-    }
-    return -1;
-}
-
-__device__ __forceinline__ const DirEntry* dir_find(const DirEntry* dir, uint32_t mask, int64_t q) {
-    uint32_t i = (uint32_t)jm::mix64((uint64_t)q) & mask;
-    for (uint32_t probe = 0; probe <= mask; ++probe) {
-        const DirEntry* e = &dir[i];
-        if (!(e->flags & 1)) return nullptr;
-        if (e->q == q) return e;
-        i = (i + 1) & mask;
-    }
-    return nullptr;
-}
-
-__device__ __forceinline__ void want_insert(unsigned long long* want, DevStatus* st, int64_t q) {
-    const unsigned long long key = jm::ord_i64(q) + 1ull;  // never 0: |q| <= 2^63/g < LONG_MAX for g >= 2
-    uint32_t i = (uint32_t)jm::mix64((uint64_t)q) & (kWantCap - 1);
-    for (int probe = 0; probe < kWantCap; ++probe) {
-        unsigned long long cur = want[i];
-        if (cur == key) return;
-        if (cur == 0ull) {
-            unsigned long long old = atomicCAS(&want[i], 0ull, key);
-            if (old == 0ull) { atomicAdd(&st->want_n, 1); return; }
-            if (old == key) return;
-        }
-        i = (i + 1) & (kWantCap - 1);
-    }
-    raise_error(st, FWA_E_OOM);
-}
-
-__device__ __forceinline__ uint64_t load_ord(const void* col, int64_t i, int kind) {
-    switch (kind) {
-        case FWA_MIN_I64: case FWA_MAX_I64: return jm::ord_i64(((const int64_t*)col)[i]);
-        case FWA_MIN_F32: case FWA_MAX_F32:
-            return jm::ord_bits64((uint64_t)__double_as_longlong((double)((const float*)col)[i]));
-        default: return jm::ord_bits64((uint64_t)__double_as_longlong(((const double*)col)[i]));
-    }
-}
-
-// One input value in its accumulator domain (i64 bits, f64 bits, or ordered key). A SQL NULL input (nul[i])
-// contributes the accumulator's identity; a hidden non-NULL counter (COUNT_COL) contributes 1 or 0.
-__device__ __forceinline__ unsigned long long acc_input(const AggDesc& d, const void* col, int64_t i,
-                                                        const uint8_t* nul = nullptr) {
-    const bool isnull = nul && nul[i];
-    if (d.kind == FWA_COUNT_COL) return isnull ? 0ull : 1ull;
-    if (isnull) return d.acc_kind == ACC_MIN_ORD ? ~0ull : 0ull;
-    switch (d.acc_kind) {
-        case ACC_ADD_I64: return ((const unsigned long long*)col)[i];
-        case ACC_ADD_F64: {
-            const double v = (d.kind == FWA_SUM_F32 || d.kind == FWA_AVG_F32) ? (double)((const float*)col)[i]
-                                                                               : ((const double*)col)[i];
-            return (unsigned long long)__double_as_longlong(v);
-        }
-        default: return load_ord(col, i, d.kind);
-    }
-}
-
-template <bool kIdx>
-__global__ void __launch_bounds__(kBlock) ingest_kernel(IngestArgs a, const EngineConst* __restrict__ cp) {
-    const EngineConst& c = *cp;
-    const int lane = threadIdx.x & 63;
-    __shared__ unsigned long long s_red[kBlock / 64][1 + kMaxAggsInt];   // hot-key group reduction
-    const int64_t stride_grid = (int64_t)gridDim.x * blockDim.x;
-    unsigned long long qmax = 0, qmin = ~0ull;
-    unsigned long long dropped = 0;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.n; t += stride_grid) {
-        const int64_t i = kIdx ? (int64_t)a.idx[t] : t;
-        const int64_t key = a.keys[i];
-        const int64_t ts = a.ts[i];
-        // key-group ownership (StateTable.getMapForKeyGroup :300-307)
-        const int32_t kg = jm::key_group_of(key, c.key_kind, a.key_hash ? a.key_hash[i] : 0, c.max_par);
-        if (kg < c.kg_lo || kg > c.kg_hi) { raise_error(a.st, FWA_E_KEYGROUP); continue; }
-        if (c.sem == FWA_SEM_DATASTREAM && ts == LONG_MIN_J) { raise_error(a.st, FWA_E_TS_MIN); continue; }
-        // slice number q = floor((ts - off) / g), Java wrap arithmetic (TimeWindow.java:264-272)
-        const int64_t d = jm::wsub(a.pcount ? ts : assign_ts(c, ts), c.off);   // partial rows: slice start, already local
-        const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
-        const uint64_t uq = jm::udiv64(ud, c.g_div);
-        int64_t q;
-        if (d >= 0) q = (int64_t)uq;
-        else q = (uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1;
-        const DirEntry* e = dir_find(a.dir, a.dir_mask, q);
-        if (e == nullptr) {                                     // slice unknown to the host: replay
-            want_insert(a.want, a.st, q);
-            const unsigned long long m = __ballot(1);
-            const int leader = __ffsll((long long)m) - 1;
-            int32_t base = 0;
-            if (lane == leader) base = atomicAdd(&a.st->spill_n, __popcll(m));
-            base = __shfl(base, leader);
-            put_idx(a.spill, base + __popcll(m & ((1ull << lane) - 1)), a.spill_cap, (int32_t)i, a.st);
-            continue;
-        }
-        const unsigned long long cadd = a.pcount ? a.pcount[i] : 1ull;   // records this row stands for
-        const bool accepted = (e->flags & 2) || a.wm < e->thr;
-        if (!accepted) { dropped += cadd; if (a.dropidx && !a.pcount) a.dropidx[atomicAdd(&a.st->drop_n, 1ull)] = (int32_t)i; continue; }
-        if (e->slot < 0) {                                      // known slice without slot: replay
-            want_insert(a.want, a.st, q);
-            const int32_t si = atomicAdd(&a.st->spill_n, 1);
-            put_idx(a.spill, si, a.spill_cap, (int32_t)i, a.st);
-            continue;
-        }
-        if (c.lateness_pos && a.wm >= e->first_maxts) {        // some window of the slice fired already:
-            const unsigned long long li = atomicAdd(&a.st->late_fire, 1ull);   // EventTimeTrigger.onElement
-            put_idx(a.late, (int64_t)li, a.spill_cap, (int32_t)i, a.st);        // FIRE -> late_fire_kernel
-            continue;
-        }
-        const uint64_t oq = jm::ord_i64(q);
-        qmax = oq > qmax ? oq : qmax;
-        qmin = oq < qmin ? oq : qmin;
-        const int64_t kid = key_slot(a.key_table, a.key_mask, a.seg_log, a.part_bits, key, a.st);
-        if (kid < 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); continue; }
-        const int32_t slot = e->slot;
-        unsigned long long* base = a.slot_base[slot];
-        if (a.touched[slot] == 0) a.touched[slot] = 1;
-        // Hot keys (skew: e.g. the bucket-overflow replay of a Zipf head key, where most lanes of a wave
-        // carry the same key): the lanes sharing the wave leader's (kid, slot) combine in LDS first, so
-        // the group costs one set of global atomics instead of one per lane on the same address.
-        // Replay launches only (kIdx): the plain v1 pass over a large uniform key space (C4) is
-        // latency-bound and lost half its rate to the extra registers.
-        if constexpr (kIdx) {
-            const unsigned long long act = __ballot(1);
-            const int leader = __ffsll((long long)act) - 1;
-            const long long lkid = __shfl((long long)kid, leader);
-            const int lslot = __shfl(slot, leader);
-            const bool grp = kid == lkid && slot == lslot;
-            const unsigned long long gm = __ballot(grp);
-            if (grp && __popcll(gm) > 1) {
-                unsigned long long* r = s_red[threadIdx.x >> 6];
-                if (lane == leader) {
-                    r[0] = cadd;
-                    for (int j = 0; j < c.naggs; ++j) {
-                        const AggDesc dsc = c.agg[j];
-                        if (dsc.acc == 0 || dsc.alias) continue;
-                        r[dsc.acc] = a.pcount ? ((const unsigned long long*)a.cols[j])[i] : acc_input(dsc, a.cols[dsc.col], i, a.nulls[dsc.col]);
-                    }
-                }
-                __threadfence_block();
-                __builtin_amdgcn_wave_barrier();
-                if (lane != leader) {
-                    atomicAdd(&r[0], cadd);
-                    for (int j = 0; j < c.naggs; ++j) {
-                        const AggDesc dsc = c.agg[j];
-                        if (dsc.acc == 0 || dsc.alias) continue;
-                        const unsigned long long x = a.pcount ? ((const unsigned long long*)a.cols[j])[i]
-                                                              : acc_input(dsc, a.cols[dsc.col], i, a.nulls[dsc.col]);
-                        unsigned long long* rp = &r[dsc.acc];
-                        switch (dsc.acc_kind) {
-                            case ACC_ADD_I64: atomicAdd(rp, x); break;
-                            case ACC_ADD_F64: atomicAdd((double*)rp, __longlong_as_double((long long)x)); break;
-                            case ACC_MIN_ORD: atomicMin(rp, x); break;
-                            case ACC_MAX_ORD: atomicMax(rp, x); break;
-                            default: break;
-                        }
-                    }
-                }
-                __threadfence_block();
-                __builtin_amdgcn_wave_barrier();
-                if (lane == leader) {
-                    atomicAdd(&base[kid], r[0]);
-                    for (int j = 0; j < c.naggs; ++j) {
-                        const AggDesc dsc = c.agg[j];
-                        if (dsc.acc == 0 || dsc.alias) continue;
-                        unsigned long long* col = base + (int64_t)dsc.acc * a.stride + kid;
-                        const unsigned long long x = r[dsc.acc];
-                        switch (dsc.acc_kind) {
-                            case ACC_ADD_I64: atomicAdd(col, x); break;
-                            case ACC_ADD_F64: atomicAdd((double*)col, __longlong_as_double((long long)x)); break;
-                            case ACC_MIN_ORD: atomicMin(col, x); break;
-                            case ACC_MAX_ORD: atomicMax(col, x); break;
-                            default: break;
-                        }
-                    }
-                }
-                continue;
-            }
-        }
-        atomicAdd(&base[kid], cadd);                            // COUNT(*)
-#pragma unroll
-        for (int j = 0; j < kMaxAggsInt; ++j) {
-            if (j >= c.naggs) break;
-            const AggDesc dsc = c.agg[j];
-            if (dsc.acc == 0 || dsc.alias) continue;
-            unsigned long long* col = base + (int64_t)dsc.acc * a.stride + kid;
-            const unsigned long long x = a.pcount ? ((const unsigned long long*)a.cols[j])[i]   // accumulator
-                                                  : acc_input(dsc, a.cols[dsc.col], i, a.nulls[dsc.col]);
-            switch (dsc.acc_kind) {
-                case ACC_ADD_I64: atomicAdd(col, x); break;
-                case ACC_ADD_F64: atomicAdd((double*)col, __longlong_as_double((long long)x)); break;
-                case ACC_MIN_ORD: atomicMin(col, x); break;
-                case ACC_MAX_ORD: atomicMax(col, x); break;
-                default: break;
-            }
-        }
-    }
-    // wave-level reductions of the per-thread tallies, one atomic per wave
-    for (int s = 32; s >= 1; s >>= 1) {
-        dropped += __shfl_xor(dropped, s);
-        unsigned long long x = __shfl_xor(qmax, s);
-        qmax = x > qmax ? x : qmax;
-        unsigned long long y = __shfl_xor(qmin, s);
-        qmin = y < qmin ? y : qmin;
-    }
-    if (lane == 0) {
-        if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
-        if (qmax) atomicMax(&a.st->max_q, qmax);
-        if (qmin != ~0ull) atomicMin(&a.st->min_q, qmin);
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// v2 ingest: two phases, no global atomics -- Flink's LocalSlicingWindowAggOperator /
-// GlobalAggCombiner split (TwoStageOptimizedWindowAggregateRule.java:88-103) done on-chip.
-//
-// Phase P (partition_kernel): a pure streaming pass. Per tile of records: Java key-group check,
-//   slice number + lateness via the read-only directory, partition p = top bits of mix64(key) (= the
-//   key-table segment that will hold the key), LDS counting sort of the tile by p, one global cursor
-//   reservation per (tile, partition), coalesced stores of the bucket runs. Carried record (SoA):
-//   key u64, up to 2 raw 8-byte value columns, rel u16 (slice number - q_base).
-// Phase A (combine_kernel): one workgroup owns one partition = one SEG-slot key-table segment. It
-//   loads the segment into LDS, streams its bucket once, finds/inserts keys in LDS (ds_cmpst_b64),
-//   accumulates into an LDS window of `sl` slices with LDS atomics, and merges a slice that leaves
-//   the window into HBM with plain coalesced read-modify-write (exclusive ownership: no atomics).
-//   Records older than the window ("stragglers") are applied in place with global atomics.
-
-constexpr int kMaxPart = 1024;
-constexpr int kRelCap = 4096;                      // slice numbers relative to q_base
-constexpr int kSub = 16;                           // sub-buckets per partition (spread cursor contention)
-// Phase P's per-launch verdict for a relative slice (built by the host from the directory and the
-// watermark): accept into a bucket, count as late-dropped, or hand to the v1 replay (directory miss,
-// slice without slot, late firing within allowed lateness, errors -- everything rare).
-constexpr uint8_t kCodeSlow = 0, kCodeAccept = 1, kCodeDrop = 2;
-
-struct PartArgs {
-    const int64_t* keys;
-    const int64_t* ts;
-    const void* cols[FWA_MAX_COLS];
-    const int32_t* key_hash;
-    int64_t n;
-    int64_t wm;
-    const uint8_t* relcode;            // [kRelCap] per relative slice: kCodeAccept / kCodeDrop / kCodeSlow
-    const int32_t* rel2slot;           // [kRelCap] slot of each relative slice (touched marking)
-    int32_t* touched;                  // per slot
-    int32_t* spill;
-    int64_t q_base;
-    int64_t base_ts;                   // off + q_base * g: first timestamp of slice q_base (fast path)
-    uint64_t fast_lim;                 // kRelCap * g (< 2^32) or 0
-    uint64_t fast_m;                   // ceil(2^fast_sh / g): exact floor(dd / g) for dd < fast_lim; 0 = no fast path
-    int32_t fast_sh, pad_fast;
-    unsigned long long* b_key;         // [np][capb]
-    unsigned long long* b_val0;
-    unsigned long long* b_val1;
-    uint16_t* b_rel;
-    uint16_t* b_n;                     // PRE: records each bucket entry stands for (tile pre-aggregation)
-    uint32_t* b_cnt;                   // [np]
-    int64_t capb;
-    uint64_t trash;                    // bucket index of a kMaxPart-entry scratch area past the buckets
-    int64_t spill_cap;
-    int32_t part_bits, np;
-    int32_t vcol[2];
-    int32_t vsize[2];                  // 4 or 8 bytes
-    int32_t* dropidx;                  // FWA_CFG_LATE_INDICES list (nullptr: not collected)
-    const uint8_t* nulls[FWA_MAX_COLS];   // SQL NULL flags of the push (records with a NULL take the v1 path)
-    int32_t any_null;                  // some nulls[] is set
-    const unsigned long long* pcount;  // fwa_push_partials (PRE only): records each row stands for (bucket n);
-                                       // rows are not merged in the tile, counts > 65535 take the v1 path
-    // PRE: a pre-aggregated entry past its sub-bucket's end is applied at once with global atomics
-    unsigned long long* key_table;
-    uint64_t key_mask;
-    int32_t seg_log, pad_p;
-    unsigned long long* const* slot_base;
-    int64_t stride;
-    DevStatus* st;
-    long long* prof;                   // optional per-block phase cycle counters (FWA_OPT_PROFILE)
-};
-
-__device__ __forceinline__ bool row_has_null(const PartArgs& a, int64_t i) {
-    bool r = false;
-#pragma unroll
-    for (int col = 0; col < FWA_MAX_COLS; ++col) r = r || (a.nulls[col] && a.nulls[col][i]);
-    return r;
-}
-
-__device__ __forceinline__ unsigned long long load_raw(const void* col, int64_t i, int size) {
-    return size == 4 ? (unsigned long long)((const uint32_t*)col)[i] : ((const unsigned long long*)col)[i];
-}
-
-// Block-wide exclusive scan of hist[0..np) into toff (np <= kMaxPart, kMaxPart % THREADS == 0).
-template <int THREADS>
-__device__ __forceinline__ void block_scan_np(const uint32_t* hist, uint32_t* toff, uint32_t* wsum, int np, uint32_t* total) {
-    constexpr int PER = kMaxPart / THREADS;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    uint32_t v[PER];
-    uint32_t x = 0;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) { v[q] = (PER * tid + q < np) ? hist[PER * tid + q] : 0u; x += v[q]; }
-    uint32_t incl = x;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d);
-        if (lane >= d) incl += y;
-    }
-    if (lane == 63) wsum[wid] = incl;
-    __syncthreads();
-    if (wid == 0) {                     // the per-wave sums, scanned by one wave (not a serial loop)
-        constexpr int NW = THREADS / 64;
-        const uint32_t v = lane < NW ? wsum[lane] : 0u;
-        uint32_t r = v;
-        for (int d = 1; d < NW; d <<= 1) {
-            const uint32_t y = __shfl_up(r, d);
-            if (lane >= d) r += y;
-        }
-        if (lane < NW) wsum[lane] = r - v;
-        if (lane == NW - 1) *total = r;
-    }
-    __syncthreads();
-    uint32_t excl = wsum[wid] + incl - x;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) { if (PER * tid + q < np) toff[PER * tid + q] = excl; excl += v[q]; }
-}
-
-// Make the compiler wait for a loaded register HERE, on every path (see partition3).
-__device__ __forceinline__ void consume(unsigned long long x) {
-    asm volatile("" : : "v"((uint32_t)x), "v"((uint32_t)(x >> 32)));
-}
-__device__ __forceinline__ void consume(int64_t x) { consume((unsigned long long)x); }
-__device__ __forceinline__ void consume(int32_t x) { asm volatile("" : : "v"(x)); }
-__device__ __forceinline__ void consume(uint32_t x) { asm volatile("" : : "v"(x)); }
-
-// partition3 (Phase P): the tile is staged in LDS in arrival order (x_*), a counting sort by partition writes only a
-// permutation (s_src) and the store loop gathers through it, so the load registers are free for the next tile's
-// loads as soon as the tile is classified; the run reservations are issued before those loads (below). The
-// key-group check and key-hash loads are compiled in only when needed (KG: 0 whole range owned, 1 hash of the key,
-// 2 supplied key.hashCode()).
-// PRE (skewed keys, COUNT [+ one BIGINT SUM] layouts): equal (key, slice) records of a tile are first merged
-// in an LDS hash table -- the wavefront/workgroup hot-key reduction of Flink's local pre-aggregation
-// (LocalSlicingWindowAggOperator) -- so a Zipf head key costs one bucket entry per tile instead of one
-// per record: no sub-bucket overflow into the v1 replay, no same-address LDS atomics in the combiner.
-// Entries carry their record count (b_n) and the partial BIGINT sum in the value column.
-__device__ __noinline__ void pre_apply_global(unsigned long long* table, uint64_t mask, int seg_log, int part_bits,
-                                              unsigned long long* base, int64_t stride, int has_sum, int64_t key,
-                                              unsigned long long n, unsigned long long sum, DevStatus* st) {
-    const int64_t kid = key_slot(table, mask, seg_log, part_bits, key, st);
-    if (kid < 0) { st->key_full = 1; raise_error(st, FWA_E_OOM); return; }
-    atomicAdd(&base[kid], n);
-    if (has_sum) atomicAdd(&base[stride + kid], sum);
-}
-
-// W16: the tile's columns are read with 16-byte loads (two records per lane per column; 8-byte loads reach
-// roughly 0.6x the 16-byte rate, MI355X_MICROARCH.md): item j of a lane is record 2 * ((j / 2) * THREADS + tid) + j % 2.
-// NW: narrow bucket entries -- key and BIGINT value as two sign-extended 32-bit halves of one u64 (10 instead of 18
-// bytes per entry with the u16 slice); a record whose key or value needs 64 bits takes the v1 replay.
-template <int NV, int ITEMS, int THREADS, int VW, int KG, int PRE = 0, int W16 = 0, int NW = 0>
-__global__ void __launch_bounds__(THREADS, 1) partition3_kernel(PartArgs a, const EngineConst* __restrict__ cp) {
-    static_assert(THREADS == kMaxPart && ITEMS <= 8, "one partition cursor per thread; trash area of 8 x kMaxPart");
-    static_assert(!PRE || NV <= 1, "pre-aggregation: COUNT [+ one BIGINT sum]");
-    static_assert(!W16 || (ITEMS % 2 == 0 && KG != 2 && NV <= 1), "paired loads: even ITEMS, no key-hash column");
-    static_assert(!NW || (NV == 1 && !PRE && (VW & 1) && W16), "narrow entries: one 8-byte value column, paired loads");
-    constexpr int kTile = THREADS * ITEMS;
-    constexpr int kHt = 2 * kTile;                     // PRE: (key, slice) hash table, load <= 0.5
-    constexpr int kHtLog = __builtin_ctz(kHt);
-    const EngineConst& c = *cp;
-    __shared__ uint32_t hist[kMaxPart];
-    __shared__ uint32_t toff[kMaxPart];
-    __shared__ uint32_t gbase[kMaxPart];
-    __shared__ uint32_t sbase[kMaxPart];   // spill-list base of the tile's overflow records, per partition
-    __shared__ unsigned long long x_key[kTile];
-    // NW: x_key holds the packed entry (key | value << 32) and x_val is not used (half the staging LDS)
-    __shared__ unsigned long long x_val[NV > 0 && !NW ? NV : 1][NV > 0 && !NW ? kTile : 1];
-    __shared__ uint16_t x_rel[kTile];
-    __shared__ uint16_t s_part[kTile];
-    __shared__ uint16_t s_src[kTile];
-    __shared__ uint32_t wsum[THREADS / 64];
-    __shared__ uint32_t s_total;
-    __shared__ uint8_t s_code[kRelCap];
-    __shared__ uint32_t ht[PRE ? kHt : 1];             // PRE: 1 + staging index of the (key, slice)'s representative
-    __shared__ uint32_t x_n[PRE ? kTile : 1];          // PRE: records merged into the representative
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    unsigned dropped = 0, wide = 0;
-    uint32_t relmax = 0, relmin = ~0u;
-    const bool ds = c.sem == FWA_SEM_DATASTREAM;
-    for (int r = tid; r < kRelCap / 4; r += THREADS) ((uint32_t*)s_code)[r] = ((const uint32_t*)a.relcode)[r];
-    const int64_t ntiles = (a.n + kTile - 1) / kTile;
-    const int sub = blockIdx.x % kSub;
-    // one tile's loaded columns
-    struct Regs { unsigned long long key[ITEMS], v0[ITEMS], v1[ITEMS]; int64_t ts[ITEMS]; int32_t kh[ITEMS]; };
-    // Column pointers resolved once (uniform, SGPRs): indexing the kernel-argument array per load
-    // made hipcc fetch the pointer with a vector load and wait vmcnt(0) before every value load,
-    // serialising the tile's loads item by item.
-    const int64_t* __restrict__ pkeys = a.keys;
-    const int64_t* __restrict__ pts = a.ts;
-    const void* pc0 = NV > 0 ? a.cols[a.vcol[0]] : nullptr;
-    const void* pc1 = NV > 1 ? a.cols[a.vcol[1]] : nullptr;
-    constexpr bool w0 = (VW & 1) != 0, w1 = (VW & 2) != 0;
-    const int32_t* __restrict__ pkh = a.key_hash;
-    const int64_t n = a.n;
-    // every load of a tile is issued before any is used; uniform branches sit outside the item loops
-    // (a per-item select between a 4- and an 8-byte load made hipcc wait vmcnt(0) at every join)
-    auto xof = [&](int j) -> int { return W16 ? 2 * ((j >> 1) * THREADS + tid) + (j & 1) : j * THREADS + tid; };
-    auto load = [&](Regs& R, int64_t t) {
-        if constexpr (W16) {   // pair p = records 2p, 2p+1 of the tile; a pair reaching past n is not loaded (its
-#pragma unroll                 // record n-1, if any, goes to the slow path below)
-            for (int jj = 0; jj < ITEMS / 2; ++jj) {
-                const int64_t pi = t * (kTile / 2) + (int64_t)jj * THREADS + tid;
-                const int64_t ip = 2 * pi + 1 < n ? pi : 0;
-                const ulonglong2 kk = reinterpret_cast<const ulonglong2*>(pkeys)[ip];
-                const longlong2 tt = reinterpret_cast<const longlong2*>(pts)[ip];
-                R.key[2 * jj] = kk.x; R.key[2 * jj + 1] = kk.y;
-                R.ts[2 * jj] = tt.x; R.ts[2 * jj + 1] = tt.y;
-                if constexpr (NV > 0) {
-                    if constexpr (w0) {
-                        const ulonglong2 vv = reinterpret_cast<const ulonglong2*>(pc0)[ip];
-                        R.v0[2 * jj] = vv.x; R.v0[2 * jj + 1] = vv.y;
-                    } else {
-                        const uint2 vv = reinterpret_cast<const uint2*>(pc0)[ip];
-                        R.v0[2 * jj] = vv.x; R.v0[2 * jj + 1] = vv.y;
-                    }
-                }
-                R.kh[2 * jj] = 0; R.kh[2 * jj + 1] = 0;
-            }
-            return;
-        }
-        int64_t ic[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const int64_t i = t * kTile + (int64_t)j * THREADS + tid;
-            ic[j] = i < n ? i : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) { R.key[j] = (unsigned long long)pkeys[ic[j]]; R.ts[j] = pts[ic[j]]; }
-        if constexpr (NV > 0) {
-            if constexpr (w0) {
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j) R.v0[j] = ((const unsigned long long*)pc0)[ic[j]];
-            } else {
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j) R.v0[j] = ((const uint32_t*)pc0)[ic[j]];
-            }
-        }
-        if constexpr (NV > 1) {
-            if constexpr (w1) {
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j) R.v1[j] = ((const unsigned long long*)pc1)[ic[j]];
-            } else {
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j) R.v1[j] = ((const uint32_t*)pc1)[ic[j]];
-            }
-        }
-        if constexpr (KG == 2) {
-#pragma unroll
-            for (int j = 0; j < ITEMS; ++j) R.kh[j] = pkh[ic[j]];
-        } else {
-#pragma unroll
-            for (int j = 0; j < ITEMS; ++j) R.kh[j] = 0;
-        }
-    };
-    long long pt = clock64();
-    long long pacc[6] = {0, 0, 0, 0, 0, 0};
-#define QMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
-    Regs ra;
-    const int64_t G = gridDim.x;
-    load(ra, blockIdx.x < ntiles ? (int64_t)blockIdx.x : 0);
-    // the memory operations of one store phase, to the trash area: hipcc's waitcnt analysis merges the
-    // loop entry with the back-edge, so an entry without the stores made the header wait vmcnt(0) on
-    // every trip (draining the previous tile's stores)
-#pragma unroll
-    for (int jj = 0; jj < ITEMS; ++jj) {
-        const uint64_t o = a.trash + (uint64_t)(jj * THREADS + tid);   // distinct: not merged by the compiler
-        a.b_key[o] = 0ull;
-        a.b_rel[o] = 0;
-        if constexpr (PRE) a.b_n[o] = 0;
-        if (NV > 0 && !NW) a.b_val0[o] = 0ull;
-        if (NV > 1) a.b_val1[o] = 0ull;
-    }
-    // one tile: classify R, scan, reserve, issue the loads of tile `nx` into R, scatter, store
-    auto step = [&](Regs& R, int64_t tile, int64_t nx) {
-        for (int i = tid; i < a.np; i += THREADS) hist[i] = 0;
-        if constexpr (PRE) for (int i = tid; i < kHt / 4; i += THREADS) ((uint4*)ht)[i] = make_uint4(0u, 0u, 0u, 0u);
-        __syncthreads();
-        QMARK(5);
-        const int64_t t0 = tile * kTile;
-        uint32_t r_pos[ITEMS];   // (p << 16 | rank) or ~0u when the record does not go to a bucket
-        // wait for the whole tile HERE, on every path: a loaded register consumed only on some paths (the
-        // value, staged for accepted records only) stays "pending" in hipcc's waitcnt analysis, and the
-        // next reuse of that register then waited vmcnt(0) -- draining the stores and the prefetch
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            consume(R.key[j]);
-            consume(R.ts[j]);
-            if constexpr (NV > 0) consume(R.v0[j]);
-            if constexpr (NV > 1) consume(R.v1[j]);
-            if constexpr (KG == 2) consume(R.kh[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const int64_t i = t0 + xof(j);
-            const int64_t key = (int64_t)R.key[j];
-            const int64_t ts = R.ts[j];
-            // slice relative to q_base: a timestamp within kRelCap slices of the base takes a 32-bit division
-            // (one 32 x 33-bit multiply); anything else (and shift time zones) the exact 64-bit floor division
-            uint64_t rel;
-            const uint64_t dd = (uint64_t)ts - (uint64_t)a.base_ts;
-            if (a.fast_m && dd < a.fast_lim) {
-                rel = (dd * a.fast_m) >> a.fast_sh;
-            } else {
-                const int64_t d = jm::wsub(PRE && a.pcount ? ts : assign_ts(c, ts), c.off);
-                const uint64_t ud = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
-                const uint64_t uq = jm::udiv64(ud, c.g_div);
-                const int64_t q = d >= 0 ? (int64_t)uq : ((uq * c.g_div.d == ud) ? -(int64_t)uq : -(int64_t)uq - 1);
-                rel = (uint64_t)(q - a.q_base);
-            }
-            uint32_t code = rel < (uint64_t)kRelCap ? s_code[rel] : kCodeSlow;
-            if constexpr (KG != 0) {
-                const int32_t kg = jm::key_group_of(key, c.key_kind, R.kh[j], c.max_par);
-                if (kg < c.kg_lo || kg > c.kg_hi) code = kCodeSlow;
-            }
-            if (ds && ts == LONG_MIN_J) code = kCodeSlow;
-            if (a.any_null && i < a.n && row_has_null(a, i)) code = kCodeSlow;   // SQL NULLs: the v1 path
-            if ((uint64_t)key == kEmptyKey) code = kCodeSlow;
-            if (W16 && i == a.n - 1 && (a.n & 1)) code = kCodeSlow;     // unpaired last record: the v1 replay
-            uint32_t rn = 1;                                          // records this row stands for
-            if constexpr (PRE) {
-                if (a.pcount && i < a.n) {
-                    const unsigned long long pc = a.pcount[i];
-                    rn = (uint32_t)pc;
-                    if (pc == 0 || pc > 0xFFFFull) code = kCodeSlow;  // does not fit a bucket's u16 count
-                }
-            }
-            if constexpr (NW) {   // (INT32_MIN and INT32_MIN + 1 are the narrow combiner's LDS markers: v1 path too)
-                if (code == kCodeAccept && ((int64_t)(int32_t)key != key || (uint32_t)key - 0x80000000u <= 1u ||
-                                            (int64_t)(int32_t)R.v0[j] != (int64_t)R.v0[j])) {
-                    code = kCodeSlow;
-                    ++wide;
-                }
-            }
-            if (i >= a.n) code = 0xff;
-            dropped += code == kCodeDrop ? rn : 0u;
-            note_drop(a.dropidx, a.st, code == kCodeDrop, i);
-            const bool slow = code == kCodeSlow;
-            const unsigned long long mk = __ballot(slow);
-            if (mk) {
-                const int leader = __ffsll((long long)mk) - 1;
-                int32_t sb = 0;
-                if (lane == leader) sb = atomicAdd(&a.st->spill_n, __popcll(mk));
-                sb = __shfl(sb, leader);
-                if (slow) put_idx(a.spill, sb + __popcll(mk & ((1ull << lane) - 1)), a.spill_cap, (int32_t)i, a.st);
-            }
-            r_pos[j] = ~0u;
-            if (code == kCodeAccept) {
-                relmax = max(relmax, (uint32_t)rel);
-                relmin = min(relmin, (uint32_t)rel);
-                const uint64_t h = jm::mix64((uint64_t)key);
-                const uint32_t p = a.part_bits ? (uint32_t)(h >> (64 - a.part_bits)) : 0u;
-                const int x = xof(j);
-                x_key[x] = R.key[j];
-                x_rel[x] = (uint16_t)rel;
-                if constexpr (NW) x_key[x] = (R.key[j] & 0xffffffffull) | (R.v0[j] << 32);
-                else if (NV > 0) x_val[0][x] = R.v0[j];
-                if (NV > 1) x_val[NV > 1 ? 1 : 0][x] = R.v1[j];
-                if constexpr (PRE) {
-                    x_n[x] = rn;
-                    r_pos[j] = a.pcount ? ((p << 16) | atomicAdd(&hist[p], 1u))   // partial rows: no merge
-                                        : (0x80000000u | p);                        // bucketed after the merge
-                }
-                else r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
-            }
-        }
-        if constexpr (PRE) {
-            __syncthreads();                        // the tile's staged (key, rel) visible to every lane
-#pragma unroll
-            for (int j = 0; j < ITEMS; ++j) {
-                if (r_pos[j] == ~0u || !(r_pos[j] & 0x80000000u)) continue;
-                const uint32_t x = (uint32_t)xof(j);
-                const unsigned long long key = R.key[j];
-                const uint32_t rel = x_rel[x];
-                uint32_t hs = ((uint32_t)key * 0x9E3779B1u + (uint32_t)(key >> 32) * 0x85EBCA77u + rel * 0xC2B2AE3Du) >> (32 - kHtLog);
-                for (int probe = 0; probe < kHt; ++probe) {
-                    const uint32_t old = atomicCAS(&ht[hs], 0u, x + 1u);
-                    if (old == 0u) {                // representative of its (key, slice) in this tile
-                        const uint32_t p = r_pos[j] & 0xffffu;
-                        r_pos[j] = (p << 16) | atomicAdd(&hist[p], 1u);
-                        break;
-                    }
-                    const uint32_t o = old - 1u;
-                    if (x_key[o] == key && x_rel[o] == rel) {   // merge into the representative
-                        atomicAdd(&x_n[o], 1u);
-                        if constexpr (NV > 0) atomicAdd(&x_val[0][o], R.v0[j]);
-                        r_pos[j] = ~0u;
-                        break;
-                    }
-                    hs = (hs + 1u) & (kHt - 1);
-                }
-            }
-        }
-        QMARK(0);
-        __syncthreads();
-        block_scan_np<THREADS>(hist, toff, wsum, a.np, &s_total);
-        __syncthreads();
-        QMARK(1);
-        // the run reservations (returning atomics) are issued BEFORE the next tile's loads: vmcnt retires
-        // in order, so waiting for the reservations does not drain the prefetch
-        const int p = tid;
-        const uint32_t h = p < a.np ? hist[p] : 0u;
-        const uint32_t g = h ? atomicAdd(&a.b_cnt[p * kSub + sub], h) : 0u;
-        load(R, nx < ntiles ? nx : tile);               // the next tile in flight from here on (unconditional)
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {               // the LDS scatter does not need the reservation: the
-            if (r_pos[j] == ~0u) continue;              // reservation's latency overlaps this loop
-            const uint32_t p = r_pos[j] >> 16;
-            const uint32_t sidx = toff[p] + (r_pos[j] & 0xffffu);
-            s_part[sidx] = (uint16_t)p;
-            s_src[sidx] = (uint16_t)xof(j);
-        }
-        if (p < a.np) {
-            gbase[p] = g;
-            // records past the sub-bucket's end (skewed keys) go to the v1 replay: one spill reservation
-            // per (tile, overflowing partition) -- a per-wave reservation on the single spill counter
-            // serialised ~100 K same-address device atomics per push under Zipf(1.1)
-            const uint64_t end = (uint64_t)g + h;
-            if (end > (uint64_t)a.capb) {
-                const uint32_t ov = (uint32_t)(end - std::max<uint64_t>(g, (uint64_t)a.capb));
-                atomicAdd(&a.st->ovf_n, (int32_t)ov);
-                if constexpr (!PRE) sbase[p] = (uint32_t)atomicAdd(&a.st->spill_n, (int32_t)ov);
-            }
-        }
-        __syncthreads();
-        QMARK(2);
-        const uint32_t total = s_total;
-        // fixed trip count, every store issued (lanes without a record write the trash area): the next
-        // classify then waits for its loads with an exact vmcnt instead of draining these stores
-#pragma unroll
-        for (int jj = 0; jj < ITEMS; ++jj) {
-            const uint32_t sidx = (uint32_t)(jj * THREADS + tid);
-            const bool valid = sidx < total;
-            const uint32_t p = valid ? s_part[sidx] : 0u;
-            const uint32_t x = valid ? s_src[sidx] : 0u;
-            const uint64_t dst = (uint64_t)gbase[p] + (sidx - toff[p]);
-            const bool inb = valid && dst < (uint64_t)a.capb;
-            if (valid && !inb) {                // sub-bucket full (skewed keys)
-                if constexpr (PRE) {            // a merged entry has no record index to replay: apply it now
-                    const int32_t slot = a.rel2slot[x_rel[x]];
-                    if (slot >= 0)
-                        pre_apply_global(a.key_table, a.key_mask, a.seg_log, a.part_bits, a.slot_base[slot], a.stride,
-                                         NV, (int64_t)x_key[x], x_n[x], NV > 0 ? x_val[0][x] : 0ull, a.st);
-                } else {                        // the v1 replay takes it
-                    const uint64_t first = std::max<uint64_t>(gbase[p], (uint64_t)a.capb);
-                    put_idx(a.spill, (int64_t)sbase[p] + (int64_t)(dst - first), a.spill_cap, (int32_t)(t0 + x), a.st);
-                }
-            }
-            const uint64_t o = !inb ? a.trash + (uint64_t)(jj * THREADS + tid)
-                                    : ((uint64_t)p * kSub + sub) * (uint64_t)a.capb + dst;
-            a.b_key[o] = x_key[x];              // NW: packed at staging
-            a.b_rel[o] = x_rel[x];
-            if constexpr (PRE) a.b_n[o] = (uint16_t)x_n[x];
-            if (NV > 0 && !NW) a.b_val0[o] = x_val[0][x];
-            if (NV > 1) a.b_val1[o] = x_val[NV > 1 ? 1 : 0][x];
-        }
-        QMARK(3);
-        __syncthreads();
-        QMARK(4);
-    };
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) step(ra, tile, tile + G);
-    if (a.prof && tid == 0) for (int q = 0; q < 6; ++q) a.prof[(int64_t)blockIdx.x * 8 + q] = pacc[q];
-#undef QMARK
-    for (int sh = 32; sh >= 1; sh >>= 1) {
-        dropped += __shfl_xor(dropped, sh);
-        if constexpr (NW) wide += __shfl_xor(wide, sh);
-        relmax = max(relmax, (uint32_t)__shfl_xor((int)relmax, sh));
-        relmin = min(relmin, (uint32_t)__shfl_xor((int)relmin, sh));
-    }
-    if (lane == 0) {
-        if (dropped) atomicAdd(&a.st->dropped, (unsigned long long)dropped);
-        if (NW && wide) atomicAdd(&a.st->wide_n, (int32_t)wide);
-        if (relmin != ~0u) {
-            atomicMax(&a.st->max_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmax));
-            atomicMin(&a.st->min_q, (unsigned long long)jm::ord_i64(a.q_base + (int64_t)relmin));
-        }
-    }
-    if (relmin != ~0u)
-        for (uint32_t r = relmin + (uint32_t)lane; r <= relmax; r += 64) {
-            const int32_t slot = a.rel2slot[r];
-            if (slot >= 0 && a.touched[slot] == 0) a.touched[slot] = 1;
-        }
-}
-
-struct CombineArgs {
-    const unsigned long long* b_key;
-    const unsigned long long* b_val0;
-    const unsigned long long* b_val1;
-    const uint16_t* b_rel;
-    const uint16_t* b_n;               // PRE buckets: records per entry (nullptr: one each)
-    const uint32_t* b_cnt;
-    int64_t capb;
-    int32_t seg_log, np, sl;           // sl: LDS slice window
-    const int32_t* rel2slot;           // [kRelCap]
-    unsigned long long* key_table;
-    unsigned long long* const* slot_base;
-    int64_t stride;
-    DevStatus* st;
-    long long* prof;                   // optional per-block phase cycle counters (FWA_OPT_PROFILE)
-};
-
-__device__ __forceinline__ unsigned long long ident_of(int acc_kind) { return acc_kind == ACC_MIN_ORD ? ~0ull : 0ull; }
-
-__device__ __forceinline__ unsigned long long carried_ord(unsigned long long raw, int kind) {
-    switch (kind) {
-        case FWA_MIN_I64: case FWA_MAX_I64: return jm::ord_i64((int64_t)raw);
-        case FWA_MIN_F32: case FWA_MAX_F32:
-            return jm::ord_bits64((uint64_t)__double_as_longlong((double)__uint_as_float((uint32_t)raw)));
-        default: return jm::ord_bits64(raw);
-    }
-}
-
-__device__ __forceinline__ double carried_f64(unsigned long long raw, int kind) {
-    return (kind == FWA_SUM_F32 || kind == FWA_AVG_F32) ? (double)__uint_as_float((uint32_t)raw)
-                                                         : __longlong_as_double((long long)raw);
-}
-
-// Apply one combiner entry (slice rel, global kid g, n records, carried values) to its slice's HBM
-// accumulators with device atomics (stragglers: their slice was already merged by this block).
-__device__ __forceinline__ void strag_apply(const CombineArgs& a, const EngineConst& c, int rel, uint32_t g, uint32_t n,
-                                            unsigned long long x0, unsigned long long x1) {
-    const int32_t slot = a.rel2slot[rel];
-    if (slot < 0) return;
-    unsigned long long* base = a.slot_base[slot];
-    atomicAdd(&base[g], (unsigned long long)n);
-    for (int jj = 0; jj < c.naggs; ++jj) {
-        const AggDesc d = c.agg[jj];
-        if (d.acc == 0 || d.alias) continue;
-        const unsigned long long raw = d.kind == FWA_COUNT_COL ? (unsigned long long)n : d.vslot == 0 ? x0 : x1;
-        unsigned long long* gp = base + (int64_t)d.acc * a.stride + g;
-        switch (d.acc_kind) {
-            case ACC_ADD_I64: atomicAdd(gp, raw); break;
-            case ACC_ADD_F64: atomicAdd((double*)gp, carried_f64(raw, d.kind)); break;
-            case ACC_MIN_ORD: atomicMin(gp, carried_ord(raw, d.kind)); break;
-            case ACC_MAX_ORD: atomicMax(gp, carried_ord(raw, d.kind)); break;
-            default: break;
-        }
-    }
-}
-
-// Stragglers of one combiner block, kept in LDS and applied after the block's last merge.
-constexpr int kStragL = 256;
-struct StragL {
-    uint32_t g, n;
-    int32_t rel, pad;
-    unsigned long long x0, x1;
-};
-
-// ------------------------------------------------------------------------------------------------
-// combine3: the Phase A combiner, restructured for latency tolerance (DESIGN.md §4, r01 clock64
-// profile: the v2 combiner spent 43 % of its time in serialised flat RMWs / scalar-load waits).
-//  * wave w streams sub-bucket w (64 lanes, coalesced); the next chunk's loads are issued before the
-//    current chunk is combined (register double buffer);
-//  * ONE barrier per chunk: each wave publishes its chunk's slice range into a double-buffered LDS
-//    slot, the block range is read back after the barrier (no LDS atomics, no second barrier);
-//  * aggregate descriptors are hoisted into registers once; the inner loop has no scalar loads;
-//  * the slice flush reads LDS into registers, then issues every HBM load of the flush before any
-//    add/store (one exposed latency per flush instead of one per slot and column), through
-//    address-space-1 pointers (global_load/store, not flat).
-typedef __attribute__((address_space(1))) unsigned long long g_u64;
-typedef const __attribute__((address_space(1))) unsigned long long* gc_u64_ptr;
-
-// LAYOUT: the accumulator columns, fixed at compile time for the common shapes so the per-record
-// path has no descriptor switch (a runtime switch over 8 columns cost ~1000 scalar instructions per
-// record from SGPR spills): 1 = COUNT + one ADD_I64 fed by value slot 0 (SUM/AVG over BIGINT);
-// 2 = COUNT only; 0 = generic (descriptor table in LDS, one column per loop trip).
-// MP: window passes (below) for chunks spanning more slices than the window; chosen per handle once a push
-// saw many stragglers (small HOP/CUMULATE slices), since the passes cost registers the common case needs.
-template <int IT, int SL, int NV, int TH, int LAYOUT, int PRE = 0, int MP = 0, int NW = 0>
-__global__ void __launch_bounds__(TH, 1) combine3_kernel(CombineArgs a, const EngineConst* __restrict__ cp) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int kWaves = TH / 64;
-    constexpr int LPS = TH / kSub;     // lanes per sub-bucket (64: one wave per sub; 32: two subs per wave)
-    static_assert(LPS == 32 || LPS == 64, "sub-bucket lane mapping");
-    const EngineConst& c = *cp;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int sub = tid / LPS, li = tid % LPS;
-    const int p = blockIdx.x;
-    const int seg = 1 << a.seg_log;
-    const uint32_t smask = (uint32_t)seg - 1u;
-    const int nacc = LAYOUT == 1 ? 2 : (LAYOUT == 2 ? 1 : c.nacc);
-    __shared__ int s_desc[kMaxAggsInt + 1];   // generic layout: per column kind | vslot << 8 | input kind << 16
-    __shared__ StragL s_strag[kStragL];
-    __shared__ int s_sn;
-    if (LAYOUT == 0 && tid == 0) {
-        for (int j = 0; j < c.naggs; ++j)
-            if (c.agg[j].acc > 0 && !c.agg[j].alias) s_desc[c.agg[j].acc] = c.agg[j].acc_kind | (c.agg[j].vslot << 8) | (c.agg[j].kind << 16);
-    }
-    unsigned long long* lkey = (unsigned long long*)smem;
-    uint32_t* lcnt = (uint32_t*)(smem + (size_t)seg * 8);
-    unsigned long long* lacc = (unsigned long long*)(smem + (size_t)seg * 8 + (size_t)SL * seg * 4);
-    int* s_mm = (int*)(smem + (size_t)seg * 8 + (size_t)SL * seg * 4 + (size_t)(nacc - 1) * SL * seg * 8);
-    // s_mm: [2][kWaves] mins, [2][kWaves] maxs, s_new
-    int* s_min = s_mm;
-    int* s_max = s_mm + 2 * kWaves;
-    int* s_new = s_mm + 4 * kWaves;
-    long long pt = clock64();
-    long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define PMARK(k) do { if (a.prof) { const long long _t = clock64(); pacc[k] += _t - pt; pt = _t; } } while (0)
-    unsigned long long* gkeys = a.key_table + ((int64_t)p << a.seg_log);
-    for (int i = tid; i < seg; i += TH) lkey[i] = gkeys[i];
-    for (int i = tid; i < SL * seg; i += TH) {
-        lcnt[i] = 0;
-    }
-    if (tid == 0) { *s_new = 0; s_sn = 0; }
-    __syncthreads();
-    for (int cc = 1; cc < nacc; ++cc) {
-        const unsigned long long id = LAYOUT == 1 ? 0ull : ident_of(s_desc[cc] & 0xff);
-        for (int i = tid; i < SL * seg; i += TH) lacc[(size_t)(cc - 1) * SL * seg + i] = id;
-    }
-    constexpr int64_t kChunk = (int64_t)IT * LPS;
-    // sub-buckets: this wave's own list
-    const int64_t my_cnt = min((int64_t)a.b_cnt[p * kSub + sub], a.capb);
-    const int64_t boff = ((int64_t)p * kSub + sub) * a.capb;
-    int64_t cnt = 0;
-    for (int s2 = 0; s2 < kSub; ++s2) cnt = max(cnt, min((int64_t)a.b_cnt[p * kSub + s2], a.capb));
-    const gc_u64_ptr bk = (const gc_u64_ptr)(a.b_key + boff);
-    const gc_u64_ptr bv0 = a.b_val0 ? (const gc_u64_ptr)(a.b_val0 + boff) : nullptr;
-    const gc_u64_ptr bv1 = a.b_val1 ? (const gc_u64_ptr)(a.b_val1 + boff) : nullptr;
-    const __attribute__((address_space(1))) uint16_t* br = (const __attribute__((address_space(1))) uint16_t*)(a.b_rel + boff);
-    const __attribute__((address_space(1))) uint16_t* bn = PRE ? (const __attribute__((address_space(1))) uint16_t*)(a.b_n + boff) : nullptr;
-    int lo = 0x7fffffff;
-    auto flush = [&](int rel) {   // merge window slice `rel` into HBM; every thread owns seg/TH slots
-        constexpr int kPer = 4096 / TH;   // seg <= 4096
-        const int w = rel & (SL - 1);
-        const int32_t slot = (rel >= 0 && rel < kRelCap) ? a.rel2slot[rel] : -1;
-        g_u64* base = slot >= 0 ? (g_u64*)a.slot_base[slot] : nullptr;
-        uint32_t k[kPer];
-        int64_t g[kPer];
-#pragma unroll
-        for (int m = 0; m < kPer; ++m) {
-            const int i = tid + m * TH;
-            k[m] = 0;
-            g[m] = ((int64_t)p << a.seg_log) + i;
-            if (i < seg) { k[m] = lcnt[w * seg + i]; lcnt[w * seg + i] = 0; }
-        }
-        if (base) {
-            unsigned long long old[kPer];
-#pragma unroll
-            for (int m = 0; m < kPer; ++m) old[m] = k[m] ? base[g[m]] : 0ull;
-#pragma unroll
-            for (int m = 0; m < kPer; ++m) if (k[m]) base[g[m]] = old[m] + k[m];
-        }
-        for (int cc = 1; cc < nacc; ++cc) {
-            const int akc = LAYOUT == 1 ? ACC_ADD_I64 : (s_desc[cc] & 0xff);
-            unsigned long long x[kPer], old[kPer];
-            const unsigned long long id = ident_of(akc);
-#pragma unroll
-            for (int m = 0; m < kPer; ++m) {
-                const int i = tid + m * TH;
-                x[m] = id;
-                if (k[m]) {
-                    unsigned long long* lp = &lacc[(size_t)(cc - 1) * SL * seg + (size_t)w * seg + i];
-                    x[m] = *lp;
-                    *lp = id;
-                }
-            }
-            if (!base) continue;
-            g_u64* col = base + (int64_t)cc * a.stride;
-#pragma unroll
-            for (int m = 0; m < kPer; ++m) old[m] = k[m] ? col[g[m]] : 0ull;
-#pragma unroll
-            for (int m = 0; m < kPer; ++m) {
-                if (!k[m]) continue;
-                unsigned long long r = old[m];
-                switch (akc) {
-                    case ACC_ADD_I64: r = old[m] + x[m]; break;
-                    case ACC_ADD_F64: r = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)old[m]) + __longlong_as_double((long long)x[m])); break;
-                    case ACC_MIN_ORD: r = x[m] < old[m] ? x[m] : old[m]; break;
-                    case ACC_MAX_ORD: r = x[m] > old[m] ? x[m] : old[m]; break;
-                    default: break;
-                }
-                col[g[m]] = r;
-            }
-        }
-    };
-    __syncthreads();
-    // register double buffer: n* = chunk in flight, c* = chunk being combined
-    unsigned long long nkey[IT], nx0[IT], nx1[IT];
-    int nrel[IT];
-    uint32_t nnn[IT];                   // PRE: records per entry
-    auto load_chunk = [&](int64_t cb) {
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            const int64_t i = cb + (int64_t)j * LPS + li;
-            const bool ok = i < my_cnt;
-            int r;
-            if constexpr (NW) {                             // narrow entry (key | value << 32), unpacked at use
-                nkey[j] = ok ? bk[i] : 0ull;
-                r = ok ? (int)br[i] : -1;
-            } else {
-                nkey[j] = ok ? bk[i] : 0ull;
-                nx0[j] = (NV > 0 && ok) ? bv0[i] : 0ull;
-                r = ok ? (int)br[i] : -1;
-            }
-            nx1[j] = (NV > 1 && ok) ? bv1[i] : 0ull;
-            nrel[j] = r;
-            nnn[j] = PRE ? (ok ? (uint32_t)bn[i] : 0u) : 1u;
-        }
-    };
-    load_chunk(0);
-    PMARK(0);
-    int it = 0;
-    for (int64_t cb = 0; cb < cnt; cb += kChunk, ++it) {
-        unsigned long long key[IT], x0[IT], x1[IT];
-        int rel[IT];
-        uint32_t nr[IT];
-        int rmin = 0x7fffffff, rmax = -1;
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            if constexpr (NW) {
-                key[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)nkey[j];
-                x0[j] = (unsigned long long)(int64_t)(int32_t)(uint32_t)(nkey[j] >> 32);
-            } else {
-                key[j] = nkey[j]; x0[j] = nx0[j];
-            }
-            x1[j] = nx1[j]; rel[j] = nrel[j]; nr[j] = nnn[j];
-            if (rel[j] >= 0) { rmin = min(rmin, rel[j]); rmax = max(rmax, rel[j]); }
-        }
-        PMARK(1);
-        if (cb + kChunk < cnt) load_chunk(cb + kChunk);
-        for (int sh = 32; sh >= 1; sh >>= 1) { rmin = min(rmin, __shfl_xor(rmin, sh)); rmax = max(rmax, __shfl_xor(rmax, sh)); }
-        const int buf = it & 1;
-        if (lane == 0) { s_min[buf * kWaves + wv] = rmin; s_max[buf * kWaves + wv] = rmax; }
-        // first probes in flight across the barrier
-        uint32_t pos[IT];
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            pos[j] = (uint32_t)jm::mix64(key[j]) & smask;
-        }
-        PMARK(2);
-        __syncthreads();
-        PMARK(3);
-        int cmin = 0x7fffffff, cmax = -1;
-#pragma unroll
-        for (int v = 0; v < kWaves; ++v) { cmin = min(cmin, s_min[buf * kWaves + v]); cmax = max(cmax, s_max[buf * kWaves + v]); }
-        if (cmax < 0) continue;
-        if (lo == 0x7fffffff) lo = cmin;
-        if constexpr (MP) {
-            if (cmin >= lo + SL) {          // the whole chunk is past the window: merge it out, jump to cmin
-                for (int r = lo; r < lo + SL; ++r) flush(r);
-                if (a.prof) pacc[7] += 1000;
-                lo = cmin;
-                __syncthreads();
-            }
-        } else if (cmax >= lo + SL) {       // slide the window up to the chunk's newest slice
-            while (cmax >= lo + SL) { flush(lo); ++lo; if (a.prof) pacc[7] += 1000; }
-            __syncthreads();
-        }
-        const int lo_c = lo;                // entries older than this are stragglers
-        PMARK(4);
-        if (a.prof) pacc[7] += 1;
-        // bucket probing: read the key's 8-slot home bucket (4 x ds_read_b128), compare all 8; only
-        // keys displaced past their bucket (a few %) take another round
-        int32_t loc[IT];
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            loc[j] = -2;
-            if (rel[j] < 0) continue;
-            const unsigned long long kk = key[j];
-            uint32_t b = pos[j] & ~(uint32_t)(kBucket - 1);
-            int32_t found = -1;
-            for (int round = 0; round <= (seg >> 3) && found < 0; ++round) {
-                const ulonglong2* bp = (const ulonglong2*)&lkey[b];
-                const ulonglong2 q0 = bp[0], q1 = bp[1], q2 = bp[2], q3 = bp[3];
-                const unsigned long long v[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
-                uint32_t eq = 0, em = 0;
-#pragma unroll
-                for (int t = 0; t < 8; ++t) { eq |= (uint32_t)(v[t] == kk) << t; em |= (uint32_t)(v[t] == kEmptyKey) << t; }
-                if (eq) { found = (int32_t)(b + __builtin_ctz(eq)); break; }
-                if (em) {                       // absent: insert at the first empty slot (CAS vs other lanes)
-                    const uint32_t sidx = b + __builtin_ctz(em);
-                    const unsigned long long old = atomicCAS(&lkey[sidx], kEmptyKey, kk);
-                    if (old == kEmptyKey) { found = (int32_t)sidx; atomicAdd(s_new, 1); break; }
-                    if (old == kk) { found = (int32_t)sidx; break; }
-                    continue;                   // lost the slot to another key: re-read this bucket
-                }
-                b = (b + kBucket) & smask;
-            }
-            loc[j] = found;
-        }
-        // window passes (MP): a chunk can span more slices than the LDS window holds (HOP/CUMULATE 1 s slices:
-        // a sub-bucket's 256-entry chunk covers seconds of event time); its entries stay in registers and are
-        // added window by window, merging out between passes only the slices the next pass needs (the window
-        // ends at the chunk's newest slice, so the next chunk's older entries still find it)
-        int from = lo_c;                    // entries below this were added by an earlier pass (or straggle)
-        for (int pass = 0;; ++pass) {
-#pragma unroll
-            for (int j = 0; j < IT; ++j) {
-                if (rel[j] < 0 || rel[j] >= lo + SL) continue;
-                const int32_t local = loc[j];
-                if (local < 0) { if (pass == 0) { a.st->key_full = 1; raise_error(a.st, FWA_E_OOM); } continue; }
-                if (rel[j] < from) {
-                    if (pass > 0) continue;     // added in an earlier pass
-                    // older than the window (its slice is already merged into HBM): listed in LDS and applied
-                    // with device atomics after the last merge (this block owns the kid; a list shared by all
-                    // blocks serialised them on one counter)
-                    if (a.prof) pacc[6] += 1000000;
-                    const uint32_t g = (uint32_t)(((int64_t)p << a.seg_log) + local);
-                    const int si = atomicAdd(&s_sn, 1);
-                    if (si < kStragL) s_strag[si] = StragL{g, PRE ? nr[j] : 1u, rel[j], 0, x0[j], x1[j]};
-                    else strag_apply(a, c, rel[j], g, PRE ? nr[j] : 1u, x0[j], x1[j]);
-                    continue;
-                }
-                const int w = rel[j] & (SL - 1);
-                atomicAdd(&lcnt[w * seg + local], PRE ? nr[j] : 1u);
-                if constexpr (LAYOUT == 1) {
-                    atomicAdd(&lacc[(size_t)w * seg + local], x0[j]);
-                } else if constexpr (LAYOUT == 0) {
-                    for (int cc = 1; cc < nacc; ++cc) {
-                        const int d = s_desc[cc];
-                        unsigned long long* lp = &lacc[(size_t)(cc - 1) * SL * seg + (size_t)w * seg + local];
-                        const int ik = d >> 16;
-                        const unsigned long long raw = ik == FWA_COUNT_COL ? 1ull   // non-NULL counter (NULL rows take the v1 path)
-                                                     : (NV > 1 && ((d >> 8) & 0xff) != 0) ? x1[j] : x0[j];
-                        switch (d & 0xff) {
-                            case ACC_ADD_I64: atomicAdd(lp, raw); break;
-                            case ACC_ADD_F64: atomicAdd((double*)lp, carried_f64(raw, ik)); break;
-                            case ACC_MIN_ORD: atomicMin(lp, carried_ord(raw, ik)); break;
-                            case ACC_MAX_ORD: atomicMax(lp, carried_ord(raw, ik)); break;
-                            default: break;
-                        }
-                    }
-                }
-            }
-            if (!MP || cmax < lo + SL) break;
-            __syncthreads();                // the window's adds done before it is merged out
-            from = lo + SL;
-            const int nl = min(lo + SL, cmax - SL + 1);
-            while (lo < nl) { flush(lo); ++lo; if (a.prof) pacc[7] += 1000; }
-            __syncthreads();                // merged and cleared before the next pass adds
-        }
-        PMARK(5);
-    }
-    __syncthreads();
-    if (lo != 0x7fffffff)
-        for (int r = lo; r < lo + SL; ++r) flush(r);
-    __syncthreads();                    // every merge of this block stored before the stragglers' atomics
-    if (tid == 0 && s_sn) atomicAdd(&a.st->strag_n, s_sn);
-    for (int t = tid; t < min(s_sn, kStragL); t += TH) {
-        const StragL se = s_strag[t];
-        strag_apply(a, c, se.rel, se.g, se.n, se.x0, se.x1);
-    }
-    if (*s_new) {                       // publish newly inserted keys (exclusive owner of this segment)
-        for (int i = tid; i < seg; i += TH) gkeys[i] = lkey[i];
-        if (tid == 0) atomicAdd(&a.st->n_keys, (unsigned long long)*s_new);
-    }
-    if (a.prof && tid == 0) for (int q = 0; q < 8; ++q) a.prof[(int64_t)p * 8 + q] = pacc[q];
-#undef PMARK
-}
+#include "ingest.inc"
 
 
 // ------------------------------------------------------------------------------------------------
@@ -4088,7 +2886,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
 #define P3LAUNCH(NV, IT, VW) do { \
         if (kgm == 0) partition3_kernel<NV, IT, 1024, VW, 0><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else if (kgm == 1) partition3_kernel<NV, IT, 1024, VW, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
-        else partition3_kernel<NV, IT, 1024, VW, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
+        else partition3_kernel<NV, IT - 2, 1024, VW, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
+    // (supplied key hashes: one column more per tile, two items fewer per lane keep the kernel free of VGPR spills)
 #define PRELAUNCH(NV) do { const int gp = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + 4095) / 4096, 256)); \
         if (kgm == 0) partition3_kernel<NV, 4, 1024, 3, 0, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); \
         else if (kgm == 1) partition3_kernel<NV, 4, 1024, 3, 1, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); \
@@ -4132,23 +2931,43 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     HIPCHK(e, hipEventRecord(e->ev[6], e->stream));
     const size_t seg3 = (size_t)1 << e->seg_log;
     const size_t lds3 = seg3 * 8 + 2 * seg3 * 4 + (size_t)(e->nacc - 1) * 2 * seg3 * 8 + 4 * 4 * kSub + 16;
-    // window passes: 2 entries per lane and chunk -- the passes' extra live state at 4 entries spilled up to 250 B per
-    // lane to scratch (1024-thread blocks cap a lane at 128 VGPRs), and that build merged wrong counts (r04: the
-    // window-pass parity failures); at 2 the spills are a few words
-#define C3M(IT, TH, NV, LY, PR) do { if (mp) combine3_kernel<2, 2, NV, TH, LY, PR, 1><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); \
-        else combine3_kernel<IT, 2, NV, TH, LY, PR, 0><<<e->np, TH, lds3, e->stream>>>(ca, e->d_ec); } while (0)
-#define C3L(IT, TH, NV) do { \
-        if (pre && layout == 1) C3M(IT, TH, 1, 1, 1); \
-        else if (pre) C3M(IT, TH, 0, 2, 1); \
-        else if (layout == 1) C3M(IT, TH, NV, 1, 0); \
-        else if (layout == 2) C3M(IT, TH, NV, 2, 0); \
-        else C3M(IT, TH, NV, 0, 0); } while (0)
-    if (narrow) {   // packed entries free the prefetch registers: 8 entries per lane and chunk (4 with window passes)
-        if (mp) combine3_kernel<2, 2, 1, 1024, 1, 0, 1, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-        else combine3_kernel<8, 2, 1, 1024, 1, 0, 0, 1><<<e->np, 1024, lds3, e->stream>>>(ca, e->d_ec);
-    } else if (e->nv == 0) C3L(4, 1024, 0);
-    else if (e->nv == 1) C3L(4, 1024, 1);
-    else C3L(4, 1024, 2);
+    // entries per lane and chunk: the largest counts whose kernels keep every value in registers at 1024 threads (a VGPR
+    // spill is not harmless here, DESIGN.md section 4 "Skewed keys"; tests/test_abi.py checks the code object): 4, 3 with
+    // two carried value columns, 6 for narrow entries, 2 with window passes. 512-thread blocks with twice the entries are
+    // spill-free too but slower (r05 A/B, profiles/r05_combine_geometry_ab.txt). -D switches for A/B builds only.
+#ifndef FWA_C3_TH
+#define FWA_C3_TH 1024
+#endif
+#ifndef FWA_C3_IT0
+#define FWA_C3_IT0 4
+#endif
+#ifndef FWA_C3_IT1
+#define FWA_C3_IT1 4
+#endif
+#ifndef FWA_C3_IT2
+#define FWA_C3_IT2 3
+#endif
+#ifndef FWA_C3_NIT
+#define FWA_C3_NIT 6
+#endif
+#ifndef FWA_MP_IT
+#define FWA_MP_IT 2
+#endif
+    constexpr int TH3 = FWA_C3_TH;
+#define C3M(IT, NV, LY, PR) do { if (mp) combine3_kernel<FWA_MP_IT, 2, NV, TH3, LY, PR, 1><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec); \
+        else combine3_kernel<IT, 2, NV, TH3, LY, PR, 0><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec); } while (0)
+#define C3L(IT, NV) do { \
+        if (pre && layout == 1) C3M(IT, 1, 1, 1); \
+        else if (pre) C3M(IT, 0, 2, 1); \
+        else if (layout == 1) C3M(IT, NV, 1, 0); \
+        else if (layout == 2) C3M(IT, NV, 2, 0); \
+        else C3M(IT, NV, 0, 0); } while (0)
+    if (narrow) {   // packed entries free the prefetch registers: more entries per lane and chunk
+        if (mp) combine3_kernel<FWA_MP_IT, 2, 1, TH3, 1, 0, 1, 1><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec);
+        else combine3_kernel<FWA_C3_NIT, 2, 1, TH3, 1, 0, 0, 1><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec);
+    } else if (e->nv == 0) C3L(FWA_C3_IT0, 0);
+    else if (e->nv == 1) C3L(FWA_C3_IT1, 1);
+    else C3L(FWA_C3_IT2, 2);
 #undef C3L
 #undef C3M
     HIPCHK(e, hipGetLastError());

@@ -1005,6 +1005,17 @@ typedef struct {
     int64_t rows; uint64_t checksum;
 } bench_arg;
 
+/* Order-free digest of one fired row (key, window, int64 aggregates): a linear mix of the fields with odd constants,
+   then a 64-bit finalizer; a watermark's digest is the sum mod 2^64 over its rows, so emission order (unspecified in
+   the reference, TimerHeapInternalTimer.comparePriorityTo) does not matter. Restated by tests/digest.py (torch). */
+uint64_t or_row_digest(int64_t key, int64_t start, int64_t end, const int64_t* aggs, int naggs) {
+    uint64_t h = (uint64_t)key * 0x9E3779B97F4A7C15ull + (uint64_t)start * 0xC2B2AE3D27D4EB4Full +
+                 (uint64_t)end * 0x165667B19E3779F9ull;
+    for (int j = 0; j < naggs; j++) h += (uint64_t)aggs[j] * (0xD6E8FEB86659FD93ull + 2ull * (uint64_t)j);
+    h ^= h >> 33; h *= 0xC4CEB9FE1A85EC53ull; h ^= h >> 29; h *= 0x94D049BB133111EBull; h ^= h >> 32;
+    return h;
+}
+
 static void* bench_worker(void* vp) {
     bench_arg* a = (bench_arg*)vp;
     fwa_config c = *a->cfg;
@@ -1016,7 +1027,7 @@ static void* bench_worker(void* vp) {
         or_push(e, a->bk[b], a->bt[b], cols, NULL, a->bn[b], NULL);
         or_advance_watermark(e, a->wms[b], &o);
         a->rows += o.n_rows;
-        for (int64_t r = 0; r < o.n_rows; r++) a->checksum += (uint64_t)o.key[r] * 31u + (uint64_t)o.win_end[r] + (c.num_aggs ? (uint64_t)((const int64_t*)o.agg[c.num_aggs - 1])[r] : 0);
+        for (int64_t r = 0; r < o.n_rows; r++) a->checksum += (uint64_t)o.key[r] * 31u + (uint64_t)o.win_end[r] + (c.num_aggs ? (uint64_t)((const aval*)o.agg[c.num_aggs - 1])[r].i : 0);
     }
     or_destroy(e);
     return NULL;
@@ -1075,5 +1086,87 @@ double or_bench_pipeline(const fwa_config* cfg, const fwa_gen_params* p, int64_t
     free(th); free(args); free(keys); free(ts); free(vv); free(wms); free(dest);
     if (rows_out) *rows_out = rows;
     if (checksum_out) *checksum_out = cs;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+
+typedef struct {
+    const fwa_config* cfg; const fwa_gen_params* p; int idx, nthreads;
+    int64_t n, batch, nb;
+    int64_t* wrows; uint64_t* wdig;     /* [nb + 1] */
+    int rc;
+} digest_arg;
+
+/* One operator instance (a key-group range) over the generated stream: every worker generates each batch itself and
+   keeps its own key groups, so the set-up is parallel and memory stays one batch per thread. */
+static void* digest_worker(void* vp) {
+    digest_arg* a = (digest_arg*)vp;
+    fwa_config c = *a->cfg;
+    const int maxp = c.max_parallelism > 0 ? c.max_parallelism : 128;
+    c.max_parallelism = maxp;
+    or_key_group_range(maxp, a->nthreads, a->idx, &c.kg_start, &c.kg_end);
+    or_engine* e;
+    a->rc = or_create(&c, &e);
+    if (a->rc) return NULL;
+    int64_t* keys = (int64_t*)malloc(8 * a->batch); int64_t* ts = (int64_t*)malloc(8 * a->batch);
+    int64_t* vv = (int64_t*)malloc(8 * a->batch);
+    int64_t max_ts = J_LONG_MIN;
+    fwa_out o;
+    int64_t av[FWA_MAX_AGGS];
+    for (int64_t b = 0; b <= a->nb; b++) {
+        int64_t m = 0, wm = J_LONG_MAX;
+        if (b < a->nb) {
+            const int64_t cnt = (b == a->nb - 1) ? a->n - b * a->batch : a->batch;
+            fwa_gen_params q = *a->p; q.first_index = a->p->first_index + b * a->batch;
+            or_generate(&q, cnt, keys, ts, vv, NULL, NULL, NULL);
+            for (int64_t i = 0; i < cnt; i++) {
+                if (ts[i] > max_ts) max_ts = ts[i];
+                const int kg = or_key_group(keys[i], c.key_kind, 0, maxp);
+                if (kg < c.kg_start || kg > c.kg_end) continue;
+                keys[m] = keys[i]; ts[m] = ts[i]; vv[m] = vv[i]; m++;
+            }
+            wm = max_ts - a->p->max_delay_ms - 1;                   /* BoundedOutOfOrdernessWatermarks :57-69 */
+        }
+        const void* cols[1] = {vv};
+        if ((a->rc = or_push(e, keys, ts, cols, NULL, m, NULL)) != 0) break;
+        if ((a->rc = or_advance_watermark(e, wm, &o)) != 0) break;
+        uint64_t d = 0;
+        for (int64_t r = 0; r < o.n_rows; r++) {
+            for (int j = 0; j < c.num_aggs; j++) av[j] = ((const aval*)o.agg[j])[r].i;   /* 16-byte result slots */
+            d += or_row_digest(o.key[r], o.win_start[r], o.win_end[r], av, c.num_aggs);
+        }
+        a->wdig[b] = d; a->wrows[b] = o.n_rows;
+    }
+    free(keys); free(ts); free(vv);
+    or_destroy(e);
+    return NULL;
+}
+
+/* The generated stream's fired rows per watermark, as (row count, or_row_digest sum) for each of the ceil(n / batch)
+   batch watermarks (max_ts - D - 1) and the final Long.MAX_VALUE one (nb + 1 entries), `threads` operator instances
+   over key-group ranges: the full-size parity check of the benched configurations (tests/test_full_size_digests_gpu.py).
+   Aggregates must be int64 (COUNT / SUM(BIGINT) / MIN / MAX over BIGINT). */
+double or_pipeline_digests(const fwa_config* cfg, const fwa_gen_params* p, int64_t n, int64_t batch, int threads,
+                           int64_t* wm_rows, uint64_t* wm_dig) {
+    const int64_t nb = (n + batch - 1) / batch;
+    digest_arg* args = (digest_arg*)calloc(threads, sizeof(digest_arg));
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < threads; t++) {
+        args[t] = (digest_arg){cfg, p, t, threads, n, batch, nb, (int64_t*)calloc(nb + 1, 8), (uint64_t*)calloc(nb + 1, 8), 0};
+        pthread_create(&th[t], NULL, digest_worker, &args[t]);
+    }
+    int rc = 0;
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    for (int64_t b = 0; b <= nb; b++) { wm_rows[b] = 0; wm_dig[b] = 0; }
+    for (int t = 0; t < threads; t++) {
+        if (args[t].rc && !rc) rc = args[t].rc;
+        for (int64_t b = 0; b <= nb; b++) { wm_rows[b] += args[t].wrows[b]; wm_dig[b] += args[t].wdig[b]; }
+        free(args[t].wrows); free(args[t].wdig);
+    }
+    free(args); free(th);
+    if (rc) return (double)rc;              /* an FWA_E_* code (negative) */
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

@@ -64,6 +64,9 @@ void or_generate(const fwa_gen_params* p, int64_t n, int64_t* keys, int64_t* ts,
  * Returns seconds spent in the operator pipeline (generation excluded); rows/checksum out. */
 double or_bench_pipeline(const fwa_config* cfg, const fwa_gen_params* p, int64_t n, int64_t batch,
                          int threads, int64_t* rows_out, uint64_t* checksum_out);
+uint64_t or_row_digest(int64_t key, int64_t start, int64_t end, const int64_t* aggs, int naggs);
+double or_pipeline_digests(const fwa_config* cfg, const fwa_gen_params* p, int64_t n, int64_t batch, int threads,
+                           int64_t* wm_rows, uint64_t* wm_dig);
 
 #ifdef __cplusplus
 }

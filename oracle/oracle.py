@@ -69,6 +69,11 @@ def lib():
         L.or_bench_pipeline.argtypes = [C.POINTER(A.Config), C.POINTER(A.GenParams), C.c_int64,
                                         C.c_int64, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
         L.or_bench_pipeline.restype = C.c_double
+        L.or_pipeline_digests.argtypes = [C.POINTER(A.Config), C.POINTER(A.GenParams), C.c_int64, C.c_int64, C.c_int,
+                                          C.c_void_p, C.c_void_p]
+        L.or_pipeline_digests.restype = C.c_double
+        L.or_row_digest.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_int]
+        L.or_row_digest.restype = C.c_uint64
         _LIB = L
     return _LIB
 
@@ -228,6 +233,24 @@ def bench_pipeline(cfg, params, n, batch, threads):
     cs = C.c_uint64(0)
     secs = lib().or_bench_pipeline(C.byref(cfg), C.byref(params), n, batch, threads, C.byref(rows), C.byref(cs))
     return secs, rows.value, cs.value
+
+
+def pipeline_digests(cfg, params, n, batch, threads):
+    """Threaded oracle over the generated stream: per batch watermark (max_ts - D - 1) and the final Long.MAX_VALUE
+    one, the fired row count and the order-free row digest (or_row_digest summed mod 2^64). Returns (secs, rows[nb+1],
+    digests[nb+1] as uint64)."""
+    nb = (n + batch - 1) // batch
+    rows = np.zeros(nb + 1, np.int64)
+    dig = np.zeros(nb + 1, np.uint64)
+    secs = lib().or_pipeline_digests(C.byref(cfg), C.byref(params), n, batch, threads, _ptr(rows), _ptr(dig))
+    if secs < 0:
+        raise OracleError(int(secs), "or_pipeline_digests")
+    return secs, rows, dig
+
+
+def row_digest(key, start, end, aggs):
+    a = np.ascontiguousarray(aggs, np.int64)
+    return lib().or_row_digest(int(key), int(start), int(end), _ptr(a), len(a))
 
 
 def wire_decode(schema, data):

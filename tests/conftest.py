@@ -12,6 +12,9 @@ def pytest_addoption(parser):
     parser.addoption("--force-record-lists", action="store_true", default=False,
                      help="every eligible TUMBLE handle keeps its state as record lists (FWA_CFG_RECORD_LISTS): runs "
                           "the parity suite over the sparse layout (tools/gpu_record_lists_suite.sh)")
+    parser.addoption("--force-option", action="append", default=[], metavar="NAME=VALUE",
+                     help="fwa_set_option applied to every handle of the session (engine.DEFAULT_OPTIONS), e.g. "
+                          "window_passes=1 to run the parity suite over the combiner's window passes")
 
 
 def _record_lists_eligible(c):
@@ -32,5 +35,9 @@ def pytest_configure(config):
                 c.flags |= A.CFG_RECORD_LISTS
             return c
         A.make_config = make_forced
+    for opt in config.getoption("--force-option"):
+        from flink_amd import engine
+        name, _, value = opt.partition("=")
+        engine.DEFAULT_OPTIONS[name] = int(value)
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP engine through the C-ABI)")
     config.addinivalue_line("markers", "slow: longer CPU test")

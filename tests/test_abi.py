@@ -71,3 +71,17 @@ def test_engine_refuses_missing_library(tmp_path, monkeypatch):
     monkeypatch.setattr(engine, "LIB_PATH", str(tmp_path / "missing.so"))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         engine.lib()
+
+
+def test_no_kernel_spills_vgprs():
+    """Every gfx950 kernel of the library keeps its values in registers. A VGPR spill is not harmless with this
+    toolchain: hipcc placed the spill stores of the combiner's prefetched entries before the exec-mask restore at a
+    control-flow join, so lanes outside that branch lost their values (rel = 0 instead of -1 for padding lanes, whose
+    key 0 was then counted in slice 0: the r04 window-pass parity failures, DESIGN.md section 4 "Skewed keys")."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from kernel_resources import kernels
+    ks = kernels(LIB)
+    assert len(ks) > 500
+    spill = [(k["name"], k["vgpr_spill_count"]) for k in ks if k.get("vgpr_spill_count", 0) > 0]
+    assert not spill, spill

@@ -151,6 +151,20 @@ def test_random_streams_vs_oracle(eng_mod, ci, aggs):
     assert dropped > 0  # the stream has late records
 
 
+@pytest.mark.parametrize("ci", range(7))
+@pytest.mark.parametrize("aggs", [I64_AGGS, F64_AGGS], ids=["i64", "f64"])
+def test_random_streams_window_passes_vs_oracle(eng_mod, ci, aggs):
+    """The combiner's window passes (FWA_OPT_WINDOW_PASSES) from the first push, over every non-session config. These
+    streams leave most lanes of a chunk as padding (rel = -1), which is what the r04 spilling build corrupted: its
+    padding lanes came back as slice 0 with key 0 (extra rows, DESIGN.md section 4 "Skewed keys")."""
+    from oracle.oracle import Oracle
+    cfg = A.make_config(aggs=aggs, key_capacity=4096, **CONFIGS[ci])
+    names = A.agg_names(cfg)
+    stream = random_stream(100 + ci, 40_000, 600, 60_000, 1500)
+    run_pair(cfg, batches_of(stream, 12, 1500), lambda c: eng_mod.WindowAggregator(c, options={"window_passes": 1}),
+             Oracle, names)
+
+
 def test_binrow_and_prehashed_keys(eng_mod):
     from oracle.oracle import Oracle
     for kind in (A.KEY_BINROW_BIGINT, A.KEY_PREHASHED):

@@ -24,6 +24,15 @@ def rows_of(r, names):
     return out
 
 
+def mix64(x):
+    """jm::mix64 (flink_amd/csrc/java_math.h): the key table's hash, to see where a key's probe starts."""
+    M = (1 << 64) - 1
+    z = x & M
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    return z ^ (z >> 31)
+
+
 def main():
     ci = int(sys.argv[1]) if len(sys.argv) > 1 else 0
     aset = sys.argv[2] if len(sys.argv) > 2 else "i64"
@@ -48,7 +57,13 @@ def main():
             print("MISMATCH at batch %d wm=%d: %d vs %d rows" % (b, wm, len(sg), len(so)))
             print("only GPU:", only_g[:20])
             print("only oracle:", only_o[:20])
-            keys = sorted({r[0] for r in only_g + only_o})[:5]
+            import collections
+            dup = [kw for kw, c in collections.Counter(r[:3] for r in sg).items() if c > 1]
+            print("(key, window) emitted more than once by the GPU:", len(dup))
+            for kw in dup[:8]:
+                print("  GPU:", [r for r in sg if r[:3] == kw], " ORA:", [r for r in so if r[:3] == kw],
+                      " mix64 bucket:", hex(mix64(kw[0])))
+            keys = sorted({r[0] for r in only_g + only_o} | {kw[0] for kw in dup})[:5]
             for kk in keys:
                 print("key %d GPU:" % kk, [r for r in sg if r[0] == kk])
                 print("key %d ORA:" % kk, [r for r in so if r[0] == kk])
