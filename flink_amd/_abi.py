@@ -25,6 +25,10 @@ AGG_KINDS = {
     "MIN_F32": 6, "MAX_F32": 7, "MIN_F64": 8, "MAX_F64": 9, "AVG_I64": 10, "AVG_F32": 11,
     "AVG_F64": 12, "COUNT_COL": 13,
     "SUM_DEC": 14, "AVG_DEC": 15, "SUM_DEC128": 16, "AVG_DEC128": 17,
+    # DataStream built-in reductions (FWA_CFG_REDUCE)
+    "SUM_I32": 18, "MIN_I32": 19, "MAX_I32": 20, "FIRST_64": 21, "FIRST_32": 22,
+    "MINBY_I64": 23, "MAXBY_I64": 24, "MINBY_I32": 25, "MAXBY_I32": 26, "MINBY_F64": 27, "MAXBY_F64": 28,
+    "MINBY_F32": 29, "MAXBY_F32": 30, "SEL_64": 31, "SEL_32": 32,
 }
 DEC_KINDS = ("SUM_DEC", "AVG_DEC", "SUM_DEC128", "AVG_DEC128")
 AGG_NAMES = {v: k for k, v in AGG_KINDS.items()}
@@ -35,6 +39,10 @@ AGG_RESULT_DTYPE = {
     "AVG_I64": "i8", "AVG_F32": "f4", "AVG_F64": "f8", "COUNT_COL": "i8",
     # DECIMAL: 16-byte unscaled two's complement; the wrappers return Python ints (object arrays)
     "SUM_DEC": "V16", "AVG_DEC": "V16", "SUM_DEC128": "V16", "AVG_DEC128": "V16",
+    # FIRST_* / SEL_*: the field's raw bits (view them as the field's type)
+    "SUM_I32": "i4", "MIN_I32": "i4", "MAX_I32": "i4", "FIRST_64": "i8", "FIRST_32": "i4",
+    "MINBY_I64": "i8", "MAXBY_I64": "i8", "MINBY_I32": "i4", "MAXBY_I32": "i4", "MINBY_F64": "f8", "MAXBY_F64": "f8",
+    "MINBY_F32": "f4", "MAXBY_F32": "f4", "SEL_64": "i8", "SEL_32": "i4",
 }
 # numpy dtype of each aggregate's INPUT column (None: no input)
 AGG_INPUT_DTYPE = {
@@ -42,6 +50,9 @@ AGG_INPUT_DTYPE = {
     "MAX_I64": "i8", "MIN_F32": "f4", "MAX_F32": "f4", "MIN_F64": "f8", "MAX_F64": "f8",
     "AVG_I64": "i8", "AVG_F32": "f4", "AVG_F64": "f8", "COUNT_COL": None,
     "SUM_DEC": "i8", "AVG_DEC": "i8", "SUM_DEC128": "V16", "AVG_DEC128": "V16",
+    "SUM_I32": "i4", "MIN_I32": "i4", "MAX_I32": "i4", "FIRST_64": "i8", "FIRST_32": "i4",
+    "MINBY_I64": "i8", "MAXBY_I64": "i8", "MINBY_I32": "i4", "MAXBY_I32": "i4", "MINBY_F64": "f8", "MAXBY_F64": "f8",
+    "MINBY_F32": "f4", "MAXBY_F32": "f4", "SEL_64": "i8", "SEL_32": "i4",
 }
 
 
@@ -71,6 +82,8 @@ STATUS = {0: "OK", -1: "E_ARG", -2: "E_TS_MIN", -3: "E_KEYGROUP", -4: "E_MERGE_L
 CFG_DYNAMIC_GAP = 0x1
 CFG_LATE_INDICES = 0x2
 CFG_RECORD_LISTS = 0x4
+CFG_REDUCE = 0x8
+CFG_BY_LAST = 0x10
 
 PUSH_DEVICE_PTRS = 0x1
 PUSH_ASYNC = 0x2
@@ -137,10 +150,12 @@ def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, sl
                 offset_ms=0, gap_ms=0, allowed_lateness_ms=0, aggs=(("COUNT", 0), ("SUM_I64", 0)),
                 key_kind=KEY_JAVA_LONG, max_parallelism=128, kg_start=0, kg_end=None, device=0,
                 output_on_device=0, key_capacity=0, max_batch=0, gap_col=None, tz=None, late_indices=False,
-                nullable_cols=(), record_lists=False):
+                nullable_cols=(), record_lists=False, reduce=False, by_last=False):
     """Build a Config struct. aggs: sequence of (agg name, value-column index). gap_col: value column of
     per-record session gaps (DynamicEventTimeSessionWindows). tz: [(utc_instant_ms, offset_ms), ...] shift
-    time zone of a TIMESTAMP_LTZ rowtime (the struct keeps a pointer to a buffer held on the struct)."""
+    time zone of a TIMESTAMP_LTZ rowtime (the struct keeps a pointer to a buffer held on the struct). reduce: a
+    DataStream built-in reduction (FWA_CFG_REDUCE, WindowedStream.sum/min/max/minBy/maxBy); by_last: minBy / maxBy
+    ties go to the last element (FWA_CFG_BY_LAST)."""
     c = Config()
     c.abi_version = FWA_ABI_VERSION
     c.window_kind = WINDOW_KINDS[window_kind] if isinstance(window_kind, str) else int(window_kind)
@@ -168,6 +183,10 @@ def make_config(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000, sl
         c.flags |= CFG_LATE_INDICES
     if record_lists:                                      # TUMBLE state as record lists (huge key spaces)
         c.flags |= CFG_RECORD_LISTS
+    if reduce:
+        c.flags |= CFG_REDUCE
+    if by_last:
+        c.flags |= CFG_BY_LAST
     for col in nullable_cols:                             # value columns that may hold SQL NULLs
         c.nullable_cols |= 1 << col
     if gap_col is not None:

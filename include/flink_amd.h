@@ -95,8 +95,37 @@ enum fwa_agg_kind {
     FWA_AVG_DEC = 15,  /* AVG(DECIMAL(p, s)), p <= 18: result DECIMAL(38, max(6, s))  [i128] */
     FWA_SUM_DEC128 = 16,/* SUM(DECIMAL(p, s)), p <= 38: 16-byte unscaled input        [i128] */
     FWA_AVG_DEC128 = 17,/* AVG(DECIMAL(p, s)), p <= 38                               [i128] */
-    FWA_AGG_KIND_COUNT = 18
+    /* DataStream built-in reductions (FWA_CFG_REDUCE handles, below) */
+    FWA_SUM_I32 = 18,  /* Integer field: Java int addition, 32-bit wrap (SumFunction.IntSum)  [i32] */
+    FWA_MIN_I32 = 19,  /* Integer field, ComparableAggregator MIN                          [i32] */
+    FWA_MAX_I32 = 20,  /* Integer field, ComparableAggregator MAX                          [i32] */
+    FWA_FIRST_64 = 21, /* 8-byte field of the window's first element (arrival order)      [i64 bits] */
+    FWA_FIRST_32 = 22, /* 4-byte field of the window's first element                        [i32 bits] */
+    FWA_MINBY_I64 = 23,/* minBy over a Long field: that field of the selected element       [i64] */
+    FWA_MAXBY_I64 = 24,/* maxBy over a Long field                                           [i64] */
+    FWA_MINBY_I32 = 25,/* minBy / maxBy over an Integer field                              [i32] */
+    FWA_MAXBY_I32 = 26,
+    FWA_MINBY_F64 = 27,/* minBy / maxBy over a Double field (Double.compareTo order)        [f64] */
+    FWA_MAXBY_F64 = 28,
+    FWA_MINBY_F32 = 29,/* minBy / maxBy over a Float field (Float.compareTo order)          [f32] */
+    FWA_MAXBY_F32 = 30,
+    FWA_SEL_64 = 31,   /* 8-byte field of the element minBy / maxBy selected                [i64 bits] */
+    FWA_SEL_32 = 32,   /* 4-byte field of the element minBy / maxBy selected                [i32 bits] */
+    FWA_AGG_KIND_COUNT = 33
 };
+/* Built-in DataStream reductions (FWA_CFG_REDUCE): WindowedStream.sum / min / max / minBy / maxBy(pos)
+ * (WindowedStream.java:680-890) reduce the window's elements in arrival order with SumAggregator
+ * (SumAggregator.java:66-76) or ComparableAggregator (ComparableAggregator.java:83-107): the result is a copy of the
+ * accumulated value1 with field pos replaced, so every other field comes from the window's FIRST element
+ * (FWA_FIRST_*), while minBy / maxBy keep a whole element -- the one with the smallest / largest pos field, ties to
+ * the first element, or to the last with FWA_CFG_BY_LAST (minBy(pos, false)) -- whose other fields are FWA_SEL_*.
+ * Comparisons are Java compareTo (Long / Integer / Double.compare / Float.compare: -0.0 < 0.0, NaN above +Inf; a MIN
+ * or MAX result NaN is returned canonical). SUM over Float is accumulated in double and rounded once (the reference
+ * adds in float, in arrival order), over Double in device order (within the tolerance of SUM_F64).
+ * A reduce handle is DATASTREAM, TUMBLE or SLIDE (non-merging windows), allowed lateness 0; at most one MINBY / MAXBY
+ * aggregate, FWA_SEL_* only with it and FWA_FIRST_* only without it; COUNT / SUM / MIN / MAX over any type may be
+ * listed; no DECIMAL, AVG, NULLs, record lists, partials or snapshots (FWA_E_UNSUPPORTED). A tuple
+ * (key, f1, ..., fn) with sum(k) maps to FIRST_* for every fi, i != k, and SUM_* for fk; minBy(k) to SEL_* and MINBY_*. */
 /* DECIMAL aggregates (Table semantics; the input column's scale s in fwa_config.dec_scale[j]). Values are unscaled
  * integers in 16-byte little-endian two's complement ([i128]: low 8 bytes, then high 8 bytes).
  *  SUM: DecimalSumAggFunction (SumAggFunction.java:150-168): the exact sum at the result type of
@@ -184,6 +213,9 @@ typedef struct fwa_config {
                                   * WindowOperator's lateDataOutputTag side output (WindowOperator.java:425-433) and the
                                   * per-record processElement() == true of SlicingWindowProcessor
                                   * (SlicingWindowOperator.java:222-226, lateRecordsDroppedRate) */
+#define FWA_CFG_REDUCE 0x8       /* DataStream built-in reduction (WindowedStream.sum/min/max/minBy/maxBy): Java
+                                  * compareTo order for MIN / MAX, FWA_FIRST_* / FWA_SEL_* / FWA_MINBY_* kinds (above) */
+#define FWA_CFG_BY_LAST 0x10     /* minBy / maxBy(pos, first = false): ties select the LAST element */
 #define FWA_CFG_RECORD_LISTS 0x4 /* TUMBLE, lateness 0, no NULLs, UTC: keep each window's state as its accepted records
                                   * (key + accumulator words) bucketed by hash partition, aggregated once when the window
                                   * fires -- for key spaces where keys barely repeat within a window (C4: 1e8 keys).

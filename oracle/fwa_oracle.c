@@ -331,6 +331,47 @@ typedef union { int64_t i; double d; float f; __int128 q; } aval;   /* q: DECIMA
    DecimalDataUtils.add (:106-121) -> DecimalData.fromBigDecimal (DecimalData.java:184-195): NULL past 38 digits */
 static int is_dec(int k) { return k >= FWA_SUM_DEC && k <= FWA_AVG_DEC128; }
 static int is_dec_avg(int k) { return k == FWA_AVG_DEC || k == FWA_AVG_DEC128; }
+
+/* ---- DataStream built-in reductions (FWA_CFG_REDUCE): SumAggregator / ComparableAggregator applied in arrival order
+   (WindowedStream.java:680-890 -> reduce(); HeapReducingState.add reduces the stored value1 with each new element) */
+static int is_byk(int k) { return k >= FWA_MINBY_I64 && k <= FWA_MAXBY_F32; }
+static int is_maxby(int k) { return k == FWA_MAXBY_I64 || k == FWA_MAXBY_I32 || k == FWA_MAXBY_F64 || k == FWA_MAXBY_F32; }
+/* Double.compare / Float.compare (Double.java compare: doubleToLongBits order, so -0.0 < 0.0 and NaN above +Inf) */
+static int64_t jbits_d(double v) { int64_t b; if (v != v) return 0x7ff8000000000000LL; memcpy(&b, &v, 8); return b; }
+static int32_t jbits_f(float v) { int32_t b; if (v != v) return 0x7fc00000; memcpy(&b, &v, 4); return b; }
+static int jcmp_d(double a, double b) {
+    if (a < b) return -1;
+    if (a > b) return 1;
+    const int64_t x = jbits_d(a), y = jbits_d(b);
+    return x == y ? 0 : (x < y ? -1 : 1);
+}
+static int jcmp_f(float a, float b) {
+    if (a < b) return -1;
+    if (a > b) return 1;
+    const int32_t x = jbits_f(a), y = jbits_f(b);
+    return x == y ? 0 : (x < y ? -1 : 1);
+}
+/* compare(state, v) of the field a by/min/max aggregate reads; 4-byte types sit in the low half of aval */
+static int red_cmp(int kind, const aval* x, const void* col, int64_t i) {
+    switch (kind) {
+    case FWA_MIN_I64: case FWA_MAX_I64: case FWA_MINBY_I64: case FWA_MAXBY_I64: {
+        const int64_t v = ((const int64_t*)col)[i]; return x->i < v ? -1 : (x->i > v ? 1 : 0); }
+    case FWA_MIN_I32: case FWA_MAX_I32: case FWA_MINBY_I32: case FWA_MAXBY_I32: {
+        const int32_t v = ((const int32_t*)col)[i], u = (int32_t)x->i; return u < v ? -1 : (u > v ? 1 : 0); }
+    case FWA_MIN_F64: case FWA_MAX_F64: case FWA_MINBY_F64: case FWA_MAXBY_F64: return jcmp_d(x->d, ((const double*)col)[i]);
+    default: return jcmp_f(x->f, ((const float*)col)[i]);
+    }
+}
+static void red_set(int kind, aval* x, const void* col, int64_t i) {   /* x := the element's field */
+    switch (kind) {
+    case FWA_FIRST_32: case FWA_SEL_32: x->i = (int64_t)((const uint32_t*)col)[i]; break;
+    case FWA_MIN_I32: case FWA_MAX_I32: case FWA_MINBY_I32: case FWA_MAXBY_I32: case FWA_SUM_I32: x->i = ((const int32_t*)col)[i]; break;
+    case FWA_MIN_F32: case FWA_MAX_F32: case FWA_MINBY_F32: case FWA_MAXBY_F32: case FWA_SUM_F32:
+        x->i = 0; x->f = ((const float*)col)[i]; break;
+    case FWA_MIN_F64: case FWA_MAX_F64: case FWA_MINBY_F64: case FWA_MAXBY_F64: case FWA_SUM_F64: x->d = ((const double*)col)[i]; break;
+    default: x->i = ((const int64_t*)col)[i]; break;
+    }
+}
 static const unsigned __int128 DEC_LIM = (unsigned __int128)10000000000000000000ull * 10000000000000000000ull; /* 10^38 */
 static int dec_fits(__int128 v) { unsigned __int128 a = v < 0 ? -(unsigned __int128)v : (unsigned __int128)v; return a < DEC_LIM; }
 static __int128 dec_input(const void* col, int64_t i, int kind) {
@@ -419,8 +460,44 @@ static void acc_free(or_engine* e, int64_t id) {
     e->free_list[e->free_n++] = id;
 }
 
+/* One element reduced into a reduce handle's window state (value1 = the state, value2 = the element). */
+static void red_add(or_engine* e, aval* a, const void* const* cols, int64_t i) {
+    const int na = e->c.num_aggs;
+    const int64_t before = a[0].i;
+    a[0].i = jladd(a[0].i, 1);
+    int sel = before == 0;                            /* minBy / maxBy: the element replaces the selected one */
+    for (int j = 0; j < na && before > 0; j++) {
+        const int k = e->c.aggs[j].kind;
+        if (!is_byk(k)) continue;
+        const int c = red_cmp(k, &a[1 + j], cols[e->c.aggs[j].col], i);   /* ComparableAggregator.reduce :83-107 */
+        sel = c == 0 ? ((e->c.flags & FWA_CFG_BY_LAST) != 0) : (is_maxby(k) ? c < 0 : c > 0);
+    }
+    for (int j = 0; j < na; j++) {
+        const int k = e->c.aggs[j].kind;
+        const void* col = k == FWA_COUNT ? NULL : cols[e->c.aggs[j].col];
+        aval* x = &a[1 + j];
+        switch (k) {
+        case FWA_COUNT: break;
+        case FWA_FIRST_64: case FWA_FIRST_32: if (before == 0) red_set(k, x, col, i); break;   /* value1's fields */
+        case FWA_SEL_64: case FWA_SEL_32: if (sel) red_set(k, x, col, i); break;
+        case FWA_SUM_I64: x->i = jladd(x->i, ((const int64_t*)col)[i]); break;              /* SumFunction */
+        case FWA_SUM_I32: x->i = (int32_t)((uint32_t)x->i + (uint32_t)((const int32_t*)col)[i]); break;
+        case FWA_SUM_F64: x->d += ((const double*)col)[i]; break;
+        case FWA_SUM_F32: x->f = x->f + ((const float*)col)[i]; break;
+        case FWA_MIN_I64: case FWA_MIN_I32: case FWA_MIN_F64: case FWA_MIN_F32:   /* isExtremal == 0 -> value2's */
+            if (before == 0 || !(red_cmp(k, x, col, i) < 0)) red_set(k, x, col, i);
+            break;
+        case FWA_MAX_I64: case FWA_MAX_I32: case FWA_MAX_F64: case FWA_MAX_F32:
+            if (before == 0 || !(red_cmp(k, x, col, i) > 0)) red_set(k, x, col, i);
+            break;
+        default: if (is_byk(k) && sel) red_set(k, x, col, i); break;
+        }
+    }
+}
+
 /* accumulate one record (AggregateFunction.add / ReduceFunction.reduce / SQL accumulate) */
 static void acc_add(or_engine* e, aval* a, const void* const* cols, int64_t i) {
+    if (e->c.flags & FWA_CFG_REDUCE) { red_add(e, a, cols, i); return; }
     const int na = e->c.num_aggs;
     a[0].i = jladd(a[0].i, 1);
     for (int j = 0; j < na; j++) {
@@ -522,6 +599,18 @@ static void emit(or_engine* e, int64_t key, int64_t ws, int64_t we, const aval* 
         const aval* x = &a[1 + j]; aval* o = &e->o_agg[j][r]; o->i = 0;
         const int64_t nn = a[1 + na + j].i;           /* non-NULL inputs */
         const int kind = e->c.aggs[j].kind;
+        if (e->c.flags & FWA_CFG_REDUCE) {            /* the reduced tuple's fields */
+            e->o_null[j][r] = 0;
+            if (kind == FWA_COUNT) o->i = a[0].i;
+            else if (kind == FWA_SUM_F32 || kind == FWA_MIN_F32 || kind == FWA_MAX_F32 || kind == FWA_MINBY_F32 ||
+                     kind == FWA_MAXBY_F32) { o->f = x->f; if (o->f != o->f) o->i = 0x7fc00000; }
+            else if (kind == FWA_SUM_F64 || kind == FWA_MIN_F64 || kind == FWA_MAX_F64 || kind == FWA_MINBY_F64 ||
+                     kind == FWA_MAXBY_F64) { o->d = x->d; if (o->d != o->d) o->i = 0x7ff8000000000000LL; }
+            else if (kind == FWA_SUM_I32 || kind == FWA_MIN_I32 || kind == FWA_MAX_I32 || kind == FWA_MINBY_I32 ||
+                     kind == FWA_MAXBY_I32 || kind == FWA_FIRST_32 || kind == FWA_SEL_32) o->i = (int64_t)(uint32_t)x->i;
+            else o->i = x->i;
+            continue;
+        }
         e->o_null[j][r] = (kind != FWA_COUNT && kind != FWA_COUNT_COL && nn == 0);   /* SQL NULL result */
         if (e->o_null[j][r]) continue;
         if (is_dec(kind)) {
@@ -565,6 +654,22 @@ int or_create(const fwa_config* c, or_engine** out) {
     if (c->window_kind == FWA_CUMULATE && (c->semantics != FWA_SEM_TABLE || c->size_ms <= 0 || c->slide_ms <= 0 || c->size_ms % c->slide_ms)) return FWA_E_ARG;
     if (c->window_kind == FWA_SESSION && c->gap_ms <= 0 && !(c->flags & FWA_CFG_DYNAMIC_GAP)) return FWA_E_ARG;
     if (c->semantics == FWA_SEM_TABLE && c->allowed_lateness_ms != 0) return FWA_E_ARG;
+    {   /* reduce kinds only in FWA_CFG_REDUCE handles, which are non-merging DataStream windows */
+        int nby = 0, nsel = 0, nfirst = 0, nred = 0;
+        for (int j = 0; j < c->num_aggs; j++) {
+            const int k = c->aggs[j].kind;
+            nby += is_byk(k); nsel += (k == FWA_SEL_64 || k == FWA_SEL_32); nfirst += (k == FWA_FIRST_64 || k == FWA_FIRST_32);
+            nred += k >= FWA_SUM_I32 && k <= FWA_SEL_32;
+            if ((c->flags & FWA_CFG_REDUCE) && (is_dec(k) || k == FWA_AVG_I64 || k == FWA_AVG_F32 || k == FWA_AVG_F64 ||
+                                                k == FWA_COUNT_COL)) return FWA_E_UNSUPPORTED;
+        }
+        if (nred && !(c->flags & FWA_CFG_REDUCE)) return FWA_E_ARG;
+        if (c->flags & FWA_CFG_REDUCE) {
+            if (nby > 1 || (nsel && !nby) || (nfirst && nby)) return FWA_E_ARG;
+            if (c->semantics != FWA_SEM_DATASTREAM || (c->window_kind != FWA_TUMBLE && c->window_kind != FWA_SLIDE) ||
+                c->allowed_lateness_ms != 0) return FWA_E_UNSUPPORTED;
+        }
+    }
     if (c->tz_n < 0 || (c->tz_n > 0 && (!c->tz || c->semantics != FWA_SEM_TABLE))) return FWA_E_ARG;
     or_engine* e = (or_engine*)calloc(1, sizeof(or_engine));
     e->c = *c;

@@ -216,3 +216,76 @@ def assert_rows_equal(a, b, names, rtol=None, ctx=""):
             bad = np.nonzero(x != y)[0]
             assert len(bad) == 0, "%s agg %s differs at %d rows, first %s vs %s" % (
                 ctx, name, len(bad), x[bad[0]], y[bad[0]])
+
+
+# ---- DataStream built-in reductions (WindowedStream.sum / min / max / minBy / maxBy over a Tuple4(key, Integer,
+# Double, Long) -- tests/golden/gen_pyflink_reduce_kats.py): value columns f1 (int32), f2 (float64), f3 (int64)
+REDUCE_FIELD_TYPES = ("I32", "F64", "I64")
+
+
+def reduce_aggs(op, pos, types=REDUCE_FIELD_TYPES):
+    """The engine aggregate list for <op>(pos) over fields 1..len(types) (column = field - 1)."""
+    by = op in ("min_by", "max_by")
+    aggs = []
+    for f, t in enumerate(types, start=1):
+        width = "32" if t in ("I32", "F32") else "64"
+        if f != pos:
+            aggs.append((("SEL_" if by else "FIRST_") + width, f - 1))
+        else:
+            aggs.append(({"sum": "SUM_", "min": "MIN_", "max": "MAX_", "min_by": "MINBY_", "max_by": "MAXBY_"}[op] + t,
+                         f - 1))
+    return aggs
+
+
+def load_reduce_kats():
+    with open(os.path.join(GOLDEN, "pyflink_reduce_kats.json")) as f:
+        return json.load(f)
+
+
+def reduce_field_values(rows, names, types=REDUCE_FIELD_TYPES):
+    """Fired rows -> list of (key, start, end, f1, f2, f3) with each field in its Python type (raw FIRST_/SEL_ bits
+    viewed as the field's type)."""
+    cols = []
+    for j, t in enumerate(types):
+        a = np.asarray(rows["agg%d" % j])
+        dt = {"I32": np.int32, "I64": np.int64, "F64": np.float64, "F32": np.float32}[t]
+        cols.append(a.view(dt) if a.dtype.itemsize == np.dtype(dt).itemsize else a.astype(dt))
+    out = []
+    for i in range(len(rows["key"])):
+        out.append((int(rows["key"][i]), int(rows["win_start"][i]), int(rows["win_end"][i])) +
+                   tuple(float(c[i]) if c.dtype.kind == "f" else int(c[i]) for c in cols))
+    return sorted(out)
+
+
+def replay_reduce_kat(case, make_engine):
+    """Feed a reduce KAT through an engine built with the case's reduction; every watermark's rows must match."""
+    import flink_amd._abi as A
+    spec = case["spec"]
+    kw = dict(window_kind=spec["window_kind"], size_ms=spec["size_ms"], offset_ms=spec["offset_ms"])
+    if spec["window_kind"] == "SLIDE":
+        kw["slide_ms"] = spec["slide_ms"]
+    cfg = A.make_config(aggs=reduce_aggs(case["op"], case["pos"]), reduce=True, **kw)
+    names = A.agg_names(cfg)
+    eng = make_engine(cfg)
+    dropped, pend = 0, []
+
+    def flush():
+        nonlocal dropped, pend
+        if pend:
+            k = np.array([p[1] for p in pend], np.int64)
+            cols = [np.array([p[2] for p in pend], np.int32), np.array([p[3] for p in pend], np.float64),
+                    np.array([p[4] for p in pend], np.int64)]
+            dropped += eng.push(k, np.array([p[5] for p in pend], np.int64), cols)
+            pend = []
+
+    for ev in case["events"]:
+        if ev[0] == "e":
+            pend.append(ev)
+        else:
+            flush()
+            got = reduce_field_values(eng.advance_watermark(ev[1]), names)
+            exp = sorted(tuple(r) for r in ev[2])
+            assert got == exp, "%s: wm=%d expected %s got %s" % (case["name"], ev[1], exp, got)
+    flush()
+    assert dropped == case["late_dropped"], "%s: late dropped %d != %d" % (case["name"], dropped, case["late_dropped"])
+    eng.close()

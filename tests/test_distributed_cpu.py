@@ -172,3 +172,33 @@ def test_choose_exchange_plan():
     assert choose_exchange(dict(key_capacity=1_000_000)) == "partials"
     assert choose_exchange(dict(key_capacity=100_000_000)) == "raw"
     assert choose_exchange(dict(key_capacity=4096, record_lists=True)) == "raw"
+
+
+def _valve_worker(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import flink_amd.distributed as D
+    from oracle import oracle as O
+    created = []
+    real_new_group = dist.new_group
+
+    def counting_new_group(*a, **kw):
+        created.append(kw.get("ranks"))
+        return real_new_group(*a, **kw)
+    D.dist.get_backend = lambda group=None: "nccl"      # take the RCCL branch; the group itself stays gloo
+    D.dist.new_group = counting_new_group
+    kw = dict(router=lambda k: torch.zeros(len(k), dtype=torch.int64), window_kind="TUMBLE", size_ms=5000,
+              aggs=[("COUNT", 0)])
+    p1 = D.KeyedWindowPipeline(rank, world, engine_factory=O.Oracle, **kw)
+    p2 = D.KeyedWindowPipeline(rank, world, engine_factory=O.Oracle, **kw)
+    assert p1.wm_group is p2.wm_group and created == [[0, 1]], created
+    assert p1.global_watermark(100 + rank) == 100 and p2.global_watermark(7 - rank) == 6
+    p1.close()
+    p2.close()
+    dist.destroy_process_group()
+
+
+def test_valve_group_created_once_per_rank_set():
+    """under RCCL the watermark valve's gloo group is created once per rank set and shared by every
+    pipeline built on it (no group per pipeline instance piling up; two pipelines on one group do not hang)."""
+    mp.spawn(_valve_worker, args=(2, _free_port()), nprocs=2, join=True)
