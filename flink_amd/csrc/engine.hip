@@ -77,7 +77,9 @@ constexpr int kFireJ = 16;                        // keys per thread per block: 
 // Final value of one aggregate (AggregateFunction.getResult / SQL getValueExpression) from its
 // accumulator column value x (i64 sum bits, f64 sum bits or an ordered MIN/MAX key) and COUNT.
 __device__ __forceinline__ int type_size_dev(int kind) {
-    return (kind == FWA_SUM_F32 || kind == FWA_MIN_F32 || kind == FWA_MAX_F32 || kind == FWA_AVG_F32) ? 4 : 8;
+    return (kind == FWA_SUM_F32 || kind == FWA_MIN_F32 || kind == FWA_MAX_F32 || kind == FWA_AVG_F32 ||
+            kind == FWA_SUM_I32 || kind == FWA_MIN_I32 || kind == FWA_MAX_I32 || kind == FWA_FIRST_32 || kind == FWA_SEL_32 ||
+            kind == FWA_MINBY_I32 || kind == FWA_MAXBY_I32 || kind == FWA_MINBY_F32 || kind == FWA_MAXBY_F32) ? 4 : 8;
 }
 
 // SQL NULLs (nn = the window's non-NULL input count of a nullable aggregate, d.nn > 0): SUM/MIN/MAX/AVG of
@@ -1941,6 +1943,11 @@ struct fwa_engine {
     int32_t h_touched_cap = 0;
     // FWA_CFG_RECORD_LISTS: TUMBLE window state as hash-partitioned record lists, aggregated at fire (sparse.inc)
     bool sparse = false;
+    // FWA_CFG_REDUCE: DataStream built-in reductions (reduce.inc): per-record (kid, slot) of the last push
+    bool red = false;
+    unsigned long long* d_rk = nullptr;
+    int64_t rk_cap = 0;
+    int64_t red_seq_base = 0;             // arrival sequence of the restored elements (red_restore)
     SpState* sp = nullptr;
     // per-handle options (fwa_set_option; the defaults are the production behaviour)
     int32_t opt_pre = -1, opt_mp = -1, opt_narrow = -1, opt_cells = -1;   // -1 adaptive, 0 never, 1 always
@@ -1972,24 +1979,34 @@ int fail(fwa_engine* e, int code, const std::string& msg) {
 int acc_kind_of(int kind) {
     switch (kind) {
         case FWA_COUNT: case FWA_COUNT_COL: return ACC_NONE;
-        case FWA_SUM_I64: case FWA_AVG_I64: return ACC_ADD_I64;
+        case FWA_SUM_I64: case FWA_AVG_I64: case FWA_SUM_I32: return ACC_ADD_I64;
+        case FWA_FIRST_64: case FWA_FIRST_32: case FWA_SEL_64: case FWA_SEL_32: return ACC_PAYLOAD;
+        case FWA_MIN_I32: case FWA_MINBY_I64: case FWA_MINBY_I32: case FWA_MINBY_F64: case FWA_MINBY_F32: return ACC_MIN_ORD;
         case FWA_SUM_F32: case FWA_SUM_F64: case FWA_AVG_F32: case FWA_AVG_F64: return ACC_ADD_F64;
         case FWA_MIN_I64: case FWA_MIN_F32: case FWA_MIN_F64: return ACC_MIN_ORD;
         default: return ACC_MAX_ORD;
     }
 }
 
-int input_class(int kind) {   // 0: BIGINT input, 1: FLOAT, 2: DOUBLE
+int input_class(int kind) {   // 0: BIGINT input, 1: FLOAT, 2: DOUBLE, 3: INT, 4 / 5: raw 4 / 8 bytes (payload fields)
     switch (kind) {
-        case FWA_SUM_F32: case FWA_MIN_F32: case FWA_MAX_F32: case FWA_AVG_F32: return 1;
-        case FWA_SUM_F64: case FWA_MIN_F64: case FWA_MAX_F64: case FWA_AVG_F64: return 2;
+        case FWA_SUM_F32: case FWA_MIN_F32: case FWA_MAX_F32: case FWA_AVG_F32: case FWA_MINBY_F32: case FWA_MAXBY_F32: return 1;
+        case FWA_SUM_F64: case FWA_MIN_F64: case FWA_MAX_F64: case FWA_AVG_F64: case FWA_MINBY_F64: case FWA_MAXBY_F64: return 2;
+        case FWA_SUM_I32: case FWA_MIN_I32: case FWA_MAX_I32: case FWA_MINBY_I32: case FWA_MAXBY_I32: return 3;
+        case FWA_FIRST_32: case FWA_SEL_32: return 4;
+        case FWA_FIRST_64: case FWA_SEL_64: return 5;
         default: return 0;
     }
 }
 
+bool is_reduce_kind(int k) { return k >= FWA_SUM_I32 && k <= FWA_SEL_32; }
+bool is_by_kind(int k) { return k >= FWA_MINBY_I64 && k <= FWA_MAXBY_F32; }
+
 size_t type_size(int kind) {  // input width == result width for every kind except COUNT
     switch (kind) {
         case FWA_SUM_F32: case FWA_MIN_F32: case FWA_MAX_F32: case FWA_AVG_F32: return 4;
+        case FWA_SUM_I32: case FWA_MIN_I32: case FWA_MAX_I32: case FWA_FIRST_32: case FWA_SEL_32:
+        case FWA_MINBY_I32: case FWA_MAXBY_I32: case FWA_MINBY_F32: case FWA_MAXBY_F32: return 4;
         default: return 8;
     }
 }
@@ -2021,7 +2038,27 @@ int validate(const fwa_config* c) {
         default:
             return FWA_E_ARG;
     }
-    if (c->flags & ~(FWA_CFG_DYNAMIC_GAP | FWA_CFG_LATE_INDICES | FWA_CFG_RECORD_LISTS)) return FWA_E_ARG;
+    if (c->flags & ~(FWA_CFG_DYNAMIC_GAP | FWA_CFG_LATE_INDICES | FWA_CFG_RECORD_LISTS | FWA_CFG_REDUCE | FWA_CFG_BY_LAST))
+        return FWA_E_ARG;
+    {   // DataStream built-in reductions (include/flink_amd.h FWA_CFG_REDUCE)
+        int nby = 0, nsel = 0, nfirst = 0, nred = 0, nother = 0;
+        for (int j = 0; j < c->num_aggs; ++j) {
+            const int k = c->aggs[j].kind;
+            nby += is_by_kind(k);
+            nsel += k == FWA_SEL_64 || k == FWA_SEL_32;
+            nfirst += k == FWA_FIRST_64 || k == FWA_FIRST_32;
+            nred += is_reduce_kind(k);
+            nother += (k >= FWA_AVG_I64 && k <= FWA_AVG_DEC128) || k == FWA_COUNT;   // AVG, COUNT, DECIMAL: not fields
+        }
+        if (nred && !(c->flags & FWA_CFG_REDUCE)) return FWA_E_ARG;
+        if ((c->flags & FWA_CFG_BY_LAST) && !(c->flags & FWA_CFG_REDUCE)) return FWA_E_ARG;
+        if (c->flags & FWA_CFG_REDUCE) {
+            if (nby > 1 || (nsel && !nby) || (nfirst && nby)) return FWA_E_ARG;
+            if (nother || c->semantics != FWA_SEM_DATASTREAM || (c->window_kind != FWA_TUMBLE && c->window_kind != FWA_SLIDE) ||
+                c->allowed_lateness_ms != 0 || (c->flags & (FWA_CFG_RECORD_LISTS | FWA_CFG_DYNAMIC_GAP)))
+                return FWA_E_UNSUPPORTED;
+        }
+    }
     if ((c->flags & FWA_CFG_RECORD_LISTS) && !(c->window_kind == FWA_TUMBLE && c->nullable_cols == 0 && c->tz_n == 0 &&
                                               (c->semantics == FWA_SEM_TABLE || c->allowed_lateness_ms == 0)))
         return FWA_E_UNSUPPORTED;
@@ -2360,6 +2397,9 @@ int reset_push_status(fwa_engine* e, bool v2bufs = false) {
 
 #include "sparse.inc"
 #include "decimal.inc"
+static const uint64_t kSnapMagic = 0x3150414E53415746ull;   // "FWASNAP1"
+enum { kSnapHdr = 32 };                                       // header words
+#include "reduce.inc"
 
 // ==================================================================================================
 // C-ABI
@@ -2392,7 +2432,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos, e->d_zslice,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4, e->d_rk};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -2519,6 +2559,26 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         d.nn = nn_acc[d.col];
         if (d.kind == FWA_COUNT_COL) { d.acc = d.nn; d.alias = 1; d.acc_kind = ACC_ADD_I64; }
     }
+    // DataStream built-in reductions: the selected element's arrival sequence (SELQ: identity ~0 to select the first
+    // element, 0 the last) and the by-value it was selected at (SELK) as two more slot columns (reduce.inc)
+    e->red = (cfg->flags & FWA_CFG_REDUCE) != 0;
+    c.red = e->red;
+    c.red_by = -1;
+    if (e->red) {
+        for (int j = 0; j < cfg->num_aggs; ++j) {
+            c.agg[j].jcmp = 1;
+            if (is_by_kind(cfg->aggs[j].kind)) {
+                c.red_by = j;
+                c.red_max = cfg->aggs[j].kind == FWA_MAXBY_I64 || cfg->aggs[j].kind == FWA_MAXBY_I32 ||
+                            cfg->aggs[j].kind == FWA_MAXBY_F64 || cfg->aggs[j].kind == FWA_MAXBY_F32;
+            }
+        }
+        c.red_last = (cfg->flags & FWA_CFG_BY_LAST) != 0;
+        c.red_selq = c.nacc;
+        c.acc_kind[c.nacc++] = c.red_last ? ACC_MAX_ORD : ACC_MIN_ORD;
+        c.red_selk = c.nacc;
+        c.acc_kind[c.nacc++] = ACC_PAYLOAD;
+    }
     e->nacc = c.nacc;
     // key-table segmentation (all paths) and v2 eligibility: <= 2 distinct carried value columns,
     // an LDS window of >= 2 slices next to the SEG-key LDS segment, <= kMaxPart partitions
@@ -2568,7 +2628,7 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         // record lists (sparse.inc): asked for, or a key space of >= 2^25 keys
         const bool want_sp = (cfg->flags & FWA_CFG_RECORD_LISTS) || kc0 >= ((int64_t)1 << 25);
         e->sparse = want_sp && sp_eligible(cfg);
-        ok = ok && np <= kMaxPart && sl >= 2 && e->kind != FWA_SESSION && !e->sparse;
+        ok = ok && np <= kMaxPart && sl >= 2 && e->kind != FWA_SESSION && !e->sparse && !e->red;
         e->v2 = ok;
         if (ok) {
             e->np = (int32_t)np;
@@ -3433,7 +3493,10 @@ static int enqueue_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const 
     // writes the hidden counters: the generic path)
     bool single = e->nacc == 2 && !(raw && e->ec.naggs > e->ec.nout);
     for (const FireWindow& w : hw) single = single && w.nslots == 1;
-    if (single) fire_kernel<1><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
+    if (e->red) {
+        f.blocks_per_win = (int32_t)((e->capacity + 1 + kBlock - 1) / kBlock);
+        red_fire_kernel<<<(unsigned)((int64_t)f.blocks_per_win * (int64_t)hw.size()), kBlock, 0, e->stream>>>(f, e->d_ec);
+    } else if (single) fire_kernel<1><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
     else fire_kernel<0><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
@@ -3827,6 +3890,11 @@ static int push_body(fwa_engine* e, const int64_t* keys, const int64_t* ts, cons
         if (late_dropped_out) *late_dropped_out = dropped;
         return FWA_OK;
     }
+    if (e->red) {                                 // DataStream reduction: v1 ingest, then the selection passes
+        const int64_t seq0 = e->red_seq_base + e->records_in;
+        int rc = push_common(e, a, n, false, false, late_dropped_out);
+        return rc ? rc : red_select(e, a, n, seq0);
+    }
     return push_common(e, a, n, true, (flags & FWA_PUSH_ASYNC) != 0, late_dropped_out);
 }
 
@@ -3834,6 +3902,7 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
                       const void* const* acc, int64_t n, int32_t flags, int64_t* late_dropped_out) {
     if (!e) return FWA_E_STATE;
     if (e->dec && !e->restoring) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of DECIMAL aggregates");
+    if (e->red) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of a DataStream reduction");
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
     if (n < 0 || (n > 0 && (!keys || !slice_ts || !count))) return fail(e, FWA_E_ARG, "null input column");
     if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "partials need a computable key hash");
@@ -3896,6 +3965,11 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
         if (e->d_late) HIPCHK(e, hipFree(e->d_late));
         HIPCHK(e, hipMalloc(&e->d_late, sizeof(int32_t) * e->spill_cap));
     }
+    if (e->red) {                                 // DataStream reduction: v1 ingest, then the selection passes
+        const int64_t seq0 = e->red_seq_base + e->records_in;
+        int rc = push_common(e, a, n, false, false, late_dropped_out);
+        return rc ? rc : red_select(e, a, n, seq0);
+    }
     return push_common(e, a, n, true, (flags & FWA_PUSH_ASYNC) != 0, late_dropped_out);
 }
 
@@ -3924,6 +3998,7 @@ static int retire_slices(fwa_engine* e, int64_t wm) {
 // accumulators of every touched slice complete at wm, reset them, forward the watermark.
 int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     if (!e || !out) return FWA_E_ARG;
+    if (e->red) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of a DataStream reduction");
     if (e->dec) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of DECIMAL aggregates");
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
     HIPCHK(e, hipSetDevice(e->cfg.device));
@@ -3996,8 +4071,6 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
 }
 
 // ---- snapshot / restore (include/flink_amd.h) ----
-static const uint64_t kSnapMagic = 0x3150414E53415746ull;   // "FWASNAP1"
-enum { kSnapHdr = 32 };                                       // header words
 // header word layout: 0 magic, 1 version, 2 window kind, 3 semantics, 4 size, 5 slide, 6 offset, 7 gap,
 // 8 allowed lateness, 9 max parallelism, 10 key kind, 11 num aggs, 12..19 agg kinds, 20 watermark,
 // 21 entries, 22 kg_start, 23 kg_end of the snapshotting handle, 24 nullable_cols, 25 hidden non-NULL
@@ -4256,6 +4329,7 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
             return fail(e, FWA_E_ARG, "snapshot size does not match its entry count");
     }
     if (e->kind == FWA_SESSION) return restore_sessions(e, blobs, n_blobs);
+    if (e->red) return red_restore(e, blobs, n_blobs);
     int64_t wm = LONG_MAX_J;
     bool any = false;
     for (int32_t b = 0; b < n_blobs; ++b) {
@@ -4537,7 +4611,7 @@ int fwa_advance_watermark(fwa_engine* e, int64_t wm, fwa_out* out) {
             }
         }
         bool slid = false;
-        if (e->kind == FWA_SLIDE && wins.size() >= 2 && e->late_rows == 0) {
+        if (e->kind == FWA_SLIDE && wins.size() >= 2 && e->late_rows == 0 && !e->red) {
             int rc = fire_slide(e, wins, wm, &nrows, &slid);
             if (rc) return rc;
         }

@@ -169,6 +169,7 @@ struct In {
 // (SlicingWindowOperator: per-slice state, so the engine's slices map 1:1), Table shift time zones and SQL NULLs.
 bool supported(const fwa_config& c, bool dict = false) {
     if (c.key_kind == FWA_KEY_PREHASHED) return false;
+    if (c.flags & FWA_CFG_REDUCE) return false;                        // a reduction keeps the reduced element
     for (int j = 0; j < c.num_aggs; ++j)                               // DECIMAL: no engine-side DecimalData writer
         if (c.aggs[j].kind >= FWA_SUM_DEC) return false;
     if ((c.key_kind == FWA_KEY_GROUP_PREFIXED) != dict) return false;   // dictionary ids <=> a key dictionary

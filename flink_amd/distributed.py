@@ -39,6 +39,25 @@ def choose_exchange(cfg_kw):
     return "raw" if kc >= 1 << 25 or cfg_kw.get("record_lists") else "partials"
 
 
+_VALVE_GROUPS = {}
+
+
+def valve_group(group=None):
+    """The process group the watermark valve's MIN-allreduce runs on. Under RCCL it is a gloo group over the same
+    ranks, so the valve works on host integers without a device synchronisation (a .item() would wait for every kernel
+    queued on the stream). One gloo group per rank set, created on first use and cached for the process: creating it is
+    collective over the WHOLE default group (torch.distributed.new_group), so the first pipeline built on a given group
+    must be constructed on every rank of the job, including ranks outside `group`; later pipelines reuse it."""
+    if dist.get_backend(group) != "nccl":
+        return group
+    ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(dist.get_world_size()))
+    g = _VALVE_GROUPS.get(ranks)
+    if g is None:
+        g = dist.new_group(ranks=list(ranks), backend="gloo")
+        _VALVE_GROUPS[ranks] = g
+    return g
+
+
 def _gpu_router(max_parallelism, world, key_kind):
     from . import engine
 
@@ -64,12 +83,7 @@ class KeyedWindowPipeline:
         self.route_on_gpu = router is None          # a custom router (tests) keeps the torch grouping
         self.names = A.agg_names(self.cfg)
         self.exchanged = 0
-        # the watermark valve is a host value: under RCCL its MIN-allreduce runs on a gloo group over the same ranks,
-        # so no device synchronisation (a .item() would wait for every kernel queued on the stream)
-        self.wm_group = group
-        if dist.get_backend(group) == "nccl":
-            ranks = None if group is None else dist.get_process_group_ranks(group)
-            self.wm_group = dist.new_group(ranks=ranks, backend="gloo")
+        self.wm_group = valve_group(group)       # host-side MIN valve (gloo under RCCL; see valve_group)
 
     def _a2a(self, x, send_splits, recv_splits):
         out = torch.empty(sum(recv_splits), dtype=x.dtype, device=x.device)

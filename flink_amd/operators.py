@@ -119,6 +119,46 @@ class WindowOperator(_Base):
         return [(r, r[2] - 1) for r in self._rows(self.engine.advance_watermark(wm))]
 
 
+_FIELD_DTYPE = {"I32": "i4", "I64": "i8", "F32": "f4", "F64": "f8"}
+_REDUCE_PREFIX = {"sum": "SUM_", "min": "MIN_", "max": "MAX_", "min_by": "MINBY_", "max_by": "MAXBY_"}
+
+
+def reduction_aggs(op, pos, field_types):
+    """Aggregate list of WindowedStream.<op>(pos) over a tuple (key, f1, ..., fn) whose fields have the given types
+    ("I32" Integer, "I64" Long, "F32" Float, "F64" Double; field i is value column i - 1): field pos is summed /
+    folded (SumAggregator / ComparableAggregator, WindowedStream.java:680-890); every other field is the window's first
+    element's (FIRST_*), or for min_by / max_by the selected element's (SEL_*)."""
+    by = op in ("min_by", "max_by")
+    aggs = []
+    for f, t in enumerate(field_types, start=1):
+        if f == pos:
+            aggs.append((_REDUCE_PREFIX[op] + t, f - 1))
+        else:
+            aggs.append((("SEL_" if by else "FIRST_") + ("32" if t in ("I32", "F32") else "64"), f - 1))
+    return aggs
+
+
+class ReduceWindowOperator(WindowOperator):
+    """DataStream window operator of the built-in reductions WindowedStream.sum / min / max / minBy / maxBy(pos)
+    (WindowedStream.java:680-890: reduce() with SumAggregator / ComparableAggregator, ReducingState folded in arrival
+    order) over tuples (key, f1, ..., fn). first=False is minBy / maxBy(pos, false): ties select the last element.
+    Emits ((key, window_start, window_end, (f1, ..., fn)), window.maxTimestamp())."""
+
+    def __init__(self, assigner: WindowSpec, op, pos, field_types, first=True, **kw):
+        self.field_types = list(field_types)
+        super().__init__(assigner, reduction_aggs(op, pos, self.field_types), reduce=True, by_last=not first, **kw)
+        self.dtypes = [_FIELD_DTYPE[t] for t in self.field_types]
+
+    def _rows(self, res):
+        cols = []
+        for j, t in enumerate(self.field_types):
+            a = np.asarray(res["agg%d" % j])
+            dt = np.dtype(_FIELD_DTYPE[t])
+            cols.append(a.view(dt) if a.dtype.itemsize == dt.itemsize else a.astype(dt))   # FIRST_* / SEL_* bits
+        return [(int(res["key"][i]), int(res["win_start"][i]), int(res["win_end"][i]),
+                 tuple(c[i].item() for c in cols)) for i in range(len(res["key"]))]
+
+
 class SlicingWindowProcessor(_Base):
     """Table window-TVF processor: one GPU processor replaces Slice{Shared,Unshared}WindowAggProcessor.
     Output rows are key ++ aggs ++ [window_start, window_end] (AbstractWindowAggProcessor.java:230-233)."""

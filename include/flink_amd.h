@@ -122,10 +122,14 @@ enum fwa_agg_kind {
  * Comparisons are Java compareTo (Long / Integer / Double.compare / Float.compare: -0.0 < 0.0, NaN above +Inf; a MIN
  * or MAX result NaN is returned canonical). SUM over Float is accumulated in double and rounded once (the reference
  * adds in float, in arrival order), over Double in device order (within the tolerance of SUM_F64).
- * A reduce handle is DATASTREAM, TUMBLE or SLIDE (non-merging windows), allowed lateness 0; at most one MINBY / MAXBY
- * aggregate, FWA_SEL_* only with it and FWA_FIRST_* only without it; COUNT / SUM / MIN / MAX over any type may be
- * listed; no DECIMAL, AVG, NULLs, record lists, partials or snapshots (FWA_E_UNSUPPORTED). A tuple
- * (key, f1, ..., fn) with sum(k) maps to FIRST_* for every fi, i != k, and SUM_* for fk; minBy(k) to SEL_* and MINBY_*. */
+ * A reduce handle is DATASTREAM, TUMBLE or SLIDE (non-merging windows), allowed lateness 0; every aggregate is a field
+ * of the reduced tuple: at most one MINBY / MAXBY, FWA_SEL_* only with it and FWA_FIRST_* only without it, SUM / MIN /
+ * MAX over any type; COUNT, AVG, DECIMAL, NULLs, record lists, partials and the heap layout are FWA_E_UNSUPPORTED.
+ * fwa_snapshot / fwa_restore work: an entry per (key, slice) holds the slice's reduced fields (acc_j: the field value,
+ * a 4-byte field zero-extended) and, in its count column, the arrival rank of the element it selected; a restore
+ * (any key-group split) pushes the entries back as elements in that order, so later windows equal an uninterrupted
+ * run. A tuple (key, f1, ..., fn) with sum(k) maps to FIRST_* for every fi, i != k, and SUM_* for fk; minBy(k) to
+ * SEL_* and MINBY_* (flink_amd/operators.py reduction_aggs). */
 /* DECIMAL aggregates (Table semantics; the input column's scale s in fwa_config.dec_scale[j]). Values are unscaled
  * integers in 16-byte little-endian two's complement ([i128]: low 8 bytes, then high 8 bytes).
  *  SUM: DecimalSumAggFunction (SumAggFunction.java:150-168): the exact sum at the result type of

@@ -661,7 +661,7 @@ int or_create(const fwa_config* c, or_engine** out) {
             nby += is_byk(k); nsel += (k == FWA_SEL_64 || k == FWA_SEL_32); nfirst += (k == FWA_FIRST_64 || k == FWA_FIRST_32);
             nred += k >= FWA_SUM_I32 && k <= FWA_SEL_32;
             if ((c->flags & FWA_CFG_REDUCE) && (is_dec(k) || k == FWA_AVG_I64 || k == FWA_AVG_F32 || k == FWA_AVG_F64 ||
-                                                k == FWA_COUNT_COL)) return FWA_E_UNSUPPORTED;
+                                                k == FWA_COUNT_COL || k == FWA_COUNT)) return FWA_E_UNSUPPORTED;
         }
         if (nred && !(c->flags & FWA_CFG_REDUCE)) return FWA_E_ARG;
         if (c->flags & FWA_CFG_REDUCE) {

@@ -225,16 +225,8 @@ REDUCE_FIELD_TYPES = ("I32", "F64", "I64")
 
 def reduce_aggs(op, pos, types=REDUCE_FIELD_TYPES):
     """The engine aggregate list for <op>(pos) over fields 1..len(types) (column = field - 1)."""
-    by = op in ("min_by", "max_by")
-    aggs = []
-    for f, t in enumerate(types, start=1):
-        width = "32" if t in ("I32", "F32") else "64"
-        if f != pos:
-            aggs.append((("SEL_" if by else "FIRST_") + width, f - 1))
-        else:
-            aggs.append(({"sum": "SUM_", "min": "MIN_", "max": "MAX_", "min_by": "MINBY_", "max_by": "MAXBY_"}[op] + t,
-                         f - 1))
-    return aggs
+    from flink_amd.operators import reduction_aggs
+    return reduction_aggs(op, pos, types)
 
 
 def load_reduce_kats():

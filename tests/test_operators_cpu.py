@@ -155,3 +155,28 @@ def test_slicing_processor_late_flags_shanghai(kind):
     proc.prepare_checkpoint()
     assert flagged == proc.num_late_records_dropped == case["late_dropped"]
     proc.close()
+
+
+@pytest.mark.parametrize("name", ["WindowOperatorTest.testTumblingEventTimeWindowsReduce",
+                                  "WindowOperatorTest.testSlidingEventTimeWindowsReduce"])
+def test_reduce_facade_on_sum_reducer_kats(name):
+    """WindowOperatorTest's SumReducer sequences (Tuple2<String, Integer>, WindowedStream.sum(1) semantics) through the
+    DataStream reduction facade (flink_amd.operators.ReduceWindowOperator) over the oracle."""
+    from flink_amd.operators import ReduceWindowOperator
+    case = KATS[name]
+    spec = (TumblingEventTimeWindows.of(case["size_ms"], case["offset_ms"]) if case["window_kind"] == "TUMBLE" else
+            SlidingEventTimeWindows.of(case["size_ms"], case["slide_ms"], case["offset_ms"]))
+    op = ReduceWindowOperator(spec, "sum", 1, ["I32"], batch_size=3, engine_factory=Oracle)
+    for ev in case["events"]:
+        if ev[0] == "e":
+            op.process_element(ev[1], [ev[2]], ev[3])
+        else:
+            got = sorted((r[0], r[1], r[2], r[3][0]) for r, ts in op.process_watermark(ev[1]))
+            assert got == sorted(tuple(x) for x in ev[2])
+    op.close()
+
+
+def test_reduction_aggs_of_windowed_stream_calls():
+    from flink_amd.operators import reduction_aggs
+    assert reduction_aggs("sum", 2, ["I64", "F64", "F32"]) == [("FIRST_64", 0), ("SUM_F64", 1), ("FIRST_32", 2)]
+    assert reduction_aggs("min_by", 3, ["I64", "F64", "F32"]) == [("SEL_64", 0), ("SEL_64", 1), ("MINBY_F32", 2)]

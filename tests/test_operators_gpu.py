@@ -85,3 +85,26 @@ def test_slicing_processor_late_flag_over_random_stream_on_gpu():
     flagged = sorted(i for i, f in enumerate(flags) if f)
     assert flagged == sorted(v[0] for _, v, _ in proc.late_records)
     proc.close()
+
+
+# WindowOperatorTest's reduce sequences (SumReducer over Tuple2<String, Integer>: WindowedStream.sum(1)'s semantics,
+# WindowOperatorTest.java:224,406,668) through the DataStream reduction facade on the GPU: non-merging, lateness 0
+REDUCE_KATS = [c for c in DS_KATS if c["window_kind"] in ("TUMBLE", "SLIDE") and c["allowed_lateness_ms"] == 0]
+
+
+@pytest.mark.parametrize("case", REDUCE_KATS, ids=[c["name"].split(" ")[0].split(".")[1] for c in REDUCE_KATS])
+@pytest.mark.parametrize("batch", [1, 1 << 20])
+def test_reduce_facade_on_gpu(case, batch):
+    from flink_amd.operators import ReduceWindowOperator
+    side = "side_output" in case
+    op = ReduceWindowOperator(_spec(case), "sum", 1, ["I32"], batch_size=batch, late_data_output=side,
+                              key_capacity=1 << 12)
+    for ev in case["events"]:
+        if ev[0] == "e":
+            op.process_element(ev[1], [ev[2]], ev[3])
+        else:
+            got = sorted((r[0], r[1], r[2], r[3][0]) for r, ts in op.process_watermark(ev[1]))
+            assert got == sorted(tuple(x) for x in ev[2]), case["name"]
+    if not side:
+        assert op.num_late_records_dropped == case["late_dropped"]
+    op.close()
