@@ -34,6 +34,7 @@
 
 #include "../../include/flink_amd.h"
 #include "java_math.h"
+#include "dec_view.h"
 
 #define LONG_MIN_J ((int64_t)0x8000000000000000LL)
 #define LONG_MAX_J ((int64_t)0x7fffffffffffffffLL)
@@ -2419,6 +2420,22 @@ int fwa_get_config(const fwa_engine* e, fwa_config* out) {
     return FWA_OK;
 }
 int fwa_set_error(fwa_engine* e, int code, const char* msg) { return fail(e, code, msg); }
+int fwa_dec_view(const fwa_engine* e, FwaDecView* v) {
+    if (!e || !v) return FWA_E_ARG;
+    memset(v, 0, sizeof(*v));
+    if (!e->dec) return FWA_OK;
+    v->active = 1;
+    v->icfg = e->cfg;
+    v->icfg.tz = e->tz.empty() ? nullptr : e->tz.data();
+    for (int j = 0; j < e->dec->ucfg.num_aggs; ++j) {
+        const DecAggMap& m = e->dec->d[j];
+        v->umap[j] = m.kind ? -1 : e->dec->umap[j];
+        v->npc[j] = m.kind ? m.npc : 0;
+        for (int k = 0; k < 4; ++k) v->pc[j][k] = m.pc_agg[k];
+        v->cnt[j] = m.kind ? m.cnt_agg : -1;
+    }
+    return FWA_OK;
+}
 
 void fwa_destroy(fwa_engine* e) {
     if (!e) return;

@@ -32,7 +32,10 @@
 //   TABLE SESSION      legacy Table WindowOperator: 0 session-window-mapping (MapSerializer of TimeWindow pairs under
 //                      VoidNamespace), 1 window-aggs (TimeWindow namespace, BinaryRowData key and accumulator), timers
 //                      at toEpochMillsForTimer(maxTimestamp) per in-flight session.
-// PREHASHED keys: FWA_E_UNSUPPORTED (FWASNAP1 covers them).
+// DECIMAL SUM / AVG (Table): the accumulator field is the DECIMAL(38, s) running sum (findSumAggType), rebuilt from the
+// engine's 32-bit piece sums (decimal.inc) and written as a non-compact DecimalData; AVG's count is COUNT(*) or the
+// column's hidden non-NULL counter, already in the row.
+// PREHASHED keys and DataStream reductions: FWA_E_UNSUPPORTED (FWASNAP1 covers them).
 #include <algorithm>
 #include <cstdint>
 #include <map>
@@ -45,6 +48,7 @@
 
 #include "../../include/flink_amd.h"
 #include "java_math.h"
+#include "dec_view.h"
 
 namespace {
 
@@ -105,7 +109,93 @@ struct Out {
         for (int i = 0; i < arity; ++i) le64(isnull && isnull[i] ? 0 : f[i]);
     }
     void raw_row(const std::vector<uint8_t>& r) { i32((int64_t)r.size()); b.insert(b.end(), r.begin(), r.end()); }
+    // an accumulator row whose fields with isdec[i] are DECIMAL(38, s) -- non-compact (DecimalData.isCompact: precision
+    // > 18), so RowDataSerializer.toBinaryRow (:196-212) writes them with AbstractBinaryWriter.writeDecimal (:164-196):
+    // 16 zeroed bytes reserved in the variable-length part, toUnscaledBytes at their start, slot = offset << 32 |
+    // length; a NULL field goes through setNullAt instead (null bit, slot 0, nothing reserved)
+    void acc_row(const uint64_t* f, int arity, const bool* isnull, const bool* isdec, const std::vector<uint8_t>* decb) {
+        const int nb = ((arity + 63 + 8) / 64) * 8;
+        std::vector<uint8_t> r((size_t)nb + 8 * (size_t)arity, 0);
+        for (int i = 0; i < arity; ++i) {
+            uint64_t v = f[i];
+            if (isnull[i]) {
+                r[(size_t)(i + 8) / 8] |= (uint8_t)(1u << ((i + 8) % 8));
+                v = 0;
+            } else if (isdec[i]) {
+                v = ((uint64_t)r.size() << 32) | (uint64_t)decb[i].size();
+                r.insert(r.end(), decb[i].begin(), decb[i].end());
+                r.resize(r.size() + 16 - decb[i].size(), 0);
+            }
+            for (int k = 0; k < 8; ++k) r[(size_t)nb + 8 * i + k] = (uint8_t)(v >> (8 * k));
+        }
+        raw_row(r);
+    }
 };
+
+typedef __int128 i128;
+typedef unsigned __int128 u128;
+
+i128 dec_bound() { i128 r = 1; for (int i = 0; i < 38; ++i) r *= 10; return r; }   // 10^38
+
+// A DECIMAL aggregate's window total T = sum_k S_k * 2^(32k) from the engine's piece sums (decimal.inc: the pieces below
+// the top one unsigned, the top one signed), in 192-bit two's complement. false: |T| has more than 38 digits
+// (DecimalData.fromBigDecimal returns NULL, DecimalData.java:184-195).
+bool dec_total(const uint64_t* S, int npc, i128* out) {
+    uint64_t t[3] = {0, 0, 0};
+    for (int k = 0; k < npc; ++k) {
+        const uint64_t ext = (k == npc - 1 && (int64_t)S[k] < 0) ? ~0ull : 0ull;
+        const uint64_t src[4] = {S[k], ext, ext, ext};
+        const int li = (32 * k) / 64, bs = (32 * k) % 64;
+        u128 carry = 0;
+        for (int m = 0; m < 3; ++m) {
+            const int i = m - li;
+            const uint64_t lo = i >= 0 ? src[i] : 0, prev = i >= 1 ? src[i - 1] : 0;
+            const uint64_t w = bs == 0 ? lo : (lo << bs) | (prev >> (64 - bs));
+            const u128 a = (u128)t[m] + w + carry;
+            t[m] = (uint64_t)a;
+            carry = a >> 64;
+        }
+    }
+    if (t[2] != (((int64_t)t[1] < 0) ? ~0ull : 0ull)) return false;
+    const i128 v = (i128)(((u128)t[1] << 64) | t[0]);
+    if (v >= dec_bound() || v <= -dec_bound()) return false;
+    *out = v;
+    return true;
+}
+
+// The inverse for a restore: piece sums totalling T. Two pieces (int64 input) hold |T| < 2^95 only.
+bool dec_split(i128 T, int npc, uint64_t* S) {
+    const u128 u = (u128)T;
+    if (npc == 2) {
+        const i128 hi = T >> 32;
+        if (hi > (i128)INT64_MAX || hi < (i128)INT64_MIN) return false;
+        S[0] = (uint64_t)(u & 0xffffffffu);
+        S[1] = (uint64_t)(int64_t)hi;
+        return true;
+    }
+    S[0] = (uint64_t)(u & 0xffffffffu);
+    S[1] = (uint64_t)((u >> 32) & 0xffffffffu);
+    S[2] = (uint64_t)((u >> 64) & 0xffffffffu);
+    S[3] = (uint64_t)(int64_t)(T >> 96);
+    return true;
+}
+
+// DecimalData.toUnscaledBytes (BigInteger.toByteArray): minimal big-endian two's complement, and back
+std::vector<uint8_t> dec_bytes(i128 v) {
+    uint8_t b[16];
+    const u128 u = (u128)v;
+    for (int i = 0; i < 16; ++i) b[i] = (uint8_t)(u >> (8 * (15 - i)));
+    int st = 0;
+    while (st < 15 && ((b[st] == 0x00 && !(b[st + 1] & 0x80)) || (b[st] == 0xff && (b[st + 1] & 0x80)))) ++st;
+    return std::vector<uint8_t>(b + st, b + 16);
+}
+bool dec_of_bytes(const uint8_t* p, uint64_t len, i128* v) {
+    if (len < 1 || len > 16) return false;
+    u128 u = (p[0] & 0x80) ? ~(u128)0 : 0;
+    for (uint64_t i = 0; i < len; ++i) u = (u << 8) | p[i];
+    *v = (i128)u;
+    return true;
+}
 
 struct In {
     const uint8_t* p;
@@ -132,6 +222,26 @@ struct In {
             else if (nl) ok = false;                                  // a NULL where the layout has none
         }
         for (int i = 0; i < arity; ++i) f[i] = get(8, true);
+    }
+    // an accumulator row (Out::acc_row): DECIMAL fields (isdec) read from the variable-length part into decv
+    void acc_row(uint64_t* f, int arity, bool* isnull, const bool* isdec, i128* decv) {
+        const int nb = ((arity + 63 + 8) / 64) * 8;
+        bool anydec = false;
+        for (int i = 0; i < arity; ++i) anydec |= isdec[i];
+        const int64_t size = i32();
+        if (!ok || size < nb + 8 * arity || (!anydec && size != nb + 8 * arity) || at + size > n) { ok = false; return; }
+        const uint8_t* r = p + at;
+        at += size;
+        if (r[0] != 0) ok = false;                                    // RowKind INSERT
+        for (int i = 0; i < arity; ++i) {
+            isnull[i] = (r[(i + 8) / 8] >> ((i + 8) % 8)) & 1;
+            uint64_t v = 0;
+            for (int k = 0; k < 8; ++k) v |= (uint64_t)r[nb + 8 * i + k] << (8 * k);
+            f[i] = isnull[i] ? 0 : v;
+            if (!isdec[i] || isnull[i]) continue;
+            const uint64_t off = v >> 32, len = v & 0xffffffffull;
+            if (off < (uint64_t)(nb + 8 * arity) || off + len > (uint64_t)size || !dec_of_bytes(r + off, len, &decv[i])) ok = false;
+        }
     }
     // a key row with STRING fields (the inverse of str_row_bytes): slots of the other fields, null bits, values;
     // *raw = the row's bytes (BinaryRowData equality is byte equality)
@@ -170,8 +280,8 @@ struct In {
 bool supported(const fwa_config& c, bool dict = false) {
     if (c.key_kind == FWA_KEY_PREHASHED) return false;
     if (c.flags & FWA_CFG_REDUCE) return false;                        // a reduction keeps the reduced element
-    for (int j = 0; j < c.num_aggs; ++j)                               // DECIMAL: no engine-side DecimalData writer
-        if (c.aggs[j].kind >= FWA_SUM_DEC) return false;
+    for (int j = 0; j < c.num_aggs; ++j)                               // reduce kinds: the reduced element, no ACC
+        if (c.aggs[j].kind >= FWA_SUM_I32) return false;
     if ((c.key_kind == FWA_KEY_GROUP_PREFIXED) != dict) return false;   // dictionary ids <=> a key dictionary
     if (dict && c.semantics != FWA_SEM_TABLE) return false;            // BinaryRowData keys: Table only
     if (c.semantics == FWA_SEM_DATASTREAM)
@@ -179,8 +289,8 @@ bool supported(const fwa_config& c, bool dict = false) {
     return c.window_kind == FWA_TUMBLE || c.window_kind == FWA_SLIDE || c.window_kind == FWA_CUMULATE ||
            c.window_kind == FWA_SESSION;
 }
-const char* kUnsupported = "heap layout: DataStream TUMBLE / SLIDE / SESSION and Table TUMBLE / HOP / CUMULATE / SESSION "
-                           "with a computable key hash";
+const char* kUnsupported = "heap layout: DataStream TUMBLE / SLIDE / SESSION aggregates and Table TUMBLE / HOP / CUMULATE / "
+                           "SESSION with a computable key hash";
 
 int64_t gcd64(int64_t a, int64_t b) { while (b) { const int64_t t = a % b; a = b; b = t; } return a; }
 
@@ -234,6 +344,82 @@ int hidden_map(const fwa_config& c, int* hid) {
         hid[j] = of_col[col];
     }
     return nh;
+}
+
+// The heap row of an accumulator against the engine's FWASNAP1 words. The heap row (the shim's ACC type) follows the
+// caller's configuration: COUNT(*), one field per aggregate, one BIGINT per hidden non-NULL counter (hidden_map). A
+// handle with DECIMAL aggregates runs an internal configuration (decimal.inc dec_plan) and its FWASNAP1 words follow
+// that one: COUNT(*), the internal aggregates (the caller's others in order, the 32-bit piece sums, the counts) and the
+// internal hidden counters; a DECIMAL field is the window total of its piece sums. Without DECIMAL both coincide.
+enum { W_COUNT = 0, W_FIELD = 1, W_PIECE = 2, W_HIDDEN = 3 };
+struct AccMap {
+    fwa_config ic;                          // the configuration of the FWASNAP1 words
+    int na = 0, nh = 0, ina = 0, inh = 0;   // caller / internal aggregates and hidden counters
+    int hid[FWA_MAX_AGGS];                  // caller aggregate -> its hidden counter (-1: none)
+    int uw[FWA_MAX_AGGS];                   // caller non-DECIMAL aggregate -> its word (-1: DECIMAL)
+    int npc[FWA_MAX_AGGS];                  // caller DECIMAL aggregate: 2 / 4 piece sums (0: not DECIMAL) ...
+    int pw[FWA_MAX_AGGS][4];                // ... and their words
+    int hw[FWA_MAX_COLS];                   // caller hidden counter -> its word
+    // restore: the source of each word (W_*), with the caller aggregate / hidden counter (sa) and piece (sk)
+    int src[1 + FWA_MAX_AGGS + FWA_MAX_COLS], sa[1 + FWA_MAX_AGGS + FWA_MAX_COLS], sk[1 + FWA_MAX_AGGS + FWA_MAX_COLS];
+    bool any_dec = false;
+};
+bool acc_map(const fwa_config& c, const FwaDecView& v, AccMap* m) {
+    m->ic = v.active ? v.icfg : c;
+    m->na = c.num_aggs;
+    m->nh = hidden_map(c, m->hid);
+    int ihid[FWA_MAX_AGGS];
+    m->ina = m->ic.num_aggs;
+    m->inh = hidden_map(m->ic, ihid);
+    int ih_of_col[FWA_MAX_COLS], uh_of_col[FWA_MAX_COLS], col_of_ih[FWA_MAX_COLS], col_of_uh[FWA_MAX_COLS];
+    for (int k = 0; k < FWA_MAX_COLS; ++k) ih_of_col[k] = uh_of_col[k] = col_of_ih[k] = col_of_uh[k] = -1;
+    for (int i = 0; i < m->ina; ++i)
+        if (ihid[i] >= 0) { ih_of_col[m->ic.aggs[i].col] = ihid[i]; col_of_ih[ihid[i]] = m->ic.aggs[i].col; }
+    for (int j = 0; j < m->na; ++j)
+        if (m->hid[j] >= 0) { uh_of_col[c.aggs[j].col] = m->hid[j]; col_of_uh[m->hid[j]] = c.aggs[j].col; }
+    for (int h = 0; h < m->nh; ++h) {
+        const int ih = ih_of_col[col_of_uh[h]];
+        if (ih < 0) return false;
+        m->hw[h] = 1 + m->ina + ih;
+    }
+    const int nw = 1 + m->ina + m->inh;
+    for (int w = 0; w < nw; ++w) m->src[w] = m->sa[w] = m->sk[w] = -1;
+    m->src[0] = W_COUNT;
+    for (int j = 0; j < m->na; ++j) {
+        m->npc[j] = (v.active && v.umap[j] < 0) ? v.npc[j] : 0;
+        if (m->npc[j]) {
+            m->any_dec = true;
+            m->uw[j] = -1;
+            for (int k = 0; k < m->npc[j]; ++k) m->pw[j][k] = 1 + v.pc[j][k];
+        } else {
+            m->uw[j] = 1 + (v.active ? v.umap[j] : j);
+            m->src[m->uw[j]] = W_FIELD;
+            m->sa[m->uw[j]] = j;
+        }
+    }
+    for (int j = 0; j < m->na; ++j)                      // piece sums shared by a SUM and an AVG of one column: the same
+        for (int k = 0; k < m->npc[j]; ++k) {            // total, any of them
+            const int w = m->pw[j][k];
+            if (m->src[w] < 0) { m->src[w] = W_PIECE; m->sa[w] = j; m->sk[w] = k; }
+        }
+    for (int i = 0; i < m->ina; ++i) {                   // the counts DECIMAL aggregates added
+        const int w = 1 + i;
+        if (m->src[w] >= 0) continue;
+        if (m->ic.aggs[i].kind == FWA_COUNT) m->src[w] = W_COUNT;
+        else if (m->ic.aggs[i].kind == FWA_COUNT_COL && uh_of_col[m->ic.aggs[i].col] >= 0) {
+            m->src[w] = W_HIDDEN;
+            m->sa[w] = uh_of_col[m->ic.aggs[i].col];
+        } else {
+            return false;
+        }
+    }
+    for (int ih = 0; ih < m->inh; ++ih) {
+        const int w = 1 + m->ina + ih, uh = uh_of_col[col_of_ih[ih]];
+        if (uh < 0) return false;
+        m->src[w] = W_HIDDEN;
+        m->sa[w] = uh;
+    }
+    return true;
 }
 
 // Key rows of a key dictionary (fwa_keydict, multi-column Table keys): the slots and null bits of every row so far,
@@ -433,21 +619,28 @@ static int snapshot_heap_impl(fwa_engine* e, fwa_keydict* dict, fwa_blob* out, i
     const bool sess = c.window_kind == FWA_SESSION;
     const bool ds_slide = ds && c.window_kind == FWA_SLIDE;
     const Ids id = ids_of(c);
-    int hid[FWA_MAX_AGGS];
-    const int nh = hidden_map(c, hid);
-    const int na = (int)s.naggs, arity = 1 + na + nh;
+    FwaDecView dv;
+    AccMap am;
+    if ((rc = fwa_dec_view(e, &dv)) || !acc_map(c, dv, &am) || am.ina != (int)s.naggs || am.inh != (int)s.nh) {
+        fwa_blob_free(&snap);
+        return fwa_set_error(e, FWA_E_STATE, "heap layout: accumulator words do not match the configuration");
+    }
+    const int na = am.na, nh = am.nh, ina = am.ina, inh = am.inh, arity = 1 + na + nh;
+    const int* hid = am.hid;
     const int64_t n = s.n, g = ds ? (ds_slide ? gcd64(c.size_ms, c.slide_ms) : s.size) : slice_width(c);
-    auto end_of = [&](int64_t i) { return sess ? s.col[(3 + na + nh) * n + i] : s.col[n + i] + g; };
+    auto end_of = [&](int64_t i) { return sess ? s.col[(3 + ina + inh) * n + i] : s.col[n + i] + g; };
     const bool fired_any = s.wm != INT64_MIN;
     Out o;
     std::vector<uint64_t> f((size_t)arity);
     std::vector<uint8_t> fnull((size_t)arity);
+    bool isdec[1 + FWA_MAX_AGGS + FWA_MAX_COLS] = {};
+    std::vector<uint8_t> decb[1 + FWA_MAX_AGGS + FWA_MAX_COLS];
     struct Row { int64_t key, start, end; uint64_t w[1 + FWA_MAX_AGGS + FWA_MAX_COLS]; };
     std::vector<Row> rows;
-    auto merge_into = [&](Row& a, const Row& b) {
+    auto merge_into = [&](Row& a, const Row& b) {                  // on the FWASNAP1 words
         a.w[0] += b.w[0];
-        for (int j = 0; j < na; ++j) a.w[1 + j] = merge_word(s.agg[j], a.w[1 + j], b.w[1 + j]);
-        for (int h = 0; h < nh; ++h) a.w[1 + na + h] += b.w[1 + na + h];
+        for (int j = 0; j < ina; ++j) a.w[1 + j] = merge_word(s.agg[j], a.w[1 + j], b.w[1 + j]);
+        for (int h = 0; h < inh; ++h) a.w[1 + ina + h] += b.w[1 + ina + h];
     };
     for (int64_t kg = c.kg_start; kg <= c.kg_end; ++kg) {
         kg_offsets[kg - c.kg_start] = (int64_t)o.b.size();
@@ -460,7 +653,7 @@ static int snapshot_heap_impl(fwa_engine* e, fwa_keydict* dict, fwa_blob* out, i
         for (int64_t i = lo; i < hi; ++i) {
             Row r{s.col[i], s.col[n + i], end_of(i), {}};
             r.w[0] = (uint64_t)s.col[2 * n + i];
-            for (int j = 0; j < na + nh; ++j) r.w[1 + j] = (uint64_t)s.col[(3 + j) * n + i];
+            for (int j = 0; j < ina + inh; ++j) r.w[1 + j] = (uint64_t)s.col[(3 + j) * n + i];
             rows.push_back(r);
         }
         if (ds_slide) {
@@ -514,12 +707,22 @@ static int snapshot_heap_impl(fwa_engine* e, fwa_keydict* dict, fwa_blob* out, i
                 f[0] = r.w[0];
                 fnull[0] = 0;
                 for (int j = 0; j < na; ++j) {
-                    f[1 + j] = acc_to_field(s.agg[j], r.w[1 + j]);
-                    // SQL: an aggregate whose input column held only NULLs has a NULL buffer (Sum/Min/MaxAggFunction);
-                    // COUNT(col) is the counter itself
-                    fnull[1 + j] = hid[j] >= 0 && s.agg[j] != FWA_COUNT_COL && r.w[1 + na + hid[j]] == 0;
+                    const int64_t kind = c.aggs[j].kind;
+                    // SQL: an aggregate whose input column held only NULLs has a NULL buffer (Sum/Min/MaxAggFunction,
+                    // DecimalSum/AvgAggFunction); COUNT(col) is the counter itself
+                    fnull[1 + j] = hid[j] >= 0 && kind != FWA_COUNT_COL && r.w[am.hw[hid[j]]] == 0;
+                    isdec[1 + j] = am.npc[j] != 0;
+                    if (!am.npc[j]) { f[1 + j] = acc_to_field(kind, r.w[am.uw[j]]); continue; }
+                    // DECIMAL: the running sum DECIMAL(38, s); NULL past 38 digits (the engine decides on the exact
+                    // total, include/flink_amd.h)
+                    uint64_t S[4];
+                    i128 T = 0;
+                    for (int k = 0; k < am.npc[j]; ++k) S[k] = r.w[am.pw[j][k]];
+                    if (!dec_total(S, am.npc[j], &T)) fnull[1 + j] = 1;
+                    f[1 + j] = 0;
+                    decb[1 + j] = dec_bytes(T);
                 }
-                for (int h = 0; h < nh; ++h) { f[1 + na + h] = r.w[1 + na + h]; fnull[1 + na + h] = 0; }
+                for (int h = 0; h < nh; ++h) { f[1 + na + h] = r.w[am.hw[h]]; fnull[1 + na + h] = 0; }
                 if (ds) {
                     o.i64((uint64_t)start); o.i64((uint64_t)end);          // TimeWindow.Serializer
                     o.i64((uint64_t)key);                                  // LongSerializer
@@ -530,7 +733,7 @@ static int snapshot_heap_impl(fwa_engine* e, fwa_keydict* dict, fwa_blob* out, i
                     keys_ok = key_row(o, key) && keys_ok;                  // key row
                     bool nl[1 + FWA_MAX_AGGS + FWA_MAX_COLS];
                     for (int k = 0; k < arity; ++k) nl[k] = fnull[k] != 0;
-                    o.row(f.data(), arity, nl);                            // accumulator row
+                    o.acc_row(f.data(), arity, nl, isdec, decb);           // accumulator row
                 }
             }
         };
@@ -622,11 +825,17 @@ static int restore_heap_impl(fwa_engine* e, fwa_keydict* dict, const void* const
     const bool sess = c.window_kind == FWA_SESSION;
     const bool ds_slide = ds && c.window_kind == FWA_SLIDE;
     const Ids id = ids_of(c);
-    int hid[FWA_MAX_AGGS];
-    const int nh = hidden_map(c, hid);
-    const int na = c.num_aggs, arity = 1 + na + nh, maxp = c.max_parallelism;
+    FwaDecView dv;
+    AccMap am;
+    if ((rc = fwa_dec_view(e, &dv)) || !acc_map(c, dv, &am))
+        return fwa_set_error(e, FWA_E_STATE, "heap layout: accumulator words do not match the configuration");
+    const int na = am.na, nh = am.nh, ina = am.ina, inh = am.inh, arity = 1 + na + nh, maxp = c.max_parallelism;
+    const fwa_config& ic = am.ic;
+    bool isdec[1 + FWA_MAX_AGGS + FWA_MAX_COLS] = {};
+    for (int j = 0; j < na; ++j) isdec[1 + j] = am.npc[j] != 0;
     const int64_t g = ds ? c.size_ms : slice_width(c);
-    const int64_t ncols = (sess ? 4 : 3) + na + nh;
+    const int64_t ncols = (sess ? 4 : 3) + ina + inh;
+    bool dec_range = true;
     std::vector<std::vector<int64_t>> blobs((size_t)n_bodies);
     std::vector<const void*> ptrs;
     std::vector<int64_t> bsz;
@@ -636,15 +845,28 @@ static int restore_heap_impl(fwa_engine* e, fwa_keydict* dict, const void* const
         int64_t lo = maxp, hi = -1, total = 0;
         std::vector<uint64_t> f((size_t)arity);
         bool fnull[1 + FWA_MAX_AGGS + FWA_MAX_COLS];
+        i128 decv[1 + FWA_MAX_AGGS + FWA_MAX_COLS] = {};
         struct Pending { int64_t kg, key, start, end; std::vector<int64_t> w; };
         std::vector<Pending> pend;
         std::map<std::tuple<int64_t, int64_t, int64_t>, std::pair<int64_t, int64_t>> actual;
-        // the engine's words of one accumulator tuple / row: COUNT(*), each aggregate (NULL: its identity), counters
+        // the engine's words of one accumulator tuple / row (AccMap): COUNT(*), each aggregate (NULL: its identity),
+        // the piece sums of a DECIMAL total (NULL: 0 -- the reference's next value restarts a NULL sum,
+        // DecimalSumAggFunction), the counts, the hidden counters
         auto words = [&](std::vector<int64_t>& v) {
-            v.push_back((int64_t)f[0]);
+            uint64_t S[FWA_MAX_AGGS][4] = {};
             for (int j = 0; j < na; ++j)
-                v.push_back((int64_t)(fnull[1 + j] ? identity_word(c.aggs[j].kind) : field_to_acc(c.aggs[j].kind, f[1 + j])));
-            for (int h = 0; h < nh; ++h) v.push_back((int64_t)f[1 + na + h]);
+                if (am.npc[j] && !fnull[1 + j] && !dec_split(decv[1 + j], am.npc[j], S[j])) dec_range = false;
+            for (int w = 0; w < 1 + ina + inh; ++w) {
+                const int j = am.sa[w];
+                switch (am.src[w]) {
+                    case W_COUNT: v.push_back((int64_t)f[0]); break;
+                    case W_FIELD:
+                        v.push_back((int64_t)(fnull[1 + j] ? identity_word(c.aggs[j].kind) : field_to_acc(c.aggs[j].kind, f[1 + j])));
+                        break;
+                    case W_PIECE: v.push_back((int64_t)S[j][am.sk[w]]); break;
+                    default: v.push_back((int64_t)f[1 + na + j]); break;
+                }
+            }
         };
         std::map<int64_t, std::map<int64_t, Words>> slide_win;    // DataStream SLIDE: key -> window start -> words
         std::vector<std::pair<int64_t, Words>> slices;
@@ -719,7 +941,7 @@ static int restore_heap_impl(fwa_engine* e, fwa_keydict* dict, const void* const
                         start = sess ? in.i64() : 0;                   // Table sessions: TimeWindow namespace
                         end = in.i64();
                         key = read_key(in);
-                        in.row(f.data(), arity, fnull);
+                        in.acc_row(f.data(), arity, fnull, isdec, decv);
                         if (fnull[0]) in.ok = false;                   // COUNT(*) is never NULL
                         if (!sess) start = end - g;
                     }
@@ -770,6 +992,8 @@ static int restore_heap_impl(fwa_engine* e, fwa_keydict* dict, const void* const
             slide_win.clear();
         }
         if (!in.ok) return fwa_set_error(e, FWA_E_ARG, "heap body: truncated or malformed");
+        if (!dec_range)
+            return fwa_set_error(e, FWA_E_UNSUPPORTED, "heap body: a DECIMAL sum of a DECIMAL(p <= 18) column past 2^95");
         if (dict && !comp_nulls.empty()) {                            // placeholder keys -> dictionary ids
             std::vector<int64_t> ids(comp_nulls.size());
             rc = dstr ? fwa_keydict_encode_host_str(dict, comp_slots.data(), comp_nulls.data(), comp_strs, (int64_t)ids.size(),
@@ -791,11 +1015,11 @@ static int restore_heap_impl(fwa_engine* e, fwa_keydict* dict, const void* const
         w.assign((size_t)(kHdr + maxp + 1 + total * ncols), 0);
         w[0] = (int64_t)kMagic; w[1] = 1; w[2] = c.window_kind; w[3] = c.semantics; w[4] = c.size_ms;
         w[5] = c.slide_ms; w[6] = c.offset_ms; w[7] = c.gap_ms; w[8] = c.allowed_lateness_ms; w[9] = maxp;
-        w[10] = c.key_kind; w[11] = na;
-        for (int j = 0; j < na; ++j) w[12 + j] = c.aggs[j].kind;
+        w[10] = c.key_kind; w[11] = ina;                              // the internal configuration's words (AccMap)
+        for (int j = 0; j < ina; ++j) w[12 + j] = ic.aggs[j].kind;
         w[20] = watermarks[b]; w[21] = total; w[22] = hi >= 0 ? lo : 0; w[23] = hi >= 0 ? hi : maxp - 1;
-        w[24] = c.nullable_cols; w[25] = nh;
-        for (int j = 0; j < na; ++j) w[26] |= (int64_t)(c.aggs[j].col & 15) << (4 * j);
+        w[24] = ic.nullable_cols; w[25] = inh;
+        for (int j = 0; j < ina; ++j) w[26] |= (int64_t)(ic.aggs[j].col & 15) << (4 * j);
         int64_t* koff = w.data() + kHdr;
         int64_t* body = koff + maxp + 1;
         int64_t d = 0;

@@ -405,13 +405,18 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
  *     written as its own state window.
  *   Table: namespace Long slice end (local time under a shift time zone), key BinaryRowData(BIGINT), value a
  *     BinaryRowData of COUNT(*), one field per aggregate (NULL bit set when the aggregate saw only NULLs) and one
- *     BIGINT per hidden non-NULL counter of a nullable handle; a CUMULATE window's fired slices are folded into its
+ *     BIGINT per hidden non-NULL counter of a nullable handle; a DECIMAL SUM / AVG field is the DECIMAL(38, s)
+ *     running sum as a non-compact DecimalData (AbstractBinaryWriter.writeDecimal: 16 bytes in the variable-length
+ *     part, BigInteger.toByteArray), NULL past 38 digits; a CUMULATE window's fired slices are folded into its
  *     first slice (the shared state SliceSharedWindowAggProcessor keeps); one timer per (key, first unfired window
  *     end of each live slice) at toEpochMillsForTimer(window end - 1) (UTC: window end - 1).
+ *   DATASTREAM SLIDE (WindowOperator per-window state, merged from the engine's slices) and TABLE SESSION (the legacy
+ *     Table WindowOperator: 0 "session-window-mapping", 1 "window-aggs", 2 / 3 timers) are written as
+ *     flink_amd/csrc/heap_snapshot.cpp describes.
  * kg_offsets[g - kg_start] receives the byte offset of key group g's section (KeyGroupRangeOffsets; the Java shim
  * writes its KeyedBackendSerializationProxy header in front and shifts them), *watermark the operator watermark
- * (union list state, SlicingWindowOperator.java:204-209). DataStream SLIDE / CUMULATE, Table SESSION or PREHASHED
- * keys: FWA_E_UNSUPPORTED (fwa_snapshot covers them). The blob is freed with fwa_blob_free. */
+ * (union list state, SlicingWindowOperator.java:204-209). PREHASHED keys and DataStream reductions (FWA_CFG_REDUCE):
+ * FWA_E_UNSUPPORTED (fwa_snapshot covers them). The blob is freed with fwa_blob_free. */
 int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark);
 
 /* Restore a fresh handle from heap-layout bodies (as written by fwa_snapshot_heap on handles with the same window

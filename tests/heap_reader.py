@@ -126,6 +126,33 @@ def ser_binrow(arity):
     return rd
 
 
+def ser_binrow_dec(arity, dec):
+    """BinaryRowDataSerializer of an accumulator row whose fields in `dec` are non-compact DECIMALs (precision > 18):
+    AbstractBinaryWriter.writeDecimal reserves 16 bytes per non-NULL one in the variable-length part, slot = offset <<
+    32 | length, the bytes DecimalData.toUnscaledBytes (minimal big-endian two's complement; the reader asserts the
+    minimal form); a NULL one is setNullAt (slot 0). -> (RowKind, null flags, fields; DECIMALs as Python ints)"""
+    def rd(r):
+        size = r.get(">i")
+        nb = ((arity + 63 + 8) // 64) * 8
+        row = r.raw(size)
+        assert size == nb + 8 * arity + 16 * sum(1 for i in dec if not (row[(i + 8) // 8] >> ((i + 8) % 8)) & 1)
+        nulls = [bool((row[(i + 8) // 8] >> ((i + 8) % 8)) & 1) for i in range(arity)]
+        f = [struct.unpack_from("<Q", row, nb + 8 * i)[0] for i in range(arity)]
+        for i in dec:
+            if nulls[i]:
+                assert f[i] == 0
+                continue
+            off, ln = f[i] >> 32, f[i] & 0xFFFFFFFF
+            assert nb + 8 * arity <= off and off + 16 <= size and 1 <= ln <= 16
+            assert not any(row[off + ln:off + 16]), "the reserved 16 bytes are zero past the value"
+            v = int.from_bytes(row[off:off + ln], "big", signed=True)
+            jbl = v.bit_length() if v >= 0 else (~v).bit_length()      # BigInteger.bitLength
+            assert ln == jbl // 8 + 1, "toUnscaledBytes is BigInteger.toByteArray (minimal)"
+            f[i] = v
+        return row[0], nulls, f
+    return rd
+
+
 # ------------------------------------------------------------------------------------------------
 # OperatorSnapshotUtil wrapper -> managed keyed state handles
 
