@@ -4432,8 +4432,14 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     if (!e->d_upos) HIPCHK(e, hipMalloc(&e->d_upos, sizeof(void*) * kSlideMaxU));
     int rc = upload(e, e->d_upos, up.data(), sizeof(void*) * m);
     if (rc) return rc;
-    // every present key emits at most one row per window: with the key count exact after the settled push the
-    // output bound holds, so the launch (which clears slices as it reads them) runs exactly once
+    // every present key emits at most one row per window. A launch that clears retiring slices as it reads them must
+    // run exactly once, so its bound comes from the device's own key count (every key inserted so far), not from the
+    // host copy of the last status sync
+    if (!cleared.empty()) {
+        HIPCHK(e, hipMemcpyAsync(&e->h_st->n_keys, &e->d_st->n_keys, sizeof(e->h_st->n_keys), hipMemcpyDeviceToHost,
+                                 e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+    }
     const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
     rc = ensure_out(e, nw * nkeys);
     if (rc) return rc;

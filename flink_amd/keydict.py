@@ -4,7 +4,9 @@ A Table job keyed by several fixed-length columns has BinaryRowData keys; KeyDic
 BinaryRowData.hashCode() (BinaryRowData.java:452-454, MurmurHashUtils.hashBytesByWords :92-170) on the GPU and maps
 each distinct key row to an id carrying its key group (bits 48-63). An engine created with
 key_kind=A.KEY_GROUP_PREFIXED aggregates on those ids; `decode` maps fired rows back to the key columns.
-Columns are torch CUDA tensors (int64 BIGINT, int32 INT, float64 DOUBLE) or numpy arrays (copied to the device); a
+Columns are torch CUDA tensors of exactly the column's dtype (int64 BIGINT, int32 INT, float64 DOUBLE) or numpy
+arrays (copied to the device); a host (CPU) torch tensor or a tensor of another dtype raises TypeError (the kernels
+would read a host pointer or past the column's end), so callers holding CPU tensors pass `.numpy()` or `.cuda()`. A
 STRING column is a sequence of str / bytes (UTF-8), or an (offsets int32 [n + 1], bytes uint8) pair of tensors.
 """
 import ctypes as C

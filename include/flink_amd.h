@@ -139,12 +139,19 @@ enum fwa_agg_kind {
  *       DecimalDataUtils.divide (DecimalDataUtils.java:40,145-148) into findAvgAggType's DECIMAL(38, max(6, s))
  *       (LogicalTypeMerging.java:261-277): the quotient rounded HALF_UP to 38 significant digits, then HALF_UP to the
  *       result scale; NULL past 38 digits or with no non-NULL input.
- * Overflow is decided on the window's exact total. The reference decides it on each running sum in arrival order (a
- * SUM whose running sum overflowed restarts from the next value): results differ only for windows in which a
- * running sum passes 38 digits. A (key, window) may hold up to 2^32 - 1 records (FWA_E_UNSUPPORTED at the fire
- * beyond). Internally each DECIMAL source column is summed as 2 (int64 input) or 4 (16-byte) 32-bit pieces, each one of
- * the handle's FWA_MAX_AGGS aggregates, plus a count; a list past that budget is FWA_E_UNSUPPORTED at fwa_create. Not
- * available for fwa_drain_partials / fwa_push_partials / fwa_snapshot_heap (FWA_E_UNSUPPORTED). */
+ * Overflow is decided on the window's exact total. The reference decides it on each running sum in arrival order,
+ * and SUM and AVG differ there:
+ *  SUM: a running sum that overflowed is NULL and restarts from the next value (ifThenElse(isNull(sum), operand, ..)),
+ *       so the reference's result is the sum of the values after the last overflow; the engine's is the exact total,
+ *       NULL if that has more than 38 digits.
+ *  AVG: DecimalAvgAggFunction has no restart (AvgAggFunction.java:79 aggDecimalPlus): once a running sum passes 38
+ *       digits the window's AVG is NULL; the engine's is the exact total over the count, non-NULL when that total
+ *       is back within 38 digits (tests/test_decimal_gpu.py::test_documented_overflow_difference pins both).
+ * Results differ only for windows in which a running sum passes 38 digits. A (key, window) may hold up to 2^32 - 1
+ * records (FWA_E_UNSUPPORTED at the fire beyond). Internally each DECIMAL source column is summed as 2 (int64 input)
+ * or 4 (16-byte) 32-bit pieces, each one of the handle's FWA_MAX_AGGS aggregates, plus a count; a list past that
+ * budget is FWA_E_UNSUPPORTED at fwa_create. Not available for fwa_drain_partials / fwa_push_partials
+ * (FWA_E_UNSUPPORTED); fwa_snapshot_heap writes the exact total as the DECIMAL(38, s) buffer. */
 /* SQL NULL semantics (fwa_config.nullable_cols, Table semantics): SUM/MIN/MAX/AVG skip NULL inputs and are
  * NULL when a window holds no non-NULL input (SumAggFunction.java:54-110, MaxAggFunction.java:63-73,
  * MinAggFunction.java:63-, AvgAggFunction.java:65-106: AVG = sum / count of non-NULL inputs); COUNT(*) counts

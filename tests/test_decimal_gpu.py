@@ -77,6 +77,16 @@ def test_documented_overflow_difference(eng_mod):
     o.push(np.full(3, 1, np.int64), np.arange(3, dtype=np.int64), [dec_input("SUM_DEC128", vals)])
     assert int(o.advance_watermark(A.LONG_MAX)["agg0"][0]) == 5
     o.close()
+    # AVG has no restart (AvgAggFunction.java:79): the reference's AVG stays NULL once a running sum passed 38 digits,
+    # the engine's is the exact total (6 * 10^37) over the count when that is back in range
+    vals = [big, big, -big]
+    assert one_window(eng_mod, "AVG_DEC128", 20, vals) == 2 * 10 ** 37
+    cfg = A.make_config(window_kind="TUMBLE", semantics="TABLE", size_ms=1000, aggs=[("AVG_DEC128", 0, 20)])
+    o = Oracle(cfg)
+    o.push(np.full(3, 1, np.int64), np.arange(3, dtype=np.int64), [dec_input("AVG_DEC128", vals)])
+    r = o.advance_watermark(A.LONG_MAX)
+    assert r["null0"][0]
+    o.close()
 
 
 CONFIGS = [
