@@ -1952,6 +1952,7 @@ struct fwa_engine {
     SpState* sp = nullptr;
     // per-handle options (fwa_set_option; the defaults are the production behaviour)
     int32_t opt_pre = -1, opt_mp = -1, opt_narrow = -1, opt_cells = -1;   // -1 adaptive, 0 never, 1 always
+    int32_t opt_variant = 0;                                              // FWA_OPT_INGEST_VARIANT (A/B builds)
     int64_t opt_out_min = 0;
     bool opt_partials_v1 = false;
     int32_t opt_profile = 0;
@@ -2813,7 +2814,7 @@ static int ensure_v2_buffers(fwa_engine* e, int64_t n, bool need_bn) {
     if (need_bn && !e->d_bn) HIPCHK(e, hipMalloc(&e->d_bn, 2 * (e->capb * e->np * kSub + 8 * kMaxPart)));
     if (!e->d_bcnt) {
         HIPCHK(e, hipMalloc(&e->d_bcnt, sizeof(uint32_t) * kMaxPart * kSub));
-        HIPCHK(e, hipMalloc(&e->d_rel2slot, (sizeof(int32_t) + 1) * kRelCap));   // rel2slot | relcode
+        HIPCHK(e, hipMalloc(&e->d_rel2slot, (sizeof(int32_t) + 2) * kRelCap));   // rel2slot | relcode | relfresh
     }
     return FWA_OK;
 }
@@ -2865,13 +2866,17 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     // rel2slot (combine) and relcode (partition): the directory restricted to [q_base, q_base + kRelCap)
     // with each slice's acceptance under the current watermark (WindowOperator.isWindowLate /
     // SlicingWindowOperator lateness, as in ingest_kernel)
-    std::vector<int32_t> r2s(kRelCap + kRelCap / 4, -1);
+    std::vector<int32_t> r2s(kRelCap + kRelCap / 2, -1);
     uint8_t* code = (uint8_t*)(r2s.data() + kRelCap);
     memset(code, kCodeSlow, kRelCap);
+    // slots no record reached yet hold their identities: the combiner's merge of such a slice stores without reading
+    uint8_t* fresh = code + kRelCap;
+    memset(fresh, 0, kRelCap);
     for (auto& kv : e->live) {
         const int64_t rel = kv.first - q_base;
         if (rel < 0 || rel >= kRelCap) continue;
         r2s[rel] = kv.second;
+        fresh[rel] = (e->touched[kv.second] || (e->opt_variant & 1)) ? 0 : 1;   // variant bit 0: A/B without
         int64_t thr;
         bool always;
         accept_threshold(e, kv.first, &thr, &always);
@@ -2879,7 +2884,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else if (e->lateness > 0 && a.wm >= trig(e, jm::wsub(first_window_end(e, kv.first), 1))) code[rel] = kCodeSlow;
         else code[rel] = kCodeAccept;
     }
-    rc = upload(e, e->d_rel2slot, r2s.data(), (sizeof(int32_t) + 1) * kRelCap);
+    rc = upload(e, e->d_rel2slot, r2s.data(), (sizeof(int32_t) + 2) * kRelCap);
     if (rc) return rc;
     rc = reset_push_status(e, true);
     if (rc) return rc;
@@ -3001,6 +3006,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.np = e->np;
     ca.sl = e->sl;
     ca.rel2slot = e->d_rel2slot;
+    ca.relfresh = (const uint8_t*)(e->d_rel2slot + kRelCap) + kRelCap;
     ca.slot_base = e->d_slot_base;
     ca.stride = e->stride;
     ca.st = e->d_st;
@@ -4799,6 +4805,7 @@ int fwa_set_option(fwa_engine* e, int32_t option, int64_t value) {
         case FWA_OPT_PARTIALS_ONE_PASS: e->opt_partials_v1 = value > 0; return FWA_OK;
         case FWA_OPT_SP_TABLE: case FWA_OPT_SP_FMAX: case FWA_OPT_SP_BUDGET: return sp_set_option(e, option, value);
         case FWA_OPT_PROFILE: e->opt_profile = value > 0 ? 1 : 0; return FWA_OK;
+        case FWA_OPT_INGEST_VARIANT: e->opt_variant = (int32_t)std::max<int64_t>(0, value); return FWA_OK;
         default: return fail(e, FWA_E_ARG, "unknown option");
     }
 }
@@ -4820,6 +4827,7 @@ int fwa_get_option(const fwa_engine* e, int32_t option, int64_t* value) {
             return FWA_OK;
         case FWA_OPT_PROFILE: *value = e->opt_profile; return FWA_OK;
         case FWA_OPT_SESSION_PATH: *value = e->sess_path; return FWA_OK;
+        case FWA_OPT_INGEST_VARIANT: *value = e->opt_variant; return FWA_OK;
         default: return FWA_E_ARG;
     }
 }

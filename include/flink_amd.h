@@ -460,8 +460,9 @@ enum fwa_option {
     FWA_OPT_SP_FMAX = 8,         /* record lists: max fine buckets per (window, partition) at fire */
     FWA_OPT_SP_BUDGET = 9,       /* record lists: live list bytes above which windows are compacted */
     FWA_OPT_PROFILE = 10,        /* 1: per-phase clock profile of Phase P / A, printed to stderr (diagnostic) */
-    FWA_OPT_SESSION_PATH = 11    /* read only: the path of the last session push -- 0 general, 1 sort-based cells,
+    FWA_OPT_SESSION_PATH = 11,   /* read only: the path of the last session push -- 0 general, 1 sort-based cells,
                                     2 cell pre-aggregation (fwa_get_option) */
+    FWA_OPT_INGEST_VARIANT = 12  /* diagnostic: alternative ingest kernel geometries for A/B measurements (0 default) */
 };
 int fwa_set_option(fwa_engine* e, int32_t option, int64_t value);
 /* The option's effective value: for the tri-state options 1 if the handle currently takes that path (forced, or

@@ -28,19 +28,22 @@ def _device_batches(seed, n, nkeys, span, delay, nb, late_frac=0.0):
     return out, dev
 
 
-@pytest.mark.parametrize("sem,aggs", [("DATASTREAM", [("COUNT", 0), ("SUM_I64", 0)]),
-                                      ("TABLE", [("COUNT", 0), ("SUM_I64", 0), ("MAX_I64", 0)]),
-                                      ("DATASTREAM", [("SUM_I64", 0), ("AVG_I64", 0)])])
+@pytest.mark.parametrize("sem,aggs,lateness", [("DATASTREAM", [("COUNT", 0), ("SUM_I64", 0)], 0),
+                                               ("TABLE", [("COUNT", 0), ("SUM_I64", 0), ("MAX_I64", 0)], 0),
+                                               ("DATASTREAM", [("SUM_I64", 0), ("AVG_I64", 0)], 0),
+                                               ("DATASTREAM", [("COUNT", 0), ("SUM_I64", 0)], 1500)])
 @pytest.mark.parametrize("late", [0.0, 0.01])
-def test_async_watermark_pipeline_vs_oracle(sem, aggs, late):
+def test_async_watermark_pipeline_vs_oracle(sem, aggs, lateness, late):
+    """Without allowed lateness the fire runs on the fire stream beside the next push (its windows retire at once);
+    with it (fired windows still take late records) on the push's stream."""
     from flink_amd import engine
     from oracle.oracle import Oracle
     host, dev = _device_batches(31, 1 << 20, 20_000, 200_000, 500, 10, late)
-    cfg = A.make_config(window_kind="TUMBLE", semantics=sem, size_ms=7_000, aggs=aggs, key_capacity=1 << 16,
-                        output_on_device=1)
+    kw = dict(window_kind="TUMBLE", semantics=sem, size_ms=7_000, aggs=aggs, key_capacity=1 << 16,
+              allowed_lateness_ms=lateness)
+    cfg = A.make_config(output_on_device=1, **kw)
     names = A.agg_names(cfg)
-    g, o = engine.WindowAggregator(cfg), Oracle(A.make_config(window_kind="TUMBLE", semantics=sem, size_ms=7_000,
-                                                               aggs=aggs, key_capacity=1 << 16))
+    g, o = engine.WindowAggregator(cfg), Oracle(A.make_config(**kw))
     expected = []
     for k, t, v, wm in host:
         o.push(k, t, [v])
