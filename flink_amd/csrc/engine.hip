@@ -2629,7 +2629,7 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         // while the partition count stays <= kMaxPart
         auto lds_need = [&](int sg) {
             const int64_t sgz = (int64_t)1 << sg;
-            return sgz * 8 + 2 * sgz * 4 + (int64_t)(c.nacc - 1) * 2 * sgz * 8 + 4 * 4 * kSub + 32 + sgz * 2 +
+            return sgz * 8 + 2 * sgz * 4 + (int64_t)(c.nacc - 1) * 2 * sgz * 8 + 4 * 4 * kSub + 16 +
                    (int64_t)sizeof(StragL) * kStragL + 256;   // + static LDS (straggler list, descriptors)
         };
         while (seg_log > 9 && lds_need(seg_log) > 160 * 1024 &&
@@ -2639,7 +2639,7 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         e->part_bits = cap_log - seg_log;
         const int64_t seg = (int64_t)1 << seg_log;
         const int64_t bps = 4 + 8 * (int64_t)(c.nacc - 1);
-        const int64_t avail = 160 * 1024 - 512 - (int64_t)sizeof(StragL) * kStragL - seg * 10;   // keys + tags
+        const int64_t avail = 160 * 1024 - 512 - (int64_t)sizeof(StragL) * kStragL - seg * 8;
         int sl = (int)std::min<int64_t>(8, avail > 0 ? avail / (bps * seg) : 0);
         if (lds_need(seg_log) > 160 * 1024) sl = 0;
         const int64_t np = (int64_t)1 << e->part_bits;
@@ -2945,26 +2945,11 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.st = e->d_st;
     if (e->opt_profile && !e->d_prof) HIPCHK(e, hipMalloc(&e->d_prof, sizeof(long long) * 8 * kMaxPart));
     pa.prof = e->opt_profile ? e->d_prof : nullptr;
-    // A/B (FWA_OPT_INGEST_VARIANT bit 3, narrow entries): the push as chunks of 2^23 records, Phase P and Phase A
-    // interleaved per chunk so that a chunk's buckets (~84 MB) can stay in the Infinity Cache between the two phases
-    const int64_t n_all = a.n;
-    const bool chunk_ok = (e->opt_variant & 8) && !pre && !a.pcount && e->nv == 1 && layout == 1 && e->vsize[0] == 8 &&
-                          e->opt_narrow != 0 && (e->opt_narrow == 1 || e->narrow);
-    const int64_t pchunk = chunk_ok ? ((int64_t)1 << 23) : n_all;
-    for (int64_t poff = 0; poff == 0 || poff < n_all; poff += pchunk) {
-    if (poff > 0) {
-        pa.keys = a.keys + poff;
-        pa.ts = a.ts + poff;
-        pa.cols[pa.vcol[0]] = (const char*)a.cols[pa.vcol[0]] + 8 * poff;
-        HIPCHK(e, hipMemsetAsync(e->d_bcnt, 0, sizeof(uint32_t) * kMaxPart * kSub, e->stream));
-    }
-    pa.n = std::min<int64_t>(pchunk, n_all - poff);
-    pa.ibase = poff;
     HIPCHK(e, hipEventRecord(e->ev[4], e->stream));
     const int threads = 1024;
     const int items = e->nv == 2 ? 4 : (e->nv == 1 ? 6 : 8);
     const int64_t tile = (int64_t)items * threads;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((pa.n + tile - 1) / tile, 256));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + tile - 1) / tile, 256));
     const int vw = (e->vsize[0] == 8 ? 1 : 0) | (e->vsize[1] == 8 ? 2 : 0);
     // ownership is checked per record unless the handle owns every key group; dictionary ids always (their key group
     // may be past max_parallelism: key group -1, rejected with FWA_E_KEYGROUP)
@@ -2991,11 +2976,6 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else partition3_kernel<NV, 4, 1024, 3, 2, 1><<<gp, 1024, 0, e->stream>>>(pa, e->d_ec); } while (0)
     if (pre) { if (e->nv == 0) PRELAUNCH(0); else PRELAUNCH(1); }
     else if (e->nv == 0) P3LAUNCH(0, 8, 3);
-    else if (narrow && (e->opt_variant & 4) && e->np <= kMaxPart / 2 && !pa.any_null && !pa.dropidx && pa.fast_m) {
-        // A/B: two 2048-record lean blocks per CU
-        const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>((a.n + 2047) / 2048, 512));
-        partition3_kernel<1, 2, 1024, 3, 0, 0, 1, 1, 2, 1><<<g2, 1024, 0, e->stream>>>(pa, e->d_ec);
-    }
     else if (narrow) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
@@ -3026,15 +3006,14 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.np = e->np;
     ca.sl = e->sl;
     ca.rel2slot = e->d_rel2slot;
-    // (a later chunk's slots hold the earlier chunks' merges: read them)
-    ca.relfresh = poff == 0 ? (const uint8_t*)(e->d_rel2slot + kRelCap) + kRelCap : nullptr;
+    ca.relfresh = (const uint8_t*)(e->d_rel2slot + kRelCap) + kRelCap;
     ca.slot_base = e->d_slot_base;
     ca.stride = e->stride;
     ca.st = e->d_st;
     ca.prof = pa.prof;
     HIPCHK(e, hipEventRecord(e->ev[6], e->stream));
     const size_t seg3 = (size_t)1 << e->seg_log;
-    const size_t lds3 = seg3 * 8 + 2 * seg3 * 4 + (size_t)(e->nacc - 1) * 2 * seg3 * 8 + 4 * 4 * kSub + 32 + seg3 * 2;
+    const size_t lds3 = seg3 * 8 + 2 * seg3 * 4 + (size_t)(e->nacc - 1) * 2 * seg3 * 8 + 4 * 4 * kSub + 16;
     // entries per lane and chunk: the largest counts whose kernels keep every value in registers at 1024 threads (a VGPR
     // spill is not harmless here, DESIGN.md section 4 "Skewed keys"; tests/test_abi.py checks the code object): 4, 3 with
     // two carried value columns, 6 for narrow entries, 2 with window passes. 512-thread blocks with twice the entries are
@@ -3068,8 +3047,6 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
         else C3M(IT, NV, 0, 0); } while (0)
     if (narrow) {   // packed entries free the prefetch registers: more entries per lane and chunk
         if (mp) combine3_kernel<FWA_MP_IT, 2, 1, TH3, 1, 0, 1, 1><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec);
-        else if (e->opt_variant & 2)   // A/B: fingerprint probes
-            combine3_kernel<FWA_C3_NIT, 2, 1, TH3, 1, 0, 0, 1, 1><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec);
         else combine3_kernel<FWA_C3_NIT, 2, 1, TH3, 1, 0, 0, 1><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec);
     } else if (e->nv == 0) C3L(FWA_C3_IT0, 0);
     else if (e->nv == 1) C3L(FWA_C3_IT1, 1);
@@ -3078,8 +3055,6 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
 #undef C3M
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[7], e->stream));
-    if (!narrow && pchunk < n_all) return fail(e, FWA_E_STATE, "chunked ingest A/B: narrow entries only");
-    }
     e->v2_timing_pending = true;
     if (e->opt_profile) {
         int rc2 = print_phase_profile(e, "aprof", e->ev[6], e->ev[7], e->np, 8);
