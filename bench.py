@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--pcie-batches", type=int, default=3)
     ap.add_argument("--no-wire", action="store_true", help="skip the wire-input (network bytes in HBM) leg")
     ap.add_argument("--wire-batches", type=int, default=4)
+    ap.add_argument("--no-wide", action="store_true", help="skip the 64-bit-key leg (C2 without narrow entries)")
+    ap.add_argument("--wide-batches", type=int, default=8)
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "c5s"], default="c2",
                     help="c2: tumbling 10s COUNT+SUM(long), 1M uniform keys (the metric's workload); "
                          "c3: HOP 60s/1s (Table slicing), Zipf(1.1) keys over 1M items; "
@@ -317,6 +319,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args, cfg_kw)
     if rank == 0 and world == 1 and not args.no_pcie and args.config == "c2":
         out["pcie_inclusive"] = pcie_leg(args, cfg_kw, keys, ts, vals, wms, dev)
+    if rank == 0 and world == 1 and not args.no_wide and args.config == "c2":
+        out["wide_keys"] = wide_keys_leg(args, cfg_kw, keys, ts, vals, wms, dev)
     if rank == 0 and world == 1 and not args.no_wire and args.config == "c2":
         out["wire_input"] = wire_leg(args, cfg_kw, keys, ts, vals, wms, dev)
     if rank == 0:
@@ -421,6 +425,40 @@ def pcie_leg(args, cfg_kw, keys, ts, vals, wms, dev):
     eng.close()
     return {"value": (nb - 1) * B / secs, "unit": "records/s", "batches_timed": nb - 1,
             "note": "host pinned input columns, H2D staging inside fwa_push, outputs left in HBM"}
+
+
+def wide_keys_leg(args, cfg_kw, keys, ts, vals, wms, dev):
+    """Secondary number: the same C2 step with keys that need 64 bits (each key + 2^40), so the
+    combiner's 10-byte narrow bucket entries (COUNT + SUM(BIGINT) with 32-bit keys and values) do not apply and
+    every record takes the 18-byte entries of the general path. Inputs in HBM, per-batch push + watermark as in the
+    main loop."""
+    import torch
+    from flink_amd import _abi as A
+    from flink_amd import engine as E
+    B = args.batch
+    nb = min(args.wide_batches, args.warmup + args.steps)
+    wk = keys[:nb * B] + (1 << 40)
+    eng = E.WindowAggregator(A.make_config(**cfg_kw))
+    views = [(wk[b * B:(b + 1) * B], ts[b * B:(b + 1) * B], [vals[b * B:(b + 1) * B]]) for b in range(nb)]
+    for b in range(2):                            # warm-up: the first push finds the 64-bit keys (narrow off)
+        eng.push(*views[b], sync=False)
+        eng.advance_watermark_raw(wms[b])
+    eng.reset_timers()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in range(2, nb):
+        eng.push(*views[b], sync=False)
+        eng.advance_watermark_raw(wms[b])
+    torch.cuda.synchronize()
+    secs = time.perf_counter() - t0
+    st = eng.stats()
+    narrow = eng.get_option("narrow_entries")
+    eng.close()
+    del wk
+    return {"value": (nb - 2) * B / secs, "unit": "records/s", "batches_timed": nb - 2,
+            "ms_per_step": secs * 1e3 / (nb - 2), "narrow_entries": bool(narrow),
+            "ingest_ms_per_step": st.ingest_ms / max(1, st.ingest_launches),
+            "note": "keys + 2^40 (64-bit keys): 18-byte bucket entries instead of the 10-byte narrow ones"}
 
 
 def encode_c2_wire(k, t, v, wm, dev):

@@ -134,6 +134,7 @@ class Stats(C.Structure):
         ("ingest_launches", C.c_int64), ("ingest_ms", C.c_double), ("ingest_records", C.c_int64),
         ("fire_launches", C.c_int64), ("fire_ms", C.c_double), ("fire_rows", C.c_int64),
         ("partition_ms", C.c_double), ("combine_ms", C.c_double), ("replay_records", C.c_int64),
+        ("dec_inexact", C.c_int64),
     ]
 
 

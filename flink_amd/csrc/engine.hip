@@ -4767,6 +4767,7 @@ int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
     s->ingest_ms = e->ingest_ms;
     s->ingest_records = e->ingest_records;
     s->replay_records = e->replay_records;
+    s->dec_inexact = e->dec ? e->dec->inexact : 0;
     s->fire_launches = e->fire_launches;
     s->fire_ms = e->fire_ms;
     s->fire_rows = e->fire_rows;

@@ -148,7 +148,8 @@ enum fwa_agg_kind {
  *       digits the window's AVG is NULL; the engine's is the exact total over the count, non-NULL when that total
  *       is back within 38 digits (tests/test_decimal_gpu.py::test_documented_overflow_difference pins both).
  * Results differ only for windows in which a running sum passes 38 digits. A (key, window) may hold up to 2^32 - 1
- * records (FWA_E_UNSUPPORTED at the fire beyond). Internally each DECIMAL source column is summed as 2 (int64 input)
+ * records: a DECIMAL result of a window with more is NULL and counted in fwa_stats.dec_inexact (the other rows of
+ * that watermark are unaffected). Internally each DECIMAL source column is summed as 2 (int64 input)
  * or 4 (16-byte) 32-bit pieces, each one of the handle's FWA_MAX_AGGS aggregates, plus a count; a list past that
  * budget is FWA_E_UNSUPPORTED at fwa_create. Not available for fwa_drain_partials / fwa_push_partials
  * (FWA_E_UNSUPPORTED); fwa_snapshot_heap writes the exact total as the DECIMAL(38, s) buffer. */
@@ -263,6 +264,8 @@ typedef struct fwa_stats {
     double partition_ms;         /* two-phase ingest split: phase P (key lookup + partition) */
     double combine_ms;           /* phase A (LDS combine + HBM merge) */
     int64_t replay_records;      /* records re-visited by slice-miss / bucket-overflow replays (not in ingest_records) */
+    int64_t dec_inexact;         /* DECIMAL results emitted NULL because their window held 2^32 or more records (the
+                                    32-bit piece sums may have wrapped; below that they are exact) */
 } fwa_stats;
 
 

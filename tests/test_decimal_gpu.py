@@ -192,3 +192,37 @@ def test_decimal_partials_unsupported(eng_mod):
         g.drain_partials(1000)
     assert "UNSUPPORTED" in str(ei.value)
     g.close()
+
+
+def test_window_past_2_32_records_gives_null_decimal_rows(eng_mod):
+    """The piece sums are exact below 2^32 records per (key, window); a window with more (forced here through a
+    restored snapshot whose COUNT(*) says 2^32 + 5) fires its DECIMAL results as NULL, counted in
+    fwa_stats.dec_inexact, and every other row of the watermark is emitted as usual."""
+    cfg = A.make_config(window_kind="TUMBLE", semantics="TABLE", size_ms=1000, key_capacity=64,
+                        aggs=[("COUNT", 0), ("SUM_DEC", 0, 2), ("AVG_DEC", 0, 2)])
+    g = eng_mod.WindowAggregator(cfg)
+    g.push(np.array([1, 2], np.int64), np.array([10, 20], np.int64), [np.array([5, 7], np.int64)])
+    w = np.frombuffer(g.snapshot(), np.int64).copy()
+    g.close()
+    maxp, n = int(w[9]), int(w[21])
+    body = 32 + maxp + 1
+    keys = w[body:body + n]
+    i = int(np.nonzero(keys == 1)[0][0])
+    big = (1 << 32) + 5
+    w[body + 2 * n + i] = big                    # COUNT(*) of key 1's slice
+    naggs = int(w[11])
+    kinds = w[12:12 + naggs]
+    for j in range(naggs):
+        if kinds[j] == A.AGG_KINDS["COUNT"]:
+            w[body + (3 + j) * n + i] = big      # ... and the COUNT aggregate's word
+    g = eng_mod.WindowAggregator(cfg)
+    g.restore(w.tobytes())
+    r = g.advance_watermark(A.LONG_MAX)
+    st = g.stats()
+    g.close()
+    rows = {int(k): j for j, k in enumerate(r["key"])}
+    assert set(rows) == {1, 2}
+    a, b = rows[1], rows[2]
+    assert int(r["agg0"][a]) == big and r["null1"][a] and r["null2"][a]
+    assert int(r["agg0"][b]) == 1 and not r["null1"][b] and int(r["agg1"][b]) == 7
+    assert st.dec_inexact == 2                   # SUM and AVG of key 1
