@@ -272,6 +272,11 @@ struct FireSlideArgs {
     void* o_agg[FWA_MAX_AGGS];
     int64_t out_cap;                         // rows past it are counted, not written (host grows, relaunches)
     DevStatus* st;
+    // carried window sums (rsum, [NA][stride]): r_u0 > 0 -- window 0 is rsum (its slices 0 .. r_u0 - 1, unchanged since
+    // the previous fire stored them) plus slices r_u0 .. L - 1; r_k > 0 -- store for the next run the sums over the
+    // slices the next run's window 0 shares with this run's last window, minus that window's last r_k slices
+    unsigned long long* rsum;
+    int32_t r_u0, r_k;
 };
 
 // NA = the handle's accumulator count (compile time: the running sums and the next window's slice values stay in
@@ -320,8 +325,14 @@ __global__ void __launch_bounds__(TB) fire_slide_kernel(FireSlideArgs f, const E
         for (int a = 0; a < NA; ++a) S[j][a] = 0;
     }
     __syncthreads();
-    // window 0: the sum of its L slices
-    for (int u = 0; u < f.L; ++u) {
+    // window 0: the sum of its L slices (or the carried sums of its first r_u0 slices plus the others)
+    if (f.r_u0 > 0) {
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int a = 0; a < NA; ++a) S[j][a] = present[j] ? f.rsum[a * st + kc[j]] : 0ull;
+    }
+    for (int u = f.r_u0; u < f.L; ++u) {
         const unsigned long long* b = slide_ptr(s_u[u]);
         unsigned long long x[J][NA];
 #pragma unroll
@@ -428,6 +439,24 @@ __global__ void __launch_bounds__(TB) fire_slide_kernel(FireSlideArgs f, const E
     }
     __syncthreads();
     if (f.nw > 0) write_rows(f.nw - 1, Sp, mp, (f.nw - 1) % 3);
+    if (f.r_k > 0 && f.nw > 0) {   // the next run's carried sums (before the retiring slices below are cleared)
+        const int lw = (f.nw - 1) * f.r;               // first slice of the last window
+        auto sub = [&](int u) {
+            const unsigned long long* b = slide_ptr(s_u[u]);
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+#pragma unroll
+                for (int a = 0; a < NA; ++a) Sp[j][a] -= present[j] ? b[a * st + kc[j]] : 0ull;
+        };
+        for (int u = lw; u < lw + f.r; ++u) sub(u);              // leave before the next window
+        for (int u = f.m - f.r_k; u < f.m; ++u) sub(u);          // may still change before the next fire
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (k0 + (int64_t)j * TB + tid >= nk) continue;      // (clamped lanes would overwrite the last kid)
+#pragma unroll
+            for (int a = 0; a < NA; ++a) f.rsum[a * st + kc[j]] = present[j] ? Sp[j][a] : 0ull;
+        }
+    }
     // retiring slices whose last window is the run's last one never left it: clear them now
     for (int u = (f.nw - 1) * f.r; u < f.m; ++u) {
         if (!slide_zero(s_u[u])) continue;
@@ -1953,6 +1982,16 @@ struct fwa_engine {
     // per-handle options (fwa_set_option; the defaults are the production behaviour)
     int32_t opt_pre = -1, opt_mp = -1, opt_narrow = -1, opt_cells = -1;   // -1 adaptive, 0 never, 1 always
     int32_t opt_variant = 0;                                              // FWA_OPT_INGEST_VARIANT (A/B builds)
+    int32_t push_epoch = 0;             // epoch of the current / last push (touched flags hold the last one per slot)
+    // fire_slide's carried window sums: valid for a run whose first window starts at slice rs_q0 while the slices
+    // [rs_q0, rs_q0 + rs_u0) have not been touched by a push after epoch rs_epoch
+    unsigned long long* d_rsum = nullptr;
+    bool rs_valid = false;
+    int64_t rs_q0 = 0;
+    int32_t rs_u0 = 0, rs_epoch = 0;
+    int32_t rs_k = 4;                   // trailing slices left out of the carried sums (doubles when a push hits them)
+    bool rs_on = true;                  // FWA_OPT_SLIDE_CARRIED
+    int64_t rs_used = 0;                // fires that reused them
     int64_t opt_out_min = 0;
     bool opt_partials_v1 = false;
     int32_t opt_profile = 0;
@@ -2449,7 +2488,7 @@ void fwa_destroy(fwa_engine* e) {
     if (e->d_lr_n) (void)hipFree(e->d_lr_n);
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_bkey, e->d_brel, e->d_bn,
-                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos, e->d_zslice,
+                    e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos, e->d_zslice, e->d_rsum,
                     e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4, e->d_rk};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
@@ -2774,6 +2813,7 @@ static int launch_ingest(fwa_engine* e, IngestArgs& a, bool replay) {
     a.spill = e->d_spill;
     a.late = e->d_late;
     a.touched = e->d_touched;
+    a.epoch = std::max<int32_t>(1, e->push_epoch);
     a.slot_base = e->d_slot_base;
     a.stride = e->stride;
     a.st = e->d_st;
@@ -2904,6 +2944,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.relcode = (const uint8_t*)(e->d_rel2slot + kRelCap);
     pa.rel2slot = e->d_rel2slot;
     pa.touched = e->d_touched;
+    pa.epoch = std::max<int32_t>(1, e->push_epoch);
     pa.spill = e->d_spill;
     pa.q_base = q_base;
     pa.fast_m = 0;
@@ -3696,6 +3737,7 @@ static int settle_pending(fwa_engine* e) {
 
 static int push_common(fwa_engine* e, IngestArgs& a, int64_t n, bool allow_v2, bool async, int64_t* late_dropped_out) {
     if (e->sparse) return sp_push(e, a, n, async ? nullptr : late_dropped_out);   // settled at once; async: count via stats
+    if (++e->push_epoch == INT32_MAX) { e->push_epoch = 1; e->rs_valid = false; }   // (epochs wrap: carried sums dropped)
     int rc = FWA_OK;
     bool ran_v2 = false;
     if (e->v2 && allow_v2) {
@@ -4021,6 +4063,7 @@ static int retire_slices(fwa_engine* e, int64_t wm) {
 // accumulators of every touched slice complete at wm, reset them, forward the watermark.
 int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     if (!e || !out) return FWA_E_ARG;
+    e->rs_valid = false;                              // the drained slices leave the carried sums behind
     if (e->red) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of a DataStream reduction");
     if (e->dec) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of DECIMAL aggregates");
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
@@ -4329,6 +4372,7 @@ void fwa_blob_free(fwa_blob* b) {
 }
 
 int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, int32_t n_blobs) {
+    if (e) e->rs_valid = false;
     if (!e) return FWA_E_STATE;
     if (n_blobs < 0 || (n_blobs > 0 && (!blobs || !sizes))) return fail(e, FWA_E_ARG, "null snapshot list");
     if (int rc0 = settle_pending(e)) return rc0;
@@ -4449,6 +4493,25 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
     rc = ensure_out(e, nw * nkeys);
     if (rc) return rc;
+    // Carried window sums (no allowed lateness: a slice changes only through pushes, which stamp its touched epoch).
+    // The previous run stored, per key, the sum over the slices its successor window shares with its last window except
+    // the last rs_k of them; this run's window 0 reuses it when it is that successor and no push touched those slices
+    // since. Otherwise (first run, a gap, a push into them: the tail rs_k doubles, up to L - r) window 0 sums all L.
+    int32_t r_u0 = 0, r_k = 0;
+    if (e->lateness == 0 && L - r >= 2 && e->rs_on) {
+        if (!e->d_rsum) HIPCHK(e, hipMalloc(&e->d_rsum, sizeof(unsigned long long) * (size_t)e->nacc * (size_t)e->stride));
+        bool use = e->rs_valid && q0 == e->rs_q0 && e->rs_u0 > 0 && e->rs_u0 <= L;
+        bool dirty = false;
+        for (int64_t q = q0; use && q < q0 + e->rs_u0; ++q) {
+            auto it = e->live.find(q);
+            if (it != e->live.end() && e->touched[it->second] > e->rs_epoch) { use = false; dirty = true; }
+        }
+        if (dirty) e->rs_k = (int32_t)std::min<int64_t>(L - r, 2 * (int64_t)e->rs_k);
+        r_u0 = use ? e->rs_u0 : 0;
+        e->rs_used += use ? 1 : 0;
+        r_k = (int32_t)std::min<int64_t>(e->rs_k, L - r - 1);
+    }
+    e->rs_valid = false;
   relaunch:
     HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
     FireSlideArgs f;
@@ -4470,6 +4533,9 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
     for (int j = 0; j < e->cfg.num_aggs; ++j) f.o_agg[j] = e->o_agg[j];
     f.out_cap = e->out_cap;
     f.st = e->d_st;
+    f.rsum = e->d_rsum;
+    f.r_u0 = r_u0;
+    f.r_k = r_k;
     const int64_t grid = (e->capacity + 1 + (int64_t)kSlideBlock * kSlideJ - 1) / ((int64_t)kSlideBlock * kSlideJ);
     HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
     switch (e->nacc) {
@@ -4490,9 +4556,16 @@ static int fire_slide(fwa_engine* e, const std::set<std::pair<int64_t, int64_t>>
         if (!cleared.empty()) return fail(e, FWA_E_STATE, "sliding fire exceeded its output bound");
         rc = ensure_out(e, *nrows);
         if (rc) return rc;
+        r_u0 = 0;                                        // the first launch already replaced the carried sums
         goto relaunch;
     }
     for (int32_t s : cleared) e->slot_clean[s] = 1;   // retire_slices releases them without a reset
+    if (r_k > 0) {                                    // what the next run's window 0 may reuse
+        e->rs_valid = true;
+        e->rs_q0 = q0 + nw * r;
+        e->rs_u0 = (int32_t)(L - r - r_k);
+        e->rs_epoch = e->push_epoch;
+    }
     float ms = 0.f;
     HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
     e->fire_ms += ms;
@@ -4807,6 +4880,7 @@ int fwa_set_option(fwa_engine* e, int32_t option, int64_t value) {
         case FWA_OPT_SP_TABLE: case FWA_OPT_SP_FMAX: case FWA_OPT_SP_BUDGET: return sp_set_option(e, option, value);
         case FWA_OPT_PROFILE: e->opt_profile = value > 0 ? 1 : 0; return FWA_OK;
         case FWA_OPT_INGEST_VARIANT: e->opt_variant = (int32_t)std::max<int64_t>(0, value); return FWA_OK;
+        case FWA_OPT_SLIDE_CARRIED: e->rs_on = value != 0; e->rs_valid = false; return FWA_OK;
         default: return fail(e, FWA_E_ARG, "unknown option");
     }
 }
@@ -4829,6 +4903,7 @@ int fwa_get_option(const fwa_engine* e, int32_t option, int64_t* value) {
         case FWA_OPT_PROFILE: *value = e->opt_profile; return FWA_OK;
         case FWA_OPT_SESSION_PATH: *value = e->sess_path; return FWA_OK;
         case FWA_OPT_INGEST_VARIANT: *value = e->opt_variant; return FWA_OK;
+        case FWA_OPT_SLIDE_CARRIED: *value = e->rs_used; return FWA_OK;
         default: return FWA_E_ARG;
     }
 }

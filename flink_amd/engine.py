@@ -131,7 +131,7 @@ def _check(rc, h=None, what=""):
 # fwa_set_option (include/flink_amd.h enum fwa_option): per-handle tuning / test options
 OPTIONS = {"skew_merge": 1, "window_passes": 2, "narrow_entries": 3, "session_cells": 4, "out_min_rows": 5,
            "partials_one_pass": 6, "sp_table": 7, "sp_fmax": 8, "sp_budget": 9, "profile": 10,
-           "session_path": 11, "ingest_variant": 12}
+           "session_path": 11, "ingest_variant": 12, "slide_carried": 13}
 # options applied to every new handle of this process before its own (test tooling sets these, e.g.
 # tests/forced_modes_check.py); empty in production
 DEFAULT_OPTIONS = {}

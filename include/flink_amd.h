@@ -465,8 +465,10 @@ enum fwa_option {
     FWA_OPT_PROFILE = 10,        /* 1: per-phase clock profile of Phase P / A, printed to stderr (diagnostic) */
     FWA_OPT_SESSION_PATH = 11,   /* read only: the path of the last session push -- 0 general, 1 sort-based cells,
                                     2 cell pre-aggregation (fwa_get_option) */
-    FWA_OPT_INGEST_VARIANT = 12  /* diagnostic A/B switches of the ingest kernels (0 default); bit 0: the combiner
+    FWA_OPT_INGEST_VARIANT = 12, /* diagnostic A/B switches of the ingest kernels (0 default); bit 0: the combiner
                                     reads a slot it merges into even when no record reached it yet */
+    FWA_OPT_SLIDE_CARRIED = 13   /* read only: sliding fires whose first window reused the previous run's carried
+                                    window sums (fwa_get_option; set: 0 disables the reuse, 1 enables it, default) */
 };
 int fwa_set_option(fwa_engine* e, int32_t option, int64_t value);
 /* The option's effective value: for the tri-state options 1 if the handle currently takes that path (forced, or
