@@ -3047,7 +3047,9 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.np = e->np;
     ca.sl = e->sl;
     ca.rel2slot = e->d_rel2slot;
-    ca.relfresh = (const uint8_t*)(e->d_rel2slot + kRelCap) + kRelCap;
+    // (not with PRE buckets: Phase P applies merged entries past a full sub-bucket to the slots with device atomics
+    // before this merge -- tests/test_skew_gpu.py::test_pre_entries_past_bucket_end_applied_with_atomics)
+    ca.relfresh = pre ? nullptr : (const uint8_t*)(e->d_rel2slot + kRelCap) + kRelCap;
     ca.slot_base = e->d_slot_base;
     ca.stride = e->stride;
     ca.st = e->d_st;
