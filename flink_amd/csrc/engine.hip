@@ -3004,7 +3004,10 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     // kernel; on by default until a push finds more than 1/64 of its records needing 64-bit keys or values
     const bool narrow = e->opt_narrow != 0 && (e->opt_narrow == 1 || e->narrow) && layout == 1 && e->nv == 1 &&
                         (vw & 1) && w16 && !pre && !a.pcount;
-    e->narrow_used = narrow;
+    // ... and for an 8-byte value column beside a 4-byte one (C5: DOUBLE and FLOAT): key and FLOAT bits share a word
+    const bool narrow2 = e->opt_narrow != 0 && (e->opt_narrow == 1 || e->narrow) && layout == 0 && e->nv == 2 && vw == 1 &&
+                         kgm == 0 && !pre && !a.pcount;
+    e->narrow_used = narrow || narrow2;
     const bool mp = e->opt_mp == 1 || (e->opt_mp != 0 && e->mp);   // combiner window passes (slices smaller than chunks)
 #define P3LAUNCH(NV, IT, VW) do { \
         if (kgm == 0) partition3_kernel<NV, IT, 1024, VW, 0><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec); \
@@ -3018,6 +3021,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     if (pre) { if (e->nv == 0) PRELAUNCH(0); else PRELAUNCH(1); }
     else if (e->nv == 0) P3LAUNCH(0, 8, 3);
     else if (narrow) partition3_kernel<1, 6, 1024, 3, 0, 0, 1, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
+    else if (narrow2) partition3_kernel<2, 4, 1024, 1, 0, 0, 0, 2><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16 && (vw & 1)) partition3_kernel<1, 6, 1024, 3, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1 && w16) partition3_kernel<1, 6, 1024, 2, 0, 0, 1><<<grid, 1024, 0, e->stream>>>(pa, e->d_ec);
     else if (e->nv == 1) { if (vw & 1) P3LAUNCH(1, 6, 3); else P3LAUNCH(1, 6, 2); }
@@ -3091,6 +3095,9 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     if (narrow) {   // packed entries free the prefetch registers: more entries per lane and chunk
         if (mp) combine3_kernel<FWA_MP_IT, 2, 1, TH3, 1, 0, 1, 1><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec);
         else combine3_kernel<FWA_C3_NIT, 2, 1, TH3, 1, 0, 0, 1><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec);
+    } else if (narrow2) {
+        if (mp) combine3_kernel<FWA_MP_IT, 2, 2, TH3, 0, 0, 1, 2><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec);
+        else combine3_kernel<4, 2, 2, TH3, 0, 0, 0, 2><<<e->np, TH3, lds3, e->stream>>>(ca, e->d_ec);
     } else if (e->nv == 0) C3L(FWA_C3_IT0, 0);
     else if (e->nv == 1) C3L(FWA_C3_IT1, 1);
     else C3L(FWA_C3_IT2, 2);

@@ -80,3 +80,49 @@ def test_wide_values_switch_the_handle_to_64bit_entries(eng_mod, monkeypatch):
     monkeypatch.delitem(eng_mod.DEFAULT_OPTIONS, "narrow_entries")
     extra = _run(eng_mod, keys, ts, vals, 8, 300).replay_records - wide
     assert 0 < extra <= (1 << 19) // 8                                  # only the first push is replayed
+
+
+# NW = 2: a DOUBLE column beside a FLOAT one (C5's aggregate list): the key's 32 bits and the FLOAT's bits share one
+# word, the DOUBLE keeps its own; keys needing 64 bits take the v1 replay (the FLOAT always fits)
+AGGS_F = [("COUNT", 0), ("SUM_F64", 1), ("AVG_F64", 1), ("MAX_F32", 0), ("MAX_F64", 1), ("MIN_F32", 0)]
+
+
+def _run_f(eng_mod, keys, ts, f, d, nb, delay, window="TUMBLE"):
+    from oracle.oracle import Oracle
+    kw = dict(window_kind=window, semantics="TABLE", aggs=AGGS_F, key_capacity=1 << 16, size_ms=2000)
+    if window == "SLIDE":
+        kw.update(size_ms=4000, slide_ms=1000)
+    cfg = A.make_config(**kw)
+    names = A.agg_names(cfg)
+    g, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
+    n, mx = len(keys), -2**63
+    for b in range(nb + 1):
+        sl = slice(b * n // nb, (b + 1) * n // nb) if b < nb else slice(0, 0)
+        if b < nb:
+            mx = max(mx, int(ts[sl].max()))
+        wm = mx - delay - 1 if b < nb else A.LONG_MAX
+        cols = [f[sl], d[sl]]
+        assert g.push(keys[sl], ts[sl], cols) == o.push(keys[sl], ts[sl], cols)
+        assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), names, rtol=1e-9, ctx="batch %d" % b)
+    st = g.stats()
+    g.close()
+    o.close()
+    return st
+
+
+@pytest.mark.parametrize("window", ["TUMBLE", "SLIDE"])
+def test_narrow_entries_double_beside_float(eng_mod, monkeypatch, window):
+    keys, ts, _ = _stream(5, 1 << 20, 50_000, 40_000, 300)
+    rng = np.random.default_rng(6)
+    f = (rng.random(len(keys)).astype(np.float32) - 0.5) * 1e4
+    f[rng.random(len(keys)) < 0.01] = np.float32(-0.0)
+    f[rng.random(len(keys)) < 0.001] = np.float32(np.inf)
+    d = rng.random(len(keys)) * 1e6 - 5e5
+    monkeypatch.setitem(eng_mod.DEFAULT_OPTIONS, "narrow_entries", 0)
+    wide = _run_f(eng_mod, keys, ts, f, d, 8, 300, window).replay_records
+    monkeypatch.setitem(eng_mod.DEFAULT_OPTIONS, "narrow_entries", 1)
+    assert _run_f(eng_mod, keys, ts, f, d, 8, 300, window).replay_records == wide
+    k = rng.random(len(keys)) < 0.004                                  # a few keys past 32 bits / at the markers
+    keys[k] = rng.choice(np.array([2**31, -2**31 - 1, 2**40 + 7, -2**31, -2**31 + 1], np.int64), k.sum())
+    monkeypatch.delitem(eng_mod.DEFAULT_OPTIONS, "narrow_entries")
+    assert _run_f(eng_mod, keys, ts, f, d, 8, 300, window).replay_records > wide

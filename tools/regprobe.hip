@@ -33,6 +33,9 @@ const void* regprobe_kernels[] = {
     (const void*)&combine3_kernel<2,2,1,1024,1,1,1,0>,
     (const void*)&combine3_kernel<2,2,1,1024,2,0,1,0>,
     (const void*)&combine3_kernel<2,2,2,1024,0,0,1,0>,
+    (const void*)&combine3_kernel<2,2,2,1024,0,0,1,2>,
+    (const void*)&combine3_kernel<4,2,2,1024,0,0,0,2>,
+    (const void*)&partition3_kernel<2,4,1024,1,0,0,0,2>,
     (const void*)&combine3_kernel<2,2,2,1024,1,0,1,0>,
     (const void*)&combine3_kernel<2,2,2,1024,2,0,1,0>,
     (const void*)&combine3_kernel<4,2,0,1024,0,0,0,0>,
