@@ -274,3 +274,25 @@ def test_record_lists_owned_range_across_watermarks():
         assert_rows_equal(g.advance_watermark(wm), o.advance_watermark(wm), names, rtol=1e-6, ctx="batch %d" % b)
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("sem", ["DATASTREAM", "TABLE"])
+def test_record_lists_narrow_entries(sem):
+    """COUNT + SUM(BIGINT) with keys and values over the signed 32-bit range: the runs hold one-word entries (int32
+    key | int32 value); a later push with keys and values past 32 bits is redone with 64-bit entries, which stay.
+    Rows equal the oracle's throughout, and the one-word runs cost no extra replay."""
+    rng = np.random.default_rng(17)
+    n = 600_000
+    keys = rng.integers(-2**31, 2**31, n).astype(np.int64)
+    rep = rng.random(n) < 0.3                                 # some keys repeat within a window
+    keys[rep] = keys[rng.integers(0, n, rep.sum())]
+    ts = np.sort(rng.integers(0, 60_000, n)).astype(np.int64) - rng.integers(0, 1001, n)
+    vi = rng.integers(-2**31, 2**31, n).astype(np.int64)
+    late_wide = slice(400_000, 500_000)                       # the fifth push carries 64-bit keys and values
+    keys[late_wide][::97] = 2**40 + 3
+    vi[late_wide][::89] = -2**50
+    cut = [0, 100_000, 200_000, 300_000, 400_000, 500_000, 600_000]
+    batches = [(keys[a:b], ts[a:b], [vi[a:b]]) for a, b in zip(cut, cut[1:])]
+    wms = [int(ts[:b].max()) - 1001 for b in cut[1:-1]] + [A.LONG_MAX]
+    run_both(dict(window_kind="TUMBLE", semantics=sem, size_ms=5000, key_capacity=1 << 26), batches, wms,
+             aggs=[("COUNT", 0), ("SUM_I64", 0)])
