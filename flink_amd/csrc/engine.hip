@@ -1803,6 +1803,7 @@ int64_t gcd64(int64_t a, int64_t b) {
 }
 
 #include "sessions4.inc"
+#include "merge_fire.inc"
 
 }  // namespace
 
@@ -1995,6 +1996,13 @@ struct fwa_engine {
     int64_t opt_out_min = 0;
     bool opt_partials_v1 = false;
     int32_t opt_profile = 0;
+    // fwa_fire_partials scratch: [3] u64 counters | b_cnt u32[NB] | bucket regions; groups per row seen last call
+    void* d_mf = nullptr;
+    size_t mf_bytes = 0;
+    double mf_groups_per_row = 1.0;
+    double mf_capx = 2.0;                 // bucket region = mean rows per bucket x this (+ slack); grows on overflow
+    int32_t opt_fire_partials = -1;       // FWA_OPT_FIRE_PARTIALS: -1 / 1 the merge-fire path where eligible, 0 never
+    int64_t mf_calls = 0, mf_fallbacks = 0;
     long long* d_prof = nullptr;          // FWA_OPT_PROFILE: per-block phase cycle counters of Phase P / A
 };
 
@@ -2489,7 +2497,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos, e->d_zslice, e->d_rsum,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4, e->d_rk};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4, e->d_rk, e->d_mf};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -4047,6 +4055,180 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
     return push_common(e, a, n, true, (flags & FWA_PUSH_ASYNC) != 0, late_dropped_out);
 }
 
+static int retire_slices(fwa_engine* e, int64_t wm);
+static int fill_out(fwa_engine* e, int64_t nrows, fwa_out* out);
+
+// fwa_fire_partials through its two defining calls: the rows' cells as columns, fwa_push_partials, then
+// fwa_advance_watermark (every case the merge-fire path does not take, and its redo).
+static int fire_partials_generic(fwa_engine* e, const int64_t* rows, int64_t n, int32_t m, const int32_t* cell,
+                                 int64_t wm, int32_t flags, fwa_out* out, int64_t* late_dropped_out) {
+    const int na = e->ec.naggs;
+    int64_t late = 0;
+    if (n > 0) {
+        const void* acc[FWA_MAX_AGGS + FWA_MAX_COLS] = {};
+        int rc = FWA_OK;
+        if (flags & FWA_PUSH_DEVICE_PTRS) {
+            int64_t* cols = nullptr;
+            HIPCHK(e, hipMalloc(&cols, (size_t)8 * n * m));
+            int64_t* colp[3 + kMaxAggsInt];
+            for (int c = 0; c < m; ++c) colp[c] = cols + (size_t)c * n;
+            if (int rc0 = wait_input_stream(e)) { (void)hipFree(cols); return rc0; }
+            rc = fwa_unpack_rows(rows, n, m, colp, e->cfg.device, e->stream);
+            if (rc == FWA_OK) {
+                for (int j = 0; j < na; ++j) if (e->ec.agg[j].acc > 0) acc[j] = colp[cell[j]];
+                hipStream_t in_saved = e->in_stream;
+                e->in_stream = nullptr;                       // the columns are ordered on the engine's own stream
+                rc = fwa_push_partials(e, colp[0], colp[1], colp[2], acc, n, FWA_PUSH_DEVICE_PTRS, &late);
+                e->in_stream = in_saved;
+            } else {
+                rc = fail(e, rc, "fwa_fire_partials: unpacking the rows failed");
+            }
+            if (hipStreamSynchronize(e->stream) != hipSuccess && rc == FWA_OK) rc = fail(e, FWA_E_DEVICE, "stream");
+            (void)hipFree(cols);
+        } else {
+            std::vector<int64_t> cols((size_t)n * m);
+            for (int64_t i = 0; i < n; ++i)
+                for (int c = 0; c < m; ++c) cols[(size_t)c * n + i] = rows[(size_t)i * m + c];
+            for (int j = 0; j < na; ++j) if (e->ec.agg[j].acc > 0) acc[j] = cols.data() + (size_t)cell[j] * n;
+            rc = fwa_push_partials(e, cols.data(), cols.data() + n, cols.data() + 2 * (size_t)n, acc, n, 0, &late);
+        }
+        if (rc) return rc;
+    }
+    if (late_dropped_out) *late_dropped_out = late;
+    return fwa_advance_watermark(e, wm, out);
+}
+
+int fwa_fire_partials(fwa_engine* e, const int64_t* rows, int64_t n, int32_t m, const int32_t* acc_cell, int64_t wm,
+                      int32_t flags, fwa_out* out, int64_t* late_dropped_out) {
+    if (!e) return FWA_E_STATE;
+    if (out) memset(out, 0, sizeof(*out));
+    if (late_dropped_out) *late_dropped_out = 0;
+    const int na = e->ec.naggs;
+    if (n < 0 || m < 3 || m > 3 + kMaxAggsInt || (n > 0 && !rows) || !acc_cell)
+        return fail(e, FWA_E_ARG, "fwa_fire_partials: rows / cells");
+    for (int j = 0; j < na; ++j)
+        if (e->ec.agg[j].acc > 0 && (acc_cell[j] < 3 || acc_cell[j] >= m))
+            return fail(e, FWA_E_ARG, "fwa_fire_partials: accumulator cell out of the row");
+    if (n > INT32_MAX) return fail(e, FWA_E_ARG, "batch too large (max 2^31-1 rows)");
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (int rcf = finish_afire(e)) return rcf;
+    e->af_pend = false;
+    if (int rc0 = settle_pending(e)) return rc0;
+    // the merge-fire path: every window merged here fires at wm and nothing else is held (TUMBLE, no lateness,
+    // no live slice with data); the redo through the defining calls covers every row it cannot place
+    bool fast = e->opt_fire_partials != 0 && n > 0 && (flags & FWA_PUSH_DEVICE_PTRS) && !e->sparse && !e->red &&
+                !e->dec && e->kind == FWA_TUMBLE && e->lateness == 0 && e->tz.empty() && e->late_rows == 0 &&
+                wm > e->wm && e->cfg.key_kind != FWA_KEY_PREHASHED;
+    if (fast) for (auto& kv : e->live) if (e->touched[kv.second]) { fast = false; break; }
+    MfArgs a;
+    memset(&a, 0, sizeof(a));
+    const int nacc = e->nacc;
+    if (fast) {
+        for (int cc = 0; cc <= kMaxAggsInt; ++cc) a.cell[cc] = -1;
+        for (int j = 0; j < na; ++j) {
+            const AggDesc& d = e->ec.agg[j];
+            if (d.acc > 0 && !d.alias) a.cell[d.acc] = acc_cell[j];
+        }
+        for (int cc = 1; cc < nacc; ++cc) fast = fast && a.cell[cc] >= 3 && e->ec.acc_kind[cc] != ACC_PAYLOAD;
+    }
+    if (!fast) return fire_partials_generic(e, rows, n, m, acc_cell, wm, flags, out, late_dropped_out);
+    e->mf_calls++;
+    static const size_t kLds = getenv("FWA_MF_LDS") ? (size_t)atoi(getenv("FWA_MF_LDS")) * 1024 : 150 * 1024;
+    const size_t ebytes = 20 + 8 * (size_t)nacc;
+    int hlog = 14;
+    while (hlog > 8 && ((size_t)1 << hlog) * ebytes + 64 > kLds) --hlog;
+    const int64_t H = (int64_t)1 << hlog;
+    // buckets: the groups expected (rows x twice the groups per row of the last call, at most one per row) at <= H/2
+    // per bucket; the redo resets the estimate
+    const double exp_groups = std::max(1.0, (double)n * std::min(1.0, 2.0 * e->mf_groups_per_row));
+    int nb_log = 0;
+    while (nb_log < 12 && (double)(H / 2) * (double)((int64_t)1 << nb_log) < exp_groups) ++nb_log;
+    const int64_t NB = (int64_t)1 << nb_log;
+    const int64_t capb = (int64_t)((double)(n / NB) * e->mf_capx) + 512;
+    int64_t tile = (int64_t)((150 * 1024 - 12 * (size_t)NB - 16) / (8 + 8 * (size_t)m));
+    tile = std::min<int64_t>(8 * kMfThreads, tile / 64 * 64);
+    if (tile < 256) return fire_partials_generic(e, rows, n, m, acc_cell, wm, flags, out, late_dropped_out);
+    const size_t hdr = 256 + ((4 * (size_t)NB + 255) & ~(size_t)255);
+    const size_t need = hdr + (size_t)NB * capb * m * 8;
+    if (need > e->mf_bytes) {
+        if (e->d_mf) HIPCHK(e, hipFree(e->d_mf));
+        e->d_mf = nullptr;
+        e->mf_bytes = 0;
+        HIPCHK(e, hipMalloc(&e->d_mf, need));
+        e->mf_bytes = need;
+    }
+    if (int rc = ensure_out(e, n)) return rc;
+    a.rows = rows;
+    a.n = n;
+    a.m = m;
+    a.nb_log = nb_log;
+    a.tile = (int32_t)tile;
+    a.hlog = hlog;
+    a.nacc = nacc;
+    a.capb = capb;
+    a.mf = (unsigned long long*)e->d_mf;
+    a.b_cnt = (uint32_t*)((char*)e->d_mf + 256);
+    a.b_rows = (int64_t*)((char*)e->d_mf + hdr);
+    a.prev_wm = e->wm;
+    a.wm = wm;
+    a.o_key = e->o_key;
+    a.o_start = e->o_start;
+    a.o_end = e->o_end;
+    for (int j = 0; j < e->cfg.num_aggs; ++j) { a.o_agg[j] = e->o_agg[j]; a.o_null[j] = e->o_null[j]; }
+    a.out_cap = e->out_cap;
+    a.st = e->d_st;
+    if (int rc1 = wait_input_stream(e)) return rc1;
+    HIPCHK(e, hipMemsetAsync(e->d_mf, 0, hdr, e->stream));
+    HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));
+    HIPCHK(e, hipMemsetAsync(&e->d_st->error, 0, 4, e->stream));
+    const size_t lds_p = (((size_t)12 * NB + 15) & ~(size_t)15) + (size_t)tile * (8 + 8 * (size_t)m);
+    const size_t lds_m = (((size_t)4 * H + 15) & ~(size_t)15) + (size_t)H * (16 + 8 * (size_t)nacc);
+    HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
+    mf_part_kernel<<<(unsigned)((n + tile - 1) / tile), kMfThreads, lds_p, e->stream>>>(a);
+    mf_merge_kernel<<<(unsigned)NB, kMfThreads, lds_m, e->stream>>>(a, e->d_ec);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
+    unsigned long long hm[3] = {0, 0, 0};
+    HIPCHK(e, hipMemcpyAsync(hm, e->d_mf, sizeof(hm), hipMemcpyDeviceToHost, e->stream));
+    if (int rc2 = sync_status(e)) return rc2;
+    const DevStatus st = *e->h_st;
+    if (st.error) {
+        const char* msg = st.error == FWA_E_KEYGROUP ? "Key group is not in the owned KeyGroupRange (StateTable.getMapForKeyGroup)"
+                                                     : "device error";
+        return fail(e, st.error, msg);
+    }
+    if (hm[2]) {   // a row this path cannot place: redo through the defining calls (no state was touched)
+        e->mf_fallbacks++;
+        // a region past its end: the rows of a key (all its windows, from every source) share one bucket, so the
+        // spread is wider than the row count suggests -- larger regions from now on, buckets sized from the groups
+        // the truncated pass still saw; a full table: buckets sized for one group per row again
+        if (hm[2] & kMfOverflow) {
+            e->mf_capx = std::min(6.0, e->mf_capx * 1.5);
+            e->mf_groups_per_row = std::max(e->mf_groups_per_row, std::min(1.0, (double)hm[1] / (double)n));
+        }
+        if (hm[2] & kMfFull) e->mf_groups_per_row = 1.0;
+        return fire_partials_generic(e, rows, n, m, acc_cell, wm, flags, out, late_dropped_out);
+    }
+    const int64_t nrows = (int64_t)st.rows;
+    if (nrows > e->out_cap) return fail(e, FWA_E_STATE, "fwa_fire_partials: rows past the output bound");
+    e->mf_groups_per_row = std::max(1.0 / 65536.0, (double)hm[1] / (double)n);
+    const int64_t dropped = (int64_t)hm[0];
+    e->records_in += n;
+    e->late_dropped += dropped;
+    if (late_dropped_out) *late_dropped_out = dropped;
+    if (int rc3 = retire_slices(e, wm)) return rc3;   // lookahead slices past cleanup (they hold no data)
+    e->wm = wm;
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+    e->fire_ms += ms;
+    e->fire_launches++;
+    e->fire_rows += nrows;
+    e->rows_out += nrows;
+    e->af_rows = nrows;
+    if (out) return fill_out(e, nrows, out);
+    return FWA_OK;
+}
+
 // Export every (key, slice) accumulator that received records since the last drain and reset those
 // slices (the local half of LocalSlicingWindowAggOperator -> GlobalAggCombiner).
 // Free slices whose every window is past cleanup at wm (last window: cleanupTime <= wm).
@@ -4890,6 +5072,7 @@ int fwa_set_option(fwa_engine* e, int32_t option, int64_t value) {
         case FWA_OPT_PROFILE: e->opt_profile = value > 0 ? 1 : 0; return FWA_OK;
         case FWA_OPT_INGEST_VARIANT: e->opt_variant = (int32_t)std::max<int64_t>(0, value); return FWA_OK;
         case FWA_OPT_SLIDE_CARRIED: e->rs_on = value != 0; e->rs_valid = false; return FWA_OK;
+        case FWA_OPT_FIRE_PARTIALS: e->opt_fire_partials = value != 0 ? 1 : 0; return FWA_OK;
         default: return fail(e, FWA_E_ARG, "unknown option");
     }
 }
@@ -4913,6 +5096,7 @@ int fwa_get_option(const fwa_engine* e, int32_t option, int64_t* value) {
         case FWA_OPT_SESSION_PATH: *value = e->sess_path; return FWA_OK;
         case FWA_OPT_INGEST_VARIANT: *value = e->opt_variant; return FWA_OK;
         case FWA_OPT_SLIDE_CARRIED: *value = e->rs_used; return FWA_OK;
+        case FWA_OPT_FIRE_PARTIALS: *value = e->mf_calls - e->mf_fallbacks; return FWA_OK;
         default: return FWA_E_ARG;
     }
 }

@@ -39,6 +39,19 @@ def choose_exchange(cfg_kw):
     return "raw" if kc >= 1 << 25 or cfg_kw.get("record_lists") else "partials"
 
 
+def owner_key_capacity(key_capacity, n_groups, max_parallelism, margin=1.25, slack=4096):
+    """Key capacity of an engine owning n_groups of max_parallelism key groups when the job's key space is
+    key_capacity keys: its share (keys spread over key groups by a murmur hash, KeyGroupRangeAssignment
+    .assignToKeyGroup) with a margin, so a dense owner's fire scans its share of the key table, not the whole job's
+    (the table is 2x the capacity, rounded up to a power of two). Record-list sized key spaces (>= 2^25 keys) keep
+    their capacity: it selects that layout (FWA_CFG_RECORD_LISTS). A share that overflows fails loudly (FWA_E_OOM)."""
+    kc = int(key_capacity or 0)
+    if kc <= 0 or kc >= 1 << 25 or n_groups >= max_parallelism:
+        return kc
+    share = -(-kc * n_groups // max_parallelism)
+    return min(kc, int(share * margin) + slack)
+
+
 _VALVE_GROUPS = {}
 
 
@@ -70,11 +83,19 @@ def _gpu_router(max_parallelism, world, key_kind):
 class KeyedWindowPipeline:
     """One Flink subtask per rank: keyBy exchange + a window engine owning this rank's key groups."""
 
-    def __init__(self, rank, world, group=None, engine_factory=None, router=None, **cfg_kw):
+    def __init__(self, rank, world, group=None, engine_factory=None, router=None, owner_capacity="share", **cfg_kw):
+        """owner_capacity: "share" sizes the owning engine's key table to its key groups' share of key_capacity
+        (owner_key_capacity), "full" keeps the job's key_capacity, an int sets it."""
         self.rank, self.world, self.group = rank, world, group
         maxp = cfg_kw.get("max_parallelism", 128)
         kg0, kg1 = key_group_range_for_operator(maxp, world, rank)
-        self.cfg = A.make_config(kg_start=kg0, kg_end=kg1, **cfg_kw)
+        okw = dict(cfg_kw)
+        if owner_capacity == "share":
+            if not cfg_kw.get("record_lists") and cfg_kw.get("key_capacity"):
+                okw["key_capacity"] = owner_key_capacity(cfg_kw.get("key_capacity", 0), kg1 - kg0, maxp)
+        elif owner_capacity != "full":
+            okw["key_capacity"] = int(owner_capacity)
+        self.cfg = A.make_config(kg_start=kg0, kg_end=kg1, **okw)
         if engine_factory is None:
             from .engine import WindowAggregator
             engine_factory = WindowAggregator
@@ -168,8 +189,10 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
     engine owning this rank's key groups. Same push / advance_watermark surface as
     KeyedWindowPipeline; pushes involve no collective."""
 
-    def __init__(self, rank, world, group=None, engine_factory=None, router=None, local_factory=None, **cfg_kw):
-        super().__init__(rank, world, group=group, engine_factory=engine_factory, router=router, **cfg_kw)
+    def __init__(self, rank, world, group=None, engine_factory=None, router=None, local_factory=None,
+                 owner_capacity="share", **cfg_kw):
+        super().__init__(rank, world, group=group, engine_factory=engine_factory, router=router,
+                         owner_capacity=owner_capacity, **cfg_kw)
         lkw = dict(cfg_kw)
         lkw["output_on_device"] = 1 if dist.get_backend(group) == "nccl" else 0
         self.local_cfg = A.make_config(**lkw)           # the pre-aggregator sees every key group
@@ -202,6 +225,12 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
             self.push(*then_push)
         recv = send_rows(self, packed, counts)
         self.partials_sent += int(cols[0].shape[0])
+        if recv.is_cuda and hasattr(self.engine, "fire_partials"):
+            # merge + fire straight from the receive buffer (fwa_fire_partials: on chip for TUMBLE windows without
+            # lateness, else push_partials + advance_watermark inside the call)
+            cells = [2 if name == "COUNT" else 3 + ship.index(j) for j, name in enumerate(self.names)] + \
+                [3 + len(ship) + h for h in range(nh)]
+            return self.engine.fire_partials(recv, cells, wm, device_output=device_output)
         if recv.is_cuda:
             from . import engine
             col = engine.unpack_rows(recv)

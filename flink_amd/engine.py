@@ -49,6 +49,9 @@ def lib():
     L.fwa_push_partials.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                     C.c_int32, C.POINTER(C.c_int64)]
     L.fwa_push_partials.restype = C.c_int
+    L.fwa_fire_partials.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.POINTER(C.c_int32), C.c_int64,
+                                    C.c_int32, C.POINTER(A.Out), C.POINTER(C.c_int64)]
+    L.fwa_fire_partials.restype = C.c_int
     L.fwa_snapshot.argtypes = [C.c_void_p, C.POINTER(Blob)]
     L.fwa_snapshot.restype = C.c_int
     L.fwa_blob_free.argtypes = [C.POINTER(Blob)]
@@ -122,6 +125,16 @@ def _ptr(x):
     return x.ctypes.data_as(C.c_void_p)
 
 
+def _same_side(device, **named):
+    """A batch is all device tensors or all host arrays: a host pointer handed over as a device one (e.g. numpy NULL
+    flags beside CUDA key columns) would be dereferenced by a kernel."""
+    for name, xs in named.items():
+        for x in (xs if isinstance(xs, (list, tuple)) else [xs]):
+            if x is not None and _is_torch_cuda(x) != device:
+                raise ValueError("%s: %s columns beside %s keys" % (name, "CUDA" if not device else "host",
+                                                                     "CUDA" if device else "host"))
+
+
 def _check(rc, h=None, what=""):
     if rc:
         msg = lib().fwa_last_error(h).decode() if h else what
@@ -131,7 +144,7 @@ def _check(rc, h=None, what=""):
 # fwa_set_option (include/flink_amd.h enum fwa_option): per-handle tuning / test options
 OPTIONS = {"skew_merge": 1, "window_passes": 2, "narrow_entries": 3, "session_cells": 4, "out_min_rows": 5,
            "partials_one_pass": 6, "sp_table": 7, "sp_fmax": 8, "sp_budget": 9, "profile": 10,
-           "session_path": 11, "ingest_variant": 12, "slide_carried": 13}
+           "session_path": 11, "ingest_variant": 12, "slide_carried": 13, "fire_partials": 14}
 # options applied to every new handle of this process before its own (test tooling sets these, e.g.
 # tests/forced_modes_check.py); empty in production
 DEFAULT_OPTIONS = {}
@@ -198,6 +211,7 @@ class WindowAggregator:
         batch is settled by the next call on the handle, and the device tensors must stay alive until
         then; late drops are then counted in stats().late_dropped only."""
         device = _is_torch_cuda(keys)
+        _same_side(device, ts=ts, cols=list(cols), key_hash=key_hash, nulls=list(nulls or ()))
         if not device:
             keys = np.ascontiguousarray(keys, np.int64)
             ts = np.ascontiguousarray(ts, np.int64)
@@ -306,6 +320,7 @@ class WindowAggregator:
         configuration) into this handle's state; returns the number of late records dropped. `hidden`: the
         hidden non-NULL counter columns of a nullable handle (drain_partials' hidden<h>)."""
         device = _is_torch_cuda(keys)
+        _same_side(device, slice_ts=slice_ts, count=count, accs=list(accs), hidden=list(hidden))
         if not device:
             keys = np.ascontiguousarray(keys, np.int64)
             slice_ts = np.ascontiguousarray(slice_ts, np.int64)
@@ -323,6 +338,35 @@ class WindowAggregator:
         self._settled()
         _check(rc, self.h)
         return dropped.value
+
+    def fire_partials(self, rows, acc_cells, wm, device_output=False):
+        """The owner's watermark step over packed partial rows (fwa_fire_partials): the rows of push_partials of the
+        rows' cells followed by advance_watermark(wm). rows: int64 [n, m] (torch CUDA: merged and fired on chip
+        where the handle allows it; numpy: the two calls), cell 0 key, 1 slice timestamp, 2 COUNT(*); acc_cells[j]:
+        the cell of aggregate j's accumulator (user aggregates, then the hidden non-NULL counters; -1 where the
+        aggregate keeps none). Returns the fired rows like advance_watermark (advance_watermark_device's torch views
+        with device_output=True); late partials are counted in stats().late_dropped."""
+        device = _is_torch_cuda(rows)
+        if device:
+            rows = rows.contiguous()
+            self._order_after_producer(rows)
+        else:
+            rows = np.ascontiguousarray(rows, np.int64)
+        n, m = int(rows.shape[0]), int(rows.shape[1]) if rows.ndim == 2 else 0
+        nslot = A.FWA_MAX_AGGS + A.FWA_MAX_COLS
+        cells = (C.c_int32 * nslot)(*([int(x) for x in acc_cells] + [-1] * (nslot - len(acc_cells))))
+        out = A.Out()
+        dropped = C.c_int64(0)
+        rc = lib().fwa_fire_partials(self.h, _ptr(rows), n, m, cells, int(wm), A.PUSH_DEVICE_PTRS if device else 0,
+                                     C.byref(out), C.byref(dropped))
+        self._settled()
+        _check(rc, self.h)
+        if not device_output:
+            return self._rows(out)
+        res = {f: dev_view(getattr(out, f), out.n_rows, np.dtype("i8")) for f in ("key", "win_start", "win_end")}
+        for j, name in enumerate(self.names):
+            res["agg%d" % j] = dev_view(out.agg[j], out.n_rows, np.dtype(A.AGG_RESULT_DTYPE[name]))
+        return res
 
     # -- checkpoint / restore (HeapSnapshotStrategy + SlicingWindowOperator watermark state) --
     def snapshot(self):

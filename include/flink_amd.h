@@ -366,6 +366,19 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out);
 int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_ts, const int64_t* count,
                       const void* const* acc, int64_t n, int32_t flags, int64_t* late_dropped_out);
 
+/* The owner's watermark step of the two-phase plan over the exchange's receive buffer: the same result as
+ * fwa_push_partials of the rows' cells followed by fwa_advance_watermark(wm, out) (GlobalAggCombiner.combine
+ * then WindowOperator.onEventTime). rows: n packed rows of m 8-byte cells -- cell 0 the key, 1 a timestamp inside
+ * the slice, 2 COUNT(*), and acc_cell[j] the cell of aggregate j's accumulator for every aggregate and hidden
+ * counter that keeps one (fwa_drain_partials' acc / hidden; ignored for the others). With FWA_PUSH_DEVICE_PTRS
+ * (rows in HBM, ordered after fwa_set_input_stream's stream) on a TUMBLE handle without allowed lateness that holds
+ * no window data, the rows are grouped per (key, window) on chip and fired directly (no slot state in between;
+ * FWA_OPT_FIRE_PARTIALS counts those calls); otherwise, and for a row whose window would not fire at wm, the call
+ * runs as the two calls above. The replacement of fwa_push_partials + fwa_advance_watermark in the owner's loop
+ * (RecordsWindowBuffer.flush -> GlobalAggCombiner -> fire, SlicingWindowOperator.processWatermark). */
+int fwa_fire_partials(fwa_engine* e, const int64_t* rows, int64_t n, int32_t m, const int32_t* acc_cell, int64_t wm,
+                      int32_t flags, fwa_out* out, int64_t* late_dropped_out);
+
 /* ---- checkpoint / restore ----
  * fwa_snapshot replaces the keyed-state half of the operator snapshot: HeapSnapshotStrategy writes the
  * window state per key group with a KeyGroupRangeOffsets index (HeapSnapshotStrategy.java:154-179,
@@ -467,8 +480,10 @@ enum fwa_option {
                                     2 cell pre-aggregation (fwa_get_option) */
     FWA_OPT_INGEST_VARIANT = 12, /* diagnostic A/B switches of the ingest kernels (0 default); bit 0: the combiner
                                     reads a slot it merges into even when no record reached it yet */
-    FWA_OPT_SLIDE_CARRIED = 13   /* read only: sliding fires whose first window reused the previous run's carried
+    FWA_OPT_SLIDE_CARRIED = 13,  /* read only: sliding fires whose first window reused the previous run's carried
                                     window sums (fwa_get_option; set: 0 disables the reuse, 1 enables it, default) */
+    FWA_OPT_FIRE_PARTIALS = 14   /* read only: fwa_fire_partials calls that merged and fired on chip (fwa_get_option;
+                                    set: 0 sends every call through fwa_push_partials + fwa_advance_watermark) */
 };
 int fwa_set_option(fwa_engine* e, int32_t option, int64_t value);
 /* The option's effective value: for the tri-state options 1 if the handle currently takes that path (forced, or

@@ -1,6 +1,14 @@
-"""Per-step cost of the N>1 two-phase plan's pieces on one GPU (C2 batch): local push, drain_partials, GPU routing
-(fwa_route_rows, world 8), owner push_partials of the whole drained set (the volume an owner merges per step under
-weak scaling). No collective: the all_to_all is priced separately from the bytes shipped."""
+"""Per-rank step cost of the N>1 two-phase plan on one GPU (C2 batch), against the N=1 step (push + fire).
+
+Each step prices the pieces one rank runs at N = WORLD (default 8) under weak scaling:
+  local  push (the rank's own 2^26 records), drain_partials, GPU routing (fwa_route_rows by key group, WORLD ways);
+  owner  what it does with what it receives -- this rank's rows for destination 0, repeated WORLD times (one copy
+         per source rank: the same keys and windows, each source holding its own partial), sources back to back as
+         in the receive buffer: "merge_fire" = fwa_fire_partials on the packed rows (the pipeline's path), "sources"
+         = unpack + push_partials + fire, "window" = the same with the rows sorted window-major first.
+The all_to_all itself is not priced here (bytes shipped are printed). The owner engine is sized to its key-group
+share (distributed.owner_key_capacity)."""
+import argparse
 import os
 import sys
 import time
@@ -11,47 +19,93 @@ import torch  # noqa: E402
 
 from flink_amd import _abi as A  # noqa: E402
 from flink_amd import engine as E  # noqa: E402
+from flink_amd.keygroups import key_group_range_for_operator  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--world", type=int, default=8)
+ap.add_argument("--steps", type=int, default=6)
+ap.add_argument("--order", default="merge_fire,sources")
+ap.add_argument("--owner-share", type=int, default=1, help="1: owner key capacity sized to its key-group share")
+ap.add_argument("--dup", type=int, default=0, help="copies of the destination-0 rows the owner receives (0: world)")
+ap.add_argument("--owner-profile", type=int, default=0, help="FWA_OPT_PROFILE on the owners (per-block phase cycles)")
+args = ap.parse_args()
 
 B = 1 << 26
-S = 4
-p = A.GenParams(seed_k=1, seed_t=2, seed_v=3, first_index=0, total_records=S * B, num_keys=1_000_000,
-                t0_ms=1_700_000_000_000, span_ms=S * B * 1_000_000 // 1_000_000_000, max_delay_ms=1000, key_dist=0, val_kind=0)
+S = args.steps
+W = args.world
+KEYS = 1_000_000
+p = A.GenParams(seed_k=1, seed_t=2, seed_v=3, first_index=0, total_records=S * B, num_keys=KEYS,
+                t0_ms=1_700_000_000_000, span_ms=S * B * 1_000_000 // 1_000_000_000, max_delay_ms=1000, key_dist=0,
+                val_kind=0)
 dev = torch.device("cuda", 0)
 keys = torch.empty(S * B, dtype=torch.int64, device=dev)
 ts = torch.empty_like(keys)
 vals = torch.empty_like(keys)
 E.generate(p, S * B, keys, ts, vals)
 torch.cuda.synchronize()
-kw = dict(window_kind="TUMBLE", size_ms=10_000, aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=1_000_000,
+bmax = ts.view(S, B).max(dim=1).values.cpu().tolist()
+kw = dict(window_kind="TUMBLE", size_ms=10_000, aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=KEYS,
           output_on_device=1)
+single = E.WindowAggregator(A.make_config(**kw))
 local = E.WindowAggregator(A.make_config(**kw))
-owner = E.WindowAggregator(A.make_config(**kw))
-m = -2**63
-for b in range(S):
-    sl = slice(b * B, (b + 1) * B)
-    m = max(m, int(ts[sl].max().item()))
-    wm = m - 1001
+kg0, kg1 = key_group_range_for_operator(128, W, 0)
+okw = dict(kw)
+if args.owner_share:
+    from flink_amd.distributed import owner_key_capacity
+    okw["key_capacity"] = owner_key_capacity(KEYS, kg1 - kg0, 128)
+orders = args.order.split(",")
+owners = {o: E.WindowAggregator(A.make_config(kg_start=kg0, kg_end=kg1, **okw)) for o in orders}
+for o in owners.values():
+    if args.owner_profile:
+        o.set_option("profile", 1)
+print("world %d, owner key groups [%d, %d), owner key capacity %d" % (W, kg0, kg1, okw["key_capacity"]), flush=True)
+
+
+def timed(fn):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    local.push(keys[sl], ts[sl], [vals[sl]])
+    r = fn()
     torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    d = local.drain_partials(wm)
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    cols = [d["key"], d["slice_start"], d["count"]] + [d["acc%d" % j] for j in range(2)]
-    packed, counts = E.route_rows(cols[0], cols, 128, 8)
-    torch.cuda.synchronize()
-    t3 = time.perf_counter()
-    c = E.unpack_rows(packed)
-    torch.cuda.synchronize()
-    t4 = time.perf_counter()
-    owner.push_partials(c[0], c[1], c[2], c[3:])
-    torch.cuda.synchronize()
-    t5 = time.perf_counter()
-    n = owner.advance_watermark_raw(wm).n_rows
-    torch.cuda.synchronize()
-    t6 = time.perf_counter()
-    print("step %d: push %.3f drain %.3f route %.3f unpack %.3f push_partials %.3f fire %.3f ms; partials %d (%.0f MB), rows %d"
-          % (b, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, (t4 - t3) * 1e3, (t5 - t4) * 1e3, (t6 - t5) * 1e3,
-             d["key"].shape[0], packed.numel() * 8 / 1e6, n), flush=True)
+    return r, (time.perf_counter() - t0) * 1e3
+
+
+m = -2**63
+tot = {}
+for b in range(S):
+    sl = slice(b * B, (b + 1) * B)
+    m = max(m, int(bmax[b]))
+    wm = m - 1001
+    t = {}
+    _, t["n1_push"] = timed(lambda: single.push(keys[sl], ts[sl], [vals[sl]]))
+    _, t["n1_fire"] = timed(lambda: single.advance_watermark_raw(wm).n_rows)
+    _, t["push"] = timed(lambda: local.push(keys[sl], ts[sl], [vals[sl]]))
+    d, t["drain"] = timed(lambda: local.drain_partials(wm))
+    cols = [d["key"], d["slice_start"], d["count"], d["acc1"]]
+    (packed, counts), t["route"] = timed(lambda: E.route_rows(cols[0], cols, 128, W))
+    n0 = int(counts[0].item())
+    recv = packed[:n0].repeat(args.dup or W, 1)                     # what the owner receives: one copy per source rank
+    cells = [2, 3]
+    for o in orders:
+        if o == "merge_fire":
+            _, t[o] = timed(lambda: owners[o].fire_partials(recv, cells, wm, device_output=True)["key"].shape[0])
+            continue
+        rv = recv
+        if o == "window":                               # window-major: all sources' rows of a window together
+            rv = recv[torch.argsort(recv[:, 1], stable=True)]
+        c, t[o + "_unpack"] = timed(lambda: E.unpack_rows(rv))
+        _, t[o + "_merge"] = timed(lambda: owners[o].push_partials(c[0], c[1], c[2], [c[2], c[3]]))
+        _, t[o + "_fire"] = timed(lambda: owners[o].advance_watermark_raw(wm).n_rows)
+    if b >= 2:
+        for k, v in t.items():
+            tot[k] = tot.get(k, 0.0) + v
+    print("step %d: " % b + " ".join("%s %.3f" % kv for kv in t.items()) +
+          " ms; partials %d (%.0f MB), owner rows %d" % (d["key"].shape[0], packed.numel() * 8 / 1e6, recv.shape[0]),
+          flush=True)
+n = S - 2
+n1 = (tot["n1_push"] + tot["n1_fire"]) / n
+print("N=1 step %.3f ms (push %.3f, fire %.3f)" % (n1, tot["n1_push"] / n, tot["n1_fire"] / n))
+for o in orders:
+    parts = ["push", "drain", "route"] + ([o] if o == "merge_fire" else [o + "_unpack", o + "_merge", o + "_fire"])
+    s = sum(tot[k] for k in parts) / n
+    print("N=%d per-rank step, owner order %s: %.3f ms = %s -> %.2fx N=1" %
+          (W, o, s, " + ".join("%s %.3f" % (k, tot[k] / n) for k in parts), s / n1))
