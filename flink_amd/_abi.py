@@ -118,6 +118,15 @@ class Out(C.Structure):
     ]
 
 
+FWA_MAX_DEST = 64
+
+
+class Routed(C.Structure):
+    """fwa_routed (include/flink_amd.h): fwa_drain_route's per-destination packed rows."""
+    _fields_ = [("n", C.c_int64), ("parallelism", C.c_int32), ("cells", C.c_int32), ("on_device", C.c_int32),
+                ("pad", C.c_int32), ("rows", C.c_void_p * FWA_MAX_DEST), ("count", C.c_int64 * FWA_MAX_DEST)]
+
+
 class Partials(C.Structure):
     _fields_ = [
         ("n", C.c_int64), ("on_device", C.c_int32), ("num_aggs", C.c_int32),

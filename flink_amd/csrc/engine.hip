@@ -244,6 +244,80 @@ __global__ void __launch_bounds__(kBlock) fire_kernel(FireArgs f, const EngineCo
     }
 }
 
+// drain_route (fwa_drain_route): the raw fire of complete slices (fwa_drain_partials) written straight into the
+// exchange's send layout -- packed partial rows grouped by owning subtask (KeyGroupStreamPartitioner.selectChannel,
+// KeyGroupStreamPartitioner.java:55-65) -- so the drain and the keyBy routing are one pass over the slot columns. One
+// block = one slice x one chunk of kBlock*kFireJ kids (fire_kernel's grid); one cursor reservation per (block,
+// destination), LDS positions inside it.
+constexpr int kMaxDest = 64;
+struct DrainRouteArgs {
+    FireArgs f;                        // key table, slots, the slices (one slot each)
+    int32_t par, m, ncell, pad;        // destinations, cells per row, accumulator cells (cells 3..m-1)
+    int32_t cell_acc[kMaxAggsInt];     // accumulator column feeding cell 3 + i (0: COUNT(*), an aggregate without one)
+    int64_t cap;                       // rows per destination region
+    int64_t* rows;                     // [par][cap][m]
+    unsigned long long* dcnt;          // [par] rows per destination (past cap: counted, not written; host relaunches)
+};
+
+constexpr int kDrJ = 8;                           // kids per thread: 2048-kid chunks per block
+__global__ void __launch_bounds__(kBlock) drain_route_kernel(DrainRouteArgs r, const EngineConst* __restrict__ cp) {
+    const EngineConst& c = *cp;
+    const int32_t w = blockIdx.x / r.f.blocks_per_win;
+    const int64_t chunk = blockIdx.x % r.f.blocks_per_win;
+    const FireWindow win = r.f.win[w];
+    const unsigned long long* __restrict__ slot0 = r.f.slot_base[r.f.win_slots[win.slot_off]];
+    const unsigned long long* __restrict__ keys = r.f.key_table;
+    const int64_t cap_k = r.f.capacity, nk = cap_k + 1, stride = r.f.stride;
+    const int tid = threadIdx.x;
+    const int par = r.par, m = r.m, ncell = r.ncell;
+    __shared__ uint32_t s_cnt[kMaxDest], s_pos[kMaxDest];
+    __shared__ unsigned long long s_base[kMaxDest];
+    __shared__ int32_t s_cell[kMaxAggsInt];
+    for (int d = tid; d < par; d += kBlock) { s_cnt[d] = 0; s_pos[d] = 0; }
+    for (int i = tid; i < ncell; i += kBlock) s_cell[i] = r.cell_acc[i];
+    __syncthreads();
+    const int64_t k0 = chunk * (int64_t)kBlock * kDrJ;
+    uint64_t cnt[kDrJ];
+    int32_t dst[kDrJ];
+#pragma unroll
+    for (int j = 0; j < kDrJ; ++j) {
+        const int64_t k = k0 + (int64_t)j * kBlock + tid;
+        cnt[j] = 0;
+        if (k < nk) {
+            const unsigned long long kv = keys[k];
+            if ((k < cap_k) ? (kv != kEmptyKey) : (kv == 1ull)) cnt[j] = slot0[k];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kDrJ; ++j) {
+        dst[j] = 0;
+        if (!cnt[j]) continue;
+        const int64_t k = k0 + (int64_t)j * kBlock + tid;
+        const int64_t key = (k < cap_k) ? (int64_t)keys[k] : LONG_MIN_J;
+        const int32_t kg = jm::key_group_of(key, c.key_kind, 0, c.max_par);
+        dst[j] = kg < 0 ? 0 : jm::operator_index(c.max_par, par, kg);
+        atomicAdd(&s_cnt[dst[j]], 1u);
+    }
+    __syncthreads();
+    for (int d = tid; d < par; d += kBlock) s_base[d] = s_cnt[d] ? atomicAdd(&r.dcnt[d], (unsigned long long)s_cnt[d]) : 0ull;
+    __syncthreads();
+    for (int j = 0; j < kDrJ; ++j) {
+        if (!cnt[j]) continue;
+        const int64_t k = k0 + (int64_t)j * kBlock + tid;
+        const int d = dst[j];
+        const unsigned long long pos = s_base[d] + atomicAdd(&s_pos[d], 1u);
+        if ((int64_t)pos >= r.cap) continue;
+        int64_t* row = r.rows + ((int64_t)d * r.cap + (int64_t)pos) * m;
+        row[0] = (k < cap_k) ? (int64_t)keys[k] : LONG_MIN_J;
+        row[1] = win.start;
+        row[2] = (int64_t)cnt[j];
+        for (int i = 0; i < ncell; ++i) {
+            const int a = s_cell[i];
+            row[3 + i] = a > 0 ? (int64_t)slot0[(int64_t)a * stride + k] : (int64_t)cnt[j];
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // fire_slide: one watermark fires a RUN of consecutive hop windows (HOP 60 s / 1 s over a batch of
 // 67 s of event time fires 67 windows of 60 slices each). The generic fire re-merges every window
@@ -2003,6 +2077,11 @@ struct fwa_engine {
     double mf_capx = 2.0;                 // bucket region = mean rows per bucket x this (+ slack); grows on overflow
     int32_t opt_fire_partials = -1;       // FWA_OPT_FIRE_PARTIALS: -1 / 1 the merge-fire path where eligible, 0 never
     int64_t mf_calls = 0, mf_fallbacks = 0;
+    // fwa_drain_route: send regions [par][dr_cap][cells] and the per-destination row counters (d_dr_cnt)
+    int64_t* d_dr = nullptr;
+    unsigned long long* d_dr_cnt = nullptr;
+    size_t dr_bytes = 0;
+    int64_t dr_cap = 0, dr_cap_used = 0;
     long long* d_prof = nullptr;          // FWA_OPT_PROFILE: per-block phase cycle counters of Phase P / A
 };
 
@@ -2497,7 +2576,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos, e->d_zslice, e->d_rsum,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4, e->d_rk, e->d_mf};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4, e->d_rk, e->d_mf, e->d_dr, e->d_dr_cnt};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -4057,6 +4136,128 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
 
 static int retire_slices(fwa_engine* e, int64_t wm);
 static int fill_out(fwa_engine* e, int64_t nrows, fwa_out* out);
+// fwa_drain_route's launch: the drained slices straight into per-destination send regions; a region past its
+// capacity is counted, the host grows the regions and launches again (the drain is idempotent until the reset).
+static int launch_drain_route(fwa_engine* e, const std::vector<FireWindow>& hw, const std::vector<int32_t>& hs, int32_t par,
+                              int32_t m, const int32_t* cell_acc, std::vector<unsigned long long>& counts) {
+    int rc = upload_windows(e, hw, hs);
+    if (rc) return rc;
+    DrainRouteArgs r;
+    memset(&r, 0, sizeof(r));
+    r.f.key_table = e->d_keys;
+    r.f.capacity = e->capacity;
+    r.f.stride = e->stride;
+    r.f.slot_base = e->d_slot_base;
+    r.f.win = e->d_win;
+    r.f.win_slots = e->d_win_slots;
+    r.f.nwin = (int32_t)hw.size();
+    r.f.blocks_per_win = (int32_t)((e->capacity + 1 + (int64_t)kBlock * kDrJ - 1) / ((int64_t)kBlock * kDrJ));
+    r.par = par;
+    r.m = m;
+    r.ncell = m - 3;
+    for (int i = 0; i < m - 3; ++i) r.cell_acc[i] = cell_acc[i];
+    if (!e->d_dr_cnt) HIPCHK(e, hipMalloc(&e->d_dr_cnt, sizeof(unsigned long long) * kMaxDest));
+    // first sizing: the last drain's largest region x 1.25 (at least 2^16 rows, at most every key of every slice)
+    const int64_t nkeys = std::max<int64_t>((int64_t)e->h_st->n_keys, 1);
+    const int64_t bound = (int64_t)hw.size() * nkeys;
+    int64_t cap = std::min<int64_t>(bound, std::max<int64_t>((int64_t)1 << 16, e->dr_cap));
+    counts.assign(par, 0);
+    for (int round = 0; round < 3; ++round) {
+        const size_t need = (size_t)par * cap * m * 8;
+        if (need > e->dr_bytes) {
+            if (e->d_dr) HIPCHK(e, hipFree(e->d_dr));
+            e->d_dr = nullptr;
+            e->dr_bytes = 0;
+            HIPCHK(e, hipMalloc(&e->d_dr, need));
+            e->dr_bytes = need;
+        }
+        r.cap = cap;
+        r.rows = e->d_dr;
+        r.dcnt = e->d_dr_cnt;
+        HIPCHK(e, hipMemsetAsync(e->d_dr_cnt, 0, sizeof(unsigned long long) * par, e->stream));
+        HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
+        const int64_t grid = (int64_t)r.f.blocks_per_win * (int64_t)hw.size();
+        drain_route_kernel<<<(unsigned)grid, kBlock, 0, e->stream>>>(r, e->d_ec);
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
+        HIPCHK(e, hipMemcpyAsync(counts.data(), e->d_dr_cnt, sizeof(unsigned long long) * par, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        int64_t mx = 0;
+        for (unsigned long long v : counts) mx = std::max<int64_t>(mx, (int64_t)v);
+        e->dr_cap = std::max<int64_t>(e->dr_cap, mx + mx / 4);
+        if (mx <= cap) {
+            e->dr_cap_used = cap;
+            float ms = 0.f;
+            HIPCHK(e, hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+            e->fire_ms += ms;
+            e->fire_launches++;
+            int64_t tot = 0;
+            for (unsigned long long v : counts) tot += (int64_t)v;
+            e->fire_rows += tot;
+            return FWA_OK;
+        }
+        cap = mx + mx / 4;                         // grow to the exact need (+25 % for the next drains), again
+    }
+    return fail(e, FWA_E_STATE, "fwa_drain_route: regions did not converge");
+}
+
+int fwa_drain_route(fwa_engine* e, int64_t wm, int32_t parallelism, fwa_routed* out) {
+    if (!e || !out) return FWA_E_ARG;
+    memset(out, 0, sizeof(*out));
+    if (parallelism < 1 || parallelism > FWA_MAX_DEST) return fail(e, FWA_E_ARG, "fwa_drain_route: parallelism");
+    if (e->red || e->dec || e->kind == FWA_SESSION || e->sparse || !e->cfg.output_on_device ||
+        e->cfg.key_kind == FWA_KEY_PREHASHED)
+        return fail(e, FWA_E_UNSUPPORTED, "fwa_drain_route: a dense slicing-window handle with output_on_device");
+    e->rs_valid = false;
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    if (int rc0 = settle_pending(e)) return rc0;
+    // cells: key, slice start, COUNT(*), one per user aggregate other than COUNT(*), one per hidden counter
+    int32_t cell_acc[kMaxAggsInt];
+    int32_t m = 3;
+    for (int j = 0; j < e->ec.nout; ++j)
+        if (e->ec.agg[j].kind != FWA_COUNT) cell_acc[m++ - 3] = e->ec.agg[j].acc;
+    for (int h = e->ec.nout; h < e->ec.naggs; ++h) cell_acc[m++ - 3] = e->ec.agg[h].acc;
+    std::vector<FireWindow> hw;
+    std::vector<int32_t> hs;
+    for (auto& kv : e->live) {
+        if (!e->touched[kv.second]) continue;
+        FireWindow f;
+        f.start = slice_start(e, kv.first);
+        f.end = jm::wadd(f.start, e->g);
+        if (wm != LONG_MAX_J && !(trig(e, jm::wsub(f.end, 1)) <= wm)) continue;   // slice not complete at wm
+        f.slot_off = (int32_t)hs.size();
+        f.nslots = 1;
+        hs.push_back(kv.second);
+        hw.push_back(f);
+    }
+    std::vector<unsigned long long> counts(parallelism, 0);
+    if (!hw.empty()) {
+        int rc = launch_drain_route(e, hw, hs, parallelism, m, cell_acc, counts);
+        if (rc) return rc;
+        for (int32_t slot : hs) {
+            rc = reset_slot(e, slot);
+            if (rc) return rc;
+        }
+        rc = flush_resets(e);
+        if (rc) return rc;
+    }
+    if (wm > e->wm) {   // forward the watermark, as fwa_drain_partials
+        int rc = retire_slices(e, wm);
+        if (rc) return rc;
+        e->wm = wm;
+    }
+    out->parallelism = parallelism;
+    out->cells = m;
+    out->on_device = 1;
+    for (int d = 0; d < parallelism; ++d) {
+        out->rows[d] = e->d_dr ? e->d_dr + (size_t)d * e->dr_cap_used * m : nullptr;
+        out->count[d] = (int64_t)counts[d];
+        out->n += (int64_t)counts[d];
+    }
+    return FWA_OK;
+}
+
+
 
 // fwa_fire_partials through its two defining calls: the rows' cells as columns, fwa_push_partials, then
 // fwa_advance_watermark (every case the merge-fire path does not take, and its redo).
@@ -4130,10 +4331,11 @@ int fwa_fire_partials(fwa_engine* e, const int64_t* rows, int64_t n, int32_t m, 
             if (d.acc > 0 && !d.alias) a.cell[d.acc] = acc_cell[j];
         }
         for (int cc = 1; cc < nacc; ++cc) fast = fast && a.cell[cc] >= 3 && e->ec.acc_kind[cc] != ACC_PAYLOAD;
+        fast = fast && nacc - 1 <= kMfAcc;
     }
     if (!fast) return fire_partials_generic(e, rows, n, m, acc_cell, wm, flags, out, late_dropped_out);
     e->mf_calls++;
-    static const size_t kLds = getenv("FWA_MF_LDS") ? (size_t)atoi(getenv("FWA_MF_LDS")) * 1024 : 150 * 1024;
+    constexpr size_t kLds = 150 * 1024;
     const size_t ebytes = 20 + 8 * (size_t)nacc;
     int hlog = 14;
     while (hlog > 8 && ((size_t)1 << hlog) * ebytes + 64 > kLds) --hlog;

@@ -22,6 +22,8 @@ Rank r owns key groups key_group_range_for_operator(maxP, world, r). Two exchang
 Each advance_watermark takes the MIN over ranks (the valve), then fires locally. No other collective
 is on the data path.
 """
+import contextlib
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -105,6 +107,18 @@ class KeyedWindowPipeline:
         self.names = A.agg_names(self.cfg)
         self.exchanged = 0
         self.wm_group = valve_group(group)       # host-side MIN valve (gloo under RCCL; see valve_group)
+        self._xstream = None
+
+    def _exchange_stream(self, t):
+        """The exchange's own torch stream for CUDA batches: routing, the all-to-all and the engine's read of the
+        received rows are ordered on the device (the engine waits for this stream through fwa_set_input_stream), so
+        no step waits on the host for torch's default stream, which the engine's stream cannot wait on."""
+        if not t.is_cuda:
+            return contextlib.nullcontext()
+        if self._xstream is None:
+            self._xstream = torch.cuda.Stream(device=t.device)
+        self._xstream.wait_stream(torch.cuda.current_stream(t.device))   # the batch's producers
+        return torch.cuda.stream(self._xstream)
 
     def _a2a(self, x, send_splits, recv_splits):
         out = torch.empty(sum(recv_splits), dtype=x.dtype, device=x.device)
@@ -114,11 +128,12 @@ class KeyedWindowPipeline:
     def push(self, keys, ts, cols=()):
         """keys/ts/cols: this rank's source records (torch tensors on the rank's device)."""
         cols = list(cols)
-        recv = exchange_rows(self, keys, [keys, ts] + cols)
-        k, t = recv[:, 0].contiguous(), recv[:, 1].contiguous()
-        c = [unpack_col(recv[:, 2 + j], x.dtype) for j, x in enumerate(cols)]
-        if k.is_cuda:
-            return self.engine.push(k, t, c)
+        with self._exchange_stream(keys):
+            recv = exchange_rows(self, keys, [keys, ts] + cols)
+            k, t = recv[:, 0].contiguous(), recv[:, 1].contiguous()
+            c = [unpack_col(recv[:, 2 + j], x.dtype) for j, x in enumerate(cols)]
+            if k.is_cuda:
+                return self.engine.push(k, t, c)
         return self.engine.push(k.numpy(), t.numpy(), [x.numpy() for x in c])
 
     def global_watermark(self, local_wm):
@@ -175,6 +190,19 @@ def send_rows(pipe, packed, counts):
     return out
 
 
+def send_parts(pipe, parts, counts, m):
+    """The exchange of fwa_drain_route's per-destination row blocks: the split sizes are the drain's host counts,
+    exchanged on the host (the valve's gloo group: no device read), then one all_to_all of the blocks (RCCL)."""
+    sc = torch.tensor(counts, dtype=torch.int64)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=pipe.wm_group)
+    recv = rc.tolist()
+    out = torch.empty((sum(recv), m), dtype=torch.int64, device=parts[0].device)
+    dist.all_to_all(list(out.split(recv)), [p.contiguous() for p in parts], group=pipe.group)
+    pipe.exchanged += sum(counts) - counts[pipe.rank]
+    return out
+
+
 def exchange_rows(pipe, keys, cols):
     """keyBy exchange of a row set: route by key group, pack the columns into one int64 [n, m] tensor grouped by
     destination, exchange (RCCL over xGMI). Returns the received rows (int64 [n_recv, m]; 4-byte columns travel
@@ -201,6 +229,8 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
             local_factory = WindowAggregator
         self.local = local_factory(self.local_cfg)
         self.partials_sent = 0
+        # the drain writes the send layout itself (fwa_drain_route) when the local engine is a device handle
+        self.routed_drain = lkw["output_on_device"] == 1 and hasattr(self.local, "drain_route")
 
     def push(self, keys, ts, cols=()):
         if keys.is_cuda:
@@ -213,6 +243,15 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
         this watermark proceed (software pipelining across steps; each engine still sees its own calls in stream
         order: drain(wm), push(next) on the local one, merge(wm), fire(wm) on the owner)."""
         wm = self.global_watermark(local_wm)
+        if self.routed_drain:
+            try:
+                parts, counts, m = self.local.drain_route(wm, self.world)
+            except RuntimeError as ex:                  # FWA_E_UNSUPPORTED (e.g. record lists): drain, then route
+                if getattr(ex, "code", None) != -7:
+                    raise
+                self.routed_drain = False
+            else:
+                return self._send_routed_and_fire(wm, parts, counts, m, device_output, then_push)
         p = self.local.drain_partials(wm)
         # a COUNT(*) aggregate's accumulator repeats the row count: it is not shipped (rebuilt on arrival)
         ship = [j for j, name in enumerate(self.names) if name != "COUNT"]
@@ -220,6 +259,22 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
         cols = [p["key"], p["slice_start"], p["count"]] + [p["acc%d" % j] for j in ship] + \
             [p["hidden%d" % h] for h in range(nh)]
         cols = [c if isinstance(c, torch.Tensor) else torch.from_numpy(c) for c in cols]
+        with self._exchange_stream(cols[0]):
+            return self._exchange_and_fire(wm, cols, ship, nh, device_output, then_push)
+
+    def _send_routed_and_fire(self, wm, parts, counts, m, device_output, then_push):
+        ship = [j for j, name in enumerate(self.names) if name != "COUNT"]
+        nh = m - 3 - len(ship)
+        with self._exchange_stream(parts[0]):
+            if then_push is not None:
+                self.push(*then_push)
+            recv = send_parts(self, parts, counts, m)
+            self.partials_sent += sum(counts)
+            cells = [2 if name == "COUNT" else 3 + ship.index(j) for j, name in enumerate(self.names)] + \
+                [3 + len(ship) + h for h in range(nh)]
+            return self.engine.fire_partials(recv, cells, wm, device_output=device_output)
+
+    def _exchange_and_fire(self, wm, cols, ship, nh, device_output, then_push):
         packed, counts = route_rows(self, cols[0], cols)    # done with the drained buffers from here on
         if then_push is not None:
             self.push(*then_push)

@@ -52,6 +52,8 @@ def lib():
     L.fwa_fire_partials.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.POINTER(C.c_int32), C.c_int64,
                                     C.c_int32, C.POINTER(A.Out), C.POINTER(C.c_int64)]
     L.fwa_fire_partials.restype = C.c_int
+    L.fwa_drain_route.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.POINTER(A.Routed)]
+    L.fwa_drain_route.restype = C.c_int
     L.fwa_snapshot.argtypes = [C.c_void_p, C.POINTER(Blob)]
     L.fwa_snapshot.restype = C.c_int
     L.fwa_blob_free.argtypes = [C.POINTER(Blob)]
@@ -314,6 +316,23 @@ class WindowAggregator:
         for h in range(out.num_hidden):                # nullable handles: hidden non-NULL counters
             res["hidden%d" % h] = conv(out.hidden[h], n, i8)
         return res
+
+    def drain_route(self, wm, parallelism):
+        """fwa_drain_route: drain_partials and the keyBy routing in one pass. Returns ([int64 [count_d, cells] torch
+        CUDA view per destination d, valid until the next call on this handle], [count_d] host ints, cells)."""
+        import torch
+        out = A.Routed()
+        rc = lib().fwa_drain_route(self.h, int(wm), int(parallelism), C.byref(out))
+        self._settled()
+        _check(rc, self.h)
+        m = out.cells
+        dev = torch.device("cuda", self.cfg.device)
+        parts = []
+        for d in range(parallelism):
+            n = out.count[d]
+            parts.append(dev_view(out.rows[d], n * m, np.dtype("i8")).view(n, m) if n and out.rows[d]
+                         else torch.empty((0, m), dtype=torch.int64, device=dev))
+        return parts, [int(out.count[d]) for d in range(parallelism)], m
 
     def push_partials(self, keys, slice_ts, count, accs, hidden=()):
         """Merge partial accumulators (from drain_partials on a handle with the same window / aggregate

@@ -25,6 +25,8 @@
  *   fwa_drain_partials     LocalSlicingWindowAggOperator -> RecordsWindowBuffer.flush (local half of two-phase)
  *                            LocalSlicingWindowAggOperator.java:111-137
  *   fwa_push_partials      GlobalAggCombiner.combine (global half)  GlobalAggCombiner.java:77-110
+ *   fwa_drain_route        fwa_drain_partials + the keyBy send side in one pass (packed rows per owning subtask)
+ *   fwa_fire_partials      the owner's GlobalAggCombiner.combine + window fire over the received packed rows
  *   fwa_route_rows         KeyGroupStreamPartitioner.selectChannel + per-channel packing (the keyBy send side)
  *   fwa_key_groups         KeyGroupRangeAssignment.assignToKeyGroup + computeOperatorIndexForKeyGroup
  *                            flink-runtime/.../state/KeyGroupRangeAssignment.java:63-127
@@ -356,6 +358,27 @@ typedef struct fwa_partials {
  * slices past cleanup are released). A handle drained this way never emits window rows itself: the
  * owner merges the partials with fwa_push_partials before advancing its own watermark to wm. */
 int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out);
+
+/* fwa_drain_route's export: the drained (key, slice) partials as packed rows grouped by owning subtask. */
+#define FWA_MAX_DEST 64
+typedef struct fwa_routed {
+    int64_t n;                        /* rows drained, all destinations */
+    int32_t parallelism, cells;       /* destinations; 8-byte cells per row */
+    int32_t on_device, pad;           /* 1: rows are device pointers (always) */
+    const int64_t* rows[FWA_MAX_DEST];/* destination d's rows, [count[d]][cells], engine-owned, valid until the next
+                                         call on the handle */
+    int64_t count[FWA_MAX_DEST];
+} fwa_routed;
+
+/* fwa_drain_partials and the keyBy send side (fwa_route_rows) in one pass: the same (key, slice) partials, each
+ * written as a packed row -- cell 0 key, 1 slice start, 2 COUNT(*), then one cell per user aggregate other than
+ * COUNT(*) (its accumulator, or COUNT(*) for an aggregate that keeps none), then one per hidden non-NULL counter --
+ * into the region of the subtask owning its key group (computeOperatorIndexForKeyGroup(max_parallelism,
+ * parallelism, assignToKeyGroup(key)), KeyGroupStreamPartitioner.selectChannel). The per-destination counts are host
+ * values: the exchange's split sizes need no device read. Dense slicing-window handles with output_on_device
+ * (FWA_E_UNSUPPORTED otherwise: use fwa_drain_partials + fwa_route_rows). The rows feed fwa_fire_partials on the
+ * owner with acc_cell[j] = the cell of aggregate j as laid out here. */
+int fwa_drain_route(fwa_engine* e, int64_t wm, int32_t parallelism, fwa_routed* out);
 
 /* Merge partial accumulators (as produced by fwa_drain_partials on another handle with the same
  * window and aggregate configuration) into this handle's state. slice_ts may be any timestamp inside

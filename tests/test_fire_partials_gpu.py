@@ -183,3 +183,40 @@ def test_fire_partials_key_group_error():
         assert ei.value.code == -3          # FWA_E_KEYGROUP
         own.close()
     loc.close()
+
+
+@pytest.mark.parametrize("par", [1, 3, 8])
+@pytest.mark.parametrize("case", ["ds_tumble_int", "table_tumble_nullable"])
+def test_drain_route_equals_drain_then_route(case, par):
+    """fwa_drain_route: the rows of fwa_drain_partials, packed in the exchange's layout and grouped by owning subtask
+    exactly as fwa_route_rows groups them (row order inside a destination aside)."""
+    from flink_amd import engine
+    cfg = A.make_config(output_on_device=1, key_capacity=4096, **CASES[case])
+    names = A.agg_names(cfg)
+    a, b = engine.WindowAggregator(cfg), engine.WindowAggregator(cfg)
+    srt = lambda x: x[np.lexsort((x[:, 1], x[:, 0]))] if len(x) else x  # noqa: E731   (key, slice): unique
+    total = 0
+    for sl, keys, ts, cols, nulls, wm in stream(case, 45, nb=6):
+        if sl.stop > sl.start:
+            for x in (a, b):
+                local_push(x, 0, sl, keys, ts, cols, nulls)
+        parts, counts, m = a.drain_route(wm, par)
+        rows, _ = pack([b.drain_partials(wm)], names)
+        packed, cnt = engine.route_rows(rows[:, 0].contiguous(), [rows[:, j].contiguous() for j in range(rows.shape[1])],
+                                        128, par)
+        assert m == rows.shape[1] and counts == cnt.tolist()
+        # float sums accumulate with LDS atomics in either handle: their bits may differ in the last place
+        ship = [j for j, nm in enumerate(names) if nm != "COUNT"]
+        fcell = [3 + i for i, j in enumerate(ship) if names[j] in ("SUM_F64", "AVG_F64", "SUM_F32", "AVG_F32")]
+        icell = [c for c in range(m) if c not in fcell]
+        off = 0
+        for d in range(par):
+            got = srt(parts[d].cpu().numpy())
+            exp = srt(packed[off:off + counts[d]].cpu().numpy())
+            off += counts[d]
+            assert np.array_equal(got[:, icell], exp[:, icell]), (case, par, d)
+            assert np.allclose(got[:, fcell].view(np.float64), exp[:, fcell].view(np.float64), rtol=1e-12, atol=1e-9)
+        total += sum(counts)
+    assert total > 1000
+    a.close()
+    b.close()

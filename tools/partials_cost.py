@@ -1,7 +1,8 @@
 """Per-rank step cost of the N>1 two-phase plan on one GPU (C2 batch), against the N=1 step (push + fire).
 
 Each step prices the pieces one rank runs at N = WORLD (default 8) under weak scaling:
-  local  push (the rank's own 2^26 records), drain_partials, GPU routing (fwa_route_rows by key group, WORLD ways);
+  local  push (the rank's own 2^26 records), then fwa_drain_route (drain + routing by key group, WORLD ways, in one
+         pass; --routed 0: drain_partials, then fwa_route_rows);
   owner  what it does with what it receives -- this rank's rows for destination 0, repeated WORLD times (one copy
          per source rank: the same keys and windows, each source holding its own partial), sources back to back as
          in the receive buffer: "merge_fire" = fwa_fire_partials on the packed rows (the pipeline's path), "sources"
@@ -27,6 +28,7 @@ ap.add_argument("--steps", type=int, default=6)
 ap.add_argument("--order", default="merge_fire,sources")
 ap.add_argument("--owner-share", type=int, default=1, help="1: owner key capacity sized to its key-group share")
 ap.add_argument("--dup", type=int, default=0, help="copies of the destination-0 rows the owner receives (0: world)")
+ap.add_argument("--routed", type=int, default=1, help="1: fwa_drain_route (drain + routing in one pass)")
 ap.add_argument("--owner-profile", type=int, default=0, help="FWA_OPT_PROFILE on the owners (per-block phase cycles)")
 args = ap.parse_args()
 
@@ -79,11 +81,17 @@ for b in range(S):
     _, t["n1_push"] = timed(lambda: single.push(keys[sl], ts[sl], [vals[sl]]))
     _, t["n1_fire"] = timed(lambda: single.advance_watermark_raw(wm).n_rows)
     _, t["push"] = timed(lambda: local.push(keys[sl], ts[sl], [vals[sl]]))
-    d, t["drain"] = timed(lambda: local.drain_partials(wm))
-    cols = [d["key"], d["slice_start"], d["count"], d["acc1"]]
-    (packed, counts), t["route"] = timed(lambda: E.route_rows(cols[0], cols, 128, W))
-    n0 = int(counts[0].item())
-    recv = packed[:n0].repeat(args.dup or W, 1)                     # what the owner receives: one copy per source rank
+    if args.routed:     # fwa_drain_route: the drain writes the per-destination send blocks itself
+        (parts, counts, m), t["drain_route"] = timed(lambda: local.drain_route(wm, W))
+        recv = parts[0].repeat(args.dup or W, 1)
+        d = {"key": torch.empty(sum(counts))}
+        packed = torch.empty((sum(counts), m), dtype=torch.int64)
+    else:
+        d, t["drain"] = timed(lambda: local.drain_partials(wm))
+        cols = [d["key"], d["slice_start"], d["count"], d["acc1"]]
+        (packed, counts), t["route"] = timed(lambda: E.route_rows(cols[0], cols, 128, W))
+        n0 = int(counts[0].item())
+        recv = packed[:n0].repeat(args.dup or W, 1)                 # what the owner receives: one copy per source rank
     cells = [2, 3]
     for o in orders:
         if o == "merge_fire":
@@ -105,7 +113,8 @@ n = S - 2
 n1 = (tot["n1_push"] + tot["n1_fire"]) / n
 print("N=1 step %.3f ms (push %.3f, fire %.3f)" % (n1, tot["n1_push"] / n, tot["n1_fire"] / n))
 for o in orders:
-    parts = ["push", "drain", "route"] + ([o] if o == "merge_fire" else [o + "_unpack", o + "_merge", o + "_fire"])
+    parts = ["push"] + (["drain_route"] if args.routed else ["drain", "route"]) + \
+        ([o] if o == "merge_fire" else [o + "_unpack", o + "_merge", o + "_fire"])
     s = sum(tot[k] for k in parts) / n
     print("N=%d per-rank step, owner order %s: %.3f ms = %s -> %.2fx N=1" %
           (W, o, s, " + ".join("%s %.3f" % (k, tot[k] / n) for k in parts), s / n1))
