@@ -197,8 +197,13 @@ def send_parts(pipe, parts, counts, m):
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc, group=pipe.wm_group)
     recv = rc.tolist()
-    out = torch.empty((sum(recv), m), dtype=torch.int64, device=parts[0].device)
-    dist.all_to_all(list(out.split(recv)), [p.contiguous() for p in parts], group=pipe.group)
+    if dist.get_backend(pipe.group) == "nccl":
+        out = torch.empty((sum(recv), m), dtype=torch.int64, device=parts[0].device)
+        dist.all_to_all(list(out.split(recv)), [p.contiguous() for p in parts], group=pipe.group)
+    else:                                              # gloo rehearsal: host staging of the device blocks
+        host = torch.empty((sum(recv), m), dtype=torch.int64)
+        dist.all_to_all_single(host, torch.cat(parts).cpu(), recv, counts, group=pipe.group)
+        out = host.to(parts[0].device)
     pipe.exchanged += sum(counts) - counts[pipe.rank]
     return out
 
@@ -218,11 +223,15 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
     KeyedWindowPipeline; pushes involve no collective."""
 
     def __init__(self, rank, world, group=None, engine_factory=None, router=None, local_factory=None,
-                 owner_capacity="share", **cfg_kw):
+                 owner_capacity="share", routed=None, **cfg_kw):
+        """routed: the drain writes the exchange's per-subtask blocks itself (fwa_drain_route); default under RCCL,
+        True forces it on a gloo group (rehearsals on one GPU: the blocks are staged through the host)."""
         super().__init__(rank, world, group=group, engine_factory=engine_factory, router=router,
                          owner_capacity=owner_capacity, **cfg_kw)
         lkw = dict(cfg_kw)
-        lkw["output_on_device"] = 1 if dist.get_backend(group) == "nccl" else 0
+        if routed is None:
+            routed = dist.get_backend(group) == "nccl"
+        lkw["output_on_device"] = 1 if (routed or dist.get_backend(group) == "nccl") else 0
         self.local_cfg = A.make_config(**lkw)           # the pre-aggregator sees every key group
         if local_factory is None:
             from .engine import WindowAggregator
@@ -230,7 +239,7 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
         self.local = local_factory(self.local_cfg)
         self.partials_sent = 0
         # the drain writes the send layout itself (fwa_drain_route) when the local engine is a device handle
-        self.routed_drain = lkw["output_on_device"] == 1 and hasattr(self.local, "drain_route")
+        self.routed_drain = bool(routed) and hasattr(self.local, "drain_route")
 
     def push(self, keys, ts, cols=()):
         if keys.is_cuda:

@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 AGGS = [("COUNT", 0), ("SUM_I64", 0), ("MIN_I64", 0), ("MAX_I64", 0)]
 CFG = dict(window_kind="SLIDE", size_ms=4000, slide_ms=1000, aggs=AGGS, key_capacity=1 << 13)
+CFG_T = dict(window_kind="TUMBLE", size_ms=2000, aggs=AGGS, key_capacity=1 << 13)   # merged + fired on chip
 NB, PER, DELAY = 6, 4000, 1500
 
 
@@ -46,20 +47,22 @@ def _wms(streams):
     return out + [A.LONG_MAX]
 
 
-def _worker(rank, world, port, outdir, two_phase):
+def _worker(rank, world, port, outdir, two_phase, routed=False, cfg=None):
+    cfg = cfg or CFG
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from flink_amd.distributed import KeyedWindowPipeline, TwoPhaseKeyedWindowPipeline
     cls = TwoPhaseKeyedWindowPipeline if two_phase else KeyedWindowPipeline
-    pipe = cls(rank, world, **CFG)
+    pipe = cls(rank, world, routed=True, **cfg) if routed else cls(rank, world, **cfg)
     keys, ts, vals = _stream(7 + rank, NB * PER)
     rows = []
+    dev = (lambda x: torch.from_numpy(x).cuda()) if routed else torch.from_numpy  # noqa: E731
     for b in range(NB + 1):
         if b < NB:
             sl = slice(b * PER, (b + 1) * PER)
-            pipe.push(torch.from_numpy(keys[sl]), torch.from_numpy(ts[sl]), [torch.from_numpy(vals[sl])])
+            pipe.push(dev(keys[sl]), dev(ts[sl]), [dev(vals[sl])])
             local_wm = int(ts[: (b + 1) * PER].max()) - DELAY - 1
         else:
             local_wm = A.LONG_MAX
@@ -73,14 +76,18 @@ def _worker(rank, world, port, outdir, two_phase):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("two_phase", [False, True], ids=["raw_records", "two_phase_partials"])
-def test_two_rank_pipeline_on_gpu(tmp_path, two_phase):
+@pytest.mark.parametrize("two_phase,routed,cfg", [(False, False, CFG), (True, False, CFG), (True, True, CFG),
+                                                  (True, True, CFG_T)],
+                         ids=["raw_records", "two_phase_partials", "two_phase_routed_device", "two_phase_routed_tumble"])
+def test_two_rank_pipeline_on_gpu(tmp_path, two_phase, routed, cfg):
+    """routed: the device path of the RCCL plan (fwa_drain_route -> block exchange -> fwa_fire_partials) with the
+    blocks staged through the host, since both ranks share the one GPU (RCCL refuses two ranks on one device)."""
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), two_phase), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), two_phase, routed, cfg), nprocs=world, join=True)
     got = np.concatenate([np.load(tmp_path / ("rank%d.npy" % r)) for r in range(world)])
     dropped = sum(int(np.load(tmp_path / ("drop%d.npy" % r))[0]) for r in range(world))
     from oracle.oracle import Oracle
-    o = Oracle(A.make_config(**CFG))
+    o = Oracle(A.make_config(**cfg))
     streams = [_stream(7 + r, NB * PER) for r in range(world)]
     exp = []
     dropped_o = 0
