@@ -4340,11 +4340,13 @@ int fwa_fire_partials(fwa_engine* e, const int64_t* rows, int64_t n, int32_t m, 
     int hlog = 14;
     while (hlog > 8 && ((size_t)1 << hlog) * ebytes + 64 > kLds) --hlog;
     const int64_t H = (int64_t)1 << hlog;
-    // buckets: the groups expected (rows x twice the groups per row of the last call, at most one per row) at <= H/2
-    // per bucket; the redo resets the estimate
-    const double exp_groups = std::max(1.0, (double)n * std::min(1.0, 2.0 * e->mf_groups_per_row));
+    // buckets: the groups expected (rows x 1.25 x the groups per row of the last call, at most one per row) at a table
+    // load <= 0.7 (C2 at N = 8: 512 buckets of ~1700 groups, load ~0.42 -- fewer, longer bucket runs for mf_part than
+    // at <= 0.5 x 2: 1.33x vs 1.36x of N = 1 per rank, profiles/r05_partials_cost.txt); a full table redoes the call
+    // and resets the estimate to one group per row
+    const double exp_groups = std::max(1.0, (double)n * std::min(1.0, 1.25 * e->mf_groups_per_row));
     int nb_log = 0;
-    while (nb_log < 12 && (double)(H / 2) * (double)((int64_t)1 << nb_log) < exp_groups) ++nb_log;
+    while (nb_log < 12 && (double)H * 0.7 * (double)((int64_t)1 << nb_log) < exp_groups) ++nb_log;
     const int64_t NB = (int64_t)1 << nb_log;
     const int64_t capb = (int64_t)((double)(n / NB) * e->mf_capx) + 512;
     int64_t tile = (int64_t)((150 * 1024 - 12 * (size_t)NB - 16) / (8 + 8 * (size_t)m));
