@@ -279,7 +279,8 @@ def main():
             "workload": workload,
             "records_per_gpu_timed": args.steps * B, "keys": args.keys, "batch": B,
             "window_ms": args.window_ms, "parallelism": "key-group dp%d" % world,
-            "exchange": ("two-phase partials (local pre-aggregation, RCCL all_to_all)" if args.exchange == "partials"
+            "exchange": ("two-phase partials (local pre-aggregation, fwa_drain_route per-subtask blocks, RCCL "
+                         "all_to_all, owner fwa_fire_partials)" if args.exchange == "partials"
                          else "raw records (RCCL all_to_all)") if world > 1 else "none",
         },
         "roofline": {
