@@ -94,7 +94,7 @@ class KeyedWindowPipeline:
         okw = dict(cfg_kw)
         if owner_capacity == "share":
             if not cfg_kw.get("record_lists") and cfg_kw.get("key_capacity"):
-                okw["key_capacity"] = owner_key_capacity(cfg_kw.get("key_capacity", 0), kg1 - kg0, maxp)
+                okw["key_capacity"] = owner_key_capacity(cfg_kw.get("key_capacity", 0), kg1 - kg0 + 1, maxp)
         elif owner_capacity != "full":
             okw["key_capacity"] = int(owner_capacity)
         self.cfg = A.make_config(kg_start=kg0, kg_end=kg1, **okw)

@@ -202,3 +202,23 @@ def test_valve_group_created_once_per_rank_set():
     """under RCCL the watermark valve's gloo group is created once per rank set and shared by every
     pipeline built on it (no group per pipeline instance piling up; two pipelines on one group do not hang)."""
     mp.spawn(_valve_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def test_owner_key_capacity_share():
+    """distributed.owner_key_capacity: an owner's key table sized to its key groups' share (+25 % and a slack), never
+    above the job's capacity; record-list sized key spaces keep theirs (the capacity selects that layout)."""
+    from flink_amd.distributed import owner_key_capacity
+    assert owner_key_capacity(1_000_000, 16, 128) == int(125_000 * 1.25) + 4096
+    assert owner_key_capacity(8192, 64, 128) == 8192                 # share + slack above the job's capacity
+    assert owner_key_capacity(1 << 25, 16, 128) == 1 << 25           # record lists
+    assert owner_key_capacity(1_000_000, 128, 128) == 1_000_000      # one owner of every key group
+    assert owner_key_capacity(0, 16, 128) == 0                       # engine default
+    # the share covers the owner's keys: key groups spread keys evenly (murmur), 8 owners of 200K random keys
+    from flink_amd.keygroups import key_group_range_for_operator
+    from oracle.oracle import lib as olib
+    L = olib()
+    keys = np.random.default_rng(3).integers(-2**62, 2**62, 200_000)
+    kg = np.array([L.or_key_group(int(k), 0, 0, 128) for k in keys.tolist()])
+    for r in range(8):
+        lo, hi = key_group_range_for_operator(128, 8, r)
+        assert int(((kg >= lo) & (kg <= hi)).sum()) <= owner_key_capacity(200_000, hi - lo + 1, 128)

@@ -54,13 +54,13 @@ kg0, kg1 = key_group_range_for_operator(128, W, 0)
 okw = dict(kw)
 if args.owner_share:
     from flink_amd.distributed import owner_key_capacity
-    okw["key_capacity"] = owner_key_capacity(KEYS, kg1 - kg0, 128)
+    okw["key_capacity"] = owner_key_capacity(KEYS, kg1 - kg0 + 1, 128)
 orders = args.order.split(",")
 owners = {o: E.WindowAggregator(A.make_config(kg_start=kg0, kg_end=kg1, **okw)) for o in orders}
 for o in owners.values():
     if args.owner_profile:
         o.set_option("profile", 1)
-print("world %d, owner key groups [%d, %d), owner key capacity %d" % (W, kg0, kg1, okw["key_capacity"]), flush=True)
+print("world %d, owner key groups [%d, %d], owner key capacity %d" % (W, kg0, kg1, okw["key_capacity"]), flush=True)
 
 
 def timed(fn):
