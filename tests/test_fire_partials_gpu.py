@@ -220,3 +220,29 @@ def test_drain_route_equals_drain_then_route(case, par):
     assert total > 1000
     a.close()
     b.close()
+
+
+def test_table_full_after_a_duplicated_call_is_redone():
+    """Buckets are sized from the groups per row the last call saw: after a call whose rows repeat each group 8 times,
+    a call of distinct groups overfills the LDS tables, the call is redone through the defining calls (same rows) and
+    the next call is sized for one group per row again and merges on chip."""
+    from flink_amd import engine
+    kw = dict(window_kind="TUMBLE", size_ms=1000, aggs=[("COUNT", 0), ("SUM_I64", 0)], key_capacity=1 << 18)
+    names = A.agg_names(A.make_config(**kw))
+    fast, slow = pair(kw)
+    cells = [2, 3]
+
+    def rows_of(keys, start, copies):
+        k = torch.as_tensor(np.repeat(keys, copies), device="cuda")
+        return torch.stack([k, torch.full_like(k, start), torch.ones_like(k), k * 7], dim=1)
+
+    steps = [(rows_of(np.arange(12_500), 0, 8), 999),            # 8 copies per group: ~1/8 group per row
+             (rows_of(np.arange(100_000), 1000, 1), 1999),       # distinct groups: the tables overfill -> redone
+             (rows_of(np.arange(100_000), 2000, 1), 2999)]       # sized for one group per row again: on chip
+    used = []
+    for rows, wm in steps:
+        assert_rows_equal(fast.fire_partials(rows, cells, wm), slow.fire_partials(rows, cells, wm), names)
+        used.append(fast.get_option("fire_partials"))
+    assert used == [1, 1, 2]
+    fast.close()
+    slow.close()
