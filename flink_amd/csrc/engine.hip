@@ -260,12 +260,11 @@ struct DrainRouteArgs {
 };
 
 constexpr int kDrJ = 8;                           // kids per thread: 2048-kid chunks per block
+// One block per kid chunk walks every drained slice: the key table is read and each key's owner computed once per
+// chunk, not once per (chunk, slice); one cursor reservation per (slice, destination).
 __global__ void __launch_bounds__(kBlock) drain_route_kernel(DrainRouteArgs r, const EngineConst* __restrict__ cp) {
     const EngineConst& c = *cp;
-    const int32_t w = blockIdx.x / r.f.blocks_per_win;
-    const int64_t chunk = blockIdx.x % r.f.blocks_per_win;
-    const FireWindow win = r.f.win[w];
-    const unsigned long long* __restrict__ slot0 = r.f.slot_base[r.f.win_slots[win.slot_off]];
+    const int64_t chunk = blockIdx.x;
     const unsigned long long* __restrict__ keys = r.f.key_table;
     const int64_t cap_k = r.f.capacity, nk = cap_k + 1, stride = r.f.stride;
     const int tid = threadIdx.x;
@@ -273,48 +272,56 @@ __global__ void __launch_bounds__(kBlock) drain_route_kernel(DrainRouteArgs r, c
     __shared__ uint32_t s_cnt[kMaxDest], s_pos[kMaxDest];
     __shared__ unsigned long long s_base[kMaxDest];
     __shared__ int32_t s_cell[kMaxAggsInt];
-    for (int d = tid; d < par; d += kBlock) { s_cnt[d] = 0; s_pos[d] = 0; }
     for (int i = tid; i < ncell; i += kBlock) s_cell[i] = r.cell_acc[i];
-    __syncthreads();
     const int64_t k0 = chunk * (int64_t)kBlock * kDrJ;
-    uint64_t cnt[kDrJ];
-    int32_t dst[kDrJ];
+    int64_t key[kDrJ];
+    int32_t dst[kDrJ];                                 // -1: no key at this kid
 #pragma unroll
     for (int j = 0; j < kDrJ; ++j) {
         const int64_t k = k0 + (int64_t)j * kBlock + tid;
-        cnt[j] = 0;
+        key[j] = 0;
+        dst[j] = -1;
         if (k < nk) {
             const unsigned long long kv = keys[k];
-            if ((k < cap_k) ? (kv != kEmptyKey) : (kv == 1ull)) cnt[j] = slot0[k];
+            if ((k < cap_k) ? (kv != kEmptyKey) : (kv == 1ull)) {
+                key[j] = (k < cap_k) ? (int64_t)kv : LONG_MIN_J;
+                const int32_t kg = jm::key_group_of(key[j], c.key_kind, 0, c.max_par);
+                dst[j] = kg < 0 ? 0 : jm::operator_index(c.max_par, par, kg);
+            }
         }
     }
+    for (int w = 0; w < r.f.nwin; ++w) {
+        const FireWindow win = r.f.win[w];
+        const unsigned long long* __restrict__ slot0 = r.f.slot_base[r.f.win_slots[win.slot_off]];
+        for (int d = tid; d < par; d += kBlock) { s_cnt[d] = 0; s_pos[d] = 0; }
+        __syncthreads();
+        uint64_t cnt[kDrJ];
 #pragma unroll
-    for (int j = 0; j < kDrJ; ++j) {
-        dst[j] = 0;
-        if (!cnt[j]) continue;
-        const int64_t k = k0 + (int64_t)j * kBlock + tid;
-        const int64_t key = (k < cap_k) ? (int64_t)keys[k] : LONG_MIN_J;
-        const int32_t kg = jm::key_group_of(key, c.key_kind, 0, c.max_par);
-        dst[j] = kg < 0 ? 0 : jm::operator_index(c.max_par, par, kg);
-        atomicAdd(&s_cnt[dst[j]], 1u);
-    }
-    __syncthreads();
-    for (int d = tid; d < par; d += kBlock) s_base[d] = s_cnt[d] ? atomicAdd(&r.dcnt[d], (unsigned long long)s_cnt[d]) : 0ull;
-    __syncthreads();
-    for (int j = 0; j < kDrJ; ++j) {
-        if (!cnt[j]) continue;
-        const int64_t k = k0 + (int64_t)j * kBlock + tid;
-        const int d = dst[j];
-        const unsigned long long pos = s_base[d] + atomicAdd(&s_pos[d], 1u);
-        if ((int64_t)pos >= r.cap) continue;
-        int64_t* row = r.rows + ((int64_t)d * r.cap + (int64_t)pos) * m;
-        row[0] = (k < cap_k) ? (int64_t)keys[k] : LONG_MIN_J;
-        row[1] = win.start;
-        row[2] = (int64_t)cnt[j];
-        for (int i = 0; i < ncell; ++i) {
-            const int a = s_cell[i];
-            row[3 + i] = a > 0 ? (int64_t)slot0[(int64_t)a * stride + k] : (int64_t)cnt[j];
+        for (int j = 0; j < kDrJ; ++j) {
+            const int64_t k = k0 + (int64_t)j * kBlock + tid;
+            cnt[j] = dst[j] >= 0 ? slot0[k] : 0ull;
         }
+#pragma unroll
+        for (int j = 0; j < kDrJ; ++j) if (cnt[j]) atomicAdd(&s_cnt[dst[j]], 1u);
+        __syncthreads();
+        for (int d = tid; d < par; d += kBlock) s_base[d] = s_cnt[d] ? atomicAdd(&r.dcnt[d], (unsigned long long)s_cnt[d]) : 0ull;
+        __syncthreads();
+        for (int j = 0; j < kDrJ; ++j) {
+            if (!cnt[j]) continue;
+            const int64_t k = k0 + (int64_t)j * kBlock + tid;
+            const int d = dst[j];
+            const unsigned long long pos = s_base[d] + atomicAdd(&s_pos[d], 1u);
+            if ((int64_t)pos >= r.cap) continue;
+            int64_t* row = r.rows + ((int64_t)d * r.cap + (int64_t)pos) * m;
+            row[0] = key[j];
+            row[1] = win.start;
+            row[2] = (int64_t)cnt[j];
+            for (int i = 0; i < ncell; ++i) {
+                const int a = s_cell[i];
+                row[3 + i] = a > 0 ? (int64_t)slot0[(int64_t)a * stride + k] : (int64_t)cnt[j];
+            }
+        }
+        __syncthreads();                               // s_cnt / s_pos / s_base reused by the next slice
     }
 }
 
@@ -4151,7 +4158,7 @@ static int launch_drain_route(fwa_engine* e, const std::vector<FireWindow>& hw, 
     r.f.win = e->d_win;
     r.f.win_slots = e->d_win_slots;
     r.f.nwin = (int32_t)hw.size();
-    r.f.blocks_per_win = (int32_t)((e->capacity + 1 + (int64_t)kBlock * kDrJ - 1) / ((int64_t)kBlock * kDrJ));
+    r.f.blocks_per_win = (int32_t)((e->capacity + 1 + (int64_t)kBlock * kDrJ - 1) / ((int64_t)kBlock * kDrJ));   // chunks
     r.par = par;
     r.m = m;
     r.ncell = m - 3;
@@ -4176,8 +4183,7 @@ static int launch_drain_route(fwa_engine* e, const std::vector<FireWindow>& hw, 
         r.dcnt = e->d_dr_cnt;
         HIPCHK(e, hipMemsetAsync(e->d_dr_cnt, 0, sizeof(unsigned long long) * par, e->stream));
         HIPCHK(e, hipEventRecord(e->ev[2], e->stream));
-        const int64_t grid = (int64_t)r.f.blocks_per_win * (int64_t)hw.size();
-        drain_route_kernel<<<(unsigned)grid, kBlock, 0, e->stream>>>(r, e->d_ec);
+        drain_route_kernel<<<(unsigned)r.f.blocks_per_win, kBlock, 0, e->stream>>>(r, e->d_ec);   // one block per chunk
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
         HIPCHK(e, hipMemcpyAsync(counts.data(), e->d_dr_cnt, sizeof(unsigned long long) * par, hipMemcpyDeviceToHost, e->stream));
