@@ -4217,6 +4217,9 @@ int fwa_drain_route(fwa_engine* e, int64_t wm, int32_t parallelism, fwa_routed* 
     e->rs_valid = false;
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
+    // the previous call's blocks may still be read on the input stream (the exchange's all-to-all): the drain
+    // rewrites them only after everything enqueued there
+    if (int rc0 = wait_input_stream(e)) return rc0;
     // cells: key, slice start, COUNT(*), one per user aggregate other than COUNT(*), one per hidden counter
     int32_t cell_acc[kMaxAggsInt];
     int32_t m = 3;
@@ -4470,6 +4473,7 @@ int fwa_drain_partials(fwa_engine* e, int64_t wm, fwa_partials* out) {
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
+    if (int rc0 = wait_input_stream(e)) return rc0;   // device columns of the last drain may still be read there
     memset(out, 0, sizeof(*out));
     std::vector<FireWindow> hw;
     std::vector<int32_t> hs;

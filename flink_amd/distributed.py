@@ -252,6 +252,10 @@ class TwoPhaseKeyedWindowPipeline(KeyedWindowPipeline):
         this watermark proceed (software pipelining across steps; each engine still sees its own calls in stream
         order: drain(wm), push(next) on the local one, merge(wm), fire(wm) on the owner)."""
         wm = self.global_watermark(local_wm)
+        if self._xstream is not None and hasattr(self.local, "order_after"):
+            # the previous watermark's exchange (its own stream) may still read the blocks / columns the last drain
+            # returned: this drain rewrites them only after everything queued there (ADVICE r05)
+            self.local.order_after(self._xstream)
         if self.routed_drain:
             try:
                 parts, counts, m = self.local.drain_route(wm, self.world)

@@ -194,6 +194,14 @@ class WindowAggregator:
             _check(lib().fwa_set_input_stream(self.h, C.c_void_p(s)), self.h)
             self._in_stream = s
 
+    def order_after(self, stream):
+        """fwa_set_input_stream(stream): the handle's next push or drain waits for everything enqueued on the torch
+        stream `stream` by then (e.g. an exchange still reading the buffers the previous drain returned)."""
+        s = stream.cuda_stream
+        if s != self._in_stream:
+            _check(lib().fwa_set_input_stream(self.h, C.c_void_p(s)), self.h)
+            self._in_stream = s
+
     def _settled(self):
         """Called after every entry point that settles a pending async push."""
         self._inflight = None

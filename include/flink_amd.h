@@ -299,7 +299,9 @@ int fwa_push_nullable(fwa_engine* e, const int64_t* keys, const int64_t* ts, con
  * input columns (e.g. the framework's current stream). Every later device-pointer push makes the engine's
  * own stream wait for the work enqueued on `stream` so far before reading the columns. NULL (default):
  * the caller guarantees the inputs are complete (e.g. it synchronised). Outputs are complete when the
- * entry point that returns them returns. */
+ * entry point that returns them returns. fwa_drain_partials and fwa_drain_route wait for the stream too before
+ * they rewrite the device buffers their previous call returned, so a consumer that reads those buffers on
+ * `stream` (the keyBy exchange's all-to-all) is never overtaken by the next drain. */
 int fwa_set_input_stream(fwa_engine* e, void* stream);
 
 /* Advance the event-time watermark; fires every window whose maxTimestamp (end-1) <= wm.

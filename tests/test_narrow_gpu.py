@@ -82,6 +82,38 @@ def test_wide_values_switch_the_handle_to_64bit_entries(eng_mod, monkeypatch):
     assert 0 < extra <= (1 << 19) // 8                                  # only the first push is replayed
 
 
+@pytest.mark.parametrize("hot", [32_767, 32_768, 65_536 + 3, 300_000])
+def test_narrow_combiner_hot_keys(eng_mod, monkeypatch, hot):
+    """Hot keys through the narrow combiner's LDS accumulators: tens of thousands of records of one (key, slice) in one
+    push (the counts around 2^15 / 2^16 a packed 16-bit count field would wrap at -- r06 measured such a layout and
+    kept the separate COUNT / SUM words), values at both ends of the signed 32-bit range, one combiner block (a small
+    key capacity: one partition) and tile pre-aggregation off; rows equal the oracle's."""
+    from oracle.oracle import Oracle
+    rng = np.random.default_rng(hot)
+    n = hot * 2 + 50_000
+    keys = rng.integers(-500, 500, n).astype(np.int64)
+    keys[rng.permutation(n)[:hot]] = 7                                  # one key with `hot` records of each slice...
+    keys[rng.permutation(n)[:hot]] = -3                                 # (two, overlapping draws)
+    ts = rng.integers(0, 1000, n).astype(np.int64)                      # ...all in one slice
+    ts[: n // 4] += 1000                                                # and a second slice for a quarter of them
+    vals = rng.choice(np.array([2**31 - 1, -2**31, -2**31 + 1, 0, -1, 1, 2**31 - 2], np.int64), n)
+    r = rng.random(n) < 0.5
+    vals[r] = rng.integers(-2**31, 2**31, r.sum())
+    cfg = A.make_config(window_kind="TUMBLE", size_ms=1000, aggs=AGGS, key_capacity=1024)
+    names = A.agg_names(cfg)
+    g, o = eng_mod.WindowAggregator(cfg, options={"skew_merge": 0, "narrow_entries": 1}), Oracle(cfg)
+    for sl in (slice(0, 2), slice(2, n)):   # the first push allocates the slices (its records are replayed)
+        k2, t2, v2 = keys[sl], ts[sl], vals[sl]
+        if sl.start == 0:
+            t2 = np.array([5, 1005], np.int64)
+        assert g.push(k2, t2, [v2]) == o.push(k2, t2, [v2])
+    assert g.get_option("narrow_entries") == 1
+    assert_rows_equal(g.advance_watermark(A.LONG_MAX), o.advance_watermark(A.LONG_MAX), names)
+    assert g.stats().replay_records < n // 8   # the first push; sub-buckets of the few tiles that overflow
+    g.close()
+    o.close()
+
+
 # NW = 2: a DOUBLE column beside a FLOAT one (C5's aggregate list): the key's 32 bits and the FLOAT's bits share one
 # word, the DOUBLE keeps its own; keys needing 64 bits take the v1 replay (the FLOAT always fits)
 AGGS_F = [("COUNT", 0), ("SUM_F64", 1), ("AVG_F64", 1), ("MAX_F32", 0), ("MAX_F64", 1), ("MIN_F32", 0)]

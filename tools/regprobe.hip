@@ -49,7 +49,7 @@ const void* regprobe_kernels[] = {
     (const void*)&combine3_kernel<4,2,2,1024,0,0,0,0>,
     (const void*)&combine3_kernel<4,2,2,1024,1,0,0,0>,
     (const void*)&combine3_kernel<4,2,2,1024,2,0,0,0>,
-    (const void*)&combine3_kernel<8,2,1,1024,1,0,0,1>,
+    (const void*)&combine3_kernel<6,2,1,1024,1,0,0,1>,
     (const void*)&partition3_kernel<0,4,1024,3,0,1,0,0>,
     (const void*)&partition3_kernel<0,4,1024,3,1,1,0,0>,
     (const void*)&partition3_kernel<0,4,1024,3,2,1,0,0>,
