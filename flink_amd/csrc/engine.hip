@@ -3074,6 +3074,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.spill_cap = e->spill_cap;
     pa.part_bits = e->part_bits;
     pa.np = e->np;
+    pa.sub_major = (e->opt_variant & 4) ? 0 : 1;   // variant bit 2: partition-major buckets (A/B)
     for (int v = 0; v < 2; ++v) { pa.vcol[v] = e->vcol[v]; pa.vsize[v] = e->vsize[v]; }
     pa.dropidx = a.pcount ? nullptr : a.dropidx;   // partial rows: no record indices (as in v1)
     for (int c = 0; c < FWA_MAX_COLS; ++c) { pa.nulls[c] = a.nulls[c]; pa.any_null |= a.nulls[c] != nullptr; }
@@ -3144,6 +3145,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.seg_log = e->seg_log;
     ca.np = e->np;
     ca.sl = e->sl;
+    ca.sub_major = pa.sub_major;
     ca.rel2slot = e->d_rel2slot;
     // (not with PRE buckets: Phase P applies merged entries past a full sub-bucket to the slots with device atomics
     // before this merge -- tests/test_skew_gpu.py::test_pre_entries_past_bucket_end_applied_with_atomics)

@@ -178,12 +178,25 @@ def route_rows(pipe, keys, cols):
     return packed, torch.bincount(dest, minlength=pipe.world)
 
 
+def host_counts(counts):
+    """The route's per-destination row counts on the host: one copy into pinned memory and one wait on the stream
+    that computed them (all_to_all_single needs host split sizes; this is the push's only host wait)."""
+    if not counts.is_cuda:
+        return counts
+    h = torch.empty(counts.shape, dtype=counts.dtype, pin_memory=True)
+    h.copy_(counts, non_blocking=True)
+    torch.cuda.current_stream(counts.device).synchronize()
+    return h
+
+
 def send_rows(pipe, packed, counts):
-    """One all_to_all of the counts and one all_to_all_single of the packed rows (RCCL over xGMI)."""
-    recv_counts = torch.empty_like(counts)
-    dist.all_to_all_single(recv_counts, counts, group=pipe.group)
-    send = counts.tolist()
-    recv = recv_counts.tolist()
+    """The split sizes travel on the host (the valve's gloo group, as send_parts), the packed rows in one
+    all_to_all_single (RCCL over xGMI): no collective kernel and no device read for the counts matrix."""
+    sc = host_counts(counts)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=pipe.wm_group)
+    send = sc.tolist()
+    recv = rc.tolist()
     out = torch.empty((sum(recv), packed.shape[1]), dtype=torch.int64, device=packed.device)
     dist.all_to_all_single(out, packed, recv, send, group=pipe.group)
     pipe.exchanged += int(sum(send)) - int(send[pipe.rank])
