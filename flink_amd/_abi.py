@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-FWA_ABI_VERSION = 4
+FWA_ABI_VERSION = 5
 FWA_MAX_AGGS = 8
 FWA_MAX_COLS = 8
 

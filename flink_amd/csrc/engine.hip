@@ -1899,6 +1899,13 @@ struct fwa_engine {
     DecPlan* dec = nullptr;
     const void* dev_override[FWA_MAX_COLS] = {};   // stage_inputs: value columns already on the device
     bool restoring = false;           // fwa_restore feeding fwa_push_partials
+    // FWA_KEY_PREHASHED: the caller's key.hashCode() of every key, by kid (the key table's slot), so a snapshot can
+    // place the keys in their key groups; filled after each push that inserted keys (khash_fill_kernel)
+    int32_t* d_khash = nullptr;
+    unsigned long long khash_nkeys = 0;   // n_keys when d_khash was last filled
+    const int32_t* rs_hash = nullptr;     // fwa_restore -> fwa_push_partials: the snapshot's hash column (host)
+    int32_t* d_rs_hash = nullptr;         // its device copy
+    int64_t rs_hash_cap = 0;
     EngineConst ec;
     EngineConst* d_ec = nullptr;
     hipStream_t stream = nullptr;
@@ -2083,6 +2090,7 @@ struct fwa_engine {
     double mf_groups_per_row = 1.0;
     double mf_capx = 2.0;                 // bucket region = mean rows per bucket x this (+ slack); grows on overflow
     int32_t opt_fire_partials = -1;       // FWA_OPT_FIRE_PARTIALS: -1 / 1 the merge-fire path where eligible, 0 never
+    int32_t opt_dec_wrap_null = 0;        // FWA_OPT_DEC_WRAP_NULL: 1 emits NULL for a wrapped DECIMAL window, 0 fails
     int64_t mf_calls = 0, mf_fallbacks = 0;
     // fwa_drain_route: send regions [par][dr_cap][cells] and the per-destination row counters (d_dr_cnt)
     int64_t* d_dr = nullptr;
@@ -2147,7 +2155,7 @@ size_t type_size(int kind) {  // input width == result width for every kind exce
 }
 
 int validate(const fwa_config* c) {
-    if (c->abi_version != FWA_ABI_VERSION && c->abi_version != 3) return FWA_E_ARG;
+    if (c->abi_version != FWA_ABI_VERSION && c->abi_version != 4 && c->abi_version != 3) return FWA_E_ARG;
     if (c->num_aggs < 0 || c->num_aggs > FWA_MAX_AGGS) return FWA_E_ARG;
     for (int j = 0; j < c->num_aggs; ++j) {
         if (c->aggs[j].kind < 0 || c->aggs[j].kind >= FWA_AGG_KIND_COUNT) return FWA_E_ARG;
@@ -2583,7 +2591,8 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos, e->d_zslice, e->d_rsum,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4, e->d_rk, e->d_mf, e->d_dr, e->d_dr_cnt};
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4, e->d_rk, e->d_mf, e->d_dr, e->d_dr_cnt,
+                    e->d_khash, e->d_rs_hash};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
     for (int q = 0; q < 2; ++q) for (void* p : {(void*)e->ss[q].kid, (void*)e->ss[q].start, (void*)e->ss[q].end, (void*)e->ss[q].acc}) if (p) (void)hipFree(p);
@@ -2611,7 +2620,7 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out);
 int fwa_create(const fwa_config* ucfg, fwa_engine** out) {
     if (!ucfg || !out) return FWA_E_ARG;
     *out = nullptr;
-    if (ucfg->abi_version != FWA_ABI_VERSION && ucfg->abi_version != 3) return FWA_E_ARG;
+    if (ucfg->abi_version != FWA_ABI_VERSION && ucfg->abi_version != 4 && ucfg->abi_version != 3) return FWA_E_ARG;
     fwa_config uc;                               // a version-3 caller's struct ends before dec_scale
     memset(&uc, 0, sizeof(uc));
     memcpy(&uc, ucfg, ucfg->abi_version == 3 ? offsetof(fwa_config, dec_scale) : sizeof(fwa_config));
@@ -2810,6 +2819,10 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         if (hipMalloc(&e->d_keys, sizeof(unsigned long long) * (cap + 1)) != hipSuccess) { rc = FWA_E_OOM; break; }
         fill_u64_kernel<<<grid_for(cap), kBlock, 0, e->stream>>>(e->d_keys, kEmptyKey, cap);
         if (hipMemsetAsync(e->d_keys + cap, 0, 8, e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        if (cfg->key_kind == FWA_KEY_PREHASHED && !e->sparse) {
+            if (hipMalloc(&e->d_khash, sizeof(int32_t) * (cap + 1)) != hipSuccess) { rc = FWA_E_OOM; break; }
+            if (hipMemsetAsync(e->d_khash, 0, sizeof(int32_t) * (cap + 1), e->stream) != hipSuccess) { rc = FWA_E_DEVICE; break; }
+        }
         if (hipMalloc(&e->d_st, sizeof(DevStatus)) != hipSuccess) { rc = FWA_E_OOM; break; }
         if (hipHostMalloc(&e->h_st, sizeof(DevStatus)) != hipSuccess) { rc = FWA_E_OOM; break; }
         if (hipHostMalloc(&e->h_af_rows, sizeof(int64_t)) != hipSuccess) { rc = FWA_E_OOM; break; }
@@ -3819,6 +3832,56 @@ static int collect_late_indices(fwa_engine* e) {
     return FWA_OK;
 }
 
+// FWA_KEY_PREHASHED: read-only probe of the key table (the key's kid, or -1), in key_slot's probe order.
+__device__ __forceinline__ int64_t key_find(const unsigned long long* table, uint64_t mask, int seg_log, int part_bits,
+                                            int64_t key) {
+    if ((uint64_t)key == kEmptyKey) return table[mask + 1] == 1ull ? (int64_t)(mask + 1) : -1;
+    const uint64_t h = jm::mix64((uint64_t)key);
+    const uint64_t base = seg_base(h, seg_log, part_bits);
+    const uint64_t smask = ((uint64_t)1 << seg_log) - 1;
+    const uint64_t home = h & smask & ~(uint64_t)(kBucket - 1);
+    for (uint64_t probe = 0; probe <= smask; ++probe) {
+        const uint64_t i = base | ((home + probe) & smask);
+        const unsigned long long cur = table[i];
+        if (cur == (unsigned long long)key) return (int64_t)i;
+        if (cur == kEmptyKey) return -1;
+    }
+    return -1;
+}
+
+// Keep each key's caller-supplied key.hashCode() by kid (after a push inserted its keys): snapshots place the keys in
+// their key groups with it (KeyGroupRangeAssignment.assignToKeyGroup(key.hashCode())).
+__global__ void __launch_bounds__(kBlock) khash_fill_kernel(const int64_t* keys, const int32_t* kh, int64_t n,
+                                                            const unsigned long long* table, uint64_t mask, int seg_log,
+                                                            int part_bits, int32_t* khash) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t kid = key_find(table, mask, seg_log, part_bits, keys[i]);
+        if (kid >= 0) khash[kid] = kh[i];
+    }
+}
+
+// The kept hash of each of n keys (0 for a key the table does not hold).
+__global__ void __launch_bounds__(kBlock) khash_rows_kernel(const int64_t* keys, int64_t n, const unsigned long long* table,
+                                                            uint64_t mask, int seg_log, int part_bits,
+                                                            const int32_t* khash, int32_t* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t kid = key_find(table, mask, seg_log, part_bits, keys[i]);
+        out[i] = kid >= 0 ? khash[kid] : 0;
+    }
+}
+
+// After a push on a PREHASHED handle that inserted keys: record their hashes (the push's own key / hash columns, still
+// valid here; the stream is waited for, since the caller may release them when the call returns).
+static int khash_fill(fwa_engine* e, const int64_t* keys, const int32_t* kh, int64_t n) {
+    if (!e->d_khash || n <= 0 || !keys || !kh || e->h_st->n_keys == e->khash_nkeys) return FWA_OK;
+    khash_fill_kernel<<<grid_for(n), kBlock, 0, e->stream>>>(keys, kh, n, e->d_keys, (uint64_t)e->capacity - 1,
+                                                             e->seg_log, e->part_bits, e->d_khash);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->khash_nkeys = e->h_st->n_keys;
+    return FWA_OK;
+}
+
 // Shared ingest driver: two-phase path when allowed, else the v1 kernel; slice-miss replays;
 // lookahead slice allocation; stats.
 static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, bool status_enqueued,
@@ -3952,6 +4015,7 @@ static int push_settle(fwa_engine* e, IngestArgs& a, int64_t n, bool ran_v2, boo
     }
     if (republish) e->dir_dirty = true;
     if (a.dropidx) { rc = collect_late_indices(e); if (rc) return rc; }
+    if (e->d_khash) { rc = khash_fill(e, a.keys, a.key_hash, n); if (rc) return rc; }
     e->records_in += n;
     e->late_dropped += dropped;
     if (late_dropped_out) *late_dropped_out = dropped;
@@ -4055,6 +4119,7 @@ static int push_body(fwa_engine* e, const int64_t* keys, const int64_t* ts, cons
                                                    : "key table full: raise fwa_config.key_capacity");
         }
         if (a.dropidx) { int rc2 = collect_late_indices(e); if (rc2) return rc2; }
+        if (e->d_khash) { int rc2 = khash_fill(e, a.keys, a.key_hash, n); if (rc2) return rc2; }
         e->records_in += n;
         e->late_dropped += dropped;
         if (late_dropped_out) *late_dropped_out = dropped;
@@ -4075,7 +4140,9 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
     if (e->red) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators of a DataStream reduction");
     if (e->kind == FWA_SESSION) return fail(e, FWA_E_UNSUPPORTED, "partial accumulators need a slicing window");
     if (n < 0 || (n > 0 && (!keys || !slice_ts || !count))) return fail(e, FWA_E_ARG, "null input column");
-    if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "partials need a computable key hash");
+    // (PREHASHED keys: only a restore, which brings the snapshot's hash column)
+    if (e->cfg.key_kind == FWA_KEY_PREHASHED && !(e->restoring && e->rs_hash))
+        return fail(e, FWA_E_UNSUPPORTED, "partials need a computable key hash");
     if (n > INT32_MAX) return fail(e, FWA_E_ARG, "batch too large (max 2^31-1 records)");
     if (late_dropped_out) *late_dropped_out = 0;
     if (n == 0) { e->late_idx.clear(); return FWA_OK; }
@@ -4124,6 +4191,16 @@ int fwa_push_partials(fwa_engine* e, const int64_t* keys, const int64_t* slice_t
     a.keys = (const int64_t*)dev[0];
     a.ts = (const int64_t*)dev[1];
     a.pcount = (const unsigned long long*)dev[2];
+    if (e->cfg.key_kind == FWA_KEY_PREHASHED) {      // restore: the snapshot's key.hashCode() column
+        if (n > e->rs_hash_cap) {
+            if (e->d_rs_hash) HIPCHK(e, hipFree(e->d_rs_hash));
+            e->d_rs_hash = nullptr;
+            HIPCHK(e, hipMalloc(&e->d_rs_hash, sizeof(int32_t) * (size_t)n));
+            e->rs_hash_cap = n;
+        }
+        HIPCHK(e, hipMemcpyAsync(e->d_rs_hash, e->rs_hash, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, e->stream));
+        a.key_hash = e->d_rs_hash;
+    }
     for (int j = 0, c = 3; j < e->ec.naggs; ++j)
         if (e->ec.agg[j].acc > 0) a.cols[j] = dev[c++];
     if (n > e->spill_cap) {
@@ -4362,7 +4439,10 @@ int fwa_fire_partials(fwa_engine* e, const int64_t* rows, int64_t n, int32_t m, 
     const int64_t capb = (int64_t)((double)(n / NB) * e->mf_capx) + 512;
     int64_t tile = (int64_t)((150 * 1024 - 12 * (size_t)NB - 16) / (8 + 8 * (size_t)m));
     tile = std::min<int64_t>(8 * kMfThreads, tile / 64 * 64);
-    if (tile < 256) return fire_partials_generic(e, rows, n, m, acc_cell, wm, flags, out, late_dropped_out);
+    if (tile < 256) {                           // (the row is too wide for an LDS tile: counted as a fallback)
+        e->mf_fallbacks++;
+        return fire_partials_generic(e, rows, n, m, acc_cell, wm, flags, out, late_dropped_out);
+    }
     const size_t hdr = 256 + ((4 * (size_t)NB + 255) & ~(size_t)255);
     const size_t need = hdr + (size_t)NB * capb * m * 8;
     if (need > e->mf_bytes) {
@@ -4578,8 +4658,12 @@ static void snap_header(const fwa_engine* e, int64_t* h, int64_t n) {
 // (WindowOperator.java:224-238 mergingSetsState / windowState), with the session end as a last column.
 static int snapshot_sessions(fwa_engine* e, fwa_blob* out) {
     const int64_t n = e->n_ss;
-    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, nh = e->ec.naggs - e->ec.nout, ncols = 4 + na + nh;
+    const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, nh = e->ec.naggs - e->ec.nout;
+    const bool ph = e->cfg.key_kind == FWA_KEY_PREHASHED;   // + one column: each entry's key.hashCode()
+    const int ncols = 4 + na + nh + (ph ? 1 : 0);
     const SessList& L = e->ss[e->ss_cur];
+    std::vector<int32_t> khash(ph ? (size_t)e->capacity + 1 : 0);
+    if (ph && n > 0) HIPCHK(e, hipMemcpy(khash.data(), e->d_khash, 4 * ((size_t)e->capacity + 1), hipMemcpyDeviceToHost));
     std::vector<uint32_t> kid((size_t)n);
     std::vector<int64_t> st((size_t)n), en((size_t)n), acc((size_t)n * e->nacc);
     std::vector<unsigned long long> table((size_t)e->capacity + 1);
@@ -4595,7 +4679,7 @@ static int snapshot_sessions(fwa_engine* e, fwa_blob* out) {
     std::vector<int64_t> off((size_t)maxp + 1, 0), key((size_t)n);
     for (int64_t i = 0; i < n; ++i) {
         key[i] = (int64_t)kid[i] < e->capacity ? (int64_t)table[kid[i]] : LONG_MIN_J;
-        kg[i] = jm::key_group_of(key[i], e->cfg.key_kind, 0, maxp);
+        kg[i] = jm::key_group_of(key[i], e->cfg.key_kind, ph ? khash[kid[i]] : 0, maxp);
         if (kg[i] < 0) return fail(e, FWA_E_STATE, "state holds a key outside every key group");
         off[kg[i] + 1]++;
     }
@@ -4618,6 +4702,7 @@ static int snapshot_sessions(fwa_engine* e, fwa_blob* out) {
         }
         for (int h = 0; h < nh; ++h) body[(size_t)(3 + na + h) * n + d] = acc[(size_t)e->ec.agg[e->ec.nout + h].acc * n + i];
         body[(size_t)(3 + na + nh) * n + d] = en[i];
+        if (ph) body[(size_t)(4 + na + nh) * n + d] = khash[kid[i]];
     }
     out->data = b;
     out->size = (int64_t)(words * 8);
@@ -4687,6 +4772,18 @@ static int restore_sessions(fwa_engine* e, const void* const* blobs, int32_t n_b
         s.st = e->d_st;
         sess2_restore_kernel<<<grid_for(m), kBlock, 0, e->stream>>>(s, d, d + m, d + 2 * m, dacc, m, e->n_ss, e->d_ec);
         HIPCHK(e, hipGetLastError());
+        if (e->d_khash) {                         // PREHASHED: the entries' key.hashCode() (last column) by kid
+            std::vector<int32_t> hv((size_t)m);
+            for (int64_t i = 0; i < m; ++i) hv[i] = (int32_t)body[(size_t)(4 + na + nh) * n + lo + i];
+            int32_t* dh = nullptr;
+            HIPCHK(e, hipMalloc(&dh, sizeof(int32_t) * (size_t)m));
+            HIPCHK(e, hipMemcpyAsync(dh, hv.data(), sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice, e->stream));
+            khash_fill_kernel<<<grid_for(m), kBlock, 0, e->stream>>>(d, dh, m, e->d_keys, (uint64_t)e->capacity - 1,
+                                                                     e->seg_log, e->part_bits, e->d_khash);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            (void)hipFree(dh);
+        }
         rc = sync_status(e);
         (void)hipFree(d);
         (void)hipFree(dacc);
@@ -4703,7 +4800,9 @@ static int restore_sessions(fwa_engine* e, const void* const* blobs, int32_t n_b
 int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
     if (!e || !out) return FWA_E_ARG;
     memset(out, 0, sizeof(*out));
-    if (e->cfg.key_kind == FWA_KEY_PREHASHED) return fail(e, FWA_E_UNSUPPORTED, "snapshot needs a computable key hash");
+    // PREHASHED keys: their key groups come from the hashes the engine kept (d_khash); record lists keep no key table
+    if (e->cfg.key_kind == FWA_KEY_PREHASHED && !e->d_khash)
+        return fail(e, FWA_E_UNSUPPORTED, "snapshot of PREHASHED keys in record lists");
     HIPCHK(e, hipSetDevice(e->cfg.device));
     if (int rc0 = settle_pending(e)) return rc0;
     if (e->kind == FWA_SESSION) return snapshot_sessions(e, out);
@@ -4741,21 +4840,35 @@ int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
         e->fire_ms = ms0;
     }
     const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, nh = e->ec.naggs - e->ec.nout, ncols = 3 + na + nh;
-    std::vector<int64_t> cols((size_t)n * ncols);
+    const bool ph = e->cfg.key_kind == FWA_KEY_PREHASHED;   // + one column: each entry's key.hashCode()
+    const int ncb = ncols + (ph ? 1 : 0);
+    std::vector<int64_t> cols((size_t)n * ncb);
     const void* src[3 + FWA_MAX_AGGS + FWA_MAX_COLS] = {e->o_key, e->o_start, e->o_count};
     for (int j = 0; j < na; ++j) src[3 + j] = e->o_agg[j];
     for (int h = 0; h < nh; ++h) src[3 + na + h] = e->o_hid[h];
     for (int c = 0; c < ncols && n > 0; ++c)
         HIPCHK(e, hipMemcpy(cols.data() + (size_t)c * n, src[c], 8 * (size_t)n, hipMemcpyDeviceToHost));
+    std::vector<int32_t> hash(ph ? (size_t)n : 0);
+    if (ph && n > 0) {
+        int32_t* dh = nullptr;
+        HIPCHK(e, hipMalloc(&dh, sizeof(int32_t) * (size_t)n));
+        khash_rows_kernel<<<grid_for(n), kBlock, 0, e->stream>>>(e->o_key, n, e->d_keys, (uint64_t)e->capacity - 1,
+                                                                 e->seg_log, e->part_bits, e->d_khash, dh);
+        const hipError_t er = hipMemcpyAsync(hash.data(), dh, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, e->stream);
+        const hipError_t es = hipStreamSynchronize(e->stream);
+        (void)hipFree(dh);
+        if (er != hipSuccess || es != hipSuccess) return fail(e, FWA_E_DEVICE, "key hash export failed");
+        for (int64_t i = 0; i < n; ++i) cols[(size_t)ncols * n + i] = hash[i];
+    }
     std::vector<int32_t> kg((size_t)n);
     std::vector<int64_t> off((size_t)maxp + 1, 0);
     for (int64_t i = 0; i < n; ++i) {
-        kg[i] = jm::key_group_of(cols[i], e->cfg.key_kind, 0, maxp);
+        kg[i] = jm::key_group_of(cols[i], e->cfg.key_kind, ph ? hash[i] : 0, maxp);
         if (kg[i] < 0) return fail(e, FWA_E_STATE, "state holds a key outside every key group");
         off[kg[i] + 1]++;
     }
     for (int g = 0; g < maxp; ++g) off[g + 1] += off[g];
-    const size_t words = kSnapHdr + (size_t)maxp + 1 + (size_t)n * ncols;
+    const size_t words = kSnapHdr + (size_t)maxp + 1 + (size_t)n * ncb;
     int64_t* b = (int64_t*)malloc(words * 8);
     if (!b) return fail(e, FWA_E_OOM, "snapshot blob allocation failed");
     snap_header(e, b, n);
@@ -4764,7 +4877,7 @@ int fwa_snapshot(fwa_engine* e, fwa_blob* out) {
     std::vector<int64_t> cur(off.begin(), off.end() - 1);
     for (int64_t i = 0; i < n; ++i) {
         const int64_t d = cur[kg[i]]++;
-        for (int c = 0; c < ncols; ++c) body[(size_t)c * n + d] = cols[(size_t)c * n + i];
+        for (int c = 0; c < ncb; ++c) body[(size_t)c * n + d] = cols[(size_t)c * n + i];
     }
     out->data = b;
     out->size = (int64_t)(words * 8);
@@ -4786,7 +4899,9 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
     if (e->records_in != 0 || e->wm != LONG_MIN_J || !e->live.empty() || e->n_ss != 0 || sp_live_windows(e) != 0)
         return fail(e, FWA_E_STATE, "restore needs a fresh handle");
     const int na = e->cfg.num_aggs, maxp = e->cfg.max_parallelism, nh = e->ec.naggs - e->ec.nout;
-    const int ncols = (e->kind == FWA_SESSION ? 4 : 3) + na + nh;
+    const bool ph = e->cfg.key_kind == FWA_KEY_PREHASHED;   // a last column holds each entry's key.hashCode()
+    const int ncols = (e->kind == FWA_SESSION ? 4 : 3) + na + nh + (ph ? 1 : 0);
+    if (ph && !e->d_khash) return fail(e, FWA_E_UNSUPPORTED, "restore of PREHASHED keys into record lists");
     int64_t ref[kSnapHdr];
     snap_header(e, ref, 0);
     // validate every blob before touching state
@@ -4820,9 +4935,13 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
         for (int j = 0; j < na; ++j) acc[j] = body + (size_t)(3 + j) * n + lo;
         for (int h = 0; h < nh; ++h) acc[na + h] = body + (size_t)(3 + na + h) * n + lo;
         int64_t late = 0;
+        std::vector<int32_t> hv(ph ? (size_t)(hi - lo) : 0);
+        for (int64_t i = lo; ph && i < hi; ++i) hv[i - lo] = (int32_t)body[(size_t)(3 + na + nh) * n + i];
         e->restoring = true;
+        e->rs_hash = ph ? hv.data() : nullptr;
         int rc = fwa_push_partials(e, body + lo, body + (size_t)n + lo, body + (size_t)2 * n + lo, acc, hi - lo, 0, &late);
         e->restoring = false;
+        e->rs_hash = nullptr;
         if (rc) return rc;
         if (late) return fail(e, FWA_E_STATE, "restored partials were dropped as late");
     }
@@ -5232,6 +5351,8 @@ int fwa_flush(fwa_engine* e) {
     return FWA_OK;
 }
 
+int64_t fwa_stats_size(void) { return (int64_t)sizeof(fwa_stats); }
+
 int fwa_get_stats(fwa_engine* e, fwa_stats* s) {
     if (!e || !s) return FWA_E_ARG;
     if (int rc0 = settle_pending(e)) return rc0;
@@ -5289,6 +5410,7 @@ int fwa_set_option(fwa_engine* e, int32_t option, int64_t value) {
         case FWA_OPT_INGEST_VARIANT: e->opt_variant = (int32_t)std::max<int64_t>(0, value); return FWA_OK;
         case FWA_OPT_SLIDE_CARRIED: e->rs_on = value != 0; e->rs_valid = false; return FWA_OK;
         case FWA_OPT_FIRE_PARTIALS: e->opt_fire_partials = value != 0 ? 1 : 0; return FWA_OK;
+        case FWA_OPT_DEC_WRAP_NULL: e->opt_dec_wrap_null = value != 0 ? 1 : 0; return FWA_OK;
         default: return fail(e, FWA_E_ARG, "unknown option");
     }
 }
@@ -5313,6 +5435,7 @@ int fwa_get_option(const fwa_engine* e, int32_t option, int64_t* value) {
         case FWA_OPT_INGEST_VARIANT: *value = e->opt_variant; return FWA_OK;
         case FWA_OPT_SLIDE_CARRIED: *value = e->rs_used; return FWA_OK;
         case FWA_OPT_FIRE_PARTIALS: *value = e->mf_calls - e->mf_fallbacks; return FWA_OK;
+        case FWA_OPT_DEC_WRAP_NULL: *value = e->opt_dec_wrap_null; return FWA_OK;
         default: return FWA_E_ARG;
     }
 }

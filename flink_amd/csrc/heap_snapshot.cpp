@@ -35,7 +35,8 @@
 // DECIMAL SUM / AVG (Table): the accumulator field is the DECIMAL(38, s) running sum (findSumAggType), rebuilt from the
 // engine's 32-bit piece sums (decimal.inc) and written as a non-compact DecimalData; AVG's count is COUNT(*) or the
 // column's hidden non-NULL counter, already in the row.
-// PREHASHED keys and DataStream reductions: FWA_E_UNSUPPORTED (FWASNAP1 covers them).
+// PREHASHED keys (their Java serialization is the caller's) and DataStream reductions: FWA_E_UNSUPPORTED; the engine
+// format (fwa_snapshot, FWASNAP1) carries both, PREHASHED keys with the hash column of their key groups.
 #include <algorithm>
 #include <cstdint>
 #include <map>

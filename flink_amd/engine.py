@@ -100,6 +100,11 @@ def lib():
     L.fwa_advance_watermark_async.restype = C.c_int
     L.fwa_fired_output.argtypes = [C.c_void_p, C.POINTER(A.Out)]
     L.fwa_fired_output.restype = C.c_int
+    L.fwa_stats_size.argtypes = []
+    L.fwa_stats_size.restype = C.c_int64
+    if L.fwa_stats_size() != C.sizeof(A.Stats):       # the library and this binding disagree on fwa_stats
+        raise RuntimeError("fwa_stats is %d bytes in %s, %d in flink_amd._abi" % (L.fwa_stats_size(), LIB_PATH,
+                                                                                 C.sizeof(A.Stats)))
     _LIB = L
     return L
 
@@ -146,7 +151,7 @@ def _check(rc, h=None, what=""):
 # fwa_set_option (include/flink_amd.h enum fwa_option): per-handle tuning / test options
 OPTIONS = {"skew_merge": 1, "window_passes": 2, "narrow_entries": 3, "session_cells": 4, "out_min_rows": 5,
            "partials_one_pass": 6, "sp_table": 7, "sp_fmax": 8, "sp_budget": 9, "profile": 10,
-           "session_path": 11, "ingest_variant": 12, "slide_carried": 13, "fire_partials": 14}
+           "session_path": 11, "ingest_variant": 12, "slide_carried": 13, "fire_partials": 14, "dec_wrap_null": 15}
 # options applied to every new handle of this process before its own (test tooling sets these, e.g.
 # tests/forced_modes_check.py); empty in production
 DEFAULT_OPTIONS = {}

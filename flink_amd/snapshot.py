@@ -19,7 +19,8 @@ def parse(blob):
         raise ValueError("not a flink_amd snapshot")
     maxp, naggs, n, nh = int(w[9]), int(w[11]), int(w[21]), int(w[25])
     session = int(w[2]) == 3                     # SESSION: a 4th leading column holds the session end (last)
-    ncols = (4 if session else 3) + naggs + nh   # nullable handles: nh hidden non-NULL counters after the acc_j
+    prehashed = int(w[10]) == 2                  # FWA_KEY_PREHASHED: a last column holds each key's key.hashCode()
+    ncols = (4 if session else 3) + naggs + nh + (1 if prehashed else 0)   # nh: hidden non-NULL counters
     need = HDR_WORDS + maxp + 1 + n * ncols
     if w.size != need:
         raise ValueError("snapshot size %d words != %d" % (w.size, need))
@@ -36,6 +37,8 @@ def parse(blob):
     }
     if session:
         out["window_end"] = body[3 + naggs + nh].copy()   # slice_start holds the session start
+    if prehashed:
+        out["key_hash"] = body[ncols - 1].astype(np.int32)
     return out
 
 

@@ -51,7 +51,9 @@
 extern "C" {
 #endif
 
-#define FWA_ABI_VERSION 4   /* 4: fwa_config.dec_scale (DECIMAL aggregates); version-3 configurations are still accepted */
+#define FWA_ABI_VERSION 5   /* 5: fwa_stats.dec_inexact, fwa_stats_size, FWA_OPT_DEC_WRAP_NULL; 4: fwa_config.dec_scale
+                             * (DECIMAL aggregates). Version-3 and -4 configurations are still accepted (same layout);
+                             * a caller built against an older header must size its fwa_stats by fwa_stats_size(). */
 #define FWA_MAX_AGGS 8
 #define FWA_MAX_COLS 8
 
@@ -150,8 +152,9 @@ enum fwa_agg_kind {
  *       digits the window's AVG is NULL; the engine's is the exact total over the count, non-NULL when that total
  *       is back within 38 digits (tests/test_decimal_gpu.py::test_documented_overflow_difference pins both).
  * Results differ only for windows in which a running sum passes 38 digits. A (key, window) may hold up to 2^32 - 1
- * records: a DECIMAL result of a window with more is NULL and counted in fwa_stats.dec_inexact (the other rows of
- * that watermark are unaffected). Internally each DECIMAL source column is summed as 2 (int64 input)
+ * records, past which the piece sums may wrap: the watermark step that fires such a window fails with
+ * FWA_E_UNSUPPORTED, or, with fwa_set_option(FWA_OPT_DEC_WRAP_NULL, 1), emits that window's DECIMAL results as NULL
+ * and counts them in fwa_stats.dec_inexact (the other rows of that watermark are unaffected). Internally each DECIMAL source column is summed as 2 (int64 input)
  * or 4 (16-byte) 32-bit pieces, each one of the handle's FWA_MAX_AGGS aggregates, plus a count; a list past that
  * budget is FWA_E_UNSUPPORTED at fwa_create. Not available for fwa_drain_partials / fwa_push_partials
  * (FWA_E_UNSUPPORTED); fwa_snapshot_heap writes the exact total as the DECIMAL(38, s) buffer. */
@@ -328,6 +331,8 @@ int fwa_fired_output(fwa_engine* e, fwa_out* out);
 int fwa_flush(fwa_engine* e);
 
 int fwa_get_stats(fwa_engine* e, fwa_stats* out);
+/* sizeof(fwa_stats) of this library (it grew in ABI 5): a caller checks it against its own before fwa_get_stats. */
+int64_t fwa_stats_size(void);
 
 /* ---- two-phase (local / global) aggregation ----
  * Flink's two-phase window plan (TwoStageOptimizedWindowAggregateRule.java:88-103):
@@ -417,7 +422,10 @@ int fwa_fire_partials(fwa_engine* e, const int64_t* rows, int64_t n, int32_t m, 
  * derived from the live slices and the watermark, as the reference re-registers them from state.
  * SESSION windows: the entries are the in-flight sessions (the MergingWindowSet mapping + window state,
  * WindowOperator.java:224-238) with slice_start = session start and one more column end[n] after the
- * acc_j columns. The blob is engine-allocated; free it with fwa_blob_free. */
+ * acc_j columns. FWA_KEY_PREHASHED handles (keys of any Java type as 64-bit ids beside their key.hashCode()): one
+ * more last column hash[n], the hashCode() each key was pushed with (the engine keeps it per key), by which the
+ * entries are placed in key groups and a restore places them again; record-list handles keep no per-key hash and
+ * refuse (FWA_E_UNSUPPORTED). The blob is engine-allocated; free it with fwa_blob_free. */
 typedef struct fwa_blob {
     void* data;
     int64_t size;   /* bytes */
@@ -463,8 +471,9 @@ int fwa_restore(fwa_engine* e, const void* const* blobs, const int64_t* sizes, i
  *     flink_amd/csrc/heap_snapshot.cpp describes.
  * kg_offsets[g - kg_start] receives the byte offset of key group g's section (KeyGroupRangeOffsets; the Java shim
  * writes its KeyedBackendSerializationProxy header in front and shifts them), *watermark the operator watermark
- * (union list state, SlicingWindowOperator.java:204-209). PREHASHED keys and DataStream reductions (FWA_CFG_REDUCE):
- * FWA_E_UNSUPPORTED (fwa_snapshot covers them). The blob is freed with fwa_blob_free. */
+ * (union list state, SlicingWindowOperator.java:204-209). PREHASHED keys (their Java serialization is the caller's)
+ * and DataStream reductions (FWA_CFG_REDUCE): FWA_E_UNSUPPORTED -- fwa_snapshot / fwa_restore carry both, PREHASHED
+ * keys with their hashes (dense and session handles). The blob is freed with fwa_blob_free. */
 int fwa_snapshot_heap(fwa_engine* e, fwa_blob* out, int64_t* kg_offsets, int64_t* watermark);
 
 /* Restore a fresh handle from heap-layout bodies (as written by fwa_snapshot_heap on handles with the same window
@@ -507,8 +516,11 @@ enum fwa_option {
                                     reads a slot it merges into even when no record reached it yet */
     FWA_OPT_SLIDE_CARRIED = 13,  /* read only: sliding fires whose first window reused the previous run's carried
                                     window sums (fwa_get_option; set: 0 disables the reuse, 1 enables it, default) */
-    FWA_OPT_FIRE_PARTIALS = 14   /* read only: fwa_fire_partials calls that merged and fired on chip (fwa_get_option;
+    FWA_OPT_FIRE_PARTIALS = 14,  /* read only: fwa_fire_partials calls that merged and fired on chip (fwa_get_option;
                                     set: 0 sends every call through fwa_push_partials + fwa_advance_watermark) */
+    FWA_OPT_DEC_WRAP_NULL = 15   /* 1: a DECIMAL SUM / AVG over 2^32 or more records of one window is emitted NULL and
+                                  * counted (fwa_stats.dec_inexact); 0 (default): that watermark step fails
+                                  * (FWA_E_UNSUPPORTED) instead of a silently different result */
 };
 int fwa_set_option(fwa_engine* e, int32_t option, int64_t value);
 /* The option's effective value: for the tri-state options 1 if the handle currently takes that path (forced, or

@@ -64,6 +64,15 @@ int main(void){printf("%zu %zu %zu %zu %zu\n", sizeof(fwa_config), sizeof(fwa_ou
     assert got == exp
 
 
+def test_stats_struct_size_pinned():
+    """fwa_stats grew in ABI 5 (dec_inexact): the library reports its size and it equals the binding's."""
+    from flink_amd import _abi as A
+    from flink_amd import engine
+    L = engine.lib()
+    assert A.FWA_ABI_VERSION == 5
+    assert L.fwa_stats_size() == ctypes.sizeof(A.Stats)
+
+
 def test_engine_refuses_missing_library(tmp_path, monkeypatch):
     """The product path fails loudly (no CPU fallback) when the HIP library is absent."""
     from flink_amd import engine

@@ -194,10 +194,12 @@ def test_decimal_partials_unsupported(eng_mod):
     g.close()
 
 
-def test_window_past_2_32_records_gives_null_decimal_rows(eng_mod):
+@pytest.mark.parametrize("wrap_null", [1, 0])
+def test_window_past_2_32_records_gives_null_decimal_rows(eng_mod, wrap_null):
     """The piece sums are exact below 2^32 records per (key, window); a window with more (forced here through a
-    restored snapshot whose COUNT(*) says 2^32 + 5) fires its DECIMAL results as NULL, counted in
-    fwa_stats.dec_inexact, and every other row of the watermark is emitted as usual."""
+    restored snapshot whose COUNT(*) says 2^32 + 5) fails the watermark step by default (FWA_E_UNSUPPORTED: the
+    reference's total would be exact), and with FWA_OPT_DEC_WRAP_NULL fires its DECIMAL results as NULL, counted in
+    fwa_stats.dec_inexact, every other row of the watermark emitted as usual."""
     cfg = A.make_config(window_kind="TUMBLE", semantics="TABLE", size_ms=1000, key_capacity=64,
                         aggs=[("COUNT", 0), ("SUM_DEC", 0, 2), ("AVG_DEC", 0, 2)])
     g = eng_mod.WindowAggregator(cfg)
@@ -215,8 +217,14 @@ def test_window_past_2_32_records_gives_null_decimal_rows(eng_mod):
     for j in range(naggs):
         if kinds[j] == A.AGG_KINDS["COUNT"]:
             w[body + (3 + j) * n + i] = big      # ... and the COUNT aggregate's word
-    g = eng_mod.WindowAggregator(cfg)
+    g = eng_mod.WindowAggregator(cfg, options={"dec_wrap_null": wrap_null})
     g.restore(w.tobytes())
+    if not wrap_null:
+        with pytest.raises(eng_mod.EngineError) as ei:
+            g.advance_watermark(A.LONG_MAX)
+        assert ei.value.code == -7 and g.stats().dec_inexact == 2
+        g.close()
+        return
     r = g.advance_watermark(A.LONG_MAX)
     st = g.stats()
     g.close()
