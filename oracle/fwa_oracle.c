@@ -239,47 +239,49 @@ static inline uint64_t k4_hash(const k4* x) {
 }
 static inline int k4_eq(const k4* a, const k4* b) { return a->k[0] == b->k[0] && a->k[1] == b->k[1] && a->k[2] == b->k[2] && a->k[3] == b->k[3]; }
 
-/* open addressing, linear probing, backward-shift deletion */
-typedef struct { k4* keys; int64_t* vals; uint8_t* used; int64_t cap, n; } hmap;
+/* open addressing, linear probing, backward-shift deletion; one slot = key, value and used flag together (one cache
+   line fetch per probe: the full-size digest oracles probe tables of tens of millions of entries) */
+typedef struct { k4 key; int64_t val; int64_t used; } hslot;
+typedef struct { hslot* s; int64_t cap, n; } hmap;
 
 static void hm_init(hmap* m, int64_t cap) {
     int64_t c = 16; while (c < cap * 2) c <<= 1;
     m->cap = c; m->n = 0;
-    m->keys = (k4*)malloc(sizeof(k4) * c); m->vals = (int64_t*)malloc(8 * c); m->used = (uint8_t*)calloc(c, 1);
+    m->s = (hslot*)calloc(c, sizeof(hslot));
 }
-static void hm_free(hmap* m) { free(m->keys); free(m->vals); free(m->used); memset(m, 0, sizeof(*m)); }
+static void hm_free(hmap* m) { free(m->s); memset(m, 0, sizeof(*m)); }
 static int64_t* hm_find(hmap* m, const k4* k) {
     uint64_t i = k4_hash(k) & (m->cap - 1);
-    while (m->used[i]) { if (k4_eq(&m->keys[i], k)) return &m->vals[i]; i = (i + 1) & (m->cap - 1); }
+    while (m->s[i].used) { if (k4_eq(&m->s[i].key, k)) return &m->s[i].val; i = (i + 1) & (m->cap - 1); }
     return NULL;
 }
 static void hm_grow(hmap* m);
 static int64_t* hm_put(hmap* m, const k4* k, int64_t v, int* inserted) {
     if ((m->n + 1) * 10 > m->cap * 7) hm_grow(m);
     uint64_t i = k4_hash(k) & (m->cap - 1);
-    while (m->used[i]) { if (k4_eq(&m->keys[i], k)) { if (inserted) *inserted = 0; return &m->vals[i]; } i = (i + 1) & (m->cap - 1); }
-    m->used[i] = 1; m->keys[i] = *k; m->vals[i] = v; m->n++;
+    while (m->s[i].used) { if (k4_eq(&m->s[i].key, k)) { if (inserted) *inserted = 0; return &m->s[i].val; } i = (i + 1) & (m->cap - 1); }
+    m->s[i].used = 1; m->s[i].key = *k; m->s[i].val = v; m->n++;
     if (inserted) *inserted = 1;
-    return &m->vals[i];
+    return &m->s[i].val;
 }
 static void hm_grow(hmap* m) {
     hmap o = *m; hm_init(m, o.cap);
-    for (int64_t i = 0; i < o.cap; i++) if (o.used[i]) hm_put(m, &o.keys[i], o.vals[i], NULL);
+    for (int64_t i = 0; i < o.cap; i++) if (o.s[i].used) hm_put(m, &o.s[i].key, o.s[i].val, NULL);
     hm_free(&o);
 }
 static int hm_del(hmap* m, const k4* k) {
     uint64_t mask = m->cap - 1, i = k4_hash(k) & mask;
-    while (m->used[i] && !k4_eq(&m->keys[i], k)) i = (i + 1) & mask;
-    if (!m->used[i]) return 0;
+    while (m->s[i].used && !k4_eq(&m->s[i].key, k)) i = (i + 1) & mask;
+    if (!m->s[i].used) return 0;
     uint64_t j = i;
     for (;;) {
         j = (j + 1) & mask;
-        if (!m->used[j]) break;
-        uint64_t h = k4_hash(&m->keys[j]) & mask;
+        if (!m->s[j].used) break;
+        uint64_t h = k4_hash(&m->s[j].key) & mask;
         /* move j back to i if h is cyclically outside (i, j] */
-        if ((i <= j) ? (h <= i || h > j) : (h <= i && h > j)) { m->keys[i] = m->keys[j]; m->vals[i] = m->vals[j]; i = j; }
+        if ((i <= j) ? (h <= i || h > j) : (h <= i && h > j)) { m->s[i].key = m->s[j].key; m->s[i].val = m->s[j].val; i = j; }
     }
-    m->used[i] = 0; m->n--;
+    m->s[i].used = 0; m->n--;
     return 1;
 }
 
@@ -1273,5 +1275,139 @@ double or_pipeline_digests(const fwa_config* cfg, const fwa_gen_params* p, int64
     }
     free(args); free(th);
     if (rc) return (double)rc;              /* an FWA_E_* code (negative) */
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ------------------------------------------------------------------ full-size digests, general form */
+
+/* The benched configurations C3 / C5 / C5s at full size (tests/test_full_size_digests_gpu.py): Zipf keys (the CDF the
+   device generator samples), the float value columns (f32 column 0, f64 column 1), any window kind. Per batch the T
+   threads first generate a 1/T share of the batch each (with its key groups; the Zipf binary search is the costly
+   part, done once), then each thread runs one operator instance over its key-group range of the whole batch
+   (KeyGroupStreamPartitioner.selectChannel), as or_pipeline_digests does. Per watermark: the row count, the order-free
+   digest of (key, start, end, the aggregates in exact_mask -- their 8-byte result words) and, for the aggregates in
+   sum_mask (double results: SUM / AVG over a DOUBLE, whose GPU order of additions differs), per bucket of rows
+   (bucket = or_row_digest(key, start, 0) & (nbuckets - 1)) the sum of the values and of their magnitudes. */
+typedef struct {
+    const fwa_config* cfg; const fwa_gen_params* p; const double* cdf;
+    int idx, nthreads, fp;
+    int64_t n, batch, nb;
+    uint32_t exact_mask, sum_mask; int nbuckets, nsum;
+    /* shared batch buffers */
+    int64_t* keys; int64_t* ts; int64_t* vi; float* vf; double* vd; int16_t* kg; int64_t* tmax;
+    pthread_barrier_t* bar;
+    int64_t* wrows; uint64_t* wdig; double* wbsum; double* wbabs;   /* [nb + 1] ([nsum][nbuckets]) */
+    int rc;
+} digest2_arg;
+
+static void* digest2_worker(void* vp) {
+    digest2_arg* a = (digest2_arg*)vp;
+    fwa_config c = *a->cfg;
+    const int maxp = c.max_parallelism > 0 ? c.max_parallelism : 128;
+    c.max_parallelism = maxp;
+    or_key_group_range(maxp, a->nthreads, a->idx, &c.kg_start, &c.kg_end);
+    or_engine* e = NULL;
+    a->rc = or_create(&c, &e);
+    int64_t* mk = (int64_t*)malloc(8 * a->batch); int64_t* mt = (int64_t*)malloc(8 * a->batch);
+    int64_t* mi = (int64_t*)malloc(8 * a->batch); float* mf = (float*)malloc(4 * a->batch);
+    double* md = (double*)malloc(8 * a->batch);
+    int64_t max_ts = J_LONG_MIN;
+    fwa_out o;
+    int64_t av[FWA_MAX_AGGS];
+    for (int64_t b = 0; b <= a->nb; b++) {
+        int64_t m = 0, wm = J_LONG_MAX;
+        if (b < a->nb) {
+            const int64_t cnt = (b == a->nb - 1) ? a->n - b * a->batch : a->batch;
+            /* phase G: this thread's share of the batch */
+            const int64_t lo = cnt * a->idx / a->nthreads, hi = cnt * (a->idx + 1) / a->nthreads;
+            fwa_gen_params q = *a->p; q.first_index = a->p->first_index + b * a->batch + lo;
+            or_generate(&q, hi - lo, a->keys + lo, a->ts + lo, a->fp ? NULL : a->vi + lo, a->fp ? a->vf + lo : NULL,
+                        a->fp ? a->vd + lo : NULL, a->cdf);
+            int64_t tm = J_LONG_MIN;
+            for (int64_t i = lo; i < hi; i++) {
+                a->kg[i] = (int16_t)or_key_group(a->keys[i], c.key_kind, 0, maxp);
+                if (a->ts[i] > tm) tm = a->ts[i];
+            }
+            a->tmax[a->idx] = tm;
+            pthread_barrier_wait(a->bar);
+            /* phase O: this operator instance's records of the whole batch, in arrival order */
+            for (int t = 0; t < a->nthreads; t++) if (a->tmax[t] > max_ts) max_ts = a->tmax[t];
+            for (int64_t i = 0; i < cnt; i++) {
+                if (a->kg[i] < c.kg_start || a->kg[i] > c.kg_end) continue;
+                mk[m] = a->keys[i]; mt[m] = a->ts[i];
+                if (a->fp) { mf[m] = a->vf[i]; md[m] = a->vd[i]; } else mi[m] = a->vi[i];
+                m++;
+            }
+            pthread_barrier_wait(a->bar);   /* the shared buffers are free for the next batch */
+            wm = max_ts - a->p->max_delay_ms - 1;                   /* BoundedOutOfOrdernessWatermarks :57-69 */
+        }
+        if (a->rc) continue;                                     /* (keep meeting the barriers) */
+        const void* cols[2] = {a->fp ? (const void*)mf : (const void*)mi, (const void*)md};
+        if ((a->rc = or_push(e, mk, mt, cols, NULL, m, NULL)) != 0) continue;
+        if ((a->rc = or_advance_watermark(e, wm, &o)) != 0) continue;
+        uint64_t d = 0;
+        double* bs = a->wbsum + (size_t)b * a->nsum * a->nbuckets;
+        double* ba = a->wbabs + (size_t)b * a->nsum * a->nbuckets;
+        for (int64_t r = 0; r < o.n_rows; r++) {
+            int k = 0, s = 0;
+            const uint64_t bk = or_row_digest(o.key[r], o.win_start[r], 0, NULL, 0) & (uint64_t)(a->nbuckets - 1);
+            for (int j = 0; j < c.num_aggs; j++) {
+                const aval* x = &((const aval*)o.agg[j])[r];
+                if (a->exact_mask >> j & 1u) av[k++] = x->i;
+                if (a->sum_mask >> j & 1u) {
+                    bs[(size_t)s * a->nbuckets + bk] += x->d;
+                    ba[(size_t)s * a->nbuckets + bk] += fabs(x->d);
+                    s++;
+                }
+            }
+            d += or_row_digest(o.key[r], o.win_start[r], o.win_end[r], av, k);
+        }
+        a->wdig[b] = d; a->wrows[b] = o.n_rows;
+    }
+    free(mk); free(mt); free(mi); free(mf); free(md);
+    if (e) or_destroy(e);
+    return NULL;
+}
+
+double or_pipeline_digests2(const fwa_config* cfg, const fwa_gen_params* p, const double* cdf, int float_cols,
+                            uint32_t exact_mask, uint32_t sum_mask, int nbuckets, int64_t n, int64_t batch, int threads,
+                            int64_t* wm_rows, uint64_t* wm_dig, double* wm_bsum, double* wm_babs) {
+    const int64_t nb = (n + batch - 1) / batch;
+    int nsum = 0;
+    for (int j = 0; j < 32; j++) nsum += (sum_mask >> j) & 1u;
+    if (nbuckets < 1 || (nbuckets & (nbuckets - 1)) || (p->key_dist && !cdf)) return (double)FWA_E_ARG;
+    digest2_arg* args = (digest2_arg*)calloc(threads, sizeof(digest2_arg));
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned)threads);
+    int64_t* keys = (int64_t*)malloc(8 * batch); int64_t* ts = (int64_t*)malloc(8 * batch);
+    int64_t* vi = float_cols ? NULL : (int64_t*)malloc(8 * batch);
+    float* vf = float_cols ? (float*)malloc(4 * batch) : NULL;
+    double* vd = float_cols ? (double*)malloc(8 * batch) : NULL;
+    int16_t* kg = (int16_t*)malloc(2 * batch);
+    int64_t* tmax = (int64_t*)calloc(threads, 8);
+    const size_t bsz = (size_t)(nb + 1) * nsum * nbuckets;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < threads; t++) {
+        args[t] = (digest2_arg){cfg, p, cdf, t, threads, float_cols != 0, n, batch, nb, exact_mask, sum_mask, nbuckets,
+                                nsum, keys, ts, vi, vf, vd, kg, tmax, &bar, (int64_t*)calloc(nb + 1, 8),
+                                (uint64_t*)calloc(nb + 1, 8), (double*)calloc(bsz + 1, 8), (double*)calloc(bsz + 1, 8), 0};
+        pthread_create(&th[t], NULL, digest2_worker, &args[t]);
+    }
+    int rc = 0;
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    for (int64_t b = 0; b <= nb; b++) { wm_rows[b] = 0; wm_dig[b] = 0; }
+    for (size_t i = 0; i < bsz; i++) { wm_bsum[i] = 0.0; wm_babs[i] = 0.0; }
+    for (int t = 0; t < threads; t++) {
+        if (args[t].rc && !rc) rc = args[t].rc;
+        for (int64_t b = 0; b <= nb; b++) { wm_rows[b] += args[t].wrows[b]; wm_dig[b] += args[t].wdig[b]; }
+        for (size_t i = 0; i < bsz; i++) { wm_bsum[i] += args[t].wbsum[i]; wm_babs[i] += args[t].wbabs[i]; }
+        free(args[t].wrows); free(args[t].wdig); free(args[t].wbsum); free(args[t].wbabs);
+    }
+    pthread_barrier_destroy(&bar);
+    free(args); free(th); free(keys); free(ts); free(vi); free(vf); free(vd); free(kg); free(tmax);
+    if (rc) return (double)rc;
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

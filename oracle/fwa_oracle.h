@@ -67,6 +67,11 @@ double or_bench_pipeline(const fwa_config* cfg, const fwa_gen_params* p, int64_t
 uint64_t or_row_digest(int64_t key, int64_t start, int64_t end, const int64_t* aggs, int naggs);
 double or_pipeline_digests(const fwa_config* cfg, const fwa_gen_params* p, int64_t n, int64_t batch, int threads,
                            int64_t* wm_rows, uint64_t* wm_dig);
+/* Full-size digests of the benched configurations beyond C2 (Zipf keys via cdf, float columns, any window kind):
+   fwa_oracle.c, "full-size digests, general form". wm_bsum / wm_babs: [(n / batch + 2)][popcount(sum_mask)][nbuckets]. */
+double or_pipeline_digests2(const fwa_config* cfg, const fwa_gen_params* p, const double* cdf, int float_cols,
+                            uint32_t exact_mask, uint32_t sum_mask, int nbuckets, int64_t n, int64_t batch, int threads,
+                            int64_t* wm_rows, uint64_t* wm_dig, double* wm_bsum, double* wm_babs);
 
 #ifdef __cplusplus
 }

@@ -72,6 +72,10 @@ def lib():
         L.or_pipeline_digests.argtypes = [C.POINTER(A.Config), C.POINTER(A.GenParams), C.c_int64, C.c_int64, C.c_int,
                                           C.c_void_p, C.c_void_p]
         L.or_pipeline_digests.restype = C.c_double
+        L.or_pipeline_digests2.argtypes = [C.POINTER(A.Config), C.POINTER(A.GenParams), C.c_void_p, C.c_int,
+                                           C.c_uint32, C.c_uint32, C.c_int, C.c_int64, C.c_int64, C.c_int,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_pipeline_digests2.restype = C.c_double
         L.or_row_digest.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_int]
         L.or_row_digest.restype = C.c_uint64
         _LIB = L
@@ -233,6 +237,26 @@ def bench_pipeline(cfg, params, n, batch, threads):
     cs = C.c_uint64(0)
     secs = lib().or_bench_pipeline(C.byref(cfg), C.byref(params), n, batch, threads, C.byref(rows), C.byref(cs))
     return secs, rows.value, cs.value
+
+
+def pipeline_digests2(cfg, params, n, batch, threads, cdf=None, float_cols=False, exact=(), sums=(), nbuckets=4096):
+    """or_pipeline_digests2: per watermark the row count, the digest of (key, start, end, the aggregates listed in
+    `exact`: their 8-byte result words) and, for the aggregates in `sums` (double results), per row bucket the sum of
+    the values and of their magnitudes. Returns (secs, rows[nb+1], digests[nb+1], bsum[nb+1][len(sums)][nbuckets],
+    babs[...])."""
+    nb = (n + batch - 1) // batch
+    rows = np.zeros(nb + 1, np.int64)
+    dig = np.zeros(nb + 1, np.uint64)
+    bsum = np.zeros((nb + 1, len(sums), nbuckets), np.float64)
+    babs = np.zeros_like(bsum)
+    em = sum(1 << j for j in exact)
+    sm = sum(1 << j for j in sums)
+    cdf_a = None if cdf is None else np.ascontiguousarray(cdf, np.float64)
+    secs = lib().or_pipeline_digests2(C.byref(cfg), C.byref(params), _ptr(cdf_a), int(bool(float_cols)), em, sm,
+                                      nbuckets, n, batch, threads, _ptr(rows), _ptr(dig), _ptr(bsum), _ptr(babs))
+    if secs < 0:
+        raise OracleError(int(secs), "or_pipeline_digests2")
+    return secs, rows, dig, bsum, babs
 
 
 def pipeline_digests(cfg, params, n, batch, threads):

@@ -18,8 +18,8 @@ def _lsr(x, s):
     return (x >> s) & ((1 << (64 - s)) - 1)
 
 
-def rows_digest(key, start, end, aggs):
-    """(row count, digest as a Python int in [0, 2^64)) of int64 torch columns on any device."""
+def row_hash(key, start, end, aggs):
+    """or_row_digest of every row (int64 torch tensor, the uint64 value's bits)."""
     h = key * _s64(_K[0]) + start * _s64(_K[1]) + end * _s64(_K[2])
     for j, a in enumerate(aggs):
         h = h + a.to(torch.int64) * _s64(_K[3] + 2 * j)
@@ -28,4 +28,31 @@ def rows_digest(key, start, end, aggs):
     h = h ^ _lsr(h, 29)
     h = h * _s64(_K[5])
     h = h ^ _lsr(h, 32)
-    return int(key.shape[0]), int(h.sum().item()) % (1 << 64)
+    return h
+
+
+def rows_digest(key, start, end, aggs):
+    """(row count, digest as a Python int in [0, 2^64)) of int64 torch columns on any device."""
+    return int(key.shape[0]), int(row_hash(key, start, end, aggs).sum().item()) % (1 << 64)
+
+
+def f32_word(x):
+    """A FLOAT result column as the oracle's 8-byte result word: the float's bits, zero-extended."""
+    return x.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+
+
+def f64_word(x):
+    """A DOUBLE result column as the oracle's 8-byte result word: the double's bits."""
+    return x.contiguous().view(torch.int64)
+
+
+def bucket_sums(key, start, vals, nbuckets):
+    """Per row bucket (or_row_digest(key, start, 0) & (nbuckets - 1)) the sums of each double column and of its
+    magnitudes: float64 [len(vals), nbuckets] twice (or_pipeline_digests2's sum_mask side)."""
+    b = row_hash(key, start, torch.zeros_like(key), []) & (nbuckets - 1)
+    s = torch.zeros((len(vals), nbuckets), dtype=torch.float64, device=key.device)
+    a = torch.zeros_like(s)
+    for i, v in enumerate(vals):
+        s[i].index_add_(0, b, v.to(torch.float64))
+        a[i].index_add_(0, b, v.to(torch.float64).abs())
+    return s, a

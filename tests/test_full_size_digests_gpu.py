@@ -1,4 +1,4 @@
-"""Full-size parity of the benched configurations: every fired row, not only totals (VERDICT r04 weak #2).
+"""Full-size parity of the benched configurations: every fired row, not only totals (VERDICT r04 weak #2, r05 #1).
 
 The C2 stream bench.py times (15 batches of 2^26 records, 1M uniform keys, tumbling 10 s COUNT + SUM(long), D = 1 s,
 async device pushes, output left in HBM) and the C4 one (1e8 uniform keys, record lists auto-selected; 5 batches of
@@ -13,7 +13,7 @@ import threading
 import numpy as np
 import pytest
 
-from digest import rows_digest
+from digest import bucket_sums, f32_word, f64_word, rows_digest
 from flink_amd import _abi as A
 
 pytestmark = pytest.mark.gpu
@@ -102,3 +102,141 @@ def test_c4_full_size_rows_vs_oracle():
     """BASELINE C4 engine shape at N=1: 1e8 keys (record lists), 5 x 2^26 records; every row of every watermark."""
     rows = _digest_run(100_000_000, 5, record_lists=True)
     assert rows > 200_000_000
+
+
+def _join_with_heartbeat(th, name, every=20.0):
+    """Wait for the oracle thread, touching gpurun_out/heartbeat_<name> every `every` seconds: a GPU run that writes
+    nothing for 3 minutes is taken to be hung, and the oracle of a full-size configuration can take longer."""
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "gpurun_out", "heartbeat_%s" % name)
+    t0 = time.time()
+    while th.is_alive():
+        th.join(timeout=every)
+        try:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            with open(path, "a") as f:
+                f.write("%s oracle running %.0f s\n" % (name, time.time() - t0))
+        except OSError:
+            pass
+
+
+# C3 / C5 / C5s as bench.py runs them (VERDICT r05 "next round" item 1): the same generator seeds, key distribution,
+# event-time density, window and aggregate list, 2^26-record pushes; per watermark the row count and the digest of
+# (key, start, end, COUNT and the other exactly-reproducible words: integer sums, MAX of FLOAT / DOUBLE) must equal the
+# oracle's, and the DOUBLE SUM / AVG results -- added in another order on the GPU -- are compared per row bucket
+# (4096 buckets by a hash of (key, window start)) as sums of the values, within 1e-9 of the sums of their magnitudes.
+FL = [("COUNT", 0), ("SUM_F64", 1), ("AVG_F64", 1), ("MAX_F32", 0), ("MAX_F64", 1)]
+BENCHED = {
+    "c3": dict(win=dict(window_kind="SLIDE", semantics="TABLE", size_ms=60_000, slide_ms=1_000),
+               aggs=[("COUNT", 0), ("SUM_I64", 0)], zipf=True, fp=False, exact=(0, 1), sums=()),
+    "c5": dict(win=dict(window_kind="TUMBLE", semantics="TABLE", size_ms=10_000), aggs=FL, zipf=False, fp=True,
+               exact=(0, 3, 4), sums=(1, 2)),
+    "c5s": dict(win=dict(window_kind="SESSION", semantics="DATASTREAM", gap_ms=5_000), aggs=FL, zipf=False, fp=True,
+                exact=(0, 3, 4), sums=(1, 2)),
+}
+NBK = 4096
+
+
+def _digest_run2(name, nbatches, nkeys=1_000_000):
+    import torch
+    from flink_amd import engine as E
+    from oracle import oracle as O
+    c = BENCHED[name]
+    n = nbatches * B
+    p = A.GenParams(seed_k=0x5eed0001, seed_t=0x5eed0002, seed_v=0x5eed0003, first_index=0, total_records=n,
+                    num_keys=nkeys, t0_ms=1_700_000_000_000, span_ms=n * 1_000_000 // 1_000_000_000,
+                    max_delay_ms=1000, key_dist=1 if c["zipf"] else 0, val_kind=1 if c["fp"] else 0)
+    cdf = None
+    if c["zipf"]:
+        w = 1.0 / np.arange(1, nkeys + 1, dtype=np.float64) ** 1.1
+        cdf = np.cumsum(w) / w.sum()
+    ocfg = A.make_config(aggs=c["aggs"], **c["win"])
+    res = {}
+
+    def oracle_leg():
+        try:
+            res["oracle"] = O.pipeline_digests2(ocfg, p, n, B, _threads(), cdf=cdf, float_cols=c["fp"],
+                                                exact=c["exact"], sums=c["sums"], nbuckets=NBK)
+        except Exception as ex:      # reported by the main thread
+            res["error"] = ex
+    th = threading.Thread(target=oracle_leg)
+    th.start()
+    got, gsum, gabs = [], [], []
+    try:
+        k = torch.empty(n, dtype=torch.int64, device="cuda")
+        t = torch.empty_like(k)
+        if c["zipf"]:
+            zc = torch.from_numpy(cdf).cuda()
+            p.zipf_cdf = zc.data_ptr()
+        if c["fp"]:
+            vf = torch.empty(n, dtype=torch.float32, device="cuda")
+            vd = torch.empty(n, dtype=torch.float64, device="cuda")
+            E.generate(p, n, k, t, None, vf, vd)
+            cols = lambda b: [vf[b * B:(b + 1) * B], vd[b * B:(b + 1) * B]]  # noqa: E731
+        else:
+            v = torch.empty_like(k)
+            E.generate(p, n, k, t, v)
+            cols = lambda b: [v[b * B:(b + 1) * B]]  # noqa: E731
+        torch.cuda.synchronize()
+        bmax = t.view(nbatches, B).max(dim=1).values.cpu().numpy()
+        cfg = A.make_config(aggs=c["aggs"], key_capacity=nkeys, output_on_device=1, **c["win"])
+        g = E.WindowAggregator(cfg)
+        word = {0: lambda x: x, 1: lambda x: x, 3: f32_word, 4: f64_word}
+        m = -2**63
+        for b in range(nbatches + 1):
+            if b < nbatches:
+                m = max(m, int(bmax[b]))
+                g.push(k[b * B:(b + 1) * B], t[b * B:(b + 1) * B], cols(b), sync=False)
+                wm = m - 1001
+            else:
+                wm = A.LONG_MAX
+            out = g.advance_watermark_device(wm)
+            got.append(rows_digest(out["key"], out["win_start"], out["win_end"],
+                                   [word[j](out["agg%d" % j]) for j in c["exact"]]))
+            if c["sums"]:
+                s_, a_ = bucket_sums(out["key"], out["win_start"], [out["agg%d" % j] for j in c["sums"]], NBK)
+                gsum.append(s_.cpu().numpy())
+                gabs.append(a_.cpu().numpy())
+        st = g.stats()
+        assert st.records_in == n
+        modes = {o: g.get_option(o) for o in ("skew_merge", "window_passes", "slide_carried", "session_path")}
+        g.close()
+        del k, t
+    finally:
+        _join_with_heartbeat(th, name)
+    if "error" in res:
+        raise res["error"]
+    _, rows, dig, bsum, babs = res["oracle"]
+    for b in range(nbatches + 1):
+        assert got[b] == (int(rows[b]), int(dig[b])), "%s watermark %d: GPU (rows, digest) %s != oracle %s" % (
+            name, b, got[b], (int(rows[b]), int(dig[b])))
+        if c["sums"]:
+            tol = 1e-9 * babs[b] + 1e-9
+            bad = np.abs(gsum[b] - bsum[b]) > tol
+            assert not bad.any(), "%s watermark %d: %d of %d bucket sums differ" % (name, b, bad.sum(), bad.size)
+            assert np.allclose(gabs[b], babs[b], rtol=1e-9, atol=1e-9)
+    return int(rows.sum()), st, modes
+
+
+def test_c3_full_size_rows_vs_oracle():
+    """C3 as benched: HOP 60 s / 1 s over Zipf(1.1) keys of 1M items, pushes of 2^26 records. The adaptive modes
+    the bench's warm-up settles -- tile pre-aggregation of the hot keys (PRE), combiner window passes, carried window
+    sums in the HOP fire -- all engage within the run (each switches on after the first push), and every row of every
+    watermark equals the oracle's. Two pushes: the oracle merges 60 slices per (key, window) for ~50M rows per push,
+    ~15 us per row per core (its timer heap and state map hold tens of millions of entries): minutes on 16 cores."""
+    rows, st, modes = _digest_run2("c3", 2)
+    assert rows > 120_000_000
+    assert modes["skew_merge"] == 1 and modes["window_passes"] == 1 and modes["slide_carried"] > 0, modes
+
+
+def test_c5_full_size_rows_vs_oracle():
+    """C5 as benched: Table TUMBLE 10 s, COUNT / SUM / AVG over DOUBLE, MAX over FLOAT and DOUBLE, 1M keys, 8 pushes."""
+    rows, st, _ = _digest_run2("c5", 8)
+    assert rows > 40_000_000
+
+
+def test_c5s_full_size_rows_vs_oracle():
+    """C5 with DataStream session windows (gap 5 s) as benched, 8 pushes: the session path's rows at every watermark."""
+    rows, st, modes = _digest_run2("c5s", 8)
+    assert rows > 500_000
