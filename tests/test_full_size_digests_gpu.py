@@ -223,10 +223,10 @@ def test_c3_full_size_rows_vs_oracle():
     """C3 as benched: HOP 60 s / 1 s over Zipf(1.1) keys of 1M items, pushes of 2^26 records. The adaptive modes
     the bench's warm-up settles -- tile pre-aggregation of the hot keys (PRE), combiner window passes, carried window
     sums in the HOP fire -- all engage within the run (each switches on after the first push), and every row of every
-    watermark equals the oracle's. Two pushes: the oracle merges 60 slices per (key, window) for ~50M rows per push,
-    ~15 us per row per core (its timer heap and state map hold tens of millions of entries): minutes on 16 cores."""
-    rows, st, modes = _digest_run2("c3", 2)
-    assert rows > 120_000_000
+    watermark (~50M rows per push) equals the oracle's; the oracle merges 60 slices per (key, window) on 16 cores,
+    about half a minute per push, so the test reports progress through gpurun_out/heartbeat_c3."""
+    rows, st, modes = _digest_run2("c3", 8)
+    assert rows > 350_000_000
     assert modes["skew_merge"] == 1 and modes["window_passes"] == 1 and modes["slide_carried"] > 0, modes
 
 

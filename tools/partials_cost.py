@@ -7,8 +7,11 @@ Each step prices the pieces one rank runs at N = WORLD (default 8) under weak sc
          per source rank: the same keys and windows, each source holding its own partial), sources back to back as
          in the receive buffer: "merge_fire" = fwa_fire_partials on the packed rows (the pipeline's path), "sources"
          = unpack + push_partials + fire, "window" = the same with the rows sorted window-major first.
-The all_to_all itself is not priced here (bytes shipped are printed). The owner engine is sized to its key-group
-share (distributed.owner_key_capacity)."""
+The all_to_all is priced by a model (it needs W GPUs): bytes this rank sends to each peer / the per-link xGMI rate
+(--link-gbps, default SURVEY.md section 5's ~153 GB/s per link and direction, one link per peer in an 8-GPU mesh, all
+links in parallel) / --link-eff; the step is printed serial (exchange added) and pipelined (bench.py overlaps the
+exchange with the next batch's push: max(local, exchange) + owner). The owner engine is sized to its key-group share
+(distributed.owner_key_capacity)."""
 import argparse
 import os
 import sys
@@ -30,6 +33,8 @@ ap.add_argument("--owner-share", type=int, default=1, help="1: owner key capacit
 ap.add_argument("--dup", type=int, default=0, help="copies of the destination-0 rows the owner receives (0: world)")
 ap.add_argument("--routed", type=int, default=1, help="1: fwa_drain_route (drain + routing in one pass)")
 ap.add_argument("--owner-profile", type=int, default=0, help="FWA_OPT_PROFILE on the owners (per-block phase cycles)")
+ap.add_argument("--link-gbps", type=float, default=153.0, help="assumed xGMI rate per link and direction (GB/s)")
+ap.add_argument("--link-eff", type=float, default=0.8, help="assumed all-to-all efficiency on those links")
 args = ap.parse_args()
 
 B = 1 << 26
@@ -83,6 +88,7 @@ for b in range(S):
     _, t["push"] = timed(lambda: local.push(keys[sl], ts[sl], [vals[sl]]))
     if args.routed:     # fwa_drain_route: the drain writes the per-destination send blocks itself
         (parts, counts, m), t["drain_route"] = timed(lambda: local.drain_route(wm, W))
+        peer_bytes = max(counts[1:]) * m * 8 if W > 1 else 0
         recv = parts[0].repeat(args.dup or W, 1)
         d = {"key": torch.empty(sum(counts))}
         packed = torch.empty((sum(counts), m), dtype=torch.int64)
@@ -91,6 +97,7 @@ for b in range(S):
         cols = [d["key"], d["slice_start"], d["count"], d["acc1"]]
         (packed, counts), t["route"] = timed(lambda: E.route_rows(cols[0], cols, 128, W))
         n0 = int(counts[0].item())
+        peer_bytes = int(counts[1:].max().item()) * len(cols) * 8 if W > 1 else 0
         recv = packed[:n0].repeat(args.dup or W, 1)                 # what the owner receives: one copy per source rank
     cells = [2, 3]
     for o in orders:
@@ -103,9 +110,12 @@ for b in range(S):
         c, t[o + "_unpack"] = timed(lambda: E.unpack_rows(rv))
         _, t[o + "_merge"] = timed(lambda: owners[o].push_partials(c[0], c[1], c[2], [c[2], c[3]]))
         _, t[o + "_fire"] = timed(lambda: owners[o].advance_watermark_raw(wm).n_rows)
+    xm = peer_bytes / (args.link_gbps * 1e9 * args.link_eff) * 1e3
     if b >= 2:
         for k, v in t.items():
             tot[k] = tot.get(k, 0.0) + v
+        tot["exchange_model"] = tot.get("exchange_model", 0.0) + xm
+        tot["peer_mb"] = tot.get("peer_mb", 0.0) + peer_bytes / 1e6
     print("step %d: " % b + " ".join("%s %.3f" % kv for kv in t.items()) +
           " ms; partials %d (%.0f MB), owner rows %d" % (d["key"].shape[0], packed.numel() * 8 / 1e6, recv.shape[0]),
           flush=True)
@@ -118,3 +128,10 @@ for o in orders:
     s = sum(tot[k] for k in parts) / n
     print("N=%d per-rank step, owner order %s: %.3f ms = %s -> %.2fx N=1" %
           (W, o, s, " + ".join("%s %.3f" % (k, tot[k] / n) for k in parts), s / n1))
+    x = tot["exchange_model"] / n
+    local = sum(tot[k] for k in parts[:2 if args.routed else 3]) / n
+    owner = s - local
+    print("  with the all-to-all (model: %.1f MB to each peer at %.0f GB/s x %.2f = %.3f ms): serial %.3f ms -> %.2fx; "
+          "pipelined max(local %.3f, exchange) + owner %.3f = %.3f ms -> %.2fx N=1" %
+          (tot["peer_mb"] / n, args.link_gbps, args.link_eff, x, s + x, (s + x) / n1, local, owner,
+           max(local, x) + owner, (max(local, x) + owner) / n1))
