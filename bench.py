@@ -55,9 +55,10 @@ def main():
                          "c4: tumbling 10s COUNT+SUM(long), 100M uniform keys, maxParallelism 128; "
                          "c5: Table TUMBLE 10s TVF COUNT, SUM(double), AVG(double), MAX(float), MAX(double); "
                          "c5s: DataStream session windows (gap 5s), same float aggregates")
-    ap.add_argument("--async-fire", action="store_true",
-                    help="N=1: take each watermark's rows after the next batch was handed over "
-                         "(fwa_advance_watermark_async; r04: 41.8 vs 47.8 G rec/s on C2, so not the default)")
+    ap.add_argument("--sync-fire", action="store_true",
+                    help="N=1: wait for each watermark's rows before the next batch is handed over "
+                         "(fwa_advance_watermark); default: fwa_advance_watermark_async, the rows taken after the next "
+                         "batch was handed over, so the next push's host work overlaps the fire (warm-up the same way)")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="fwa_set_option on the measured engine(s) (flink_amd.engine.OPTIONS), e.g. profile=1")
     ap.add_argument("--exchange", choices=["auto", "partials", "raw"], default="auto",
@@ -167,9 +168,17 @@ def main():
         engines = [eng]
 
     rows = 0
+    async_fire = world == 1 and not args.sync_fire
     for b in range(args.warmup):
         push(b)
-        rows += fire(b)
+        if async_fire:        # the same calls as the timed loop (output buffers grown, modes settled before timing)
+            if b > 0:
+                rows += eng.fired_output_raw().n_rows
+            eng.advance_watermark_async(wms[b])
+        else:
+            rows += fire(b)
+    if async_fire and args.warmup > 0:
+        rows += eng.fired_output_raw().n_rows
     for x in engines:
         x.reset_timers()
     if world > 1:
@@ -184,7 +193,7 @@ def main():
             rows_t += pipelined(b, b + 1 if b + 1 < S else None)
             if (b - args.warmup) % 4 == 3:
                 log("step %d/%d  %.2fs" % (b - args.warmup + 1, args.steps, time.perf_counter() - t0))
-    elif world == 1 and args.async_fire:
+    elif async_fire:
         # the watermark step returns while its fire runs (fwa_advance_watermark_async); the fired rows are taken
         # after the next batch was handed over, so the host's work for batch b+1 overlaps the fire of batch b
         for b in range(args.warmup, S):

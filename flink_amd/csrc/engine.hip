@@ -1814,12 +1814,17 @@ __global__ void reset_slots_kernel(unsigned long long* const* slot_base, const i
         return;
     }
     unsigned long long* base = slot_base[slot];
+    // 4 x 16-byte stores in flight per thread and trip (one store per thread and launch made a 32 MB C2 slot reset a
+    // 30 us launch-overhead-bound kernel)
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    const int64_t m = stride / 2;                                      // stride % 64 == 0: 16 B stores
     for (int col = 0; col < c.nacc; ++col) {
         const unsigned long long v = (col > 0 && c.acc_kind[col] == ACC_MIN_ORD) ? ~0ull : 0ull;
-        ulonglong2* p = (ulonglong2*)(base + (int64_t)col * stride);   // stride % 64 == 0: 16 B stores
+        ulonglong2* p = (ulonglong2*)(base + (int64_t)col * stride);
         const ulonglong2 v2 = make_ulonglong2(v, v);
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < stride / 2; i += step) p[i] = v2;
+        int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        for (; i + 3 * step < m; i += 4 * step) { p[i] = v2; p[i + step] = v2; p[i + 2 * step] = v2; p[i + 3 * step] = v2; }
+        for (; i < m; i += step) p[i] = v2;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) touched[slot] = 0;
 }
@@ -2198,7 +2203,7 @@ int validate(const fwa_config* c) {
         if (c->flags & FWA_CFG_REDUCE) {
             if (nby > 1 || (nsel && !nby) || (nfirst && nby)) return FWA_E_ARG;
             if (nother || c->semantics != FWA_SEM_DATASTREAM || (c->window_kind != FWA_TUMBLE && c->window_kind != FWA_SLIDE) ||
-                c->allowed_lateness_ms != 0 || (c->flags & (FWA_CFG_RECORD_LISTS | FWA_CFG_DYNAMIC_GAP)))
+                (c->flags & (FWA_CFG_RECORD_LISTS | FWA_CFG_DYNAMIC_GAP)))
                 return FWA_E_UNSUPPORTED;
         }
     }
@@ -2378,9 +2383,10 @@ int flush_resets(fwa_engine* e) {
         int rc = upload(e, e->d_reset_list, e->pending_reset.data(), sizeof(int32_t) * n);
         if (rc) return rc;
     }
-    const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 1024 / n), (e->stride / 2 + 1023) / 1024);
-    reset_slots_kernel<<<dim3((unsigned)blocks, (unsigned)n), 1024, 0, e->stream>>>(e->d_slot_base, e->d_reset_list, inl,
-                                                                                   e->stride, e->d_touched, e->d_ec);
+    // about two 256-thread blocks per CU over all the slots, each thread storing 4 x 16 B per trip
+    const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 512 / n), (e->stride / 2 + 4095) / 4096);
+    reset_slots_kernel<<<dim3((unsigned)blocks, (unsigned)n), 256, 0, e->stream>>>(e->d_slot_base, e->d_reset_list, inl,
+                                                                                  e->stride, e->d_touched, e->d_ec);
     HIPCHK(e, hipGetLastError());
     e->pending_reset.clear();
     return FWA_OK;
@@ -3801,7 +3807,8 @@ static int process_late(fwa_engine* e, const IngestArgs& a0, std::vector<int32_t
     L.o_end = e->lr_col[2];
     for (int j = 0; j < e->cfg.num_aggs; ++j) L.o_agg[j] = e->lr_col[3 + j];
     L.rows = e->d_lr_n;
-    late_fire_kernel<<<1, 64, 0, e->stream>>>(L, e->d_ec);
+    if (e->red) red_late_fire_kernel<<<1, 64, 0, e->stream>>>(L, e->d_ec, e->red_seq_base + e->records_in);
+    else late_fire_kernel<<<1, 64, 0, e->stream>>>(L, e->d_ec);
     HIPCHK(e, hipGetLastError());
     unsigned long long rows = 0;
     HIPCHK(e, hipMemcpyAsync(&rows, e->d_lr_n, 8, hipMemcpyDeviceToHost, e->stream));
@@ -5306,10 +5313,14 @@ int fwa_advance_watermark_async(fwa_engine* e, int64_t wm) {
             hs.push_back(kv.second);
             hw.push_back(f);
         }
-        if (!hw.empty()) {
-            // every row of the fire must fit: windows x keys (keys known at the last status + the pending push's)
-            const int64_t nk = std::min<int64_t>(e->capacity + 1, (int64_t)e->h_st->n_keys + e->pend_n);
-            int rc = ensure_out(e, (int64_t)hw.size() * std::max<int64_t>(nk, 1));
+        // every row of the fire must fit: windows x keys (keys known at the last status + the pending push's). When
+        // the output columns would have to grow (hipFree synchronises the device, e.g. the final watermark firing
+        // several windows at once) the synchronous path counts the rows and sizes them instead.
+        const int64_t nk = std::min<int64_t>(e->capacity + 1, (int64_t)e->h_st->n_keys + e->pend_n);
+        const int64_t need = (int64_t)hw.size() * std::max<int64_t>(nk, 1);
+        const int64_t floor_rows = e->opt_out_min > 0 ? e->opt_out_min : ((int64_t)1 << 22);
+        if (!hw.empty() && (need <= e->out_cap || e->out_cap < floor_rows)) {
+            int rc = ensure_out(e, need);
             if (rc) return rc;
             if ((rc = upload_windows(e, hw, hs))) return rc;
             HIPCHK(e, hipMemsetAsync(&e->d_st->rows, 0, 8, e->stream));

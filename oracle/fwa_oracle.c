@@ -668,8 +668,8 @@ int or_create(const fwa_config* c, or_engine** out) {
         if (nred && !(c->flags & FWA_CFG_REDUCE)) return FWA_E_ARG;
         if (c->flags & FWA_CFG_REDUCE) {
             if (nby > 1 || (nsel && !nby) || (nfirst && nby)) return FWA_E_ARG;
-            if (c->semantics != FWA_SEM_DATASTREAM || (c->window_kind != FWA_TUMBLE && c->window_kind != FWA_SLIDE) ||
-                c->allowed_lateness_ms != 0) return FWA_E_UNSUPPORTED;
+            if (c->semantics != FWA_SEM_DATASTREAM || (c->window_kind != FWA_TUMBLE && c->window_kind != FWA_SLIDE))
+                return FWA_E_UNSUPPORTED;
         }
     }
     if (c->tz_n < 0 || (c->tz_n > 0 && (!c->tz || c->semantics != FWA_SEM_TABLE))) return FWA_E_ARG;

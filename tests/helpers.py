@@ -256,6 +256,7 @@ def replay_reduce_kat(case, make_engine):
     kw = dict(window_kind=spec["window_kind"], size_ms=spec["size_ms"], offset_ms=spec["offset_ms"])
     if spec["window_kind"] == "SLIDE":
         kw["slide_ms"] = spec["slide_ms"]
+    kw["allowed_lateness_ms"] = spec.get("allowed_lateness_ms", 0)
     cfg = A.make_config(aggs=reduce_aggs(case["op"], case["pos"]), reduce=True, **kw)
     names = A.agg_names(cfg)
     eng = make_engine(cfg)

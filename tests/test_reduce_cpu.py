@@ -54,10 +54,9 @@ def test_double_compare_order_and_tie_rule():
     assert np.isnan(r["agg0"][0]) and int(r["agg1"][0]) == 10
 
 
-def test_reduce_handles_refuse_merging_windows_and_lateness():
+def test_reduce_handles_refuse_merging_windows():
     from oracle.oracle import Oracle, OracleError
-    for kw in (dict(window_kind="SESSION", gap_ms=10, size_ms=0), dict(window_kind="TUMBLE", allowed_lateness_ms=5),
-               dict(window_kind="TUMBLE", semantics="TABLE")):
+    for kw in (dict(window_kind="SESSION", gap_ms=10, size_ms=0), dict(window_kind="TUMBLE", semantics="TABLE")):
         with pytest.raises(OracleError):
             Oracle(A.make_config(aggs=[("SUM_I64", 0), ("FIRST_64", 1)], reduce=True, **kw))
     with pytest.raises(OracleError):                        # FIRST_* needs FWA_CFG_REDUCE

@@ -2,7 +2,8 @@
 WindowedStream.java:680-890): the reference's own Python WindowOperator sequences (tests/golden/
 gen_pyflink_reduce_kats.py), random streams against the oracle's arrival-order fold (every field of the reduced tuple,
 bit-exact except Double / Float sums, whose device order differs: relative 1e-9 / 2e-4 as SUM_F64 / SUM_F32 elsewhere),
-ties in both directions, and Java's wrap-around and compareTo order."""
+ties in both directions, allowed lateness (late firings of the reduced element, in arrival order), and Java's
+wrap-around and compareTo order."""
 import numpy as np
 import pytest
 
@@ -53,8 +54,11 @@ def _close(a, b, names):
 @pytest.mark.parametrize("op,pos", [("sum", 1), ("sum", 2), ("sum", 3), ("min", 2), ("max", 3), ("min", 1),
                                     ("min_by", 2), ("max_by", 1), ("min_by", 3), ("max_by", 2)])
 @pytest.mark.parametrize("win", [dict(window_kind="TUMBLE", size_ms=1000),
-                                 dict(window_kind="SLIDE", size_ms=3000, slide_ms=1000, offset_ms=300)],
-                         ids=["tumble", "slide"])
+                                 dict(window_kind="SLIDE", size_ms=3000, slide_ms=1000, offset_ms=300),
+                                 dict(window_kind="TUMBLE", size_ms=1000, allowed_lateness_ms=1500),
+                                 dict(window_kind="SLIDE", size_ms=3000, slide_ms=1000, offset_ms=300,
+                                      allowed_lateness_ms=2000)],
+                         ids=["tumble", "slide", "tumble_late", "slide_late"])
 def test_random_reductions_vs_oracle(eng_mod, win, op, pos, by_last, ties):
     from oracle.oracle import Oracle
     if by_last and not op.endswith("_by"):
@@ -105,7 +109,7 @@ def test_java_semantics_on_gpu(eng_mod):
 
 
 def test_reduce_handle_refusals(eng_mod):
-    for kw in (dict(window_kind="SESSION", gap_ms=10, size_ms=0), dict(window_kind="TUMBLE", allowed_lateness_ms=5)):
+    for kw in (dict(window_kind="SESSION", gap_ms=10, size_ms=0),):
         with pytest.raises(eng_mod.EngineError) as ei:
             eng_mod.WindowAggregator(A.make_config(aggs=[("SUM_I64", 0), ("FIRST_64", 1)], reduce=True, **kw))
         assert ei.value.code == -7
@@ -119,7 +123,9 @@ def test_reduce_handle_refusals(eng_mod):
 
 @pytest.mark.parametrize("op,pos,by_last", [("sum", 2, False), ("min_by", 2, False), ("max_by", 1, True), ("min", 3, False)])
 @pytest.mark.parametrize("win", [dict(window_kind="TUMBLE", size_ms=1000),
-                                 dict(window_kind="SLIDE", size_ms=3000, slide_ms=1000)], ids=["tumble", "slide"])
+                                 dict(window_kind="SLIDE", size_ms=3000, slide_ms=1000),
+                                 dict(window_kind="SLIDE", size_ms=3000, slide_ms=1000, allowed_lateness_ms=2000)],
+                         ids=["tumble", "slide", "slide_late"])
 def test_reduction_snapshot_restore_rescale(eng_mod, win, op, pos, by_last):
     """fwa_snapshot / fwa_restore of a reduction mid-stream, 1 subtask -> 2 subtasks (key-group halves) and back into
     one: every later watermark's rows equal an uninterrupted oracle run (the restored elements are pushed back in their

@@ -78,5 +78,6 @@ if __name__ == "__main__":
     exp = np.concatenate(exp)
     srt = lambda a: a[np.lexsort(a.T[::-1])]  # noqa: E731
     ok = got.shape == exp.shape and np.array_equal(srt(got), srt(exp))
-    print("2-rank two-phase pipeline (routed drain, fire_partials) rows %d vs oracle %d: %s" % (len(got), len(exp), "EQUAL" if ok else "DIFFERENT"))
+    print("2-rank two-phase pipeline on ONE GPU over gloo (host-staged row blocks, not RCCL; routed drain, fire_partials) "
+          "rows %d vs oracle %d: %s" % (len(got), len(exp), "EQUAL" if ok else "DIFFERENT"))
     sys.exit(0 if ok else 1)
