@@ -1,8 +1,9 @@
 """Benchmark: records/sec aggregated by the MI355X window engine (BASELINE.json metric).
 
 Workload (N=1): config C2 of BASELINE.json -- event-time tumbling 10 s window, COUNT + SUM(long), over
-synthetic (long key, long ts, long val) records, 1M uniform keys, 1e9 records (15 batches of 2^26 =
-1.007e9), bounded out-of-orderness D = 1 s, wm = max_ts - D - 1 after every batch, final wm = Long.MAX.
+synthetic (long key, long ts, long val) records, 1M uniform keys, batches of 2^26 records (defaults: 1 warm-up + 14
+timed = 1.007e9 records; the driver runs --warmup 5 --steps 20), bounded out-of-orderness D = 1 s,
+wm = max_ts - D - 1 after every batch, final wm = Long.MAX.
 A step = one batch pushed through the engine + the watermark advance that fires its windows. Inputs are
 generated into HBM before timing; outputs stay in HBM.
 
@@ -49,12 +50,14 @@ def main():
     ap.add_argument("--wire-batches", type=int, default=4)
     ap.add_argument("--no-wide", action="store_true", help="skip the 64-bit-key leg (C2 without narrow entries)")
     ap.add_argument("--wide-batches", type=int, default=8)
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "c5s"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "c5s", "reduce"], default="c2",
                     help="c2: tumbling 10s COUNT+SUM(long), 1M uniform keys (the metric's workload); "
                          "c3: HOP 60s/1s (Table slicing), Zipf(1.1) keys over 1M items; "
                          "c4: tumbling 10s COUNT+SUM(long), 100M uniform keys, maxParallelism 128; "
                          "c5: Table TUMBLE 10s TVF COUNT, SUM(double), AVG(double), MAX(float), MAX(double); "
-                         "c5s: DataStream session windows (gap 5s), same float aggregates")
+                         "c5s: DataStream session windows (gap 5s), same float aggregates; "
+                         "reduce: the C2 stream through a DataStream built-in reduction, WindowedStream.sum(1) over "
+                         "Tuple3<Long key, Long val, Long ts> (the reduced tuple keeps the first element's ts)")
     ap.add_argument("--sync-fire", action="store_true",
                     help="N=1: wait for each watermark's rows before the next batch is handed over "
                          "(fwa_advance_watermark); default: fwa_advance_watermark_async, the rows taken after the next "
@@ -130,6 +133,8 @@ def main():
     if args.config == "c3":
         win_kw = dict(window_kind="SLIDE", semantics="TABLE", size_ms=60_000, slide_ms=1_000)
     aggs = [("COUNT", 0), ("SUM_I64", 0)]
+    if args.config == "reduce":   # FWA_CFG_REDUCE: field 1 summed, field 2 the window's first element's
+        aggs = [("SUM_I64", 0), ("FIRST_64", 1)]
     if fp:   # C5: column 0 = f (FLOAT), column 1 = d (DOUBLE)
         aggs = [("COUNT", 0), ("SUM_F64", 1), ("AVG_F64", 1), ("MAX_F32", 0), ("MAX_F64", 1)]
         win_kw = dict(window_kind="TUMBLE", semantics="TABLE", size_ms=args.window_ms)
@@ -137,13 +142,14 @@ def main():
             win_kw = dict(window_kind="SESSION", semantics="DATASTREAM", gap_ms=5_000)
     cfg_kw = dict(**win_kw,
                   aggs=aggs, key_capacity=int(args.keys * float(os.environ.get("FWA_KCAP", "1"))),
-                  output_on_device=1, device=local_rank)
+                  output_on_device=1, device=local_rank, reduce=args.config == "reduce")
     cols_of = (lambda b: [vals[b * B:(b + 1) * B], vals_d[b * B:(b + 1) * B]]) if fp else \
+        (lambda b: [vals[b * B:(b + 1) * B], ts[b * B:(b + 1) * B]]) if args.config == "reduce" else \
         (lambda b: [vals[b * B:(b + 1) * B]])
     pipelined = None
     if args.exchange == "auto":
         from flink_amd.distributed import choose_exchange
-        args.exchange = choose_exchange(cfg_kw)
+        args.exchange = "raw" if args.config == "reduce" else choose_exchange(cfg_kw)   # reductions: no partials
     if world > 1:
         from flink_amd.distributed import KeyedWindowPipeline, TwoPhaseKeyedWindowPipeline
         cls = TwoPhaseKeyedWindowPipeline if args.exchange == "partials" else KeyedWindowPipeline
@@ -260,6 +266,11 @@ def main():
         workload = ("C4: event-time tumbling %ds COUNT+SUM(long), %d uniform keys, %d records/GPU "
                     "(%d batches of %d), D=%dms" % (args.window_ms // 1000, args.keys, args.steps * B,
                                                     args.steps, B, args.delay_ms))
+    elif args.config == "reduce":
+        metric = "records/sec aggregated (DataStream reduce: WindowedStream.sum(1), 1M-key tumbling)"
+        workload = ("reduce: event-time tumbling %ds WindowedStream.sum(1) over Tuple3<Long,Long,Long> (f0 key, f1 "
+                    "summed, f2 = ts kept from the first element), %d uniform keys, %d records/GPU (%d batches of %d), "
+                    "D=%dms" % (args.window_ms // 1000, args.keys, args.steps * B, args.steps, B, args.delay_ms))
     elif fp:
         kind = "Table TUMBLE %ds TVF" % (args.window_ms // 1000) if args.config == "c5" else "DataStream SESSION gap 5s"
         metric = "records/sec aggregated (C5: %s, COUNT/SUM/AVG(double)/MAX(float,double))" % kind
@@ -346,6 +357,8 @@ def ingest_kernels(args, eng):
                 "(cell pre-aggregation; sess3_* sort-based cells or sess2_* when a push leaves its range)")
     if eng.record_lists:
         return "sp_range_kernel+sp_hist_kernel+sp_scan_kernel+sp_scatter_kernel (record lists)"
+    if args.config == "reduce":
+        return "ingest_kernel+red_index_kernel+red_pick_kernel+red_payload_kernel (v1 atomics + selection passes)"
     return "partition3_kernel+combine3_kernel" if eng.stats().partition_ms > 0 else "ingest_kernel"
 
 
@@ -355,6 +368,8 @@ def fire_kernels(args, eng):
         return "sess2_fire_kernel"
     if eng.record_lists:
         return "sp_refine_kernel+sp_agg_kernel (record lists)"
+    if args.config == "reduce":
+        return "red_fire_kernel"
     return "fire_slide_kernel" if args.config == "c3" else "fire_kernel"
 
 

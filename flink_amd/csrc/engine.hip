@@ -1927,6 +1927,7 @@ struct fwa_engine {
     // accumulators
     int64_t stride = 0;
     int32_t nacc = 1;
+    int32_t nacc_comb = 1;                // EngineConst::nacc_comb
     std::vector<void*> chunks;
     std::vector<unsigned long long*> slot_ptr;
     unsigned long long** d_slot_base = nullptr;
@@ -2070,6 +2071,10 @@ struct fwa_engine {
     // FWA_CFG_REDUCE: DataStream built-in reductions (reduce.inc): per-record (kid, slot) of the last push
     bool red = false;
     unsigned long long* d_rk = nullptr;
+    int64_t* d_iota = nullptr;            // red_iota: the push's arrival sequence column (kIotaCol)
+    int64_t iota_cap = 0;
+    int32_t* d_rslots = nullptr;          // red_iota: slots the payload pass scans
+    int64_t rslots_cap = 0;
     int64_t rk_cap = 0;
     int64_t red_seq_base = 0;             // arrival sequence of the restored elements (red_restore)
     SpState* sp = nullptr;
@@ -2597,7 +2602,7 @@ void fwa_destroy(fwa_engine* e) {
     void* bufs[] = {e->d_ec, e->d_keys, e->d_slot_base, e->d_touched, e->d_dir, e->d_want, e->d_spill, e->d_replay,
                     e->d_st, e->d_in, e->o_key, e->o_start, e->o_end, e->d_win, e->d_bkey, e->d_brel, e->d_bn,
                     e->d_bval[0], e->d_bval[1], e->d_bcnt, e->d_rel2slot, e->d_reset_list, e->d_upos, e->d_zslice, e->d_rsum,
-                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4, e->d_rk, e->d_mf, e->d_dr, e->d_dr_cnt,
+                    e->d_rkid, e->d_kflag, e->d_sctr, e->d_tz, e->d_dropidx, e->d_send2, e->d_smax, e->d_scid, e->d_sc, e->d_sort_tmp, e->o_count, e->d_spk, e->d_spe, e->d_sg, e->d_prof, e->d_s4, e->d_rk, e->d_iota, e->d_rslots, e->d_mf, e->d_dr, e->d_dr_cnt,
                     e->d_khash, e->d_rs_hash};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int q = 0; q < 4; ++q) { if (e->d_skey[q]) (void)hipFree(e->d_skey[q]); if (e->d_sval[q]) (void)hipFree(e->d_sval[q]); }
@@ -2685,22 +2690,45 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
     c.naggs = cfg->num_aggs;
     c.nacc = 1;
     c.acc_kind[0] = ACC_ADD_I64;
-    for (int j = 0; j < cfg->num_aggs; ++j) {
-        AggDesc& d = c.agg[j];
-        d.kind = cfg->aggs[j].kind;
-        d.col = cfg->aggs[j].col;
-        d.acc_kind = acc_kind_of(d.kind);
-        d.alias = 0;
-        if (d.acc_kind == ACC_NONE) { d.acc = 0; continue; }
-        int share = -1;   // same accumulator kind over the same input column and input type: one column
-        for (int i = 0; i < j && share < 0; ++i)
-            if (c.agg[i].acc > 0 && !c.agg[i].alias && c.agg[i].acc_kind == d.acc_kind && c.agg[i].col == d.col &&
-                input_class(c.agg[i].kind) == input_class(d.kind))
-                share = i;
-        if (share >= 0) { d.acc = c.agg[share].acc; d.alias = 1; continue; }
-        d.acc = c.nacc;
-        c.acc_kind[c.nacc] = d.acc_kind;
-        c.nacc++;
+    // a reduce handle's payload fields get their columns after the accumulating ones (the combiner merges only those);
+    // a first- / last-element reduction (no MINBY / MAXBY) selects through an accumulator: SELQ = MIN (MAX) over the
+    // arrival sequence, a hidden aggregate over the engine's sequence column kIotaCol (reduce.inc), placed before them
+    bool red_iota = (cfg->flags & FWA_CFG_REDUCE) != 0;
+    for (int j = 0; j < cfg->num_aggs; ++j)
+        if (is_by_kind(cfg->aggs[j].kind) || cfg->aggs[j].col == kIotaCol) red_iota = false;
+    c.red_iota = red_iota;
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1 && red_iota) {
+            const bool last = (cfg->flags & FWA_CFG_BY_LAST) != 0;
+            AggDesc& h = c.agg[c.naggs++];
+            memset(&h, 0, sizeof(h));
+            h.kind = last ? FWA_MAX_I64 : FWA_MIN_I64;
+            h.col = kIotaCol;
+            h.acc_kind = last ? ACC_MAX_ORD : ACC_MIN_ORD;
+            h.acc = c.nacc;
+            c.acc_kind[c.nacc] = h.acc_kind;
+            c.red_selq = c.nacc++;
+        }
+        for (int j = 0; j < cfg->num_aggs; ++j) {
+            AggDesc& d = c.agg[j];
+            d.kind = cfg->aggs[j].kind;
+            d.col = cfg->aggs[j].col;
+            d.acc_kind = acc_kind_of(d.kind);
+            if ((d.acc_kind == ACC_PAYLOAD) != (pass == 1)) continue;
+            d.alias = 0;
+            d.acc = 0;
+            if (d.acc_kind == ACC_NONE) continue;
+            int share = -1;   // same accumulator kind over the same input column and input type: one column
+            for (int i = 0; i < cfg->num_aggs && share < 0; ++i)
+                if (i != j && c.agg[i].acc > 0 && !c.agg[i].alias && c.agg[i].acc_kind == d.acc_kind &&
+                    c.agg[i].col == d.col && input_class(c.agg[i].kind) == input_class(d.kind) &&
+                    ((pass == 0 && i < j) || (pass == 1 && c.agg[i].acc_kind == ACC_PAYLOAD && i < j)))
+                    share = i;
+            if (share >= 0) { d.acc = c.agg[share].acc; d.alias = 1; continue; }
+            d.acc = c.nacc;
+            c.acc_kind[c.nacc] = d.acc_kind;
+            c.nacc++;
+        }
     }
     // SQL NULLs: one hidden non-NULL counter per nullable input column (an ADD_I64 column fed 1 per
     // non-NULL value, AvgAggFunction's count / the null flag of Sum/Min/MaxAggFunction's buffer); COUNT(col)
@@ -2740,12 +2768,21 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
             }
         }
         c.red_last = (cfg->flags & FWA_CFG_BY_LAST) != 0;
-        c.red_selq = c.nacc;
-        c.acc_kind[c.nacc++] = c.red_last ? ACC_MAX_ORD : ACC_MIN_ORD;
+        if (!c.red_iota) {
+            c.red_selq = c.nacc;
+            c.acc_kind[c.nacc++] = c.red_last ? ACC_MAX_ORD : ACC_MIN_ORD;
+        }
         c.red_selk = c.nacc;
         c.acc_kind[c.nacc++] = ACC_PAYLOAD;
     }
     e->nacc = c.nacc;
+    c.nacc_comb = c.nacc;
+    if (e->red) {
+        c.nacc_comb = 1;
+        for (int j = 0; j < c.naggs; ++j)
+            if (c.agg[j].acc > 0 && c.agg[j].acc_kind != ACC_PAYLOAD) c.nacc_comb = std::max(c.nacc_comb, c.agg[j].acc + 1);
+    }
+    e->nacc_comb = c.nacc_comb;
     // key-table segmentation (all paths) and v2 eligibility: <= 2 distinct carried value columns,
     // an LDS window of >= 2 slices next to the SEG-key LDS segment, <= kMaxPart partitions
     {
@@ -2759,7 +2796,7 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         bool ok = true;
         for (int j = 0; j < c.naggs; ++j) {
             AggDesc& d = c.agg[j];
-            if (d.acc == 0) continue;
+            if (d.acc == 0 || d.acc_kind == ACC_PAYLOAD) continue;   // payload: written by the selection passes
             if (d.kind == FWA_COUNT_COL) { d.vslot = 0; continue; }   // counts rows: no value carried
             int slot = -1;
             for (int v = 0; v < nv; ++v) if (cols[v] == d.col) slot = v;
@@ -2777,7 +2814,7 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         // while the partition count stays <= kMaxPart
         auto lds_need = [&](int sg) {
             const int64_t sgz = (int64_t)1 << sg;
-            return sgz * 8 + 2 * sgz * 4 + (int64_t)(c.nacc - 1) * 2 * sgz * 8 + 4 * 4 * kSub + 16 +
+            return sgz * 8 + 2 * sgz * 4 + (int64_t)(c.nacc_comb - 1) * 2 * sgz * 8 + 4 * 4 * kSub + 16 +
                    (int64_t)sizeof(StragL) * kStragL + 256;   // + static LDS (straggler list, descriptors)
         };
         while (seg_log > 9 && lds_need(seg_log) > 160 * 1024 &&
@@ -2786,7 +2823,7 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         e->seg_log = seg_log;
         e->part_bits = cap_log - seg_log;
         const int64_t seg = (int64_t)1 << seg_log;
-        const int64_t bps = 4 + 8 * (int64_t)(c.nacc - 1);
+        const int64_t bps = 4 + 8 * (int64_t)(c.nacc_comb - 1);
         const int64_t avail = 160 * 1024 - 512 - (int64_t)sizeof(StragL) * kStragL - seg * 8;
         int sl = (int)std::min<int64_t>(8, avail > 0 ? avail / (bps * seg) : 0);
         if (lds_need(seg_log) > 160 * 1024) sl = 0;
@@ -2794,7 +2831,16 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         // record lists (sparse.inc): asked for, or a key space of >= 2^25 keys
         const bool want_sp = (cfg->flags & FWA_CFG_RECORD_LISTS) || kc0 >= ((int64_t)1 << 25);
         e->sparse = want_sp && sp_eligible(cfg);
-        ok = ok && np <= kMaxPart && sl >= 2 && e->kind != FWA_SESSION && !e->sparse && !e->red;
+        // reductions: two-phase accumulators when every reduced field is a BIGINT SUM / MIN / MAX / MINBY / MAXBY or a
+        // DOUBLE SUM over an 8-byte column (the combiner's carried-value arithmetic; other fields keep the v1 ingest)
+        bool red_ok = true;
+        for (int j = 0; e->red && j < c.naggs; ++j) {
+            const int k = c.agg[j].kind;
+            if (c.agg[j].acc_kind == ACC_PAYLOAD || c.agg[j].acc == 0) continue;
+            red_ok = red_ok && (k == FWA_SUM_I64 || k == FWA_SUM_F64 || k == FWA_MIN_I64 || k == FWA_MAX_I64 ||
+                                k == FWA_MINBY_I64 || k == FWA_MAXBY_I64);
+        }
+        ok = ok && np <= kMaxPart && sl >= 2 && e->kind != FWA_SESSION && !e->sparse && (!e->red || red_ok);
         e->v2 = ok;
         if (ok) {
             e->np = (int32_t)np;
@@ -2802,7 +2848,7 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
             e->nv = nv;
             for (int v = 0; v < 2; ++v) { e->vcol[v] = cols[v] < 0 ? 0 : cols[v]; e->vsize[v] = sizes[v]; }
             e->combine_lds = (size_t)seg * 8 + (((size_t)sl * seg * 4 + 15) & ~(size_t)15) +
-                             (size_t)(c.nacc - 1) * sl * seg * 8 + 16;
+                             (size_t)(c.nacc_comb - 1) * sl * seg * 8 + 16;
         }
     }
     if (hipSetDevice(cfg->device) != hipSuccess) { delete e; return FWA_E_DEVICE; }
@@ -3003,8 +3049,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     *ran = false;
     // combiner accumulator layout (compile-time in combine3) and the skew mode (PRE, partition3)
     int layout = 0;
-    if (e->nacc == 1) layout = 2;
-    else if (e->nacc == 2 && e->ec.acc_kind[1] == ACC_ADD_I64) {
+    if (e->nacc_comb == 1) layout = 2;
+    else if (e->nacc_comb == 2 && e->ec.acc_kind[1] == ACC_ADD_I64) {
         for (int j = 0; j < e->cfg.num_aggs; ++j)
             if (e->ec.agg[j].acc == 1 && e->ec.agg[j].vslot == 0) layout = 1;
     }
@@ -3175,7 +3221,7 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     ca.prof = pa.prof;
     HIPCHK(e, hipEventRecord(e->ev[6], e->stream));
     const size_t seg3 = (size_t)1 << e->seg_log;
-    const size_t lds3 = seg3 * 8 + 2 * seg3 * 4 + (size_t)(e->nacc - 1) * 2 * seg3 * 8 + 4 * 4 * kSub + 16;
+    const size_t lds3 = seg3 * 8 + 2 * seg3 * 4 + (size_t)(e->nacc_comb - 1) * 2 * seg3 * 8 + 4 * 4 * kSub + 16;
     // entries per lane and chunk: the largest counts whose kernels keep every value in registers at 1024 threads (a VGPR
     // spill is not harmless here, DESIGN.md section 4 "Skewed keys"; tests/test_abi.py checks the code object): 4, 3 with
     // two carried value columns, 6 for narrow entries, 2 with window passes. 512-thread blocks with twice the entries are
@@ -3681,10 +3727,8 @@ static int enqueue_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const 
     // writes the hidden counters: the generic path)
     bool single = e->nacc == 2 && !(raw && e->ec.naggs > e->ec.nout);
     for (const FireWindow& w : hw) single = single && w.nslots == 1;
-    if (e->red) {
-        f.blocks_per_win = (int32_t)((e->capacity + 1 + kBlock - 1) / kBlock);
-        red_fire_kernel<<<(unsigned)((int64_t)f.blocks_per_win * (int64_t)hw.size()), kBlock, 0, e->stream>>>(f, e->d_ec);
-    } else if (single) fire_kernel<1><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
+    if (e->red) red_fire_kernel<<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
+    else if (single) fire_kernel<1><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
     else fire_kernel<0><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
@@ -4132,9 +4176,20 @@ static int push_body(fwa_engine* e, const int64_t* keys, const int64_t* ts, cons
         if (late_dropped_out) *late_dropped_out = dropped;
         return FWA_OK;
     }
-    if (e->red) {                                 // DataStream reduction: v1 ingest, then the selection passes
+    if (e->red) {   // DataStream reduction: the accumulators (two-phase when eligible), then the selection passes
         const int64_t seq0 = e->red_seq_base + e->records_in;
-        int rc = push_common(e, a, n, false, false, late_dropped_out);
+        if (e->ec.red_iota) {   // the arrival sequence column the SELQ accumulator reads
+            if (n > e->iota_cap) {
+                if (e->d_iota) HIPCHK(e, hipFree(e->d_iota));
+                e->d_iota = nullptr;
+                HIPCHK(e, hipMalloc(&e->d_iota, 8 * (size_t)n));
+                e->iota_cap = n;
+            }
+            iota_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(e->d_iota, seq0, n);
+            HIPCHK(e, hipGetLastError());
+            a.cols[kIotaCol] = e->d_iota;
+        }
+        int rc = push_common(e, a, n, true, false, late_dropped_out);
         return rc ? rc : red_select(e, a, n, seq0);
     }
     return push_common(e, a, n, true, (flags & FWA_PUSH_ASYNC) != 0, late_dropped_out);
