@@ -244,7 +244,7 @@ def main():
     # HBM traffic per ingest launch (Phase P + Phase A) from the committed rocprofv3 PMC passes of this
     # same workload (counters need their own runs: tools/gpu_pmc.sh); null for other shapes
     traffic, traffic_src, traffic_bounds = None, None, None
-    for tag in ("r05", "r04", "r03", "r02"):
+    for tag in ("r06", "r05", "r04", "r03", "r02"):
         pmc_path = os.path.join(ROOT, "profiles", "%s_pmc_%s.json" % (tag, args.config))
         if world != 1 or not os.path.exists(pmc_path):
             continue

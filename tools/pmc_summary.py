@@ -55,7 +55,7 @@ def read(path):
 
 def main(root, tag, steps=3):
     out_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
-    for cfg in ("c2", "c3", "c4", "c5", "c5s"):
+    for cfg in ("c2", "c3", "c4", "c5", "c5s", "reduce"):
         fe = read(os.path.join(root, "%s_FETCH_SIZE" % cfg))
         wr = read(os.path.join(root, "%s_WRITE_SIZE" % cfg))
         if not fe or not wr:
