@@ -157,7 +157,10 @@ enum fwa_agg_kind {
  * and counts them in fwa_stats.dec_inexact (the other rows of that watermark are unaffected). Internally each DECIMAL source column is summed as 2 (int64 input)
  * or 4 (16-byte) 32-bit pieces, each one of the handle's FWA_MAX_AGGS aggregates, plus a count; a list past that
  * budget is FWA_E_UNSUPPORTED at fwa_create. Not available for fwa_drain_partials / fwa_push_partials
- * (FWA_E_UNSUPPORTED); fwa_snapshot_heap writes the exact total as the DECIMAL(38, s) buffer. */
+ * (FWA_E_UNSUPPORTED); fwa_snapshot_heap writes the exact total as the DECIMAL(38, s) buffer, a NULL buffer when it
+ * has more than 38 digits, and fwa_restore_heap reads a NULL buffer back as a zero sum with the window's counts kept:
+ * after a restore of such a window its SUM restarts from the later values (the reference's SUM behaviour) and so does
+ * its AVG, where the reference's AVG would stay NULL (parity across a restore of an overflowed window is unpinned). */
 /* SQL NULL semantics (fwa_config.nullable_cols, Table semantics): SUM/MIN/MAX/AVG skip NULL inputs and are
  * NULL when a window holds no non-NULL input (SumAggFunction.java:54-110, MaxAggFunction.java:63-73,
  * MinAggFunction.java:63-, AvgAggFunction.java:65-106: AVG = sum / count of non-NULL inputs); COUNT(*) counts
