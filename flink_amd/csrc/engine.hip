@@ -5368,13 +5368,13 @@ int fwa_advance_watermark_async(fwa_engine* e, int64_t wm) {
             hs.push_back(kv.second);
             hw.push_back(f);
         }
-        // every row of the fire must fit: windows x keys (keys known at the last status + the pending push's). When
-        // the output columns would have to grow (hipFree synchronises the device, e.g. the final watermark firing
-        // several windows at once) the synchronous path counts the rows and sizes them instead.
+        // every row of the fire must fit: windows x keys (keys known at the last status + the pending push's). The
+        // end-of-input watermark (Long.MAX_VALUE) lists every live slice, the lookahead's included, and would grow the
+        // output columns far past the rows it fires (hipFree synchronises the device): the synchronous path counts
+        // its rows and sizes them instead.
         const int64_t nk = std::min<int64_t>(e->capacity + 1, (int64_t)e->h_st->n_keys + e->pend_n);
         const int64_t need = (int64_t)hw.size() * std::max<int64_t>(nk, 1);
-        const int64_t floor_rows = e->opt_out_min > 0 ? e->opt_out_min : ((int64_t)1 << 22);
-        if (!hw.empty() && (need <= e->out_cap || e->out_cap < floor_rows)) {
+        if (!hw.empty() && (need <= e->out_cap || wm != LONG_MAX_J)) {
             int rc = ensure_out(e, need);
             if (rc) return rc;
             if ((rc = upload_windows(e, hw, hs))) return rc;

@@ -1342,7 +1342,8 @@ static void* digest2_worker(void* vp) {
             wm = max_ts - a->p->max_delay_ms - 1;                   /* BoundedOutOfOrdernessWatermarks :57-69 */
         }
         if (a->rc) continue;                                     /* (keep meeting the barriers) */
-        const void* cols[2] = {a->fp ? (const void*)mf : (const void*)mi, (const void*)md};
+        /* integer streams: column 1 is the timestamp (bench.py --config reduce keeps it as the tuple's f2) */
+        const void* cols[2] = {a->fp ? (const void*)mf : (const void*)mi, a->fp ? (const void*)md : (const void*)mt};
         if ((a->rc = or_push(e, mk, mt, cols, NULL, m, NULL)) != 0) continue;
         if ((a->rc = or_advance_watermark(e, wm, &o)) != 0) continue;
         uint64_t d = 0;

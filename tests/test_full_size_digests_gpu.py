@@ -134,6 +134,10 @@ BENCHED = {
                exact=(0, 3, 4), sums=(1, 2)),
     "c5s": dict(win=dict(window_kind="SESSION", semantics="DATASTREAM", gap_ms=5_000), aggs=FL, zipf=False, fp=True,
                 exact=(0, 3, 4), sums=(1, 2)),
+    # bench.py --config reduce: WindowedStream.sum(1) over Tuple3<key, val, ts> -- the summed field and the first
+    # element's ts (the two-phase ingest, the arrival-sequence selection and its payload pass)
+    "reduce": dict(win=dict(window_kind="TUMBLE", semantics="DATASTREAM", size_ms=10_000),
+                   aggs=[("SUM_I64", 0), ("FIRST_64", 1)], reduce=True, zipf=False, fp=False, exact=(0, 1), sums=()),
 }
 NBK = 4096
 
@@ -151,7 +155,7 @@ def _digest_run2(name, nbatches, nkeys=1_000_000):
     if c["zipf"]:
         w = 1.0 / np.arange(1, nkeys + 1, dtype=np.float64) ** 1.1
         cdf = np.cumsum(w) / w.sum()
-    ocfg = A.make_config(aggs=c["aggs"], **c["win"])
+    ocfg = A.make_config(aggs=c["aggs"], reduce=c.get("reduce", False), **c["win"])
     res = {}
 
     def oracle_leg():
@@ -177,10 +181,11 @@ def _digest_run2(name, nbatches, nkeys=1_000_000):
         else:
             v = torch.empty_like(k)
             E.generate(p, n, k, t, v)
-            cols = lambda b: [v[b * B:(b + 1) * B]]  # noqa: E731
+            cols = lambda b: [v[b * B:(b + 1) * B]] + ([t[b * B:(b + 1) * B]] if c.get("reduce") else [])  # noqa: E731
         torch.cuda.synchronize()
         bmax = t.view(nbatches, B).max(dim=1).values.cpu().numpy()
-        cfg = A.make_config(aggs=c["aggs"], key_capacity=nkeys, output_on_device=1, **c["win"])
+        cfg = A.make_config(aggs=c["aggs"], key_capacity=nkeys, output_on_device=1, reduce=c.get("reduce", False),
+                            **c["win"])
         g = E.WindowAggregator(cfg)
         word = {0: lambda x: x, 1: lambda x: x, 3: f32_word, 4: f64_word}
         m = -2**63
@@ -240,3 +245,10 @@ def test_c5s_full_size_rows_vs_oracle():
     """C5 with DataStream session windows (gap 5 s) as benched, 8 pushes: the session path's rows at every watermark."""
     rows, st, modes = _digest_run2("c5s", 8)
     assert rows > 500_000
+
+
+def test_reduce_full_size_rows_vs_oracle():
+    """The reduce bench line's workload, 8 pushes: per watermark every (key, window) row's summed field and first
+    element's ts equal the oracle's arrival-order fold (ReducingState per window, WindowOperator.java:288-389)."""
+    rows, st, _ = _digest_run2("reduce", 8)
+    assert rows > 40_000_000
