@@ -282,6 +282,7 @@ def main():
         workload = ("C2: event-time tumbling %ds COUNT+SUM(long), %d uniform keys, %d records/GPU "
                     "(%d batches of %d), D=%dms" % (args.window_ms // 1000, args.keys, args.steps * B,
                                                     args.steps, B, args.delay_ms))
+    xname = "RCCL" if backend == "nccl" else backend + " (rehearsal: blocks staged through the host)"
     out = {
         "metric": metric,
         "value": value,
@@ -299,9 +300,9 @@ def main():
             "workload": workload,
             "records_per_gpu_timed": args.steps * B, "keys": args.keys, "batch": B,
             "window_ms": args.window_ms, "parallelism": "key-group dp%d" % world,
-            "exchange": ("two-phase partials (local pre-aggregation, fwa_drain_route per-subtask blocks, RCCL "
-                         "all_to_all, owner fwa_fire_partials)" if args.exchange == "partials"
-                         else "raw records (RCCL all_to_all)") if world > 1 else "none",
+            "exchange": ("two-phase partials (local pre-aggregation, fwa_drain_route per-subtask blocks, %s "
+                         "all_to_all, owner fwa_fire_partials)" % xname if args.exchange == "partials"
+                         else "raw records (%s all_to_all)" % xname) if world > 1 else "none",
         },
         "roofline": {
             "bound": "hbm", "kernel": ingest_kernels(args, eng),
