@@ -2817,7 +2817,9 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
             return sgz * 8 + 2 * sgz * 4 + (int64_t)(c.nacc_comb - 1) * 2 * sgz * 8 + 4 * 4 * kSub + 16 +
                    (int64_t)sizeof(StragL) * kStragL + 256;   // + static LDS (straggler list, descriptors)
         };
-        while (seg_log > 9 && lds_need(seg_log) > 160 * 1024 &&
+        // (session handles never run the combiner: their segments stay at 4096 keys, which the s5 route of the cell
+        // pre-aggregation resolves in LDS -- sessions4.inc)
+        while (e->kind != FWA_SESSION && seg_log > 9 && lds_need(seg_log) > 160 * 1024 &&
                ((int64_t)1 << (cap_log - seg_log + 1)) <= kMaxPart)
             --seg_log;
         e->seg_log = seg_log;
