@@ -2789,7 +2789,8 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         const int64_t kc0 = cfg->key_capacity > 0 ? cfg->key_capacity : (1 << 20);
         int cap_log = 10;
         while (((int64_t)1 << cap_log) < 2 * kc0) ++cap_log;
-        int seg_log = std::max(6, std::min(12, cap_log));
+        // (session handles: 8192-key segments, half the partitions for the s5 route -- sessions4.inc)
+        int seg_log = std::max(6, std::min(e->kind == FWA_SESSION ? 13 : 12, cap_log));
         e->seg_log = seg_log;
         e->part_bits = cap_log - seg_log;
         int cols[2] = {-1, -1}, sizes[2] = {8, 8}, nv = 0;
