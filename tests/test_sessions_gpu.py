@@ -208,11 +208,14 @@ def test_cell_path_redo_on_order_sensitive_records(eng_mod):
 
 
 # ---- cell pre-aggregation (sessions4.inc: <= 16 cells per push, <= 8 in-flight sessions per key) ------------------
-def _run_paths(eng_mod, cfg, batches):
-    """_run, recording the path each push took (FWA_OPT_SESSION_PATH: 0 general, 1 sort-based cells, 2 pre-agg)."""
+def _run_paths(eng_mod, cfg, batches, variant=0):
+    """_run, recording the path each push took (FWA_OPT_SESSION_PATH: 0 general, 1 sort-based cells, 2 pre-agg).
+    variant 8: the pre-aggregation path's s4 probe route instead of the s5 hash route (FWA_OPT_INGEST_VARIANT)."""
     from oracle.oracle import Oracle
     names = A.agg_names(cfg)
     g, o = eng_mod.WindowAggregator(cfg), Oracle(cfg)
+    if variant:
+        g.set_option("ingest_variant", variant)
     paths, dg, do = [], 0, 0
     for k, t, cols, wm in batches:
         dg += g.push(k, t, cols)
@@ -227,15 +230,28 @@ def _run_paths(eng_mod, cfg, batches):
     return paths, st
 
 
+@pytest.mark.parametrize("route", [0, 8], ids=["s5_hash_route", "s4_probe_route"])
 @pytest.mark.parametrize("sem", ["DATASTREAM", "TABLE"])
 @pytest.mark.parametrize("nacc", [1, 2, 3, 4, 5])
-def test_cell_preagg_vs_oracle(eng_mod, nacc, sem):
+def test_cell_preagg_vs_oracle(eng_mod, nacc, sem, route):
     """Pushes of 50 s of event time with a 5 s gap (about 11 cells): every push on the pre-aggregation path, sessions
-    kept in flight across pushes, closed and fired between them."""
+    kept in flight across pushes, closed and fired between them; both routes of the path."""
     keys, ts, vi, vd = _stream(200 + nacc, 200_000, 3000, 600_000, 300, 0.0)
     cfg = A.make_config(window_kind="SESSION", semantics=sem, gap_ms=5000, aggs=CELL_AGGS[nacc], key_capacity=8192)
-    paths, st = _run_paths(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 12, 300))
+    paths, st = _run_paths(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 12, 300), variant=route)
     assert paths == [2] * 12
+    assert st.replay_records == 0
+
+
+@pytest.mark.parametrize("route", [0, 8], ids=["s5_hash_route", "s4_probe_route"])
+def test_cell_preagg_many_partitions_vs_oracle(eng_mod, route):
+    """A key table of 2^18 slots (32 partitions of 8192 keys; the s5 route resolves each in its own workgroup), 60K keys
+    with the sentinel key among them, 8 pushes; the key table the route built serves the later pushes' probes."""
+    keys, ts, vi, vd = _stream(77, 400_000, 60_000, 400_000, 300, 0.0)
+    keys[::997] = -2**63
+    cfg = A.make_config(window_kind="SESSION", gap_ms=5000, aggs=AGGS, key_capacity=1 << 17)
+    paths, st = _run_paths(eng_mod, cfg, _batches(keys, ts, [vi, vi, vd], 8, 300), variant=route)
+    assert paths == [2] * 8
     assert st.replay_records == 0
 
 
