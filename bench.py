@@ -354,12 +354,13 @@ def main():
 def ingest_kernels(args, eng):
     """Names of the kernels whose device time `roofline.achieved` divides by (HIP events around them)."""
     if args.config == "c5s":
-        return ("s4_route+s4_hist+s4_colscan+scan+s4_part<1>+s4_hist2+s4_part<2>+s4_sess_count/scatter+s4_group "
-                "(cell pre-aggregation; sess3_* sort-based cells or sess2_* when a push leaves its range)")
+        return ("s5_hist+s5_colscan+scan+s5_part+s5_resolve+s4_sess_count/scatter+s4_group+s4_compact (cell "
+                "pre-aggregation, hash route; sess3_* sort-based cells or sess2_* when a push leaves its range)")
     if eng.record_lists:
         return "sp_range_kernel+sp_hist_kernel+sp_scan_kernel+sp_scatter_kernel (record lists)"
     if args.config == "reduce":
-        return "ingest_kernel+red_index_kernel+red_pick_kernel+red_payload_kernel (v1 atomics + selection passes)"
+        return ("iota_kernel+partition3_kernel+combine3_kernel+red_iota_payload_kernel (two-phase ingest with the "
+                "arrival-sequence accumulator, then the payload pass)")
     return "partition3_kernel+combine3_kernel" if eng.stats().partition_ms > 0 else "ingest_kernel"
 
 

@@ -4188,11 +4188,18 @@ static int push_body(fwa_engine* e, const int64_t* keys, const int64_t* ts, cons
                 HIPCHK(e, hipMalloc(&e->d_iota, 8 * (size_t)n));
                 e->iota_cap = n;
             }
+            HIPCHK(e, hipEventRecord(e->ev[8], e->stream));      // (ev[8] / ev[9]: record lists only otherwise)
             iota_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(e->d_iota, seq0, n);
             HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipEventRecord(e->ev[9], e->stream));
             a.cols[kIotaCol] = e->d_iota;
         }
         int rc = push_common(e, a, n, true, false, late_dropped_out);
+        if (!rc && e->ec.red_iota) {                               // the sequence column counts as ingest time
+            float ms = 0.f;
+            HIPCHK(e, hipEventElapsedTime(&ms, e->ev[8], e->ev[9]));
+            e->ingest_ms += ms;
+        }
         return rc ? rc : red_select(e, a, n, seq0);
     }
     return push_common(e, a, n, true, (flags & FWA_PUSH_ASYNC) != 0, late_dropped_out);

@@ -13,7 +13,8 @@ Families (regexes over the kernel name):
   ingest (C2/C3/C5): partition3_kernel / partition2_kernel + combine3_kernel (one of each per push),
                     ingest_kernel replays are listed separately;
   push (C4 record lists): sp_range + sp_hist + sp_scan + sp_scatter;  fire: sp_refine + sp_agg;
-  sessions (C5s): s4_* (cell pre-aggregation) or sess3_* / sess2_* + hipcub radix sort / scan.
+  sessions (C5s): s5_* / s4_* (cell pre-aggregation) or sess3_* / sess2_* + hipcub radix sort / scan;
+  reduce: the ingest family plus iota_kernel and red_iota_payload_kernel.
 frac = algorithmic bytes per launch (bench line `roofline.alg_bytes_per_launch`) / average launch time / peak.
 """
 import argparse
@@ -24,16 +25,16 @@ import statistics
 import sys
 
 FAMILIES = {
-    "ingest": re.compile(r"partition[23]_kernel|combine3_kernel"),
+    "ingest": re.compile(r"partition[23]_kernel|combine3_kernel|iota_kernel|red_iota_payload_kernel"),
     "replay": re.compile(r"\bingest_kernel"),
     "push_rl": re.compile(r"sp_(range|hist|scan|scatter)_kernel"),
     "fire_rl": re.compile(r"sp_(refine|agg)_kernel"),
     "fire": re.compile(r"fire_kernel|fire_slide_kernel|sess2_fire_kernel"),
-    "sessions": re.compile(r"sess2_(?!fire)|sess3_|s4_|DeviceRadixSort|DeviceScan|radix|onesweep|lookback", re.I),
+    "sessions": re.compile(r"sess2_(?!fire)|sess3_|s4_|s5_|DeviceRadixSort|DeviceScan|radix|onesweep|lookback", re.I),
 }
 # the first kernel of every step of each config: counts steps in dispatch order
 STEP_MARK = {"ingest": re.compile(r"partition[23]_kernel"), "push_rl": re.compile(r"sp_hist_kernel"),
-             "sessions": re.compile(r"s4_route_kernel|sess3_min_kernel|sess2_classify_kernel")}
+             "sessions": re.compile(r"s5_hist_kernel|s4_route_kernel|sess3_min_kernel|sess2_classify_kernel")}
 
 
 def load(path):
@@ -59,7 +60,7 @@ def main():
     peak = rl["peak"]
     rows = load(args.trace)
     kern = rl.get("kernel", "")
-    fam = "sessions" if ("sess" in kern or "s4_" in kern) else ("push_rl" if "sp_range" in kern else "ingest")
+    fam = "sessions" if ("sess" in kern or "s4_" in kern or "s5_" in kern) else ("push_rl" if "sp_range" in kern else "ingest")
     mark = STEP_MARK[fam]
     firsts = [r for r in rows if mark.search(r["Kernel_Name"])]
     if len(firsts) < W + K:
