@@ -62,6 +62,8 @@ def main():
                     help="N=1: wait for each watermark's rows before the next batch is handed over "
                          "(fwa_advance_watermark); default: fwa_advance_watermark_async, the rows taken after the next "
                          "batch was handed over, so the next push's host work overlaps the fire (warm-up the same way)")
+    ap.add_argument("--reduce-op", choices=["sum", "max_by"], default="sum",
+                    help="--config reduce: WindowedStream.sum(1) (default) or maxBy(1) (the by-value selection passes)")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="fwa_set_option on the measured engine(s) (flink_amd.engine.OPTIONS), e.g. profile=1")
     ap.add_argument("--exchange", choices=["auto", "partials", "raw"], default="auto",
@@ -135,6 +137,8 @@ def main():
     aggs = [("COUNT", 0), ("SUM_I64", 0)]
     if args.config == "reduce":   # FWA_CFG_REDUCE: field 1 summed, field 2 the window's first element's
         aggs = [("SUM_I64", 0), ("FIRST_64", 1)]
+        if args.reduce_op == "max_by":   # maxBy(1): the element with the largest f1 (ties: the first), f2 its own
+            aggs = [("MAXBY_I64", 0), ("SEL_64", 1)]
     if fp:   # C5: column 0 = f (FLOAT), column 1 = d (DOUBLE)
         aggs = [("COUNT", 0), ("SUM_F64", 1), ("AVG_F64", 1), ("MAX_F32", 0), ("MAX_F64", 1)]
         win_kw = dict(window_kind="TUMBLE", semantics="TABLE", size_ms=args.window_ms)
@@ -267,10 +271,11 @@ def main():
                     "(%d batches of %d), D=%dms" % (args.window_ms // 1000, args.keys, args.steps * B,
                                                     args.steps, B, args.delay_ms))
     elif args.config == "reduce":
-        metric = "records/sec aggregated (DataStream reduce: WindowedStream.sum(1), 1M-key tumbling)"
-        workload = ("reduce: event-time tumbling %ds WindowedStream.sum(1) over Tuple3<Long,Long,Long> (f0 key, f1 "
-                    "summed, f2 = ts kept from the first element), %d uniform keys, %d records/GPU (%d batches of %d), "
-                    "D=%dms" % (args.window_ms // 1000, args.keys, args.steps * B, args.steps, B, args.delay_ms))
+        op = "sum(1)" if args.reduce_op == "sum" else "maxBy(1)"
+        metric = "records/sec aggregated (DataStream reduce: WindowedStream.%s, 1M-key tumbling)" % op
+        workload = ("reduce: event-time tumbling %ds WindowedStream.%s over Tuple3<Long,Long,Long> (f0 key, f1 "
+                    "reduced, f2 = ts of the selected element), %d uniform keys, %d records/GPU (%d batches of %d), "
+                    "D=%dms" % (args.window_ms // 1000, op, args.keys, args.steps * B, args.steps, B, args.delay_ms))
     elif fp:
         kind = "Table TUMBLE %ds TVF" % (args.window_ms // 1000) if args.config == "c5" else "DataStream SESSION gap 5s"
         metric = "records/sec aggregated (C5: %s, COUNT/SUM/AVG(double)/MAX(float,double))" % kind
