@@ -162,6 +162,69 @@ __device__ __forceinline__ void emit_row(const FireArgs& f, const EngineConst& c
         }
 }
 
+// TUMBLE fire of a handle with 3..5 accumulator columns (COUNT included; every window one slot, not raw): every column
+// of the block's kids is loaded before the first row store -- the generic emit_row reloads each column behind the
+// previous row's stores (a possible alias), which held C5's fire (five aggregates over four columns) near 1.5 TB/s.
+// One block = one window x kBlock * 4 kids; one row reservation per block as fire_kernel.
+template <int NA>
+__global__ void __launch_bounds__(kBlock) fire_multi_kernel(FireArgs f, const EngineConst* __restrict__ cp) {
+    constexpr int J = 4;
+    const EngineConst& c = *cp;
+    const int32_t w = blockIdx.x / f.blocks_per_win;
+    const int64_t k0 = (int64_t)(blockIdx.x % f.blocks_per_win) * kBlock * J;
+    const FireWindow win = f.win[w];
+    const int64_t nk = f.capacity + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int kWaves = kBlock / 64;
+    __shared__ uint32_t woff[J][kWaves];
+    __shared__ unsigned long long s_base;
+    const unsigned long long* slot = f.slot_base[f.win_slots[win.slot_off]];
+    unsigned long long kvs[J], x[J][NA], masks[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {                       // clamped index: unconditional loads
+        const int64_t k = min(k0 + (int64_t)j * kBlock + tid, nk - 1);
+        kvs[j] = f.key_table[k];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) x[j][a] = slot[(int64_t)a * f.stride + k];
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int64_t k = k0 + (int64_t)j * kBlock + tid;
+        const bool present = k < nk && ((k < f.capacity) ? (kvs[j] != kEmptyKey) : (kvs[j] == 1ull));
+        masks[j] = __ballot(present && x[j][0] != 0);
+        if (lane == 0) woff[j][wid] = (uint32_t)__popcll(masks[j]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int j = 0; j < J; ++j)
+            for (int v = 0; v < kWaves; ++v) { const uint32_t t = woff[j][v]; woff[j][v] = run; run += t; }
+        s_base = run ? atomicAdd(&f.st->rows, (unsigned long long)run) : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        if (!((masks[j] >> lane) & 1ull)) continue;
+        const int64_t k = k0 + (int64_t)j * kBlock + tid;
+        const int64_t row = (int64_t)s_base + woff[j][wid] + __popcll(masks[j] & lt);
+        if (row >= f.out_cap) continue;
+        f.o_key[row] = (k < f.capacity) ? (int64_t)kvs[j] : LONG_MIN_J;
+        f.o_start[row] = win.start;
+        f.o_end[row] = win.end;
+        for (int a = 0; a < c.nout; ++a) {
+            const AggDesc d = c.agg[a];
+            unsigned long long xv = ident_of(d.acc_kind), nn = 0;
+#pragma unroll
+            for (int q = 1; q < NA; ++q) {                 // register selects, no dynamic index
+                if (q == d.acc) xv = x[j][q];
+                if (q == d.nn) nn = x[j][q];
+            }
+            write_agg(d, x[j][0], xv, nn, f.o_agg[a], f.o_null[a], row);
+        }
+    }
+}
+
 // One block = one window x one chunk of kBlock*kFireJ consecutive kids. Pass 1 sums COUNT over the
 // window's slices and ballots the emitting keys; one atomic reserves the block's rows; pass 2 writes
 // rows j-major so every wave store is contiguous.
@@ -3730,8 +3793,16 @@ static int enqueue_fire(fwa_engine* e, const std::vector<FireWindow>& hw, const 
     // writes the hidden counters: the generic path)
     bool single = e->nacc == 2 && !(raw && e->ec.naggs > e->ec.nout);
     for (const FireWindow& w : hw) single = single && w.nslots == 1;
+    const bool multi = !raw && e->nacc >= 3 && e->nacc <= 5 && !(e->opt_variant & 32) &&   // variant bit 5: A/B
+                       std::all_of(hw.begin(), hw.end(), [](const FireWindow& w) { return w.nslots == 1; });
     if (e->red) red_fire_kernel<<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
-    else if (single) fire_kernel<1><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
+    else if (multi) {
+        f.blocks_per_win = (int32_t)((e->capacity + 1 + (int64_t)kBlock * 4 - 1) / ((int64_t)kBlock * 4));
+        const unsigned g2 = (unsigned)((int64_t)f.blocks_per_win * (int64_t)hw.size());
+        if (e->nacc == 3) fire_multi_kernel<3><<<g2, kBlock, 0, e->stream>>>(f, e->d_ec);
+        else if (e->nacc == 4) fire_multi_kernel<4><<<g2, kBlock, 0, e->stream>>>(f, e->d_ec);
+        else fire_multi_kernel<5><<<g2, kBlock, 0, e->stream>>>(f, e->d_ec);
+    } else if (single) fire_kernel<1><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
     else fire_kernel<0><<<(unsigned)grid, kBlock, 0, e->stream>>>(f, e->d_ec);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->ev[3], e->stream));
