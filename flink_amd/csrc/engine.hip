@@ -2837,6 +2837,10 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         }
         c.red_selk = c.nacc;
         c.acc_kind[c.nacc++] = ACC_PAYLOAD;
+        if (c.red_by >= 0) {   // scratch: identity between pushes (red_by_payload_kernel restores it)
+            c.red_scr = c.nacc;
+            c.acc_kind[c.nacc++] = c.red_last ? ACC_MAX_ORD : ACC_MIN_ORD;
+        }
     }
     e->nacc = c.nacc;
     c.nacc_comb = c.nacc;
