@@ -29,7 +29,7 @@ FAMILIES = {
     "replay": re.compile(r"\bingest_kernel"),
     "push_rl": re.compile(r"sp_(range|hist|scan|scatter)_kernel"),
     "fire_rl": re.compile(r"sp_(refine|agg)_kernel"),
-    "fire": re.compile(r"fire_kernel|fire_slide_kernel|sess2_fire_kernel"),
+    "fire": re.compile(r"fire_kernel|fire_multi_kernel|fire_slide_kernel|sess2_fire_kernel"),
     "sessions": re.compile(r"sess2_(?!fire)|sess3_|s4_|s5_|DeviceRadixSort|DeviceScan|radix|onesweep|lookback", re.I),
 }
 # the first kernel of every step of each config: counts steps in dispatch order
