@@ -116,6 +116,15 @@ __device__ __forceinline__ void write_agg(const AggDesc& d, uint64_t cnt, unsign
         case FWA_MIN_F64: case FWA_MAX_F64:
             ((double*)out)[row] = __longlong_as_double((long long)jm::unord_bits64(x));
             break;
+        // the reduced field of a session reduction (FWA_CFG_REDUCE over session windows; reduce.inc red_write otherwise)
+        case FWA_SUM_I32: ((uint32_t*)out)[row] = (uint32_t)x; break;
+        case FWA_MIN_I32: case FWA_MAX_I32: case FWA_MINBY_I32: case FWA_MAXBY_I32:
+            ((int32_t*)out)[row] = (int32_t)jm::unord_i64(x); break;
+        case FWA_MINBY_I64: case FWA_MAXBY_I64: ((int64_t*)out)[row] = jm::unord_i64(x); break;
+        case FWA_MINBY_F32: case FWA_MAXBY_F32:
+            ((float*)out)[row] = (float)__longlong_as_double((long long)jm::unord_bits64(x)); break;
+        case FWA_MINBY_F64: case FWA_MAXBY_F64:
+            ((double*)out)[row] = __longlong_as_double((long long)jm::unord_bits64(x)); break;
         default: break;
     }
 }
@@ -2270,8 +2279,12 @@ int validate(const fwa_config* c) {
         if ((c->flags & FWA_CFG_BY_LAST) && !(c->flags & FWA_CFG_REDUCE)) return FWA_E_ARG;
         if (c->flags & FWA_CFG_REDUCE) {
             if (nby > 1 || (nsel && !nby) || (nfirst && nby)) return FWA_E_ARG;
-            if (nother || c->semantics != FWA_SEM_DATASTREAM || (c->window_kind != FWA_TUMBLE && c->window_kind != FWA_SLIDE) ||
-                (c->flags & (FWA_CFG_RECORD_LISTS | FWA_CFG_DYNAMIC_GAP)))
+            // session windows: only a tuple whose one value field is the reduced one (Tuple2<key, f1>): merging
+            // sessions then cannot pick another element's fields, which the reference leaves to HashSet order (§2)
+            const bool sess_ok = c->window_kind == FWA_SESSION && c->num_aggs == 1 && !nsel && !nfirst;
+            if (nother || c->semantics != FWA_SEM_DATASTREAM ||
+                (c->window_kind != FWA_TUMBLE && c->window_kind != FWA_SLIDE && !sess_ok) ||
+                (c->flags & FWA_CFG_RECORD_LISTS) || ((c->flags & FWA_CFG_DYNAMIC_GAP) && !sess_ok))
                 return FWA_E_UNSUPPORTED;
         }
     }
@@ -2756,7 +2769,7 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
     // a reduce handle's payload fields get their columns after the accumulating ones (the combiner merges only those);
     // a first- / last-element reduction (no MINBY / MAXBY) selects through an accumulator: SELQ = MIN (MAX) over the
     // arrival sequence, a hidden aggregate over the engine's sequence column kIotaCol (reduce.inc), placed before them
-    bool red_iota = (cfg->flags & FWA_CFG_REDUCE) != 0;
+    bool red_iota = (cfg->flags & FWA_CFG_REDUCE) != 0 && cfg->window_kind != FWA_SESSION;
     for (int j = 0; j < cfg->num_aggs; ++j)
         if (is_by_kind(cfg->aggs[j].kind) || cfg->aggs[j].col == kIotaCol) red_iota = false;
     c.red_iota = red_iota;
@@ -2831,15 +2844,17 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
             }
         }
         c.red_last = (cfg->flags & FWA_CFG_BY_LAST) != 0;
-        if (!c.red_iota) {
-            c.red_selq = c.nacc;
-            c.acc_kind[c.nacc++] = c.red_last ? ACC_MAX_ORD : ACC_MIN_ORD;
-        }
-        c.red_selk = c.nacc;
-        c.acc_kind[c.nacc++] = ACC_PAYLOAD;
-        if (c.red_by >= 0) {   // scratch: identity between pushes (red_by_payload_kernel restores it)
-            c.red_scr = c.nacc;
-            c.acc_kind[c.nacc++] = c.red_last ? ACC_MAX_ORD : ACC_MIN_ORD;
+        if (cfg->window_kind != FWA_SESSION) {   // (a session reduction's one field is its only column: no selection)
+            if (!c.red_iota) {
+                c.red_selq = c.nacc;
+                c.acc_kind[c.nacc++] = c.red_last ? ACC_MAX_ORD : ACC_MIN_ORD;
+            }
+            c.red_selk = c.nacc;
+            c.acc_kind[c.nacc++] = ACC_PAYLOAD;
+            if (c.red_by >= 0) {   // scratch: identity between pushes (red_by_payload_kernel restores it)
+                c.red_scr = c.nacc;
+                c.acc_kind[c.nacc++] = c.red_last ? ACC_MAX_ORD : ACC_MIN_ORD;
+            }
         }
     }
     e->nacc = c.nacc;

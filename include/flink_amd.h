@@ -126,8 +126,10 @@ enum fwa_agg_kind {
  * Comparisons are Java compareTo (Long / Integer / Double.compare / Float.compare: -0.0 < 0.0, NaN above +Inf; a MIN
  * or MAX result NaN is returned canonical). SUM over Float is accumulated in double and rounded once (the reference
  * adds in float, in arrival order), over Double in device order (within the tolerance of SUM_F64).
- * A reduce handle is DATASTREAM, TUMBLE or SLIDE (non-merging windows: MergingWindowSet merges state namespaces in
- * java.util.HashSet order, which leaves the other fields of a merged session to hash order), with any allowed lateness
+ * A reduce handle is DATASTREAM, TUMBLE or SLIDE, or SESSION over a Tuple2<key, f1> (exactly one aggregate, SUM / MIN /
+ * MAX / MINBY / MAXBY of f1: MergingWindowSet merges state namespaces in java.util.HashSet order, which leaves any
+ * other field of a merged session, and the by-tie among them, to hash order; the reduced field itself is
+ * order-free, float sums aside), with any allowed lateness
  * (late firings emit the reduced element after each late element, in arrival order); every aggregate is a field
  * of the reduced tuple: at most one MINBY / MAXBY, FWA_SEL_* only with it and FWA_FIRST_* only without it, SUM / MIN /
  * MAX over any type; COUNT, AVG, DECIMAL, NULLs, record lists, partials and the heap layout are FWA_E_UNSUPPORTED.

@@ -542,8 +542,42 @@ static void acc_add(or_engine* e, aval* a, const void* const* cols, int64_t i) {
 }
 
 /* merge accumulator b into a (AggregateFunction.merge / SQL mergeExpressions) */
+/* HeapReducingState.mergeState(a, b) = reduce(a, b) (AbstractHeapMergingState.mergeNamespaces :65-90): the merged
+   session keeps value1's fields and folds field pos -- the only value field of a session reduction (the engine's
+   scope), so the merge order MergingWindowSet's HashSet gives does not matter except for float sums' rounding */
+static void red_merge(or_engine* e, aval* a, const aval* b) {
+    const int64_t before = a[0].i;
+    a[0].i = jladd(a[0].i, b[0].i);
+    for (int j = 0; j < e->c.num_aggs; j++) {
+        const int k = e->c.aggs[j].kind;
+        aval* x = &a[1 + j]; const aval* y = &b[1 + j];
+        if (before == 0) { *x = *y; continue; }
+        switch (k) {
+        case FWA_SUM_I64: x->i = jladd(x->i, y->i); break;
+        case FWA_SUM_I32: x->i = (int32_t)((uint32_t)x->i + (uint32_t)y->i); break;
+        case FWA_SUM_F64: x->d += y->d; break;
+        case FWA_SUM_F32: x->f = x->f + y->f; break;
+        default: {                                       /* MIN / MAX / MINBY / MAXBY of field pos */
+            int c;
+            switch (k) {
+            case FWA_MIN_I64: case FWA_MAX_I64: case FWA_MINBY_I64: case FWA_MAXBY_I64:
+                c = x->i < y->i ? -1 : (x->i > y->i ? 1 : 0); break;
+            case FWA_MIN_I32: case FWA_MAX_I32: case FWA_MINBY_I32: case FWA_MAXBY_I32: {
+                const int32_t u = (int32_t)x->i, v = (int32_t)y->i; c = u < v ? -1 : (u > v ? 1 : 0); break; }
+            case FWA_MIN_F64: case FWA_MAX_F64: case FWA_MINBY_F64: case FWA_MAXBY_F64: c = jcmp_d(x->d, y->d); break;
+            default: c = jcmp_f(x->f, y->f); break;
+            }
+            const int wantmax = k == FWA_MAX_I64 || k == FWA_MAX_I32 || k == FWA_MAX_F64 || k == FWA_MAX_F32 || is_maxby(k);
+            if (is_byk(k)) { if (c == 0 ? (e->c.flags & FWA_CFG_BY_LAST) != 0 : (wantmax ? c < 0 : c > 0)) *x = *y; }
+            else if (wantmax ? !(c > 0) : !(c < 0)) *x = *y;   /* isExtremal == 0 -> value2's */
+        }
+        }
+    }
+}
+
 static void acc_merge(or_engine* e, aval* a, const aval* b) {
     if (b[0].i == 0) return;
+    if (e->c.flags & FWA_CFG_REDUCE) { red_merge(e, a, b); return; }
     const int na = e->c.num_aggs;
     a[0].i = jladd(a[0].i, b[0].i);
     for (int j = 0; j < na; j++) {
@@ -668,7 +702,9 @@ int or_create(const fwa_config* c, or_engine** out) {
         if (nred && !(c->flags & FWA_CFG_REDUCE)) return FWA_E_ARG;
         if (c->flags & FWA_CFG_REDUCE) {
             if (nby > 1 || (nsel && !nby) || (nfirst && nby)) return FWA_E_ARG;
-            if (c->semantics != FWA_SEM_DATASTREAM || (c->window_kind != FWA_TUMBLE && c->window_kind != FWA_SLIDE))
+            /* session windows: a tuple whose one value field is the reduced one (Tuple2<key, f1>) -- the engine's scope */
+            const int sess_ok = c->window_kind == FWA_SESSION && c->num_aggs == 1 && !nsel && !nfirst;
+            if (c->semantics != FWA_SEM_DATASTREAM || (c->window_kind != FWA_TUMBLE && c->window_kind != FWA_SLIDE && !sess_ok))
                 return FWA_E_UNSUPPORTED;
         }
     }
