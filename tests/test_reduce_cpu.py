@@ -69,3 +69,30 @@ def test_reduce_aggs_mapping():
     assert reduce_field_values({"key": [1], "win_start": [0], "win_end": [5], "agg0": np.array([3], np.int32),
                                 "agg1": np.array([1.5]).view(np.int64), "agg2": np.array([9])}, None) == \
         [(1, 0, 5, 3, 1.5, 9)]
+
+
+@pytest.mark.parametrize("kind", ["SUM_I64", "MIN_I64", "MAX_I64", "MINBY_I64", "MAXBY_I64"])
+def test_oracle_session_reduction_matches_model(kind):
+    """The oracle's session reduction (red_merge restating reduce(a, b) for MergingWindowSet merges) against a direct
+    model: sessions of gap 50 per key from the sorted timestamps, the field reduced over each; records arrive shuffled
+    within a push so that sessions merge."""
+    from oracle.oracle import Oracle
+    rng = np.random.default_rng(5)
+    n = 3000
+    keys = rng.integers(0, 20, n).astype(np.int64)
+    ts = rng.integers(0, 20_000, n).astype(np.int64)
+    v = rng.integers(-2**62, 2**62, n).astype(np.int64)
+    cfg = A.make_config(window_kind="SESSION", gap_ms=50, size_ms=0, aggs=[(kind, 0)], reduce=True)
+    o = Oracle(cfg)
+    o.push(keys, ts, [v])
+    got = reduce_field_values(o.advance_watermark(A.LONG_MAX), A.agg_names(cfg), ["I64"])
+    o.close()
+    f = {"SUM": lambda x: int(np.sum(x.astype(np.uint64)).astype(np.int64)), "MIN": min, "MAX": max}[kind[:3]]
+    want = []
+    for k in np.unique(keys):
+        sel = np.argsort(ts[keys == k], kind="stable")
+        t, x = ts[keys == k][sel], v[keys == k][sel]
+        cut = np.flatnonzero(np.diff(t) > 50) + 1          # TimeWindow.intersects: touching windows merge
+        for tt, xx in zip(np.split(t, cut), np.split(x, cut)):
+            want.append((int(k), int(tt[0]), int(tt[-1]) + 50, int(f(xx))))
+    assert got == sorted(want)
