@@ -249,3 +249,51 @@ def test_session_reduction_cell_preagg_vs_oracle(eng_mod, kind, col, route):
     assert paths == [2] * nb
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("lateness", [0, 1500], ids=["no_lateness", "lateness"])
+@pytest.mark.parametrize("kind,col", [("SUM_I64", 2), ("MIN_I32", 0), ("MAXBY_F64", 1), ("MINBY_F32", 3)])
+def test_session_reduction_snapshot_restore_rescale(eng_mod, kind, col, lateness):
+    """A session reduction checkpointed mid-stream (fwa_snapshot: its in-flight sessions) and restored into two subtasks
+    (key-group halves): every later watermark's rows equal an uninterrupted oracle run."""
+    from oracle.oracle import Oracle
+    keys, ts, cols = _stream(61 + col, 20_000, 300, 30_000, False)
+    cols = cols + [(cols[1] * 3).astype(np.float32)]
+    kw = dict(window_kind="SESSION", gap_ms=500, size_ms=0, aggs=[(kind, col)], reduce=True,
+              allowed_lateness_ms=lateness, key_capacity=4096)
+    cfg = A.make_config(**kw)
+    names, ty = A.agg_names(cfg), [("I32", "F64", "I64", "F32")[col]]
+    o, g = Oracle(cfg), eng_mod.WindowAggregator(cfg)
+    nb, mx, cut, subs = 8, -2**63, 4, None
+    for b in range(nb + 1):
+        sl = slice(b * len(keys) // nb, (b + 1) * len(keys) // nb) if b < nb else slice(0, 0)
+        c = [x[sl] for x in cols]
+        if b == cut:
+            blob = g.snapshot()
+            g.close()
+            subs = []
+            for lo, hi in ((0, 63), (64, 127)):
+                h = eng_mod.WindowAggregator(A.make_config(kg_start=lo, kg_end=hi, **kw))
+                h.restore([blob])
+                subs.append((h, lo, hi))
+        o.push(keys[sl], ts[sl], c)
+        if b < nb:
+            mx = max(mx, int(ts[sl].max()))
+        wm = mx - 801 if b < nb else A.LONG_MAX
+        exp = reduce_field_values(o.advance_watermark(wm), names, ty)
+        if subs is None:
+            g.push(keys[sl], ts[sl], c)
+            got = reduce_field_values(g.advance_watermark(wm), names, ty)
+        else:
+            kg, _ = eng_mod.key_groups(keys[sl], 128, 1) if len(keys[sl]) else (np.zeros(0, np.int32), None)
+            kg = np.asarray(kg)
+            got = []
+            for h, lo, hi in subs:
+                m = (kg >= lo) & (kg <= hi)
+                h.push(keys[sl][m], ts[sl][m], [x[m] for x in c])
+                got += reduce_field_values(h.advance_watermark(wm), names, ty)
+            got = sorted(got)
+        _close(got, exp, names)
+    for h, _, _ in subs:
+        h.close()
+    o.close()
