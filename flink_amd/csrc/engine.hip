@@ -2143,7 +2143,7 @@ struct fwa_engine {
     // FWA_CFG_REDUCE: DataStream built-in reductions (reduce.inc): per-record (kid, slot) of the last push
     bool red = false;
     unsigned long long* d_rk = nullptr;
-    int64_t* d_iota = nullptr;            // red_iota: the push's arrival sequence column (kIotaCol)
+    int32_t* d_iota = nullptr;            // red_iota: the push's record index column (kIotaCol)
     int64_t iota_cap = 0;
     int32_t* d_rslots = nullptr;          // red_iota: slots the payload pass scans
     int64_t rslots_cap = 0;
@@ -2767,8 +2767,9 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
     c.nacc = 1;
     c.acc_kind[0] = ACC_ADD_I64;
     // a reduce handle's payload fields get their columns after the accumulating ones (the combiner merges only those);
-    // a first- / last-element reduction (no MINBY / MAXBY) selects through an accumulator: SELQ = MIN (MAX) over the
-    // arrival sequence, a hidden aggregate over the engine's sequence column kIotaCol (reduce.inc), placed before them
+    // a first- / last-element reduction (no MINBY / MAXBY) selects through an accumulator: MIN (MAX) over the
+    // push's record index, a hidden aggregate (SCR) over the engine's index column kIotaCol (reduce.inc), placed before
+    // them; the payload pass turns it into the arrival sequence SELQ
     bool red_iota = (cfg->flags & FWA_CFG_REDUCE) != 0 && cfg->window_kind != FWA_SESSION;
     for (int j = 0; j < cfg->num_aggs; ++j)
         if (is_by_kind(cfg->aggs[j].kind) || cfg->aggs[j].col == kIotaCol) red_iota = false;
@@ -2778,12 +2779,12 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
             const bool last = (cfg->flags & FWA_CFG_BY_LAST) != 0;
             AggDesc& h = c.agg[c.naggs++];
             memset(&h, 0, sizeof(h));
-            h.kind = last ? FWA_MAX_I64 : FWA_MIN_I64;
+            h.kind = last ? FWA_MAX_I32 : FWA_MIN_I32;    // over the push's record index (4-byte column)
             h.col = kIotaCol;
             h.acc_kind = last ? ACC_MAX_ORD : ACC_MIN_ORD;
             h.acc = c.nacc;
             c.acc_kind[c.nacc] = h.acc_kind;
-            c.red_selq = c.nacc++;
+            c.red_scr = c.nacc++;
         }
         for (int j = 0; j < cfg->num_aggs; ++j) {
             AggDesc& d = c.agg[j];
@@ -2845,10 +2846,8 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
         }
         c.red_last = (cfg->flags & FWA_CFG_BY_LAST) != 0;
         if (cfg->window_kind != FWA_SESSION) {   // (a session reduction's one field is its only column: no selection)
-            if (!c.red_iota) {
-                c.red_selq = c.nacc;
-                c.acc_kind[c.nacc++] = c.red_last ? ACC_MAX_ORD : ACC_MIN_ORD;
-            }
+            c.red_selq = c.nacc;                   // (red_iota: the payload pass moves the push's selection here)
+            c.acc_kind[c.nacc++] = c.red_last ? ACC_MAX_ORD : ACC_MIN_ORD;
             c.red_selk = c.nacc;
             c.acc_kind[c.nacc++] = ACC_PAYLOAD;
             if (c.red_by >= 0) {   // scratch: identity between pushes (red_by_payload_kernel restores it)
@@ -2923,7 +2922,8 @@ static int create_engine(const fwa_config* cfg, fwa_engine** out) {
             const int k = c.agg[j].kind;
             if (c.agg[j].acc_kind == ACC_PAYLOAD || c.agg[j].acc == 0) continue;
             red_ok = red_ok && (k == FWA_SUM_I64 || k == FWA_SUM_F64 || k == FWA_MIN_I64 || k == FWA_MAX_I64 ||
-                                k == FWA_MINBY_I64 || k == FWA_MAXBY_I64);
+                                k == FWA_MINBY_I64 || k == FWA_MAXBY_I64 ||
+                                (c.agg[j].col == kIotaCol && (k == FWA_MIN_I32 || k == FWA_MAX_I32)));
         }
         ok = ok && np <= kMaxPart && sl >= 2 && e->kind != FWA_SESSION && !e->sparse && (!e->red || red_ok);
         e->v2 = ok;
@@ -4275,11 +4275,11 @@ static int push_body(fwa_engine* e, const int64_t* keys, const int64_t* ts, cons
             if (n > e->iota_cap) {
                 if (e->d_iota) HIPCHK(e, hipFree(e->d_iota));
                 e->d_iota = nullptr;
-                HIPCHK(e, hipMalloc(&e->d_iota, 8 * (size_t)n));
+                HIPCHK(e, hipMalloc(&e->d_iota, 4 * (size_t)n));
                 e->iota_cap = n;
             }
             HIPCHK(e, hipEventRecord(e->ev[8], e->stream));      // (ev[8] / ev[9]: record lists only otherwise)
-            iota_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(e->d_iota, seq0, n);
+            iota_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(e->d_iota, n);
             HIPCHK(e, hipGetLastError());
             HIPCHK(e, hipEventRecord(e->ev[9], e->stream));
             a.cols[kIotaCol] = e->d_iota;
