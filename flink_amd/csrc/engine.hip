@@ -2145,6 +2145,8 @@ struct fwa_engine {
     unsigned long long* d_rk = nullptr;
     int32_t* d_iota = nullptr;            // red_iota: the push's record index column (kIotaCol)
     int64_t iota_cap = 0;
+    int64_t iota_n = 0;                   // its length; filled on first use (ensure_iota): partition3 computes the index
+    bool iota_pending = false, iota_ran = false;
     int32_t* d_rslots = nullptr;          // red_iota: slots the payload pass scans
     int64_t rslots_cap = 0;
     int64_t rk_cap = 0;
@@ -3044,8 +3046,22 @@ static int wait_input_stream(fwa_engine* e) {
     return FWA_OK;
 }
 
+// red_iota: the record index column, written only when a reader of the column runs this push (the v1 ingest -- a whole
+// push or its miss replays -- or partition3 under variant bit 16); the two-phase ingest derives the index itself.
+static int ensure_iota(fwa_engine* e) {
+    if (!e->iota_pending) return FWA_OK;
+    e->iota_pending = false;
+    e->iota_ran = true;
+    HIPCHK(e, hipEventRecord(e->ev[8], e->stream));      // (ev[8] / ev[9]: record lists only otherwise)
+    iota_kernel<<<grid_for(e->iota_n, 256 * 32), kBlock, 0, e->stream>>>(e->d_iota, e->iota_n);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->ev[9], e->stream));
+    return FWA_OK;
+}
+
 static int launch_ingest(fwa_engine* e, IngestArgs& a, bool replay) {
     if (e->dir_dirty) { int rc = publish_dir(e); if (rc) return rc; }
+    if (e->iota_pending) { int rc = ensure_iota(e); if (rc) return rc; }
     a.spill_cap = e->spill_cap;
     a.key_table = e->d_keys;
     a.key_mask = (uint64_t)e->capacity - 1;
@@ -3225,6 +3241,8 @@ static int push_v2(fwa_engine* e, IngestArgs& a, bool* ran) {
     pa.part_bits = e->part_bits;
     pa.np = e->np;
     pa.sub_major = (e->opt_variant & 4) ? 0 : 1;   // variant bit 2: partition-major buckets (A/B)
+    pa.iota1 = e->ec.red_iota && e->nv == 2 && e->vcol[1] == kIotaCol && e->vsize[1] == 4 && !(e->opt_variant & 16);
+    if (e->iota_pending && !pa.iota1) { int rc = ensure_iota(e); if (rc) return rc; }
     for (int v = 0; v < 2; ++v) { pa.vcol[v] = e->vcol[v]; pa.vsize[v] = e->vsize[v]; }
     pa.dropidx = a.pcount ? nullptr : a.dropidx;   // partial rows: no record indices (as in v1)
     for (int c = 0; c < FWA_MAX_COLS; ++c) { pa.nulls[c] = a.nulls[c]; pa.any_null |= a.nulls[c] != nullptr; }
@@ -4278,14 +4296,14 @@ static int push_body(fwa_engine* e, const int64_t* keys, const int64_t* ts, cons
                 HIPCHK(e, hipMalloc(&e->d_iota, 4 * (size_t)n));
                 e->iota_cap = n;
             }
-            HIPCHK(e, hipEventRecord(e->ev[8], e->stream));      // (ev[8] / ev[9]: record lists only otherwise)
-            iota_kernel<<<grid_for(n, 256 * 32), kBlock, 0, e->stream>>>(e->d_iota, n);
-            HIPCHK(e, hipGetLastError());
-            HIPCHK(e, hipEventRecord(e->ev[9], e->stream));
+            e->iota_n = n;
+            e->iota_pending = true;                              // written on first use (ensure_iota)
+            e->iota_ran = false;
             a.cols[kIotaCol] = e->d_iota;
         }
         int rc = push_common(e, a, n, true, false, late_dropped_out);
-        if (!rc && e->ec.red_iota) {                               // the sequence column counts as ingest time
+        e->iota_pending = false;
+        if (!rc && e->iota_ran) {                                  // the index column counts as ingest time
             float ms = 0.f;
             HIPCHK(e, hipEventElapsedTime(&ms, e->ev[8], e->ev[9]));
             e->ingest_ms += ms;
