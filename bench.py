@@ -364,8 +364,8 @@ def ingest_kernels(args, eng):
     if eng.record_lists:
         return "sp_range_kernel+sp_hist_kernel+sp_scan_kernel+sp_scatter_kernel (record lists)"
     if args.config == "reduce":
-        return ("iota_kernel+partition3_kernel+combine3_kernel+red_iota_payload_kernel (two-phase ingest with the "
-                "record-index accumulator in narrow entries, then the payload pass)")
+        return ("partition3_kernel+combine3_kernel+red_iota_payload_kernel (two-phase ingest with the record-index "
+                "accumulator in narrow entries, the index derived in partition3, then the payload pass)")
     return "partition3_kernel+combine3_kernel" if eng.stats().partition_ms > 0 else "ingest_kernel"
 
 
